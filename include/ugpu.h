@@ -1,0 +1,159 @@
+/*
+ * ugpu.h -- C ABI of the MI355X DFA buffer-scan engine (ugrep_amd).
+ *
+ * This is the drop-in boundary for ugrep's hot path: the FIND loop of
+ * reflex::Matcher::match(Const::FIND) (reference lib/matcher.cpp:42-750), i.e.
+ * the adv_ prefilters (lib/matcher.cpp:797-954, lib/matcher_avx2.cpp:78-799,
+ * lib/matcher_avx512bw.cpp:50-463) plus the DFA opcode walk (lib/matcher.cpp:
+ * 125-546), driven by `while (matcher->find())` (src/ugrep.cpp:10544, :10869).
+ *
+ * Input artifact: the reference's compiled pattern, Pattern::opc_[0..nop_)
+ * (include/reflex/pattern.h:1302-1304; word format :1155-1247; produced by
+ * Pattern::encode_dfa, lib/pattern.cpp:2823-3063).  The same words are what the
+ * reference's precompiled-table constructor Pattern(const Opcode*, ...) takes
+ * (include/reflex/pattern.h:151-159), so a caller passes pattern.opc_ as is.
+ *
+ * Semantics: identical match records (start, length, accept index) to
+ * Matcher::find() on a fully buffered input (AbstractMatcher::buffer(),
+ * include/reflex/absmatcher.h:542-591): leftmost-longest, non-overlapping,
+ * empty matches rejected (option N off), options A/W off.  Tables with
+ * anchors/word-boundary meta edges, lookahead HEAD/TAIL or REDO words return
+ * UGPU_UNSUPPORTED; the caller keeps its CPU matcher for those
+ * (include/reflex/pattern.h:1194-1217).
+ *
+ * All functions return an int status; no exceptions cross this ABI (reference
+ * errors: regex_error lib/pattern.cpp:162-169, std::bad_alloc absmatcher.h:401).
+ * Handles are opaque.  A ugpu_dfa is immutable after creation and may be shared
+ * by threads (the reference shares one Pattern across GrepWorker clones,
+ * src/ugrep.cpp:4146-4149, :4206); a ugpu_scanner is per thread/stream.
+ */
+#ifndef UGPU_H
+#define UGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define UGPU_OK 0
+#define UGPU_UNSUPPORTED 1 /* table needs anchors/lookahead/REDO/W: use the CPU matcher */
+#define UGPU_INVAL 2       /* bad argument or malformed opcode table */
+#define UGPU_NOMEM 3       /* host or device allocation failed */
+#define UGPU_DEVICE 4      /* HIP runtime error (see ugpu_last_error) */
+#define UGPU_HALO 5        /* a match walked past readable bytes of a non-final shard */
+#define UGPU_CAPACITY 6    /* more matches than the caller's output capacity */
+
+/* scan modes */
+#define UGPU_MODE_COUNT 0   /* count + digests only */
+#define UGPU_MODE_OFFSETS 1 /* also materialize (start, len, cap) records */
+
+typedef struct ugpu_dfa ugpu_dfa;
+typedef struct ugpu_scanner ugpu_scanner;
+
+typedef struct ugpu_dfa_info
+{
+  uint32_t states;      /* DFA states including the dead state */
+  uint32_t classes;     /* byte equivalence classes */
+  uint32_t row;         /* table row width (256 = byte-indexed, else class-indexed, pow2) */
+  uint32_t format;      /* 0 = next[state][byte], 1 = cls[byte] + next[state][class] */
+  uint32_t table_bytes; /* bytes of the transition table staged in LDS */
+  uint32_t needles;     /* number of first bytes when <= 4 (SWAR prefilter), else 0 */
+  uint32_t first_bytes; /* number of bytes that can start a match (|fst_|) */
+  uint32_t accepting;   /* accepting states */
+} ugpu_dfa_info;
+
+/* Totals of one scan.  digest = sum(start*31 + len), dcap = sum((start+1)*cap),
+   both mod 2^64, start = byte offset + bias. */
+typedef struct ugpu_totals
+{
+  uint64_t count;
+  uint64_t digest;
+  uint64_t dcap;
+  uint64_t entry;  /* chain position entering the range (== lo for a fresh scan) */
+  uint64_t exit;   /* first chain position >= hi: where the search resumes after the range */
+  uint32_t flags;  /* bit0: a walk hit the readable end of a non-final shard (UGPU_HALO) */
+  uint32_t fix_rounds;
+} ugpu_totals;
+
+/* Library-owned match list for ugpu_find_all. */
+typedef struct ugpu_result
+{
+  uint64_t count;
+  uint64_t digest;
+  uint64_t dcap;
+  uint64_t *start; /* count entries, byte offsets relative to buf */
+  uint32_t *len;
+  uint32_t *cap;   /* accept index (Matcher::accept(), absmatcher.h:605-609) */
+} ugpu_result;
+
+/* --- pattern tables (replaces the Pattern -> Matcher table consumer) --- */
+
+/* Build the dense device tables from opcode words and upload them once to the
+   current device.  pattern_flags: reserved (pass 0). */
+int ugpu_dfa_create(const uint32_t *opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa **out);
+int ugpu_dfa_destroy(ugpu_dfa *dfa);
+int ugpu_dfa_info_get(const ugpu_dfa *dfa, ugpu_dfa_info *info);
+
+/* Host-only: build the dense tables without touching a device (inspection and
+   CPU tests).  trans gets states*row u16 entries (entry = target_state*row,
+   0 = dead), cls 256 bytes, caps `states` accept indices; *start is the start
+   entry, *accb the first accepting entry.  Pass NULL arrays to query sizes
+   through info first. */
+int ugpu_tables_build_host(const uint32_t *opc, uint32_t nop, ugpu_dfa_info *info, uint16_t *trans,
+                           uint32_t trans_cap, uint8_t *cls, uint32_t *caps, uint32_t caps_cap, uint32_t *start,
+                           uint32_t *accb);
+
+/* --- whole-buffer FIND (Matcher::buffer(); while (find()) ...) --- */
+
+/* buf may be host or device memory, len bytes, search starts at `start`
+   (the matcher's cur_).  Synchronous.  mode: UGPU_MODE_COUNT or _OFFSETS. */
+int ugpu_find_all(const ugpu_dfa *dfa, const uint8_t *buf, uint64_t len, uint64_t start, uint32_t mode,
+                  ugpu_result **out);
+int ugpu_result_free(ugpu_result *res);
+
+/* --- device-resident scanning (benchmarks, multi-GPU shards) --- */
+
+/* Workspace for scans of device buffers on the current device. */
+int ugpu_scanner_create(const ugpu_dfa *dfa, ugpu_scanner **out);
+int ugpu_scanner_destroy(ugpu_scanner *sc);
+
+/* Enqueue a COUNT scan of dbuf[lo..hi) on `stream` (hipStream_t, NULL = default).
+   Walks may read up to read_end; at_eof says read_end is the end of the whole
+   stream.  Reported starts are offset by `bias` (global shard offset).
+   Asynchronous: results are read with ugpu_scan_totals. */
+int ugpu_scan(ugpu_scanner *sc, const uint8_t *dbuf, uint64_t lo, uint64_t hi, uint64_t read_end, int at_eof,
+              uint64_t bias, void *stream);
+/* Synchronize the scanner's stream and return the totals of the last scan. */
+int ugpu_scan_totals(ugpu_scanner *sc, ugpu_totals *out);
+/* After ugpu_scan + ugpu_scan_totals: write the match records of the last scan
+   into device arrays (capacity entries each) on `stream`. */
+int ugpu_scan_offsets(ugpu_scanner *sc, uint64_t *d_start, uint32_t *d_len, uint32_t *d_cap, uint64_t capacity,
+                      void *stream);
+/* Shard-boundary stitch: the scan of [lo,hi) assumed the chain entered at
+   old_entry; the true chain enters at new_entry.  Returns the correction to add
+   to the totals and the (possibly changed) exit.  Synchronous. */
+int ugpu_chain_fix(ugpu_scanner *sc, const uint8_t *dbuf, uint64_t lo, uint64_t hi, uint64_t read_end, int at_eof,
+                   uint64_t bias, uint64_t old_entry, uint64_t new_entry, ugpu_totals *delta, void *stream);
+/* Time (ms) of the scan kernel of the last ugpu_scan, measured with HIP events
+   recorded on the scan stream around that launch. */
+int ugpu_scan_kernel_ms(ugpu_scanner *sc, float *ms);
+
+/* --- synthetic corpora, generated on device --- */
+#define UGPU_GEN_WORDS 1
+#define UGPU_GEN_PLANTED 2
+#define UGPU_GEN_CODE 3
+#define UGPU_GEN_UTF8 4
+/* Write bytes [off, off+len) of corpus `kind` with `seed` into dbuf. */
+int ugpu_gen(int kind, uint64_t seed, uint64_t off, uint8_t *dbuf, uint64_t len, void *stream);
+
+const char *ugpu_last_error(void);
+const char *ugpu_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UGPU_H */

@@ -1,0 +1,236 @@
+"""GPU parity: the HIP engine (through the C ABI) against the reference's golden
+outputs and the oracle restatement, bit-exact on every match record.
+
+Sizes: golden small cases (full lists), 64 MiB config digests computed by the
+reference, and size-independent properties at up to 1 GiB (planted known
+answer, grid-size invariance, shard split + stitch == whole)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+UNSUPPORTED = {"anchor_bol", "anchor_eol", "word_boundary", "lookahead"}
+
+
+@pytest.fixture(scope="module")
+def U():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd
+    return ugrep_amd
+
+
+@pytest.fixture(scope="module")
+def pats(U, patterns):
+    return {k: U.Pattern(v["opc"]) for k, v in patterns.items() if k not in UNSUPPORTED}
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(arr):
+    t = torch.from_numpy(np.ascontiguousarray(arr)).to("cuda")
+    torch.cuda.synchronize()
+    return t
+
+
+def _gen_dev(U, kind, seed, off, n, pad=0):
+    t = torch.empty(n + pad + 16, dtype=torch.uint8, device="cuda")
+    U.gen(kind, seed, off, t.data_ptr() + pad, n, _stream())
+    torch.cuda.synchronize()
+    return t
+
+
+def test_unsupported_rejected_on_device(U, patterns):
+    for name in UNSUPPORTED:
+        with pytest.raises(U.Unsupported):
+            U.Pattern(patterns[name]["opc"])
+
+
+def test_generator_matches_oracle(U):
+    from oracle_lib import gen
+    for kind in (1, 2, 3, 4):
+        for off, n, pad in ((0, 1 << 20, 0), (777, 100003, 5)):
+            t = _gen_dev(U, kind, 3, off, n, pad)
+            dev = t[pad:pad + n].cpu().numpy()
+            assert np.array_equal(dev, gen(kind, 3, off, n)), (kind, off)
+
+
+def test_golden_small_cases_offsets(U, pats, cases):
+    from oracle_lib import case_input
+    n = 0
+    for c in cases:
+        if c.get("big") or c["pattern"] in UNSUPPORTED:
+            continue
+        data = case_input(c["input"])
+        r = U.find_all(pats[c["pattern"]], data.tobytes(), offsets=True)
+        assert (r.count, r.digest, r.dcap) == (c["count"], c["digest"], c["dcap"]), (c["pattern"], c["input"])
+        if c["matches"] is not None:
+            assert r.triples() == c["matches"], (c["pattern"], c["input"])
+        n += 1
+    assert n > 300
+
+
+def test_golden_cases_device_buffers_count_mode(U, pats, cases):
+    """Same cases from a device buffer at an unaligned address, COUNT mode."""
+    from oracle_lib import case_input
+    for c in cases:
+        if c.get("big") or c["pattern"] in UNSUPPORTED or c["input"]["type"] == "hex":
+            continue
+        data = case_input(c["input"])
+        t = torch.zeros(data.size + 32, dtype=torch.uint8, device="cuda")
+        t[3:3 + data.size] = torch.from_numpy(data.copy()).to("cuda")
+        torch.cuda.synchronize()
+        sc = U.Scanner(pats[c["pattern"]])
+        sc.scan(t.data_ptr() + 3, 0, data.size, data.size, True, 0, _stream())
+        tot = sc.totals()
+        assert (tot.count, tot.digest, tot.dcap) == (c["count"], c["digest"], c["dcap"]), (c["pattern"], c["input"])
+        assert tot.exit >= data.size
+
+
+def test_refgold_matcher_api(U, pats, refgold):
+    """reflex-style Matcher loop reproduces the reference's tests/out offsets."""
+    from oracle_lib import case_input
+    for pname in ("hello", "hello_wnhS"):
+        data = case_input(dict(type="file", name=refgold[pname]["file"])).tobytes()
+        m = U.Matcher(pats[pname], data)
+        starts = []
+        while m.find():
+            starts.append(m.first())
+        assert starts == refgold[pname]["starts"]
+
+
+@pytest.mark.parametrize("pname,kind", [("c2_foobarbaz", 1), ("c2_foobarbaz", 2), ("c3_ident", 3), ("c4_word", 4)])
+def test_config_digests_64mib(U, pats, cases, pname, kind):
+    c = [c for c in cases if c.get("big") and c["pattern"] == pname and c["input"].get("kind") == kind][0]
+    n = c["input"]["len"]
+    t = _gen_dev(U, kind, c["input"]["seed"], 0, n)
+    sc = U.Scanner(pats[pname])
+    sc.scan(t.data_ptr(), 0, n, n, True, 0, _stream())
+    tot = sc.totals()
+    assert (tot.count, tot.digest, tot.dcap) == (c["count"], c["digest"], c["dcap"])
+
+
+def test_c1_anchor_64mib(U, pats):
+    from oracle_lib import case_input
+    data = case_input(dict(type="file", name="lorem.utf8.txt", total=1 << 26))
+    t = _dev(data)
+    sc = U.Scanner(pats["c1_lorem"])
+    sc.scan(t.data_ptr(), 0, data.size, data.size, True, 0, _stream())
+    tot = sc.totals()
+    assert (tot.count, tot.digest) == (14250, 14823334357500)
+
+
+def _planted_count(seed, n):
+    """Planted cells of the C2' corpus, from the cell seeds (vectorised splitmix64)."""
+    cells = np.arange(n // 64, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        s = np.uint64(seed) ^ (cells * np.uint64(0xD1B54A32D192ED03))
+        z = s + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = z ^ (z >> np.uint64(31))
+    return int(np.count_nonzero(((x >> np.uint64(1)) & np.uint64(63)) == 0))
+
+
+def test_planted_known_answer_1gib(U, pats):
+    n = 1 << 30
+    t = _gen_dev(U, 2, 2024, 0, n)
+    sc = U.Scanner(pats["c2_foobarbaz"])
+    sc.scan(t.data_ptr(), 0, n, n, True, 0, _stream())
+    tot = sc.totals()
+    assert tot.count == _planted_count(2024, n)
+    del t
+    torch.cuda.empty_cache()
+
+
+def test_grid_size_invariance(U, pats):
+    """Different block counts move every stitch point; totals must not change."""
+    n = 48 << 20
+    for pname, kind in (("c3_ident", 3), ("c4_word", 4), ("c2_foobarbaz", 1)):
+        t = _gen_dev(U, kind, 77, 0, n)
+        res = set()
+        for g in ("1", "7", "64", "1000", ""):
+            if g:
+                os.environ["UGPU_MAX_GRID"] = g
+            else:
+                os.environ.pop("UGPU_MAX_GRID", None)
+            sc = U.Scanner(pats[pname])
+            sc.scan(t.data_ptr(), 0, n, n, True, 0, _stream())
+            tot = sc.totals()
+            res.add((tot.count, tot.digest, tot.dcap, tot.exit))
+        os.environ.pop("UGPU_MAX_GRID", None)
+        assert len(res) == 1, (pname, res)
+
+
+def test_shard_split_and_stitch(U, pats):
+    """Two shards at an arbitrary (non-newline) offset + ugpu_chain_fix == one scan."""
+    from oracle_lib import OracleDfa, gen
+    n = 8 << 20
+    for pname, kind in (("c3_ident", 3), ("c4_word", 4), ("aa", 1), ("s_plus", 4)):
+        host = gen(kind, 11, 0, n)
+        t = _dev(host)
+        whole = U.Scanner(pats[pname])
+        whole.scan(t.data_ptr(), 0, n, n, True, 0, _stream())
+        w = whole.totals()
+        for cut in (n // 2 + 1, 3 * n // 4 + 17):
+            a, b = U.Scanner(pats[pname]), U.Scanner(pats[pname])
+            a.scan(t.data_ptr(), 0, cut, n, True, 0, _stream())
+            ta = a.totals()
+            b.scan(t.data_ptr(), cut, n, n, True, 0, _stream())
+            tb = b.totals()
+            cnt, dg, dc, ex = ta.count + tb.count, ta.digest + tb.digest, ta.dcap + tb.dcap, tb.exit
+            if ta.exit != cut:
+                d = b.chain_fix(t.data_ptr(), cut, n, n, True, 0, cut, ta.exit, _stream())
+                cnt, dg, dc = cnt + d.count, (dg + d.digest) % (1 << 64), (dc + d.dcap) % (1 << 64)
+            assert (cnt % (1 << 64), dg % (1 << 64), dc % (1 << 64)) == (w.count, w.digest, w.dcap), (pname, cut)
+        o = OracleDfa(pats[pname].opc)
+        assert o.find(host)[:3] == (w.count, w.digest, w.dcap)
+
+
+def test_nonsynchronising_chain(U, pats):
+    """'aa' over b + a^N: the speculative chains never meet (parity alternates), so
+    every lane, tile and block boundary needs the full stitch."""
+    from oracle_lib import OracleDfa
+    for n in (1 << 16, (1 << 22) + 5):
+        data = np.full(n, ord("a"), np.uint8)
+        data[0] = ord("b")
+        for g in ("3", ""):
+            if g:
+                os.environ["UGPU_MAX_GRID"] = g
+            else:
+                os.environ.pop("UGPU_MAX_GRID", None)
+            r = U.find_all(pats["aa"], data.tobytes(), offsets=False)
+            o = OracleDfa(pats["aa"].opc).find(data)
+            assert (r.count, r.digest, r.dcap) == o[:3]
+        os.environ.pop("UGPU_MAX_GRID", None)
+
+
+def test_offsets_at_scale(U, pats):
+    """Full match lists at 16 MiB (dense C3/C4 matches) equal the oracle's."""
+    from oracle_lib import OracleDfa, gen
+    n = 16 << 20
+    for pname, kind in (("c3_ident", 3), ("c4_word", 4), ("c2_foobarbaz", 1)):
+        host = gen(kind, 8, 0, n)
+        r = U.find_all(pats[pname], host.tobytes(), offsets=True)
+        cnt, dg, dc, lst = OracleDfa(pats[pname].opc).find(host, want_list=True)
+        assert (r.count, r.digest, r.dcap) == (cnt, dg, dc)
+        ref = np.asarray(lst, dtype=np.uint64).reshape(-1, 3)
+        assert np.array_equal(r.start, ref[:, 0]) and np.array_equal(r.length, ref[:, 1].astype(np.uint32))
+        assert np.array_equal(r.cap, ref[:, 2].astype(np.uint32))
+
+
+def test_start_offset(U, pats):
+    """find from a nonzero cursor (Matcher cur_) equals the oracle from that cursor."""
+    from oracle_lib import OracleDfa, gen
+    host = gen(3, 4, 0, 1 << 20)
+    for start in (1, 12345, 65535, 700001):
+        r = U.find_all(pats["c3_ident"], host.tobytes(), start=start, offsets=True)
+        o = OracleDfa(pats["c3_ident"].opc).find(host, start=start, want_list=True)
+        assert (r.count, r.digest, r.dcap) == o[:3]
+        assert r.triples() == o[3]

@@ -1,0 +1,11 @@
+"""ugrep_amd -- MI355X-native engine for ugrep's RE/flex DFA buffer-scan hot path.
+
+The C ABI (include/ugpu.h, libugrep_amd.so) is the product boundary; this
+package mirrors the reference's Pattern/Matcher FIND interface on top of it and
+holds the multi-GPU shard stitching (dist.py).
+"""
+from ._lib import (GEN_CODE, GEN_PLANTED, GEN_UTF8, GEN_WORDS, MODE_COUNT, MODE_OFFSETS, UgpuError,  # noqa: F401
+                   Unsupported, lib)
+from .matcher import Matcher, Pattern, Scanner, find_all, gen, host_tables  # noqa: F401
+
+__all__ = ["Pattern", "Matcher", "Scanner", "find_all", "gen", "host_tables", "Unsupported", "UgpuError"]

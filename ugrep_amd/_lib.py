@@ -1,0 +1,109 @@
+"""ctypes binding of the in-tree engine library libugrep_amd.so (include/ugpu.h).
+
+The product path is the HIP engine only: if the library is missing this module
+raises ImportError instead of falling back to any CPU implementation.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libugrep_amd.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "ugpu.h")
+
+UGPU_OK = 0
+UGPU_UNSUPPORTED = 1
+UGPU_INVAL = 2
+UGPU_NOMEM = 3
+UGPU_DEVICE = 4
+UGPU_HALO = 5
+UGPU_CAPACITY = 6
+
+MODE_COUNT = 0
+MODE_OFFSETS = 1
+
+GEN_WORDS, GEN_PLANTED, GEN_CODE, GEN_UTF8 = 1, 2, 3, 4
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u16p = ctypes.POINTER(ctypes.c_uint16)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+class DfaInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in
+                ("states", "classes", "row", "format", "table_bytes", "needles", "first_bytes", "accepting")]
+
+
+class Totals(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint64), ("digest", ctypes.c_uint64), ("dcap", ctypes.c_uint64),
+                ("entry", ctypes.c_uint64), ("exit", ctypes.c_uint64), ("flags", ctypes.c_uint32),
+                ("fix_rounds", ctypes.c_uint32)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint64), ("digest", ctypes.c_uint64), ("dcap", ctypes.c_uint64),
+                ("start", c_u64p), ("len", c_u32p), ("cap", c_u32p)]
+
+
+class UgpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("ugpu error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Unsupported(UgpuError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libugrep_amd.so not built (%s); run __graft_entry__.build() or make -C ugrep_amd"
+                          % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    V = ctypes.c_void_p
+    P = ctypes.POINTER
+    sig = {
+        "ugpu_dfa_create": (ctypes.c_int, [c_u32p, ctypes.c_uint32, ctypes.c_uint32, P(V)]),
+        "ugpu_dfa_destroy": (ctypes.c_int, [V]),
+        "ugpu_dfa_info_get": (ctypes.c_int, [V, P(DfaInfo)]),
+        "ugpu_tables_build_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, P(DfaInfo), c_u16p, ctypes.c_uint32,
+                                                  c_u8p, c_u32p, ctypes.c_uint32, c_u32p, c_u32p]),
+        "ugpu_find_all": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P(P(Result))]),
+        "ugpu_result_free": (ctypes.c_int, [P(Result)]),
+        "ugpu_scanner_create": (ctypes.c_int, [V, P(V)]),
+        "ugpu_scanner_destroy": (ctypes.c_int, [V]),
+        "ugpu_scan": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                     ctypes.c_uint64, V]),
+        "ugpu_scan_totals": (ctypes.c_int, [V, P(Totals)]),
+        "ugpu_scan_offsets": (ctypes.c_int, [V, V, V, V, ctypes.c_uint64, V]),
+        "ugpu_chain_fix": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, P(Totals), V]),
+        "ugpu_scan_kernel_ms": (ctypes.c_int, [V, P(ctypes.c_float)]),
+        "ugpu_gen": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, V, ctypes.c_uint64, V]),
+        "ugpu_last_error": (ctypes.c_char_p, []),
+        "ugpu_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc):
+    if rc != UGPU_OK:
+        msg = lib.ugpu_last_error().decode(errors="replace")
+        if rc == UGPU_UNSUPPORTED:
+            raise Unsupported(rc, msg)
+        raise UgpuError(rc, msg)
+    return rc
+
+
+def declared_symbols(header=HEADER):
+    """Function names declared in include/ugpu.h."""
+    import re
+    txt = open(header).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(ugpu_\w+)\s*\(", txt, re.M)))

@@ -1,0 +1,482 @@
+// engine.hip -- host side of the C ABI declared in include/ugpu.h.
+//
+// Pipeline of one whole-buffer FIND (what Matcher::find() computes lazily, one
+// match per call, lib/matcher.cpp:42-750):
+//   scan_kernel<.., WRITE=false>  persistent grid, speculative per-block chains,
+//                                 per-block (entry, exit, count, digests)
+//   fix_kernel                    stitch block entries, totals, output bases
+//   scan_kernel<.., WRITE=true>   (OFFSETS only) re-walk from exact entries and
+//                                 store (start, len, cap) records
+// Tables are uploaded once per ugpu_dfa (one Pattern), shared by all scanners.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "../../include/ugpu.h"
+#include "scan_kernels.hpp"
+#include "tables.hpp"
+
+using namespace ugpu;
+
+struct ugpu_dfa {
+  DfaTables t;
+  int device = 0;
+  uint32_t ntrans_pad = 0;
+  uint16_t* d_trans = nullptr;
+  uint8_t* d_cls = nullptr;
+  uint32_t* d_caps = nullptr;
+};
+
+struct ugpu_scanner {
+  const ugpu_dfa* dfa = nullptr;
+  int device = 0;
+  int max_grid = 0;
+  size_t smem = 0;
+  BlockRec* d_recs = nullptr;
+  uint64_t* d_entries = nullptr;
+  uint64_t* d_obase = nullptr;
+  DevTotals* d_tot = nullptr;
+  uint32_t* d_flags = nullptr;
+  DevTotals* h_tot = nullptr;  // pinned
+  uint32_t* h_flags = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipStream_t stream = nullptr;
+  ScanParams last{};
+  uint64_t off = 0;  // alignment shift of the last scan
+  bool have_scan = false;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg)
+{
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what)
+{
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return UGPU_DEVICE;
+}
+
+#define HIP_TRY(expr)                              \
+  do {                                             \
+    hipError_t _e = (expr);                        \
+    if (_e != hipSuccess) return hip_fail(_e, #expr); \
+  } while (0)
+
+void fill_tables(ScanParams& P, const ugpu_dfa* d)
+{
+  P.trans = d->d_trans;
+  P.cls = d->d_cls;
+  P.caps = d->d_caps;
+  P.ntrans_pad = d->ntrans_pad;
+  P.start = d->t.start;
+  P.accb = d->t.accb;
+  P.log_row = d->t.log_row;
+  P.needles = d->t.needles[0] | (d->t.needles[1] << 8) | (d->t.needles[2] << 16) | ((uint32_t)d->t.needles[3] << 24);
+}
+
+// Translate a byte range of dbuf into the 16-byte aligned base coordinates
+// the kernels use, and fix the grid geometry.
+void geometry(ScanParams& P, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint64_t read_end, int max_grid,
+              uint64_t& off)
+{
+  off = reinterpret_cast<uintptr_t>(dbuf) & 15u;
+  P.g = dbuf - off;
+  P.lo = lo + off;
+  P.hi = hi + off;
+  P.rend = read_end + off;
+  const uint64_t t0 = P.lo / kTile;
+  uint64_t t1 = (P.hi + kTile - 1) / kTile;
+  if (t1 <= t0) t1 = t0 + 1;
+  const uint64_t nt = t1 - t0;
+  uint64_t grid = nt < (uint64_t)max_grid ? nt : (uint64_t)max_grid;
+  if (grid == 0) grid = 1;
+  const uint64_t tpb = (nt + grid - 1) / grid;
+  grid = (nt + tpb - 1) / tpb;
+  P.t0 = t0;
+  P.t1 = t1;
+  P.tpb = tpb;
+  P.grid = (uint32_t)grid;
+}
+
+bool is_device_ptr(const void* p)
+{
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ugpu_last_error(void) { return g_err.c_str(); }
+
+const char* ugpu_version(void) { return "ugrep_amd 0.1 (gfx950)"; }
+
+int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa** out)
+{
+  (void)pattern_flags;
+  if (!out) return fail(UGPU_INVAL, "out is NULL");
+  *out = nullptr;
+  ugpu_dfa* d = new (std::nothrow) ugpu_dfa();
+  if (!d) return fail(UGPU_NOMEM, "host allocation");
+  std::string err;
+  int rc = build_tables(opc, nop, d->t, err);
+  if (rc != 0) {
+    delete d;
+    return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  }
+  hipError_t e = hipGetDevice(&d->device);
+  if (e != hipSuccess) {
+    delete d;
+    return hip_fail(e, "hipGetDevice");
+  }
+  const size_t n = d->t.trans.size();
+  d->ntrans_pad = (uint32_t)((n + 7) & ~size_t(7));
+  std::vector<uint16_t> tr(d->ntrans_pad, 0);
+  std::copy(d->t.trans.begin(), d->t.trans.end(), tr.begin());
+  if ((e = hipMalloc(&d->d_trans, tr.size() * 2)) != hipSuccess ||
+      (e = hipMalloc(&d->d_cls, 256)) != hipSuccess ||
+      (e = hipMalloc(&d->d_caps, d->t.caps.size() * 4)) != hipSuccess ||
+      (e = hipMemcpy(d->d_trans, tr.data(), tr.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(d->d_cls, d->t.cls.data(), 256, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(d->d_caps, d->t.caps.data(), d->t.caps.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+    ugpu_dfa_destroy(d);
+    return hip_fail(e, "table upload");
+  }
+  *out = d;
+  return UGPU_OK;
+}
+
+int ugpu_dfa_destroy(ugpu_dfa* d)
+{
+  if (!d) return UGPU_OK;
+  if (d->d_trans) (void)hipFree(d->d_trans);
+  if (d->d_cls) (void)hipFree(d->d_cls);
+  if (d->d_caps) (void)hipFree(d->d_caps);
+  delete d;
+  return UGPU_OK;
+}
+
+int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
+{
+  if (!d || !info) return fail(UGPU_INVAL, "NULL argument");
+  info->states = d->t.states;
+  info->classes = d->t.classes;
+  info->row = d->t.row;
+  info->format = d->t.format;
+  info->table_bytes = (uint32_t)(d->t.trans.size() * 2 + (d->t.format == FMT_CLASS ? 256 : 0));
+  info->needles = d->t.nneedle;
+  info->first_bytes = d->t.first_bytes;
+  info->accepting = d->t.accepting;
+  return UGPU_OK;
+}
+
+int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* info, uint16_t* trans,
+                           uint32_t trans_cap, uint8_t* cls, uint32_t* caps, uint32_t caps_cap, uint32_t* start,
+                           uint32_t* accb)
+{
+  if (!info) return fail(UGPU_INVAL, "info is NULL");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  info->states = t.states;
+  info->classes = t.classes;
+  info->row = t.row;
+  info->format = t.format;
+  info->table_bytes = (uint32_t)(t.trans.size() * 2 + (t.format == FMT_CLASS ? 256 : 0));
+  info->needles = t.nneedle;
+  info->first_bytes = t.first_bytes;
+  info->accepting = t.accepting;
+  if (start) *start = t.start;
+  if (accb) *accb = t.accb;
+  if (trans) {
+    if (trans_cap < t.trans.size()) return fail(UGPU_CAPACITY, "trans capacity");
+    std::copy(t.trans.begin(), t.trans.end(), trans);
+  }
+  if (cls) std::copy(t.cls.begin(), t.cls.end(), cls);
+  if (caps) {
+    if (caps_cap < t.caps.size()) return fail(UGPU_CAPACITY, "caps capacity");
+    std::copy(t.caps.begin(), t.caps.end(), caps);
+  }
+  return UGPU_OK;
+}
+
+int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
+{
+  if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
+  *out = nullptr;
+  ugpu_scanner* s = new (std::nothrow) ugpu_scanner();
+  if (!s) return fail(UGPU_NOMEM, "host allocation");
+  s->dfa = dfa;
+  HIP_TRY(hipGetDevice(&s->device));
+  s->smem = scan_smem_bytes(dfa->ntrans_pad, dfa->t.format);
+  if (s->smem > 160 * 1024) {
+    delete s;
+    return fail(UGPU_UNSUPPORTED, "tables do not fit in LDS");
+  }
+  int per_cu = 0;
+  HIP_TRY(scan_occupancy(dfa->t.format, dfa->t.nneedle, s->smem, &per_cu));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, s->device));
+  if (per_cu < 1) per_cu = 1;
+  int g = prop.multiProcessorCount * per_cu;
+  if (g > kMaxGrid) g = kMaxGrid;
+  s->max_grid = g;
+  if (const char* env = std::getenv("UGPU_MAX_GRID")) {
+    int v = std::atoi(env);
+    if (v >= 1 && v <= kMaxGrid) s->max_grid = v;
+  }
+  HIP_TRY(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxGrid));
+  HIP_TRY(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxGrid));
+  HIP_TRY(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxGrid));
+  HIP_TRY(hipMalloc(&s->d_tot, sizeof(DevTotals)));
+  HIP_TRY(hipMalloc(&s->d_flags, sizeof(uint32_t)));
+  HIP_TRY(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
+  HIP_TRY(hipHostMalloc(&s->h_flags, sizeof(uint32_t)));
+  HIP_TRY(hipEventCreate(&s->ev0));
+  HIP_TRY(hipEventCreate(&s->ev1));
+  *out = s;
+  return UGPU_OK;
+}
+
+int ugpu_scanner_destroy(ugpu_scanner* s)
+{
+  if (!s) return UGPU_OK;
+  (void)hipFree(s->d_recs);
+  (void)hipFree(s->d_entries);
+  (void)hipFree(s->d_obase);
+  (void)hipFree(s->d_tot);
+  (void)hipFree(s->d_flags);
+  (void)hipHostFree(s->h_tot);
+  (void)hipHostFree(s->h_flags);
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
+  delete s;
+  return UGPU_OK;
+}
+
+int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint64_t read_end, int at_eof,
+              uint64_t bias, void* stream)
+{
+  if (!s || !dbuf) return fail(UGPU_INVAL, "NULL argument");
+  if (lo > hi || hi > read_end) return fail(UGPU_INVAL, "need lo <= hi <= read_end");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ScanParams P{};
+  fill_tables(P, s->dfa);
+  geometry(P, dbuf, lo, hi, read_end, s->max_grid, s->off);
+  P.delta = (int64_t)bias - (int64_t)s->off;
+  P.at_eof = at_eof ? 1u : 0u;
+  P.recs = s->d_recs;
+  P.flags = s->d_flags;
+  P.totals = s->d_tot;
+  P.entries_out = s->d_entries;
+  P.out_base_out = s->d_obase;
+  HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
+  HIP_TRY(hipEventRecord(s->ev0, st));
+  HIP_TRY(launch_scan(P, s->dfa->t.format, s->dfa->t.nneedle, false, s->smem, st));
+  HIP_TRY(hipEventRecord(s->ev1, st));
+  HIP_TRY(launch_fix(P, s->dfa->t.format, st));
+  HIP_TRY(hipMemcpyAsync(s->h_tot, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  s->last = P;
+  s->stream = st;
+  s->have_scan = true;
+  return UGPU_OK;
+}
+
+int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
+{
+  if (!s || !out) return fail(UGPU_INVAL, "NULL argument");
+  if (!s->have_scan) return fail(UGPU_INVAL, "no scan issued");
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  const DevTotals& t = *s->h_tot;
+  out->count = t.count;
+  out->digest = t.digest;
+  out->dcap = t.dcap;
+  out->entry = t.entry - s->off;
+  out->exit = t.exit - s->off;
+  out->flags = *s->h_flags;
+  out->fix_rounds = t.rounds;
+  if (out->flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
+  return UGPU_OK;
+}
+
+int ugpu_scan_kernel_ms(ugpu_scanner* s, float* ms)
+{
+  if (!s || !ms) return fail(UGPU_INVAL, "NULL argument");
+  HIP_TRY(hipEventSynchronize(s->ev1));
+  HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
+  return UGPU_OK;
+}
+
+int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint32_t* d_cap, uint64_t capacity,
+                      void* stream)
+{
+  if (!s || !s->have_scan) return fail(UGPU_INVAL, "no scan issued");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ScanParams P = s->last;
+  P.entries = s->d_entries;
+  P.out_base = s->d_obase;
+  P.out_start = d_start;
+  P.out_len = d_len;
+  P.out_cap = d_cap;
+  P.out_capacity = capacity;
+  HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
+  HIP_TRY(launch_scan(P, s->dfa->t.format, s->dfa->t.nneedle, true, s->smem, st));
+  HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (*s->h_flags & UGPU_FLAG_CAPACITY) return fail(UGPU_CAPACITY, "output capacity exceeded");
+  if (*s->h_flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
+  return UGPU_OK;
+}
+
+int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint64_t read_end, int at_eof,
+                   uint64_t bias, uint64_t old_entry, uint64_t new_entry, ugpu_totals* delta, void* stream)
+{
+  if (!s || !dbuf || !delta) return fail(UGPU_INVAL, "NULL argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ScanParams P{};
+  fill_tables(P, s->dfa);
+  uint64_t off = 0;
+  geometry(P, dbuf, lo, hi, read_end, s->max_grid, off);
+  P.delta = (int64_t)bias - (int64_t)off;
+  P.at_eof = at_eof ? 1u : 0u;
+  P.totals = s->d_tot;
+  HIP_TRY(launch_chain_fix(P, s->dfa->t.format, old_entry + off, new_entry + off, st));
+  DevTotals t;
+  HIP_TRY(hipMemcpyAsync(&t, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  delta->count = t.count;
+  delta->digest = t.digest;
+  delta->dcap = t.dcap;
+  delta->entry = new_entry;
+  delta->exit = (t.exit == ~0ull) ? ~0ull : t.exit - off;
+  delta->flags = t.flags;
+  delta->fix_rounds = t.rounds;
+  if (t.flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
+  return UGPU_OK;
+}
+
+int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_t start, uint32_t mode,
+                  ugpu_result** out)
+{
+  if (!dfa || !out || (!buf && len)) return fail(UGPU_INVAL, "NULL argument");
+  *out = nullptr;
+  if (start > len) start = len;
+  ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
+  if (!r) return fail(UGPU_NOMEM, "host allocation");
+  ugpu_scanner* s = nullptr;
+  int rc = ugpu_scanner_create(dfa, &s);
+  if (rc) {
+    std::free(r);
+    return rc;
+  }
+  const bool dev = len > 0 && is_device_ptr(buf);
+  uint8_t* dcopy = nullptr;
+  const uint8_t* dbuf = buf;
+  uint64_t* d_start = nullptr;
+  uint32_t* d_len = nullptr;
+  uint32_t* d_cap = nullptr;
+  ugpu_totals tot{};
+  auto cleanup = [&]() {
+    if (dcopy) (void)hipFree(dcopy);
+    if (d_start) (void)hipFree(d_start);
+    if (d_len) (void)hipFree(d_len);
+    if (d_cap) (void)hipFree(d_cap);
+    ugpu_scanner_destroy(s);
+  };
+  hipError_t e;
+  if (!dev) {
+    if ((e = hipMalloc(&dcopy, len + 16)) != hipSuccess) {
+      cleanup();
+      std::free(r);
+      return hip_fail(e, "hipMalloc input");
+    }
+    if (len && (e = hipMemcpy(dcopy, buf, len, hipMemcpyHostToDevice)) != hipSuccess) {
+      cleanup();
+      std::free(r);
+      return hip_fail(e, "hipMemcpy input");
+    }
+    dbuf = dcopy;
+  }
+  static const uint8_t zero16[16] = {0};
+  if (len == 0 && !dcopy) dbuf = zero16;  // never read
+  if (len == 0) {
+    cleanup();
+    *out = r;
+    return UGPU_OK;
+  }
+  rc = ugpu_scan(s, dbuf, start, len, len, 1, 0, nullptr);
+  if (!rc) rc = ugpu_scan_totals(s, &tot);
+  if (rc) {
+    cleanup();
+    std::free(r);
+    return rc;
+  }
+  r->count = tot.count;
+  r->digest = tot.digest;
+  r->dcap = tot.dcap;
+  if (mode == UGPU_MODE_OFFSETS && tot.count > 0) {
+    const uint64_t n = tot.count;
+    r->start = static_cast<uint64_t*>(std::malloc(n * 8));
+    r->len = static_cast<uint32_t*>(std::malloc(n * 4));
+    r->cap = static_cast<uint32_t*>(std::malloc(n * 4));
+    if (!r->start || !r->len || !r->cap || hipMalloc(&d_start, n * 8) != hipSuccess ||
+        hipMalloc(&d_len, n * 4) != hipSuccess || hipMalloc(&d_cap, n * 4) != hipSuccess) {
+      cleanup();
+      ugpu_result_free(r);
+      return fail(UGPU_NOMEM, "match list allocation");
+    }
+    rc = ugpu_scan_offsets(s, d_start, d_len, d_cap, n, nullptr);
+    if (!rc) {
+      if ((e = hipMemcpy(r->start, d_start, n * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
+          (e = hipMemcpy(r->len, d_len, n * 4, hipMemcpyDeviceToHost)) != hipSuccess ||
+          (e = hipMemcpy(r->cap, d_cap, n * 4, hipMemcpyDeviceToHost)) != hipSuccess)
+        rc = hip_fail(e, "hipMemcpy matches");
+    }
+    if (rc) {
+      cleanup();
+      ugpu_result_free(r);
+      return rc;
+    }
+  }
+  cleanup();
+  *out = r;
+  return UGPU_OK;
+}
+
+int ugpu_result_free(ugpu_result* r)
+{
+  if (!r) return UGPU_OK;
+  std::free(r->start);
+  std::free(r->len);
+  std::free(r->cap);
+  std::free(r);
+  return UGPU_OK;
+}
+
+int ugpu_gen(int kind, uint64_t seed, uint64_t off, uint8_t* dbuf, uint64_t len, void* stream)
+{
+  if (kind < 1 || kind > 4) return fail(UGPU_INVAL, "unknown corpus kind");
+  if (!dbuf && len) return fail(UGPU_INVAL, "NULL buffer");
+  HIP_TRY(launch_gen(kind, seed, off, dbuf, len, reinterpret_cast<hipStream_t>(stream)));
+  return UGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// scan_kernels.hpp -- device side of the MI355X FIND engine.
+//
+// One chain = the sequence of search positions the reference's FIND loop visits
+// (lib/matcher.cpp:42-750): at position p walk the DFA,
+// remember the last accepting state, emit the longest non-empty match and jump
+// to its end, else move to p+1.  The chain is sequential; the GPU cuts the
+// input into lane SEGMENTS (64 B), runs every segment's chain speculatively
+// from the segment start, and stitches the true chain back together:
+//
+//   * the true chain enters segment k at the exit x of segment k-1 (x >= start);
+//   * if x differs from the speculative entry, the lane re-walks both chains in
+//     lock step, subtracting the speculative matches and adding the true ones,
+//     until the two chains meet (then everything after is identical) or both
+//     leave the segment (then the exit changed and the next lane repeats this).
+//
+// Within a 16 KiB tile the lanes resolve this in LDS rounds; tiles of one block
+// are processed in order so a block's chain is exact from its entry; block
+// entries are fixed by fix_kernel the same way (rarely more than one round).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace ugpu {
+
+constexpr int kBlock = 256;            // threads per workgroup (4 waves)
+constexpr int kSeg = 64;               // bytes per lane segment
+constexpr int kTile = kBlock * kSeg;   // 16 KiB staged per tile
+constexpr int kHalo = 256;             // bytes staged past the tile end
+constexpr int kMaxGrid = 4096;         // block records fixed by one fix_kernel block
+constexpr int kFixThreads = 1024;
+
+struct BlockRec {
+  uint64_t entry, exit, cnt, dg, dc, pad0, pad1, pad2;
+};
+
+struct DevTotals {
+  uint64_t count, digest, dcap, entry, exit;
+  uint32_t flags, rounds;
+};
+
+#define UGPU_FLAG_HALO 1u
+#define UGPU_FLAG_CAPACITY 2u
+
+struct ScanParams {
+  const uint8_t* g;   // 16-byte aligned base of the scanned bytes
+  uint64_t lo, hi;    // chain positions [lo, hi) (base coordinates)
+  uint64_t rend;      // walks may read bytes < rend
+  int64_t delta;      // reported start = position + delta
+  uint32_t at_eof;    // rend is the end of the stream
+  uint32_t pad;
+  uint64_t t0, t1, tpb;  // tiles [t0, t1), tiles per block
+  const uint16_t* trans;
+  const uint8_t* cls;
+  const uint32_t* caps;
+  uint32_t ntrans_pad;   // u16 entries, multiple of 8
+  uint32_t start, accb, log_row;
+  uint32_t needles;      // packed first bytes (nneedle <= 4)
+  uint32_t grid;
+  BlockRec* recs;
+  const uint64_t* entries;   // OFFSETS pass: exact block entries
+  const uint64_t* out_base;  // OFFSETS pass: first output index per block
+  uint64_t* out_start;
+  uint32_t* out_len;
+  uint32_t* out_cap;
+  uint64_t out_capacity;
+  uint32_t* flags;
+  DevTotals* totals;
+  uint64_t* entries_out;     // fix_kernel: exact block entries
+  uint64_t* out_base_out;    // fix_kernel: exclusive scan of block counts
+};
+
+// launchers (scan_kernels.hip)
+hipError_t launch_scan(const ScanParams& P, uint32_t format, uint32_t nneedle, bool write, size_t smem,
+                       hipStream_t stream);
+hipError_t launch_fix(const ScanParams& P, uint32_t format, hipStream_t stream);
+hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_entry, uint64_t new_entry,
+                            hipStream_t stream);
+hipError_t scan_occupancy(uint32_t format, uint32_t nneedle, size_t smem, int* blocks_per_cu);
+hipError_t launch_gen(int kind, uint64_t seed, uint64_t off, uint8_t* dbuf, uint64_t len, hipStream_t stream);
+size_t scan_smem_bytes(uint32_t ntrans_pad, uint32_t format);
+
+}  // namespace ugpu

@@ -1,0 +1,200 @@
+// tables.cpp -- RE/flex opcode words -> dense DFA tables (see tables.hpp).
+//
+// Opcode word format: include/reflex/pattern.h:1155-1247
+//   goto  lo<<24 | hi<<16 | index16        (HALT index 0xFFFF, LONG index 0xFFFE
+//                                            + next word 0xFF000000|index24)
+//   halt  0x00FFFFFF
+//   take  0xFE000000 | accept                (head of an accepting state block)
+//   redo  0xFD000000, tail 0xFC.., head 0xFB.., meta gotos (hi byte 0)
+// State block layout (lib/pattern.cpp:2943-3063): [REDO|TAKE]? TAIL* HEAD*
+// then gotos in descending lo order; the interpreter takes the first goto whose
+// [lo,hi] holds the byte (lib/matcher.cpp:467-502).
+#include "tables.hpp"
+
+#include <algorithm>
+#include <map>
+#include <unordered_map>
+
+namespace ugpu {
+
+namespace {
+
+inline bool word_is_goto(uint32_t w) { return (uint32_t)(w << 8) >= (w & 0xff000000u); }
+inline bool word_is_meta(uint32_t w) { return (w & 0x00ff0000u) == 0 && (w >> 24) > 0; }
+
+constexpr uint32_t kHalt = 0xffff;
+constexpr uint32_t kLong = 0xfffe;
+constexpr int64_t kDead = -1;
+
+struct RawState {
+  uint32_t pc;
+  uint32_t cap;
+  int64_t target_pc[256];
+};
+
+}  // namespace
+
+int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string& err)
+{
+  if (opc == nullptr || nop == 0) {
+    err = "empty opcode table";
+    return 2;
+  }
+  std::vector<RawState> raw;
+  std::unordered_map<uint32_t, uint32_t> index_of_pc;  // pc -> raw index
+  raw.reserve(64);
+  raw.push_back(RawState{0, 0, {}});
+  index_of_pc[0] = 0;
+  for (size_t qi = 0; qi < raw.size(); ++qi) {
+    uint32_t pc = raw[qi].pc;
+    uint32_t k = pc;
+    uint32_t cap = 0;
+    // block header
+    while (k < nop && !word_is_goto(opc[k])) {
+      uint32_t op = opc[k] >> 24;
+      if (op == 0xfe) {
+        cap = opc[k] & 0xffffff;
+      } else {
+        err = "opcode table uses REDO/TAIL/HEAD/indent words";
+        return 1;
+      }
+      ++k;
+    }
+    int64_t tgt[256];
+    bool have[256];
+    std::fill(have, have + 256, false);
+    int remaining = 256;
+    while (remaining > 0) {
+      if (k >= nop) {
+        err = "state block runs past the end of the opcode table";
+        return 2;
+      }
+      uint32_t w = opc[k];
+      if (!word_is_goto(w)) {
+        err = "state block does not cover every byte";
+        return 2;
+      }
+      if (word_is_meta(w)) {
+        err = "opcode table uses meta edges (anchors / word boundaries)";
+        return 1;
+      }
+      uint32_t lo = w >> 24, hi = (w >> 16) & 0xff, idx = w & 0xffff;
+      int64_t t;
+      if (idx == kHalt) {
+        t = kDead;
+      } else if (idx == kLong) {
+        if (k + 1 >= nop) {
+          err = "LONG goto without index word";
+          return 2;
+        }
+        t = opc[k + 1] & 0xffffff;
+      } else {
+        t = idx;
+      }
+      if (t != kDead && (uint64_t)t >= nop) {
+        err = "goto target out of range";
+        return 2;
+      }
+      for (uint32_t c = lo; c <= hi; ++c)
+        if (!have[c]) {
+          have[c] = true;
+          tgt[c] = t;
+          --remaining;
+        }
+      k += (idx == kLong) ? 2 : 1;
+    }
+    for (int c = 0; c < 256; ++c) {
+      int64_t t = tgt[c];
+      if (t != kDead && index_of_pc.find((uint32_t)t) == index_of_pc.end()) {
+        index_of_pc[(uint32_t)t] = (uint32_t)raw.size();
+        raw.push_back(RawState{(uint32_t)t, 0, {}});
+      }
+    }
+    raw[qi].cap = cap;
+    std::copy(tgt, tgt + 256, raw[qi].target_pc);
+  }
+
+  // renumber: dead = 0, non-accepting states, then accepting states
+  const uint32_t n = (uint32_t)raw.size();
+  std::vector<uint32_t> sid(n);
+  uint32_t next_id = 1;
+  for (uint32_t i = 0; i < n; ++i)
+    if (raw[i].cap == 0) sid[i] = next_id++;
+  const uint32_t first_acc = next_id;
+  for (uint32_t i = 0; i < n; ++i)
+    if (raw[i].cap != 0) sid[i] = next_id++;
+  const uint32_t S = next_id;
+
+  // dense next[sid][byte] in new ids
+  std::vector<uint32_t> nxt((size_t)S * 256, 0);
+  std::vector<uint32_t> caps(S, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    caps[sid[i]] = raw[i].cap;
+    for (int c = 0; c < 256; ++c) {
+      int64_t t = raw[i].target_pc[c];
+      nxt[(size_t)sid[i] * 256 + c] = (t == kDead) ? 0 : sid[index_of_pc[(uint32_t)t]];
+    }
+  }
+
+  // byte equivalence classes (identical columns over all states)
+  std::map<std::vector<uint32_t>, uint32_t> colmap;
+  std::vector<uint8_t> cls(256);
+  for (int c = 0; c < 256; ++c) {
+    std::vector<uint32_t> col(S);
+    for (uint32_t s = 0; s < S; ++s) col[s] = nxt[(size_t)s * 256 + c];
+    auto it = colmap.find(col);
+    if (it == colmap.end()) it = colmap.emplace(col, (uint32_t)colmap.size()).first;
+    cls[c] = (uint8_t)it->second;
+  }
+  const uint32_t C = (uint32_t)colmap.size();
+
+  DfaTables t;
+  t.states = S;
+  t.classes = C;
+  if ((uint64_t)S * 256 <= 65536) {
+    t.format = FMT_BYTE;
+    t.row = 256;
+    t.log_row = 8;
+  } else {
+    uint32_t r = 1, lr = 0;
+    while (r < C) {
+      r <<= 1;
+      ++lr;
+    }
+    if ((uint64_t)S * r > 65536) {
+      err = "DFA too large for 16-bit device tables";
+      return 1;
+    }
+    t.format = FMT_CLASS;
+    t.row = r;
+    t.log_row = lr;
+  }
+  const uint32_t R = t.row;
+  t.trans.assign((size_t)S * R, 0);
+  if (t.format == FMT_BYTE) {
+    for (uint32_t s = 0; s < S; ++s)
+      for (int c = 0; c < 256; ++c) t.trans[(size_t)s * R + c] = (uint16_t)(nxt[(size_t)s * 256 + c] * R);
+    for (int c = 0; c < 256; ++c) t.cls.push_back((uint8_t)c);
+  } else {
+    t.cls = cls;
+    for (uint32_t s = 0; s < S; ++s)
+      for (int c = 0; c < 256; ++c) t.trans[(size_t)s * R + cls[c]] = (uint16_t)(nxt[(size_t)s * 256 + c] * R);
+  }
+  t.caps = caps;
+  const uint32_t start_sid = sid[0];
+  t.start = start_sid * R;
+  t.accepting = S - first_acc;
+  t.accb = (t.accepting > 0) ? first_acc * R : 0x10000u;
+  uint32_t nf = 0;
+  for (int c = 0; c < 256; ++c)
+    if (nxt[(size_t)start_sid * 256 + c] != 0) {
+      if (nf < 4) t.needles[nf] = (uint8_t)c;
+      ++nf;
+    }
+  t.first_bytes = nf;
+  t.nneedle = (nf >= 1 && nf <= 4) ? nf : 0;
+  out = std::move(t);
+  return 0;
+}
+
+}  // namespace ugpu

@@ -1,0 +1,232 @@
+"""Host-side mirror of the reference matcher interface for the FIND hot path.
+
+    reflex::Pattern(const Opcode *code, ...)   include/reflex/pattern.h:151-159
+    reflex::Matcher(pattern); m.buffer(base, size); while (m.find()) ...
+        find  = AbstractMatcher::Operation, include/reflex/absmatcher.h:276-280, :1401
+        first = absmatcher.h:901-905, size = :651-658, accept = :605-609
+
+`Pattern` takes the compiled opcode words (Pattern::opc_) and uploads the dense
+tables once; `Matcher` serves find() from one whole-buffer GPU scan, the way a
+ugrep worker consumes matches from a mmap'd file (src/ugrep.cpp:3936-3940,
+:10544).  Everything runs through the HIP engine (libugrep_amd.so); there is no
+CPU fallback in this module: tables the engine does not support raise
+`Unsupported`, as ugpu_dfa_create returns UGPU_UNSUPPORTED.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _as_u32(opc):
+    a = np.ascontiguousarray(np.asarray(opc, dtype=np.uint32))
+    return a, a.ctypes.data_as(_lib.c_u32p)
+
+
+def host_tables(opc):
+    """Dense tables built on the host (no device needed): dict of numpy arrays."""
+    a, p = _as_u32(opc)
+    info = _lib.DfaInfo()
+    check(lib.ugpu_tables_build_host(p, len(a), ctypes.byref(info), None, 0, None, None, 0, None, None))
+    trans = np.zeros(info.states * info.row, np.uint16)
+    cls = np.zeros(256, np.uint8)
+    caps = np.zeros(info.states, np.uint32)
+    start = ctypes.c_uint32()
+    accb = ctypes.c_uint32()
+    check(lib.ugpu_tables_build_host(p, len(a), ctypes.byref(info), trans.ctypes.data_as(_lib.c_u16p), len(trans),
+                                     cls.ctypes.data_as(_lib.c_u8p), caps.ctypes.data_as(_lib.c_u32p), len(caps),
+                                     ctypes.byref(start), ctypes.byref(accb)))
+    return dict(info={f: getattr(info, f) for f, _ in _lib.DfaInfo._fields_}, trans=trans, cls=cls, caps=caps,
+                start=start.value, accb=accb.value)
+
+
+class Pattern:
+    """Compiled pattern (opcode words) with its device tables."""
+
+    def __init__(self, opc):
+        self.opc, p = _as_u32(opc)
+        h = ctypes.c_void_p()
+        check(lib.ugpu_dfa_create(p, len(self.opc), 0, ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self):
+        info = _lib.DfaInfo()
+        check(lib.ugpu_dfa_info_get(self._h, ctypes.byref(info)))
+        return {f: getattr(info, f) for f, _ in _lib.DfaInfo._fields_}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.ugpu_dfa_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _buffer_ptr(data):
+    """(pointer, length, keepalive) of bytes / numpy / torch (host or device) data."""
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        arr = np.frombuffer(bytes(data), dtype=np.uint8)
+        return arr.ctypes.data, arr.size, arr
+    if isinstance(data, np.ndarray):
+        arr = np.ascontiguousarray(data.view(np.uint8).reshape(-1))
+        return arr.ctypes.data, arr.size, arr
+    if hasattr(data, "data_ptr"):  # torch tensor, host or device
+        t = data.contiguous()
+        return t.data_ptr(), t.numel() * t.element_size(), t
+    raise TypeError("unsupported buffer type %r" % type(data))
+
+
+class FindResult:
+    def __init__(self, count, digest, dcap, start=None, length=None, cap=None):
+        self.count, self.digest, self.dcap = count, digest, dcap
+        self.start, self.length, self.cap = start, length, cap
+
+    def triples(self):
+        return [[int(s), int(l), int(c)] for s, l, c in zip(self.start, self.length, self.cap)]
+
+
+def find_all(pattern, data, start=0, offsets=True):
+    """ugpu_find_all: every FIND match of `data` from position `start`."""
+    ptr, n, keep = _buffer_ptr(data)
+    res = ctypes.POINTER(_lib.Result)()
+    check(lib.ugpu_find_all(pattern.handle, ctypes.c_void_p(ptr), n, start,
+                            _lib.MODE_OFFSETS if offsets else _lib.MODE_COUNT, ctypes.byref(res)))
+    try:
+        r = res.contents
+        if offsets and r.count:
+            st = np.ctypeslib.as_array(r.start, shape=(r.count,)).copy()
+            ln = np.ctypeslib.as_array(r.len, shape=(r.count,)).copy()
+            cp = np.ctypeslib.as_array(r.cap, shape=(r.count,)).copy()
+        else:
+            st = np.zeros(0, np.uint64)
+            ln = np.zeros(0, np.uint32)
+            cp = np.zeros(0, np.uint32)
+        out = FindResult(r.count, r.digest, r.dcap, st, ln, cp)
+    finally:
+        lib.ugpu_result_free(res)
+    del keep
+    return out
+
+
+class Matcher:
+    """FIND over a fully buffered input: m = Matcher(pat, data); while m.find(): m.first(), m.size()."""
+
+    def __init__(self, pattern, data=None):
+        self.pattern = pattern
+        self._data = None
+        if data is not None:
+            self.buffer(data)
+
+    def buffer(self, data):
+        """AbstractMatcher::buffer(base, size): whole input, cursor at 0 (absmatcher.h:542-591)."""
+        self._data = data
+        self._cur = 0
+        self._res = None
+        self._i = 0
+        self._first = 0
+        self._size = 0
+        self._cap = 0
+        return self
+
+    def find(self):
+        """Next match at or after the cursor; returns its accept index, 0 when exhausted."""
+        if self._res is None:
+            self._res = find_all(self.pattern, self._data, self._cur, offsets=True)
+            self._i = 0
+        r = self._res
+        # re-synchronise after skip(): drop records before the cursor (exact for
+        # patterns whose matches cannot contain '\n')
+        while self._i < r.count and int(r.start[self._i]) < self._cur:
+            self._i += 1
+        if self._i >= r.count:
+            self._cap = 0
+            self._size = 0
+            return 0
+        self._first = int(r.start[self._i])
+        self._size = int(r.length[self._i])
+        self._cap = int(r.cap[self._i])
+        self._cur = self._first + self._size
+        self._i += 1
+        return self._cap
+
+    def first(self):
+        return self._first
+
+    def size(self):
+        return self._size
+
+    def last(self):
+        return self._first + self._size
+
+    def accept(self):
+        return self._cap
+
+    def skip_to(self, pos):
+        """Advance the cursor (the effect of skip('\\n') on cur_ between finds)."""
+        self._cur = max(self._cur, pos)
+
+    def __iter__(self):
+        while self.find():
+            yield self._first, self._size, self._cap
+
+
+class Scanner:
+    """Device-resident scans (ugpu_scanner): one per stream/thread."""
+
+    def __init__(self, pattern):
+        self.pattern = pattern
+        h = ctypes.c_void_p()
+        check(lib.ugpu_scanner_create(pattern.handle, ctypes.byref(h)))
+        self._h = h
+
+    def scan(self, dptr, lo, hi, read_end=None, at_eof=True, bias=0, stream=0):
+        if read_end is None:
+            read_end = hi
+        check(lib.ugpu_scan(self._h, ctypes.c_void_p(dptr), lo, hi, read_end, 1 if at_eof else 0, bias,
+                            ctypes.c_void_p(stream)))
+
+    def totals(self):
+        t = _lib.Totals()
+        check(lib.ugpu_scan_totals(self._h, ctypes.byref(t)))
+        return t
+
+    def kernel_ms(self):
+        ms = ctypes.c_float()
+        check(lib.ugpu_scan_kernel_ms(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    def offsets(self, d_start, d_len, d_cap, capacity, stream=0):
+        check(lib.ugpu_scan_offsets(self._h, ctypes.c_void_p(d_start), ctypes.c_void_p(d_len),
+                                    ctypes.c_void_p(d_cap), capacity, ctypes.c_void_p(stream)))
+
+    def chain_fix(self, dptr, lo, hi, read_end, at_eof, bias, old_entry, new_entry, stream=0):
+        t = _lib.Totals()
+        check(lib.ugpu_chain_fix(self._h, ctypes.c_void_p(dptr), lo, hi, read_end, 1 if at_eof else 0, bias,
+                                 old_entry, new_entry, ctypes.byref(t), ctypes.c_void_p(stream)))
+        return t
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.ugpu_scanner_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gen(kind, seed, off, dptr, length, stream=0):
+    """Generate corpus bytes [off, off+length) on the device (ugpu_gen)."""
+    check(lib.ugpu_gen(kind, seed, off, ctypes.c_void_p(dptr), length, ctypes.c_void_p(stream)))
