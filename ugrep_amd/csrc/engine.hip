@@ -82,7 +82,13 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.start = d->t.start;
   P.accb = d->t.accb;
   P.log_row = d->t.log_row;
-  P.needles = d->t.needles[0] | (d->t.needles[1] << 8) | (d->t.needles[2] << 16) | ((uint32_t)d->t.needles[3] << 24);
+  P.nA = d->t.nA;
+  P.nB = d->t.nB;
+  P.nC = d->t.nC;
+  for (int i = 0; i < 12; ++i) {
+    P.tm[i] = d->t.tm[i] * 0x01010101u;
+    P.tv[i] = d->t.tv[i] * 0x01010101u;
+  }
 }
 
 // Translate a byte range of dbuf into the 16-byte aligned base coordinates
@@ -180,7 +186,7 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->row = d->t.row;
   info->format = d->t.format;
   info->table_bytes = (uint32_t)(d->t.trans.size() * 2 + (d->t.format == FMT_CLASS ? 256 : 0));
-  info->needles = d->t.nneedle;
+  info->needles = d->t.filter ? d->t.nA + d->t.nB : 0;
   info->first_bytes = d->t.first_bytes;
   info->accepting = d->t.accepting;
   return UGPU_OK;
@@ -200,7 +206,7 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   info->row = t.row;
   info->format = t.format;
   info->table_bytes = (uint32_t)(t.trans.size() * 2 + (t.format == FMT_CLASS ? 256 : 0));
-  info->needles = t.nneedle;
+  info->needles = t.filter ? t.nA + t.nB : 0;
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
   if (start) *start = t.start;
@@ -231,7 +237,7 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
     return fail(UGPU_UNSUPPORTED, "tables do not fit in LDS");
   }
   int per_cu = 0;
-  HIP_TRY(scan_occupancy(dfa->t.format, dfa->t.nneedle, s->smem, &per_cu));
+  HIP_TRY(scan_occupancy(dfa->t.format, dfa->t.filter, s->smem, &per_cu));
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, s->device));
   if (per_cu < 1) per_cu = 1;
@@ -289,7 +295,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   P.out_base_out = s->d_obase;
   HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
   HIP_TRY(hipEventRecord(s->ev0, st));
-  HIP_TRY(launch_scan(P, s->dfa->t.format, s->dfa->t.nneedle, false, s->smem, st));
+  HIP_TRY(launch_scan(P, s->dfa->t.format, s->dfa->t.filter, false, s->smem, st));
   HIP_TRY(hipEventRecord(s->ev1, st));
   HIP_TRY(launch_fix(P, s->dfa->t.format, st));
   HIP_TRY(hipMemcpyAsync(s->h_tot, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
@@ -338,7 +344,7 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
   P.out_cap = d_cap;
   P.out_capacity = capacity;
   HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
-  HIP_TRY(launch_scan(P, s->dfa->t.format, s->dfa->t.nneedle, true, s->smem, st));
+  HIP_TRY(launch_scan(P, s->dfa->t.format, s->dfa->t.filter, true, s->smem, st));
   HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (*s->h_flags & UGPU_FLAG_CAPACITY) return fail(UGPU_CAPACITY, "output capacity exceeded");

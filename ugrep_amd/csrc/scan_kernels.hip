@@ -4,8 +4,8 @@
 // Reference hot loops replaced here:
 //   * needle prefilter simd_advance_pattern_pinN_*_avx2 (lib/matcher_avx2.cpp:
 //     303-799) / simd_advance_string_* (lib/matcher_avx512bw.cpp:281-463):
-//     per-lane SWAR compare of the segment's 64 staged bytes against the DFA's
-//     first bytes -> 64-bit candidate mask (needle_mask);
+//     per-lane SWAR test of the segment's 64 staged bytes against the DFA's
+//     first/second-byte terms -> 64-bit candidate mask (filter_mask);
 //   * DFA opcode interpreter (lib/matcher.cpp:125-546): one dependent LDS
 //     lookup per byte in the flattened table (walk);
 //   * FIND restart/accept logic (lib/matcher.cpp:621-746): chain_step.
@@ -117,16 +117,16 @@ struct WriteEm {
   }
 };
 
-// One step of the FIND chain from p (< e).  With needles (NN > 0), positions
+// One step of the FIND chain from p (< e).  With the prefilter (FILT), positions
 // whose byte cannot start a match are skipped via the candidate mask of the
 // lane's 64-byte segment [sa, sa+64): their step is p+1 with no match.
-template <int FMT, int NN, class Em>
+template <int FMT, bool FILT, class Em>
 __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t p,
                                                uint64_t sa, uint64_t e, uint64_t mask, Em& em, int sign,
                                                uint32_t& ovf)
 {
   uint64_t c0 = p;
-  if constexpr (NN > 0) {
+  if constexpr (FILT) {
     uint64_t off = p - sa;
     uint64_t m = off < 64 ? (mask & (~0ull << off)) : 0ull;
     if (m == 0) return e;
@@ -141,18 +141,18 @@ __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, 
   return c0 + 1;
 }
 
-template <int FMT, int NN, class Em>
+template <int FMT, bool FILT, class Em>
 __device__ __forceinline__ uint64_t run_seg(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t x, uint64_t sa,
                                             uint64_t e, uint64_t mask, Em& em, uint32_t& ovf)
 {
   uint64_t p = x;
-  while (p < e) p = chain_step<FMT, NN>(T, w, c, p, sa, e, mask, em, +1, ovf);
+  while (p < e) p = chain_step<FMT, FILT>(T, w, c, p, sa, e, mask, em, +1, ovf);
   return p;
 }
 
 // Re-enter [.., e) at xn instead of xo.  Adds (true - speculative) matches to em.
 // Returns true if the chains met (exit unchanged), else sets nexit.
-template <int FMT, int NN>
+template <int FMT, bool FILT>
 __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t xo, uint64_t xn,
                                       uint64_t sa, uint64_t e, uint64_t mask, CountEm& em, uint64_t& nexit,
                                       uint32_t& ovf)
@@ -165,39 +165,63 @@ __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx
       return false;
     }
     if (po < pn)
-      po = chain_step<FMT, NN>(T, w, c, po, sa, e, mask, em, -1, ovf);
+      po = chain_step<FMT, FILT>(T, w, c, po, sa, e, mask, em, -1, ovf);
     else
-      pn = chain_step<FMT, NN>(T, w, c, pn, sa, e, mask, em, +1, ovf);
+      pn = chain_step<FMT, FILT>(T, w, c, pn, sa, e, mask, em, +1, ovf);
   }
 }
 
-// SWAR candidate mask: bit i set iff byte i of the 64-byte LDS segment equals
-// one of the NN first bytes (exact per-byte zero test, no borrow leakage).
-template <int NN>
-__device__ __forceinline__ uint64_t needle_mask(const uint8_t* seg, uint32_t needles)
+// SWAR candidate mask of a 64-byte LDS segment: bit i set iff byte i may start
+// a match, i.e. B[i] in A, or B[i] in B and B[i+1] in C (tables.hpp).  A set
+// test is an OR over (mask, value) terms, each an exact per-byte zero test
+// ((t & 0x7f..) + 0x7f..) | t  (bit 7 = byte nonzero, no borrow leakage).
+// `nxt` holds the 4 bytes after the segment (the pair test reads byte 64).
+struct Filter {
+  uint32_t nA, nB, nC;
+  uint32_t tm[12], tv[12];
+};
+
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t t) { return ((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t; }
+
+// bit 7 of each byte set iff the byte matches NO term of the set [o, o+n)
+__device__ __forceinline__ uint32_t no_match(const Filter& F, int o, uint32_t n, uint32_t x)
+{
+  uint32_t r = 0xffffffffu;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if ((uint32_t)i < n) r &= nz_bytes((x & F.tm[o + i]) ^ F.tv[o + i]);
+  return r;
+}
+
+__device__ __forceinline__ uint64_t filter_mask(const uint8_t* seg, uint32_t nxt, const Filter& F)
 {
   const uint4* v = reinterpret_cast<const uint4*>(seg);
-  uint32_t lo = 0, hi = 0;
+  uint32_t wd[17];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     uint4 x = v[i];
-    uint32_t wd[4] = {x.x, x.y, x.z, x.w};
+    wd[4 * i] = x.x;
+    wd[4 * i + 1] = x.y;
+    wd[4 * i + 2] = x.z;
+    wd[4 * i + 3] = x.w;
+  }
+  wd[16] = nxt;
+  uint32_t lo = 0, hi = 0;
+  uint32_t noC_next = F.nC ? no_match(F, 8, F.nC, wd[0]) : 0u;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint32_t z = 0;
-#pragma unroll
-      for (int n = 0; n < NN; ++n) {
-        uint32_t t = wd[j] ^ (((needles >> (8 * n)) & 0xffu) * 0x01010101u);
-        z |= ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t);
-      }
-      z &= 0x80808080u;
-      uint32_t nib = (((z >> 7) * 0x00204081u) >> 21) & 0xfu;
-      const int sh = 16 * i + 4 * j;
-      if (sh < 32)
-        lo |= nib << sh;
-      else
-        hi |= nib << (sh - 32);
-    }
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t noC = noC_next;
+    noC_next = F.nC ? no_match(F, 8, F.nC, wd[j + 1]) : 0u;
+    // byte i of the shifted word = C-test of byte i+1
+    const uint32_t noCs = __builtin_amdgcn_alignbyte(noC_next, noC, 1);
+    const uint32_t noA = no_match(F, 0, F.nA, wd[j]);
+    const uint32_t noB = no_match(F, 4, F.nB, wd[j]);
+    const uint32_t cand = ~(noA & (noB | noCs)) & 0x80808080u;
+    const uint32_t nib = (((cand >> 7) * 0x00204081u) >> 21) & 0xfu;
+    if (j < 8)
+      lo |= nib << (4 * j);
+    else
+      hi |= nib << (4 * (j - 8));
   }
   return ((uint64_t)hi << 32) | lo;
 }
@@ -226,7 +250,7 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v)
 }
 
 // ---------------------------------------------------------------- scan kernel
-template <int FMT, int NN, bool WRITE>
+template <int FMT, bool FILT, bool WRITE>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -249,6 +273,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
   }
   const Tab<FMT> T{ltrans, lcls, P.start, P.accb};
   const Ctx C{P.caps, P.log_row, P.delta};
+  Filter F;
+  if constexpr (FILT) {
+    F.nA = P.nA;
+    F.nB = P.nB;
+    F.nC = P.nC;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      F.tm[i] = P.tm[i];
+      F.tv[i] = P.tv[i];
+    }
+  }
 
   const uint64_t b = blockIdx.x;
   uint64_t tb = P.t0 + b * P.tpb;
@@ -295,27 +330,36 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
     const uint64_t s = clampu(sa, blo, bhi);
     const uint64_t e = clampu(sa + kSeg, blo, bhi);
     uint64_t mask = 0;
-    if constexpr (NN > 0) {
-      mask = needle_mask<NN>(tile + tid * kSeg, P.needles);
+    if constexpr (FILT) {
+      const uint32_t nxt = *reinterpret_cast<const uint32_t*>(tile + tid * kSeg + kSeg);
+      mask = filter_mask(tile + tid * kSeg, nxt, F);
       mask &= lowbits(e - sa) & ~lowbits(s - sa);
     }
     uint64_t x = (tid == 0) ? x0 : s;
     CountEm la;
-    ex[tid] = run_seg<FMT, NN>(T, w, C, x, sa, e, mask, la, ovf);
-    // resolve the true chain entry of every lane (rounds propagate left->right)
-    for (;;) {
-      __syncthreads();
-      const uint64_t nx = (tid == 0) ? x0 : ex[tid - 1];
-      const bool ch = nx != x;
-      __syncthreads();
-      if (ch) {
-        uint64_t ne;
-        if (!merge<FMT, NN>(T, w, C, x, nx, sa, e, mask, la, ne, ovf)) ex[tid] = ne;
-        x = nx;
+    const uint64_t xe = run_seg<FMT, FILT>(T, w, C, x, sa, e, mask, la, ovf);
+    // The true chain enters lane k at lane k-1's exit.  It differs from the
+    // speculative entry s_k only where some lane's chain left its segment past
+    // the segment end (a match crossing the boundary).
+    if (__syncthreads_or(xe > e)) {
+      ex[tid] = xe;
+      // resolve the true chain entry of every lane (rounds propagate left->right)
+      for (;;) {
+        __syncthreads();
+        const uint64_t nx = (tid == 0) ? x0 : ex[tid - 1];
+        const bool ch = nx != x;
+        __syncthreads();
+        if (ch) {
+          uint64_t ne;
+          if (!merge<FMT, FILT>(T, w, C, x, nx, sa, e, mask, la, ne, ovf)) ex[tid] = ne;
+          x = nx;
+        }
+        if (!__syncthreads_or(ch)) break;
       }
-      if (!__syncthreads_or(ch)) break;
+      x0 = ex[kBlock - 1];
+    } else {
+      x0 = clampu(ts + kTile, blo, bhi);  // == exit of the last lane
     }
-    x0 = ex[kBlock - 1];
     if constexpr (WRITE) {
       // exclusive prefix of the lanes' match counts, then re-walk and store
       uint64_t v = la.cnt, incl = v;
@@ -333,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
         all += red[k];
       }
       WriteEm we{wbase + off + incl - v, P.out_capacity, P.out_start, P.out_len, P.out_cap};
-      run_seg<FMT, NN>(T, w, C, x, sa, e, mask, we, ovf);
+      run_seg<FMT, FILT>(T, w, C, x, sa, e, mask, we, ovf);
       wover |= we.overflow;
       wbase += all;
       __syncthreads();  // red reused next tile
@@ -525,38 +569,29 @@ __global__ void chain_fix_kernel(ScanParams P, uint64_t old_entry, uint64_t new_
 }
 
 // ---------------------------------------------------------------- launchers
-template <int FMT, int NN, bool WRITE>
+template <int FMT, bool FILT, bool WRITE>
 static hipError_t launch_one(const ScanParams& P, size_t smem, hipStream_t stream)
 {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_kernel<FMT, NN, WRITE>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static size_t attr_smem = 65536;
+  if (smem > attr_smem) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_kernel<FMT, FILT, WRITE>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_smem = smem;
   }
-  hipLaunchKernelGGL((scan_kernel<FMT, NN, WRITE>), dim3(P.grid), dim3(kBlock), smem, stream, P);
+  hipLaunchKernelGGL((scan_kernel<FMT, FILT, WRITE>), dim3(P.grid), dim3(kBlock), smem, stream, P);
   return hipGetLastError();
 }
 
-template <int FMT, bool WRITE>
-static hipError_t launch_nn(const ScanParams& P, uint32_t nn, size_t smem, hipStream_t stream)
-{
-  switch (nn) {
-    case 1: return launch_one<FMT, 1, WRITE>(P, smem, stream);
-    case 2: return launch_one<FMT, 2, WRITE>(P, smem, stream);
-    case 3: return launch_one<FMT, 3, WRITE>(P, smem, stream);
-    case 4: return launch_one<FMT, 4, WRITE>(P, smem, stream);
-    default: return launch_one<FMT, 0, WRITE>(P, smem, stream);
-  }
-}
-
-hipError_t launch_scan(const ScanParams& P, uint32_t format, uint32_t nneedle, bool write, size_t smem,
+hipError_t launch_scan(const ScanParams& P, uint32_t format, bool filter, bool write, size_t smem,
                        hipStream_t stream)
 {
-  if (format == 0)
-    return write ? launch_nn<0, true>(P, nneedle, smem, stream) : launch_nn<0, false>(P, nneedle, smem, stream);
-  return write ? launch_nn<1, true>(P, nneedle, smem, stream) : launch_nn<1, false>(P, nneedle, smem, stream);
+  if (format == 0) {
+    if (filter) return write ? launch_one<0, true, true>(P, smem, stream) : launch_one<0, true, false>(P, smem, stream);
+    return write ? launch_one<0, false, true>(P, smem, stream) : launch_one<0, false, false>(P, smem, stream);
+  }
+  if (filter) return write ? launch_one<1, true, true>(P, smem, stream) : launch_one<1, true, false>(P, smem, stream);
+  return write ? launch_one<1, false, true>(P, smem, stream) : launch_one<1, false, false>(P, smem, stream);
 }
 
 hipError_t launch_fix(const ScanParams& P, uint32_t format, hipStream_t stream)
@@ -578,31 +613,16 @@ hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_e
   return hipGetLastError();
 }
 
-template <int FMT, int NN>
+template <int FMT, bool FILT>
 static hipError_t occ_one(size_t smem, int* n)
 {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, scan_kernel<FMT, NN, false>, kBlock, smem);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, scan_kernel<FMT, FILT, false>, kBlock, smem);
 }
 
-hipError_t scan_occupancy(uint32_t format, uint32_t nneedle, size_t smem, int* n)
+hipError_t scan_occupancy(uint32_t format, bool filter, size_t smem, int* n)
 {
-  const uint32_t nn = nneedle > 4 ? 0 : nneedle;
-  if (format == 0) {
-    switch (nn) {
-      case 1: return occ_one<0, 1>(smem, n);
-      case 2: return occ_one<0, 2>(smem, n);
-      case 3: return occ_one<0, 3>(smem, n);
-      case 4: return occ_one<0, 4>(smem, n);
-      default: return occ_one<0, 0>(smem, n);
-    }
-  }
-  switch (nn) {
-    case 1: return occ_one<1, 1>(smem, n);
-    case 2: return occ_one<1, 2>(smem, n);
-    case 3: return occ_one<1, 3>(smem, n);
-    case 4: return occ_one<1, 4>(smem, n);
-    default: return occ_one<1, 0>(smem, n);
-  }
+  if (format == 0) return filter ? occ_one<0, true>(smem, n) : occ_one<0, false>(smem, n);
+  return filter ? occ_one<1, true>(smem, n) : occ_one<1, false>(smem, n);
 }
 
 size_t scan_smem_bytes(uint32_t ntrans_pad, uint32_t format)

@@ -54,7 +54,8 @@ struct ScanParams {
   const uint32_t* caps;
   uint32_t ntrans_pad;   // u16 entries, multiple of 8
   uint32_t start, accb, log_row;
-  uint32_t needles;      // packed first bytes (nneedle <= 4)
+  uint32_t nA, nB, nC;   // prefilter term counts (tables.hpp)
+  uint32_t tm[12], tv[12];  // term masks / values replicated to 4 bytes
   uint32_t grid;
   BlockRec* recs;
   const uint64_t* entries;   // OFFSETS pass: exact block entries
@@ -70,12 +71,12 @@ struct ScanParams {
 };
 
 // launchers (scan_kernels.hip)
-hipError_t launch_scan(const ScanParams& P, uint32_t format, uint32_t nneedle, bool write, size_t smem,
+hipError_t launch_scan(const ScanParams& P, uint32_t format, bool filter, bool write, size_t smem,
                        hipStream_t stream);
 hipError_t launch_fix(const ScanParams& P, uint32_t format, hipStream_t stream);
 hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_entry, uint64_t new_entry,
                             hipStream_t stream);
-hipError_t scan_occupancy(uint32_t format, uint32_t nneedle, size_t smem, int* blocks_per_cu);
+hipError_t scan_occupancy(uint32_t format, bool filter, size_t smem, int* blocks_per_cu);
 hipError_t launch_gen(int kind, uint64_t seed, uint64_t off, uint8_t* dbuf, uint64_t len, hipStream_t stream);
 size_t scan_smem_bytes(uint32_t ntrans_pad, uint32_t format);
 

@@ -32,6 +32,58 @@ struct RawState {
   int64_t target_pc[256];
 };
 
+struct Term {
+  uint8_t m, v;  // byte b matches iff (b & m) == v
+  bool operator<(const Term& o) const { return m != o.m ? m < o.m : v < o.v; }
+  bool operator==(const Term& o) const { return m == o.m && v == o.v; }
+};
+
+// Exact cover of a byte set by (mask, value) terms: prime implicants by
+// pairwise merging (Quine-McCluskey over 8 bits), then a greedy set cover.
+std::vector<Term> cover_terms(const bool in[256])
+{
+  std::vector<Term> cur, primes;
+  for (int b = 0; b < 256; ++b)
+    if (in[b]) cur.push_back(Term{0xff, (uint8_t)b});
+  while (!cur.empty()) {
+    std::vector<Term> next;
+    std::vector<bool> used(cur.size(), false);
+    for (size_t i = 0; i < cur.size(); ++i)
+      for (size_t j = i + 1; j < cur.size(); ++j) {
+        if (cur[i].m != cur[j].m) continue;
+        uint8_t d = cur[i].v ^ cur[j].v;
+        if (d && (d & (d - 1)) == 0) {
+          next.push_back(Term{(uint8_t)(cur[i].m & ~d), (uint8_t)(cur[i].v & ~d)});
+          used[i] = used[j] = true;
+        }
+      }
+    for (size_t i = 0; i < cur.size(); ++i)
+      if (!used[i]) primes.push_back(cur[i]);
+    std::sort(next.begin(), next.end());
+    next.erase(std::unique(next.begin(), next.end()), next.end());
+    cur.swap(next);
+  }
+  std::vector<Term> chosen;
+  bool covered[256] = {};
+  for (;;) {
+    int best = -1, best_n = 0;
+    for (size_t i = 0; i < primes.size(); ++i) {
+      int n = 0;
+      for (int b = 0; b < 256; ++b)
+        if (in[b] && !covered[b] && (b & primes[i].m) == primes[i].v) ++n;
+      if (n > best_n) {
+        best_n = n;
+        best = (int)i;
+      }
+    }
+    if (best < 0) break;
+    chosen.push_back(primes[best]);
+    for (int b = 0; b < 256; ++b)
+      if ((b & primes[best].m) == primes[best].v) covered[b] = true;
+  }
+  return chosen;
+}
+
 }  // namespace
 
 int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string& err)
@@ -185,14 +237,34 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   t.start = start_sid * R;
   t.accepting = S - first_acc;
   t.accb = (t.accepting > 0) ? first_acc * R : 0x10000u;
-  uint32_t nf = 0;
-  for (int c = 0; c < 256; ++c)
-    if (nxt[(size_t)start_sid * 256 + c] != 0) {
-      if (nf < 4) t.needles[nf] = (uint8_t)c;
-      ++nf;
+  // prefilter sets (see tables.hpp): A = first bytes that complete a match,
+  // B = other first bytes, C = bytes that can follow a byte of B
+  bool setA[256] = {}, setB[256] = {}, setC[256] = {};
+  uint32_t nf = 0, nAB = 0;
+  for (int c = 0; c < 256; ++c) {
+    const uint32_t s1 = nxt[(size_t)start_sid * 256 + c];
+    if (s1 == 0) continue;
+    ++nf;
+    if (s1 >= first_acc) {
+      setA[c] = true;
+    } else {
+      setB[c] = true;
+      for (int d = 0; d < 256; ++d)
+        if (nxt[(size_t)s1 * 256 + d] != 0) setC[d] = true;
     }
+  }
   t.first_bytes = nf;
-  t.nneedle = (nf >= 1 && nf <= 4) ? nf : 0;
+  std::vector<Term> ta = cover_terms(setA), tb = cover_terms(setB), tc = cover_terms(setC);
+  nAB = (uint32_t)(ta.size() + tb.size());
+  if (nf > 0 && ta.size() <= 4 && tb.size() <= 4 && nAB <= 4 && nf <= 32) {
+    t.filter = true;
+    t.nA = (uint32_t)ta.size();
+    t.nB = (uint32_t)tb.size();
+    t.nC = tc.size() <= 4 ? (uint32_t)tc.size() : 0;  // too wide: no second-byte test
+    for (uint32_t i = 0; i < t.nA; ++i) t.tm[i] = ta[i].m, t.tv[i] = ta[i].v;
+    for (uint32_t i = 0; i < t.nB; ++i) t.tm[4 + i] = tb[i].m, t.tv[4 + i] = tb[i].v;
+    for (uint32_t i = 0; i < t.nC; ++i) t.tm[8 + i] = tc[i].m, t.tv[8 + i] = tc[i].v;
+  }
   out = std::move(t);
   return 0;
 }

@@ -30,8 +30,14 @@ struct DfaTables {
   uint32_t start = 0;    // start entry = start_sid * R
   uint32_t accb = 0;     // first accepting entry (A * R)
   uint32_t accepting = 0;
-  uint32_t nneedle = 0;  // first-byte count if <= 4, else 0
-  uint8_t needles[4] = {0, 0, 0, 0};
+  // Candidate prefilter (replaces the reference's needle/pin prefilters,
+  // lib/matcher_avx2.cpp:303-799): a position p can start a match only if
+  //   B[p] in A  (1-byte match possible)  or  B[p] in B and B[p+1] in C.
+  // Each set is an exact cover by (mask, value) terms: b matches a term iff
+  // (b & mask) == value.  filter == false: no prefilter (dense patterns).
+  bool filter = false;
+  uint32_t nA = 0, nB = 0, nC = 0;  // nC == 0: no second-byte test
+  uint8_t tm[12] = {}, tv[12] = {};  // terms: A at [0,nA), B at [4,4+nB), C at [8,8+nC)
   uint32_t first_bytes = 0;
   std::vector<uint16_t> trans;  // states * row
   std::vector<uint8_t> cls;     // 256
