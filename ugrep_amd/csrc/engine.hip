@@ -288,6 +288,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   geometry(P, dbuf, lo, hi, read_end, s->max_grid, s->off);
   P.delta = (int64_t)bias - (int64_t)s->off;
   P.at_eof = at_eof ? 1u : 0u;
+  if (const char* ab = std::getenv("UGPU_ABLATE")) P.ablate = (uint32_t)std::atoi(ab);
   P.recs = s->d_recs;
   P.flags = s->d_flags;
   P.totals = s->d_tot;

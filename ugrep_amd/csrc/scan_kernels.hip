@@ -176,25 +176,29 @@ __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx
 // test is an OR over (mask, value) terms, each an exact per-byte zero test
 // ((t & 0x7f..) + 0x7f..) | t  (bit 7 = byte nonzero, no borrow leakage).
 // `nxt` holds the 4 bytes after the segment (the pair test reads byte 64).
+// The term counts are compile-time (filter code FC, see fcode()).
+constexpr int fcode(int na, int nb, int nc) { return 1 + na * 9 + nb * 3 + nc; }
+
 struct Filter {
-  uint32_t nA, nB, nC;
   uint32_t tm[12], tv[12];
 };
 
 __device__ __forceinline__ uint32_t nz_bytes(uint32_t t) { return ((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t; }
 
-// bit 7 of each byte set iff the byte matches NO term of the set [o, o+n)
-__device__ __forceinline__ uint32_t no_match(const Filter& F, int o, uint32_t n, uint32_t x)
+// bit 7 of each byte set iff the byte matches NO term of the set [o, o+N)
+template <int N>
+__device__ __forceinline__ uint32_t no_match(const Filter& F, int o, uint32_t x)
 {
   uint32_t r = 0xffffffffu;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if ((uint32_t)i < n) r &= nz_bytes((x & F.tm[o + i]) ^ F.tv[o + i]);
+  for (int i = 0; i < N; ++i) r &= nz_bytes((x & F.tm[o + i]) ^ F.tv[o + i]);
   return r;
 }
 
+template <int FC>
 __device__ __forceinline__ uint64_t filter_mask(const uint8_t* seg, uint32_t nxt, const Filter& F)
 {
+  constexpr int NA = (FC - 1) / 9, NB = ((FC - 1) / 3) % 3, NC = (FC - 1) % 3;
   const uint4* v = reinterpret_cast<const uint4*>(seg);
   uint32_t wd[17];
 #pragma unroll
@@ -207,16 +211,18 @@ __device__ __forceinline__ uint64_t filter_mask(const uint8_t* seg, uint32_t nxt
   }
   wd[16] = nxt;
   uint32_t lo = 0, hi = 0;
-  uint32_t noC_next = F.nC ? no_match(F, 8, F.nC, wd[0]) : 0u;
+  uint32_t noC_next = NC ? no_match<NC>(F, 8, wd[0]) : 0u;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const uint32_t noC = noC_next;
-    noC_next = F.nC ? no_match(F, 8, F.nC, wd[j + 1]) : 0u;
-    // byte i of the shifted word = C-test of byte i+1
-    const uint32_t noCs = __builtin_amdgcn_alignbyte(noC_next, noC, 1);
-    const uint32_t noA = no_match(F, 0, F.nA, wd[j]);
-    const uint32_t noB = no_match(F, 4, F.nB, wd[j]);
-    const uint32_t cand = ~(noA & (noB | noCs)) & 0x80808080u;
+    uint32_t noBC = 0xffffffffu;
+    if constexpr (NB > 0) {
+      const uint32_t noC = noC_next;
+      noC_next = NC ? no_match<NC>(F, 8, wd[j + 1]) : 0u;
+      // byte i of the shifted word = C-test of byte i+1
+      const uint32_t noCs = __builtin_amdgcn_alignbyte(noC_next, noC, 1);
+      noBC = no_match<NB>(F, 4, wd[j]) | noCs;
+    }
+    const uint32_t cand = ~(no_match<NA>(F, 0, wd[j]) & noBC) & 0x80808080u;
     const uint32_t nib = (((cand >> 7) * 0x00204081u) >> 21) & 0xfu;
     if (j < 8)
       lo |= nib << (4 * j);
@@ -250,9 +256,10 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v)
 }
 
 // ---------------------------------------------------------------- scan kernel
-template <int FMT, bool FILT, bool WRITE>
+template <int FMT, int FC, bool WRITE>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
 {
+  constexpr bool FILT = FC != 0;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tile = smem;
   uint64_t* ex = reinterpret_cast<uint64_t*>(smem + kTile + kHalo);
@@ -275,9 +282,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
   const Ctx C{P.caps, P.log_row, P.delta};
   Filter F;
   if constexpr (FILT) {
-    F.nA = P.nA;
-    F.nB = P.nB;
-    F.nC = P.nC;
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
       F.tm[i] = P.tm[i];
@@ -330,10 +334,20 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
     const uint64_t s = clampu(sa, blo, bhi);
     const uint64_t e = clampu(sa + kSeg, blo, bhi);
     uint64_t mask = 0;
+    if (P.ablate == 1) {  // keep x0 consistent so fix_kernel has nothing to stitch
+      tot.cnt += tile[tid];
+      x0 = clampu(ts + kTile, blo, bhi);
+      continue;
+    }
     if constexpr (FILT) {
       const uint32_t nxt = *reinterpret_cast<const uint32_t*>(tile + tid * kSeg + kSeg);
-      mask = filter_mask(tile + tid * kSeg, nxt, F);
+      mask = filter_mask<FC>(tile + tid * kSeg, nxt, F);
       mask &= lowbits(e - sa) & ~lowbits(s - sa);
+    }
+    if (P.ablate == 2) {
+      tot.cnt += __popcll(mask);
+      x0 = clampu(ts + kTile, blo, bhi);
+      continue;
     }
     uint64_t x = (tid == 0) ? x0 : s;
     CountEm la;
@@ -569,29 +583,43 @@ __global__ void chain_fix_kernel(ScanParams P, uint64_t old_entry, uint64_t new_
 }
 
 // ---------------------------------------------------------------- launchers
-template <int FMT, bool FILT, bool WRITE>
+template <int FMT, int FC, bool WRITE>
 static hipError_t launch_one(const ScanParams& P, size_t smem, hipStream_t stream)
 {
   static size_t attr_smem = 65536;
   if (smem > attr_smem) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_kernel<FMT, FILT, WRITE>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_kernel<FMT, FC, WRITE>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_smem = smem;
   }
-  hipLaunchKernelGGL((scan_kernel<FMT, FILT, WRITE>), dim3(P.grid), dim3(kBlock), smem, stream, P);
+  hipLaunchKernelGGL((scan_kernel<FMT, FC, WRITE>), dim3(P.grid), dim3(kBlock), smem, stream, P);
   return hipGetLastError();
+}
+
+// filter codes with instantiated kernels: NA + NB in {1, 2}, NC in {0, 1, 2} (tables.cpp)
+#define UGPU_FOR_FCODES(X) \
+  X(fcode(1, 0, 0)) X(fcode(2, 0, 0)) X(fcode(0, 1, 0)) X(fcode(0, 1, 1)) X(fcode(0, 1, 2)) X(fcode(1, 1, 0)) \
+  X(fcode(1, 1, 1)) X(fcode(1, 1, 2)) X(fcode(0, 2, 0)) X(fcode(0, 2, 1)) X(fcode(0, 2, 2))
+
+template <bool WRITE>
+static hipError_t launch_byte(const ScanParams& P, int fc, size_t smem, hipStream_t stream)
+{
+  switch (fc) {
+#define X(c) \
+  case c: return launch_one<0, c, WRITE>(P, smem, stream);
+    UGPU_FOR_FCODES(X)
+#undef X
+    default: return launch_one<0, 0, WRITE>(P, smem, stream);
+  }
 }
 
 hipError_t launch_scan(const ScanParams& P, uint32_t format, bool filter, bool write, size_t smem,
                        hipStream_t stream)
 {
-  if (format == 0) {
-    if (filter) return write ? launch_one<0, true, true>(P, smem, stream) : launch_one<0, true, false>(P, smem, stream);
-    return write ? launch_one<0, false, true>(P, smem, stream) : launch_one<0, false, false>(P, smem, stream);
-  }
-  if (filter) return write ? launch_one<1, true, true>(P, smem, stream) : launch_one<1, true, false>(P, smem, stream);
-  return write ? launch_one<1, false, true>(P, smem, stream) : launch_one<1, false, false>(P, smem, stream);
+  const int fc = filter ? fcode((int)P.nA, (int)P.nB, (int)P.nC) : 0;
+  if (format == 0) return write ? launch_byte<true>(P, fc, smem, stream) : launch_byte<false>(P, fc, smem, stream);
+  return write ? launch_one<1, 0, true>(P, smem, stream) : launch_one<1, 0, false>(P, smem, stream);
 }
 
 hipError_t launch_fix(const ScanParams& P, uint32_t format, hipStream_t stream)
@@ -613,16 +641,17 @@ hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_e
   return hipGetLastError();
 }
 
-template <int FMT, bool FILT>
+template <int FMT, int FC>
 static hipError_t occ_one(size_t smem, int* n)
 {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, scan_kernel<FMT, FILT, false>, kBlock, smem);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, scan_kernel<FMT, FC, false>, kBlock, smem);
 }
 
 hipError_t scan_occupancy(uint32_t format, bool filter, size_t smem, int* n)
 {
-  if (format == 0) return filter ? occ_one<0, true>(smem, n) : occ_one<0, false>(smem, n);
-  return filter ? occ_one<1, true>(smem, n) : occ_one<1, false>(smem, n);
+  // all filter variants share the same resource shape; the common C2 one answers
+  if (format == 0) return filter ? occ_one<0, fcode(0, 1, 2)>(smem, n) : occ_one<0, 0>(smem, n);
+  return occ_one<1, 0>(smem, n);
 }
 
 size_t scan_smem_bytes(uint32_t ntrans_pad, uint32_t format)

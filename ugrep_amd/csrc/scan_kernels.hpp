@@ -47,7 +47,7 @@ struct ScanParams {
   uint64_t rend;      // walks may read bytes < rend
   int64_t delta;      // reported start = position + delta
   uint32_t at_eof;    // rend is the end of the stream
-  uint32_t pad;
+  uint32_t ablate;    // benchmarking only (UGPU_ABLATE): 1 = stage tiles only, 2 = + prefilter
   uint64_t t0, t1, tpb;  // tiles [t0, t1), tiles per block
   const uint16_t* trans;
   const uint8_t* cls;

@@ -256,11 +256,13 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   t.first_bytes = nf;
   std::vector<Term> ta = cover_terms(setA), tb = cover_terms(setB), tc = cover_terms(setC);
   nAB = (uint32_t)(ta.size() + tb.size());
-  if (nf > 0 && ta.size() <= 4 && tb.size() <= 4 && nAB <= 4 && nf <= 32) {
+  // kernels are instantiated for nA + nB in {1, 2} and nC in {0, 1, 2}
+  // (scan_kernels.hip UGPU_FOR_FCODES); byte-row tables only
+  if (t.format == FMT_BYTE && nf > 0 && nAB <= 2) {
     t.filter = true;
     t.nA = (uint32_t)ta.size();
     t.nB = (uint32_t)tb.size();
-    t.nC = tc.size() <= 4 ? (uint32_t)tc.size() : 0;  // too wide: no second-byte test
+    t.nC = (t.nB > 0 && tc.size() <= 2) ? (uint32_t)tc.size() : 0;  // too wide: no second-byte test
     for (uint32_t i = 0; i < t.nA; ++i) t.tm[i] = ta[i].m, t.tv[i] = ta[i].v;
     for (uint32_t i = 0; i < t.nB; ++i) t.tm[4 + i] = tb[i].m, t.tv[4 + i] = tb[i].v;
     for (uint32_t i = 0; i < t.nC; ++i) t.tm[8 + i] = tc[i].m, t.tv[8 + i] = tc[i].v;
