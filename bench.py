@@ -187,7 +187,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc, "config": args.config, "pattern": rx, "bytes_per_gpu": per_gpu,
                    "total_bytes": total, "corpus_kind": kind, "parallelism": "shard%d" % world,
-                   "dfa_states": info["states"], "dfa_row": info["row"], "needles": info["needles"]},
+                   "dfa_states": info["states"], "dfa_row": info["row"], "prefilter_ppm": info["prefilter_ppm"]},
         "matches": res["count"],
         "matches_per_s": round(matches_per_s, 1),
         "digest": res["digest"],

@@ -60,7 +60,7 @@ typedef struct ugpu_dfa_info
   uint32_t row;         /* table row width (256 = byte-indexed, else class-indexed, pow2) */
   uint32_t format;      /* 0 = next[state][byte], 1 = cls[byte] + next[state][class] */
   uint32_t table_bytes; /* bytes of the transition table staged in LDS */
-  uint32_t needles;     /* number of first bytes when <= 4 (SWAR prefilter), else 0 */
+  uint32_t prefilter_ppm; /* prefiltered (sparse) scan: est. candidate positions per million + 1; 0 = dense scan */
   uint32_t first_bytes; /* number of bytes that can start a match (|fst_|) */
   uint32_t accepting;   /* accepting states */
 } ugpu_dfa_info;
@@ -105,6 +105,11 @@ int ugpu_dfa_info_get(const ugpu_dfa *dfa, ugpu_dfa_info *info);
 int ugpu_tables_build_host(const uint32_t *opc, uint32_t nop, ugpu_dfa_info *info, uint16_t *trans,
                            uint32_t trans_cap, uint8_t *cls, uint32_t *caps, uint32_t caps_cap, uint32_t *start,
                            uint32_t *accb);
+
+/* Host-only: the prefilter lookup tables (T0[8], T1[8], T2[4] bucket bytes, see
+   ugrep_amd/csrc/tables.hpp) into ft[20]; returns UGPU_OK and sets *enabled to 1
+   when the sparse (prefiltered) kernel is used for this table. */
+int ugpu_tables_prefilter_host(const uint32_t *opc, uint32_t nop, uint8_t *ft, int *enabled);
 
 /* --- whole-buffer FIND (Matcher::buffer(); while (find()) ...) --- */
 

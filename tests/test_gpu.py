@@ -128,25 +128,45 @@ def test_c1_anchor_64mib(U, pats):
 
 def _planted_count(seed, n):
     """Planted cells of the C2' corpus, from the cell seeds (vectorised splitmix64)."""
-    cells = np.arange(n // 64, dtype=np.uint64)
-    with np.errstate(over="ignore"):
-        s = np.uint64(seed) ^ (cells * np.uint64(0xD1B54A32D192ED03))
-        z = s + np.uint64(0x9E3779B97F4A7C15)
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        x = z ^ (z >> np.uint64(31))
-    return int(np.count_nonzero(((x >> np.uint64(1)) & np.uint64(63)) == 0))
+    total = 0
+    ncell = n // 64
+    for c0 in range(0, ncell, 1 << 24):
+        cells = np.arange(c0, min(ncell, c0 + (1 << 24)), dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            s = np.uint64(seed) ^ (cells * np.uint64(0xD1B54A32D192ED03))
+            z = s + np.uint64(0x9E3779B97F4A7C15)
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            x = z ^ (z >> np.uint64(31))
+        total += int(np.count_nonzero(((x >> np.uint64(1)) & np.uint64(63)) == 0))
+    return total
 
 
-def test_planted_known_answer_1gib(U, pats):
-    n = 1 << 30
+def test_planted_known_answer_5gib(U, pats):
+    """Known answer past the 2^31 and 2^32 byte offsets (positions are 64-bit)."""
+    n = 5 << 30
     t = _gen_dev(U, 2, 2024, 0, n)
     sc = U.Scanner(pats["c2_foobarbaz"])
     sc.scan(t.data_ptr(), 0, n, n, True, 0, _stream())
     tot = sc.totals()
     assert tot.count == _planted_count(2024, n)
-    del t
+    assert tot.exit == n
+    del t, sc
     torch.cuda.empty_cache()
+
+
+def test_large_bias_digest(U, pats):
+    """Reported starts carry the shard bias (here > 2^40) through the digests."""
+    from oracle_lib import OracleDfa, gen
+    n = 1 << 22
+    host = gen(3, 9, 0, n)
+    t = _dev(host)
+    bias = (1 << 40) + 12345
+    for pname in ("c3_ident", "c2_foobarbaz"):
+        sc = U.Scanner(pats[pname])
+        sc.scan(t.data_ptr(), 0, n, n, True, bias, _stream())
+        tot = sc.totals()
+        assert (tot.count, tot.digest, tot.dcap) == OracleDfa(pats[pname].opc).find(host, bias=bias)[:3]
 
 
 def test_grid_size_invariance(U, pats):

@@ -46,7 +46,8 @@ def test_config_table_shapes(patterns):
     # true column-equivalence classes: 99 (the survey counted 110 range-boundary classes)
     assert t["info"]["classes"] <= 110
     t = ugrep_amd.host_tables(patterns["c2_foobarbaz"]["opc"])
-    assert t["info"]["needles"] == 1  # first bytes {b, f} = one term (b & 0xfb) == 0x62
+    assert 0 < t["info"]["prefilter_ppm"] < 5000  # sparse prefilter: b/f, then a/o, then o/r/z
+    assert ugrep_amd.host_tables(patterns["c3_ident"]["opc"])["info"]["prefilter_ppm"] == 0  # dense
 
 
 def _py_find(t, data):
@@ -83,6 +84,51 @@ def test_host_tables_reproduce_reference_matches(patterns, cases):
         assert _py_find(t, data) == c["matches"], (c["pattern"], c["input"]["name"])
         done += 1
     assert done > 200
+
+
+def _bucket_bits(ft, b):
+    return ft[b & 7] & ft[8 + ((b >> 3) & 7)] & ft[16 + (b >> 6)]
+
+
+def _prefilter_candidates(ft, data):
+    """Positions passing A(i) | (B(i) & C(i+1) & D(i+2)), as sparse_kernel.hip
+    computes them (bytes past the end pass their tests)."""
+    R = [_bucket_bits(ft, b) for b in data] + [0xFF, 0xFF]
+    U = [r | (r >> 1) for r in R]
+    return {i for i in range(len(data))
+            if (R[i] & 1) or ((U[i] >> 1) & 1 and (U[i + 1] >> 3) & 1 and (U[i + 2] >> 5) & 1)}
+
+
+def test_prefilter_keeps_every_match_start(patterns, cases):
+    """The prefilter may pass extra positions but never drops a match start."""
+    seen_sparse = set()
+    for c in cases:
+        if c["pattern"] in UNSUPPORTED or c["matches"] is None or not c["matches"]:
+            continue
+        enabled, ft = ugrep_amd.host_prefilter(patterns[c["pattern"]]["opc"])
+        if not enabled:
+            continue
+        seen_sparse.add(c["pattern"])
+        cand = _prefilter_candidates(ft.tolist(), case_input(c["input"]).tolist())
+        starts = [m[0] for m in c["matches"]]
+        assert all(s in cand for s in starts), (c["pattern"], c["input"].get("name"))
+    assert {"c1_lorem", "c2_foobarbaz", "hello", "the_then", "aa"} <= seen_sparse
+
+
+def test_prefilter_selectivity_c2():
+    """foo|bar|baz: the three-byte buckets are exact (no aliasing) on [a-z]."""
+    import json, os
+    opc = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "patterns.json")))["c2_foobarbaz"]["opc"]
+    enabled, ft = ugrep_amd.host_prefilter(opc)
+    assert enabled
+    ft = ft.tolist()
+    letters = [ord(ch) for ch in "abcdefghijklmnopqrstuvwxyz"]
+    first = {b for b in letters if (_bucket_bits(ft, b) >> 1) & 3}
+    second = {b for b in letters if (_bucket_bits(ft, b) >> 3) & 3}
+    third = {b for b in letters if (_bucket_bits(ft, b) >> 5) & 3}
+    assert first == {ord("b"), ord("f")}
+    assert second == {ord("a"), ord("o")}
+    assert third == {ord("o"), ord("r"), ord("z")}
 
 
 def test_result_struct_layout():

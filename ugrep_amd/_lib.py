@@ -31,7 +31,7 @@ c_u64p = ctypes.POINTER(ctypes.c_uint64)
 
 class DfaInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in
-                ("states", "classes", "row", "format", "table_bytes", "needles", "first_bytes", "accepting")]
+                ("states", "classes", "row", "format", "table_bytes", "prefilter_ppm", "first_bytes", "accepting")]
 
 
 class Totals(ctypes.Structure):
@@ -68,6 +68,7 @@ def _load():
         "ugpu_dfa_info_get": (ctypes.c_int, [V, P(DfaInfo)]),
         "ugpu_tables_build_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, P(DfaInfo), c_u16p, ctypes.c_uint32,
                                                   c_u8p, c_u32p, ctypes.c_uint32, c_u32p, c_u32p]),
+        "ugpu_tables_prefilter_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, c_u8p, P(ctypes.c_int)]),
         "ugpu_find_all": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P(P(Result))]),
         "ugpu_result_free": (ctypes.c_int, [P(Result)]),
         "ugpu_scanner_create": (ctypes.c_int, [V, P(V)]),

@@ -35,7 +35,8 @@ struct ugpu_dfa {
 struct ugpu_scanner {
   const ugpu_dfa* dfa = nullptr;
   int device = 0;
-  int max_grid = 0;
+  int max_rec = 0;       // chain records per scan (blocks or waves)
+  bool sparse = false;   // prefiltered wave-persistent kernel (sparse_kernel.hip)
   size_t smem = 0;
   BlockRec* d_recs = nullptr;
   uint64_t* d_entries = nullptr;
@@ -82,37 +83,53 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.start = d->t.start;
   P.accb = d->t.accb;
   P.log_row = d->t.log_row;
-  P.nA = d->t.nA;
-  P.nB = d->t.nB;
-  P.nC = d->t.nC;
-  for (int i = 0; i < 12; ++i) {
-    P.tm[i] = d->t.tm[i] * 0x01010101u;
-    P.tv[i] = d->t.tv[i] * 0x01010101u;
-  }
+  P.nstates = d->t.states;
+  for (int i = 0; i < 5; ++i)
+    P.ft[i] = (uint32_t)d->t.ft[4 * i] | ((uint32_t)d->t.ft[4 * i + 1] << 8) | ((uint32_t)d->t.ft[4 * i + 2] << 16) |
+              ((uint32_t)d->t.ft[4 * i + 3] << 24);
 }
 
 // Translate a byte range of dbuf into the 16-byte aligned base coordinates
-// the kernels use, and fix the grid geometry.
-void geometry(ScanParams& P, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint64_t read_end, int max_grid,
-              uint64_t& off)
+// the kernels use, and fix the geometry: `unit`-byte tiles, dealt in equal
+// contiguous runs to at most max_rec chain records (per = records per block).
+void geometry(ScanParams& P, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint64_t read_end, int max_rec,
+              uint32_t unit, uint32_t per, uint64_t& off)
 {
   off = reinterpret_cast<uintptr_t>(dbuf) & 15u;
   P.g = dbuf - off;
   P.lo = lo + off;
   P.hi = hi + off;
   P.rend = read_end + off;
-  const uint64_t t0 = P.lo / kTile;
-  uint64_t t1 = (P.hi + kTile - 1) / kTile;
+  const uint64_t t0 = P.lo / unit;
+  uint64_t t1 = (P.hi + unit - 1) / unit;
   if (t1 <= t0) t1 = t0 + 1;
   const uint64_t nt = t1 - t0;
-  uint64_t grid = nt < (uint64_t)max_grid ? nt : (uint64_t)max_grid;
-  if (grid == 0) grid = 1;
-  const uint64_t tpb = (nt + grid - 1) / grid;
-  grid = (nt + tpb - 1) / tpb;
+  uint64_t nrec = nt < (uint64_t)max_rec ? nt : (uint64_t)max_rec;
+  if (nrec == 0) nrec = 1;
+  const uint64_t tpr = (nt + nrec - 1) / nrec;
+  nrec = (nt + tpr - 1) / tpr;
+  const uint64_t grid = (nrec + per - 1) / per;
   P.t0 = t0;
   P.t1 = t1;
-  P.tpb = tpb;
+  P.tpb = tpr;
+  P.unit = unit;
   P.grid = (uint32_t)grid;
+  P.nrec = (uint32_t)(grid * per);
+}
+
+void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi,
+                  uint64_t read_end, uint64_t& off)
+{
+  if (s->sparse)
+    geometry(P, dbuf, lo, hi, read_end, s->max_rec, kWaveTile, kSpWaves, off);
+  else
+    geometry(P, dbuf, lo, hi, read_end, s->max_rec, kTile, 1, off);
+}
+
+hipError_t launch_main(const ugpu_scanner* s, const ScanParams& P, bool write, hipStream_t st)
+{
+  if (s->sparse) return launch_sparse(P, write, s->smem, st);
+  return launch_scan(P, s->dfa->t.format, s->dfa->t.filter, write, s->smem, st);
 }
 
 bool is_device_ptr(const void* p)
@@ -186,7 +203,7 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->row = d->t.row;
   info->format = d->t.format;
   info->table_bytes = (uint32_t)(d->t.trans.size() * 2 + (d->t.format == FMT_CLASS ? 256 : 0));
-  info->needles = d->t.filter ? d->t.nA + d->t.nB : 0;
+  info->prefilter_ppm = d->t.filter ? (uint32_t)(d->t.fdensity * 1e6) + 1 : 0;
   info->first_bytes = d->t.first_bytes;
   info->accepting = d->t.accepting;
   return UGPU_OK;
@@ -206,7 +223,7 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   info->row = t.row;
   info->format = t.format;
   info->table_bytes = (uint32_t)(t.trans.size() * 2 + (t.format == FMT_CLASS ? 256 : 0));
-  info->needles = t.filter ? t.nA + t.nB : 0;
+  info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
   if (start) *start = t.start;
@@ -223,6 +240,18 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   return UGPU_OK;
 }
 
+int ugpu_tables_prefilter_host(const uint32_t* opc, uint32_t nop, uint8_t* ft, int* enabled)
+{
+  if (!ft || !enabled) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  std::copy(t.ft, t.ft + 20, ft);
+  *enabled = t.filter ? 1 : 0;
+  return UGPU_OK;
+}
+
 int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
 {
   if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
@@ -231,26 +260,33 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   if (!s) return fail(UGPU_NOMEM, "host allocation");
   s->dfa = dfa;
   HIP_TRY(hipGetDevice(&s->device));
-  s->smem = scan_smem_bytes(dfa->ntrans_pad, dfa->t.format);
+  s->sparse = dfa->t.filter && dfa->t.format == FMT_BYTE;
+  s->smem = s->sparse ? sparse_smem_bytes(dfa->ntrans_pad, dfa->t.states)
+                      : scan_smem_bytes(dfa->ntrans_pad, dfa->t.format);
   if (s->smem > 160 * 1024) {
     delete s;
     return fail(UGPU_UNSUPPORTED, "tables do not fit in LDS");
   }
   int per_cu = 0;
-  HIP_TRY(scan_occupancy(dfa->t.format, dfa->t.filter, s->smem, &per_cu));
+  if (s->sparse) {
+    ScanParams probe{};
+    HIP_TRY(sparse_occupancy(probe, s->smem, &per_cu));
+  } else {
+    HIP_TRY(scan_occupancy(dfa->t.format, dfa->t.filter, s->smem, &per_cu));
+  }
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, s->device));
   if (per_cu < 1) per_cu = 1;
-  int g = prop.multiProcessorCount * per_cu;
-  if (g > kMaxGrid) g = kMaxGrid;
-  s->max_grid = g;
+  int g = prop.multiProcessorCount * per_cu * (s->sparse ? kSpWaves : 1);
+  if (g > kMaxRec) g = kMaxRec;
+  s->max_rec = g;
   if (const char* env = std::getenv("UGPU_MAX_GRID")) {
     int v = std::atoi(env);
-    if (v >= 1 && v <= kMaxGrid) s->max_grid = v;
+    if (v >= 1 && v <= kMaxRec) s->max_rec = v;
   }
-  HIP_TRY(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxGrid));
-  HIP_TRY(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxGrid));
-  HIP_TRY(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxGrid));
+  HIP_TRY(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
+  HIP_TRY(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
+  HIP_TRY(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
   HIP_TRY(hipMalloc(&s->d_tot, sizeof(DevTotals)));
   HIP_TRY(hipMalloc(&s->d_flags, sizeof(uint32_t)));
   HIP_TRY(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
@@ -285,7 +321,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P{};
   fill_tables(P, s->dfa);
-  geometry(P, dbuf, lo, hi, read_end, s->max_grid, s->off);
+  geometry_for(P, s, dbuf, lo, hi, read_end, s->off);
   P.delta = (int64_t)bias - (int64_t)s->off;
   P.at_eof = at_eof ? 1u : 0u;
   if (const char* ab = std::getenv("UGPU_ABLATE")) P.ablate = (uint32_t)std::atoi(ab);
@@ -296,7 +332,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   P.out_base_out = s->d_obase;
   HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
   HIP_TRY(hipEventRecord(s->ev0, st));
-  HIP_TRY(launch_scan(P, s->dfa->t.format, s->dfa->t.filter, false, s->smem, st));
+  HIP_TRY(launch_main(s, P, false, st));
   HIP_TRY(hipEventRecord(s->ev1, st));
   HIP_TRY(launch_fix(P, s->dfa->t.format, st));
   HIP_TRY(hipMemcpyAsync(s->h_tot, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
@@ -345,7 +381,7 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
   P.out_cap = d_cap;
   P.out_capacity = capacity;
   HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
-  HIP_TRY(launch_scan(P, s->dfa->t.format, s->dfa->t.filter, true, s->smem, st));
+  HIP_TRY(launch_main(s, P, true, st));
   HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (*s->h_flags & UGPU_FLAG_CAPACITY) return fail(UGPU_CAPACITY, "output capacity exceeded");
@@ -361,7 +397,7 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
   ScanParams P{};
   fill_tables(P, s->dfa);
   uint64_t off = 0;
-  geometry(P, dbuf, lo, hi, read_end, s->max_grid, off);
+  geometry_for(P, s, dbuf, lo, hi, read_end, off);
   P.delta = (int64_t)bias - (int64_t)off;
   P.at_eof = at_eof ? 1u : 0u;
   P.totals = s->d_tot;

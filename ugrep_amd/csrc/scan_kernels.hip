@@ -9,251 +9,9 @@
 //   * DFA opcode interpreter (lib/matcher.cpp:125-546): one dependent LDS
 //     lookup per byte in the flattened table (walk);
 //   * FIND restart/accept logic (lib/matcher.cpp:621-746): chain_step.
-#include "scan_kernels.hpp"
+#include "device_common.hpp"
 
 namespace ugpu {
-
-// ---------------------------------------------------------------- tables
-template <int FMT>
-struct Tab {
-  const uint16_t* trans;
-  const uint8_t* cls;
-  uint32_t start, accb;
-  __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t b) const
-  {
-    if constexpr (FMT == 0)
-      return trans[s | b];
-    else
-      return trans[s + cls[b]];
-  }
-};
-
-// bytes [base, lend) are staged in LDS; anything else is read from global
-struct Win {
-  const uint8_t* lds;
-  uint64_t base, lend;
-  const uint8_t* g;
-  uint64_t rend;
-  uint32_t eof;
-};
-
-// Longest match starting at p (0 = none).  `le` = entry of the last accepting
-// state (its row identifies the accept index).  Mirrors the reference walk:
-// TAKE on entering an accepting state (lib/matcher.cpp:207-217), stop on HALT
-// (:528-541) or EOF (:460-465).
-template <int FMT>
-__device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64_t p, uint32_t& le, uint32_t& ovf)
-{
-  uint32_t s = T.start;
-  uint64_t q = p, last = p;
-  le = 0;
-  const uint64_t l1 = w.lend < w.rend ? w.lend : w.rend;
-  while (q < l1) {
-    uint32_t e = T.step(s, w.lds[q - w.base]);
-    if (e == 0) return last - p;
-    s = e;
-    ++q;
-    if (e >= T.accb) {
-      last = q;
-      le = e;
-    }
-  }
-  while (q < w.rend) {
-    uint32_t e = T.step(s, w.g[q]);
-    if (e == 0) return last - p;
-    s = e;
-    ++q;
-    if (e >= T.accb) {
-      last = q;
-      le = e;
-    }
-  }
-  if (!w.eof) ovf = 1;  // a live walk ran into the end of this shard's readable bytes
-  return last - p;
-}
-
-struct Ctx {
-  const uint32_t* caps;
-  uint32_t log_row;
-  int64_t delta;
-};
-
-struct CountEm {
-  uint64_t cnt = 0, dg = 0, dc = 0;
-  __device__ __forceinline__ void put(const Ctx& c, uint64_t pos, uint64_t len, uint32_t le, int sign)
-  {
-    uint64_t st = pos + (uint64_t)c.delta;
-    uint64_t cap = c.caps[le >> c.log_row];
-    uint64_t d1 = st * 31 + len, d2 = (st + 1) * cap;
-    if (sign > 0) {
-      ++cnt;
-      dg += d1;
-      dc += d2;
-    } else {
-      --cnt;
-      dg -= d1;
-      dc -= d2;
-    }
-  }
-};
-
-struct WriteEm {
-  uint64_t idx;
-  uint64_t capacity;
-  uint64_t* start;
-  uint32_t* len;
-  uint32_t* cap;
-  uint32_t overflow = 0;
-  __device__ __forceinline__ void put(const Ctx& c, uint64_t pos, uint64_t l, uint32_t le, int)
-  {
-    if (idx < capacity) {
-      start[idx] = pos + (uint64_t)c.delta;
-      len[idx] = (uint32_t)l;
-      cap[idx] = c.caps[le >> c.log_row];
-    } else {
-      overflow = 1;
-    }
-    ++idx;
-  }
-};
-
-// One step of the FIND chain from p (< e).  With the prefilter (FILT), positions
-// whose byte cannot start a match are skipped via the candidate mask of the
-// lane's 64-byte segment [sa, sa+64): their step is p+1 with no match.
-template <int FMT, bool FILT, class Em>
-__device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t p,
-                                               uint64_t sa, uint64_t e, uint64_t mask, Em& em, int sign,
-                                               uint32_t& ovf)
-{
-  uint64_t c0 = p;
-  if constexpr (FILT) {
-    uint64_t off = p - sa;
-    uint64_t m = off < 64 ? (mask & (~0ull << off)) : 0ull;
-    if (m == 0) return e;
-    c0 = sa + (uint64_t)__builtin_ctzll(m);
-  }
-  uint32_t le;
-  uint64_t len = walk<FMT>(T, w, c0, le, ovf);
-  if (len) {
-    em.put(c, c0, len, le, sign);
-    return c0 + len;
-  }
-  return c0 + 1;
-}
-
-template <int FMT, bool FILT, class Em>
-__device__ __forceinline__ uint64_t run_seg(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t x, uint64_t sa,
-                                            uint64_t e, uint64_t mask, Em& em, uint32_t& ovf)
-{
-  uint64_t p = x;
-  while (p < e) p = chain_step<FMT, FILT>(T, w, c, p, sa, e, mask, em, +1, ovf);
-  return p;
-}
-
-// Re-enter [.., e) at xn instead of xo.  Adds (true - speculative) matches to em.
-// Returns true if the chains met (exit unchanged), else sets nexit.
-template <int FMT, bool FILT>
-__device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t xo, uint64_t xn,
-                                      uint64_t sa, uint64_t e, uint64_t mask, CountEm& em, uint64_t& nexit,
-                                      uint32_t& ovf)
-{
-  uint64_t po = xo, pn = xn;
-  for (;;) {
-    if (po == pn) return true;
-    if (po >= e && pn >= e) {
-      nexit = pn;
-      return false;
-    }
-    if (po < pn)
-      po = chain_step<FMT, FILT>(T, w, c, po, sa, e, mask, em, -1, ovf);
-    else
-      pn = chain_step<FMT, FILT>(T, w, c, pn, sa, e, mask, em, +1, ovf);
-  }
-}
-
-// SWAR candidate mask of a 64-byte LDS segment: bit i set iff byte i may start
-// a match, i.e. B[i] in A, or B[i] in B and B[i+1] in C (tables.hpp).  A set
-// test is an OR over (mask, value) terms, each an exact per-byte zero test
-// ((t & 0x7f..) + 0x7f..) | t  (bit 7 = byte nonzero, no borrow leakage).
-// `nxt` holds the 4 bytes after the segment (the pair test reads byte 64).
-// The term counts are compile-time (filter code FC, see fcode()).
-constexpr int fcode(int na, int nb, int nc) { return 1 + na * 9 + nb * 3 + nc; }
-
-struct Filter {
-  uint32_t tm[12], tv[12];
-};
-
-__device__ __forceinline__ uint32_t nz_bytes(uint32_t t) { return ((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t; }
-
-// bit 7 of each byte set iff the byte matches NO term of the set [o, o+N)
-template <int N>
-__device__ __forceinline__ uint32_t no_match(const Filter& F, int o, uint32_t x)
-{
-  uint32_t r = 0xffffffffu;
-#pragma unroll
-  for (int i = 0; i < N; ++i) r &= nz_bytes((x & F.tm[o + i]) ^ F.tv[o + i]);
-  return r;
-}
-
-template <int FC>
-__device__ __forceinline__ uint64_t filter_mask(const uint8_t* seg, uint32_t nxt, const Filter& F)
-{
-  constexpr int NA = (FC - 1) / 9, NB = ((FC - 1) / 3) % 3, NC = (FC - 1) % 3;
-  const uint4* v = reinterpret_cast<const uint4*>(seg);
-  uint32_t wd[17];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    uint4 x = v[i];
-    wd[4 * i] = x.x;
-    wd[4 * i + 1] = x.y;
-    wd[4 * i + 2] = x.z;
-    wd[4 * i + 3] = x.w;
-  }
-  wd[16] = nxt;
-  uint32_t lo = 0, hi = 0;
-  uint32_t noC_next = NC ? no_match<NC>(F, 8, wd[0]) : 0u;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    uint32_t noBC = 0xffffffffu;
-    if constexpr (NB > 0) {
-      const uint32_t noC = noC_next;
-      noC_next = NC ? no_match<NC>(F, 8, wd[j + 1]) : 0u;
-      // byte i of the shifted word = C-test of byte i+1
-      const uint32_t noCs = __builtin_amdgcn_alignbyte(noC_next, noC, 1);
-      noBC = no_match<NB>(F, 4, wd[j]) | noCs;
-    }
-    const uint32_t cand = ~(no_match<NA>(F, 0, wd[j]) & noBC) & 0x80808080u;
-    const uint32_t nib = (((cand >> 7) * 0x00204081u) >> 21) & 0xfu;
-    if (j < 8)
-      lo |= nib << (4 * j);
-    else
-      hi |= nib << (4 * (j - 8));
-  }
-  return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t lowbits(uint64_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }
-
-__device__ __forceinline__ uint64_t clampu(uint64_t v, uint64_t a, uint64_t b) { return v < a ? a : (v > b ? b : v); }
-
-__device__ __forceinline__ uint4 load_chunk(const uint8_t* g, uint64_t pos, uint64_t rend)
-{
-  // A 16-byte aligned chunk holding at least one readable byte lies in a mapped
-  // page, so it is loaded whole; bytes >= rend are never consulted.
-  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-  if (pos < rend) {
-    v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(g + pos));
-    return make_uint4(v.x, v.y, v.z, v.w);
-  }
-  return make_uint4(0, 0, 0, 0);
-}
-
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v)
-{
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 // ---------------------------------------------------------------- scan kernel
 template <int FMT, int FC, bool WRITE>
@@ -280,14 +38,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
   }
   const Tab<FMT> T{ltrans, lcls, P.start, P.accb};
   const Ctx C{P.caps, P.log_row, P.delta};
-  Filter F;
-  if constexpr (FILT) {
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      F.tm[i] = P.tm[i];
-      F.tv[i] = P.tv[i];
-    }
-  }
+  static_assert(!FILT, "prefiltered patterns use sparse_kernel.hip");
 
   const uint64_t b = blockIdx.x;
   uint64_t tb = P.t0 + b * P.tpb;
@@ -338,11 +89,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
       tot.cnt += tile[tid];
       x0 = clampu(ts + kTile, blo, bhi);
       continue;
-    }
-    if constexpr (FILT) {
-      const uint32_t nxt = *reinterpret_cast<const uint32_t*>(tile + tid * kSeg + kSeg);
-      mask = filter_mask<FC>(tile + tid * kSeg, nxt, F);
-      mask &= lowbits(e - sa) & ~lowbits(s - sa);
     }
     if (P.ablate == 2) {
       tot.cnt += __popcll(mask);
@@ -434,12 +180,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams P)
 template <int FMT>
 __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
 {
-  __shared__ uint64_t ent[kMaxGrid], exi[kMaxGrid];
+  __shared__ uint64_t ent[kMaxRec], exi[kMaxRec];
   __shared__ uint64_t wred[3][kFixThreads / 64];
   __shared__ uint64_t wscan[kFixThreads / 64];
-  constexpr int PER = kMaxGrid / kFixThreads;
+  constexpr int PER = kMaxRec / kFixThreads;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int G = (int)P.grid;
+  const int G = (int)P.nrec;
   const Tab<FMT> T{P.trans, P.cls, P.start, P.accb};
   const Ctx C{P.caps, P.log_row, P.delta};
   Win w;
@@ -489,9 +235,7 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
       uint64_t tb = P.t0 + b * P.tpb;
       uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
       if (tb > te) tb = te;
-      const uint64_t blo = clampu(tb * kTile, P.lo, P.hi);
-      const uint64_t bhi = clampu(te * kTile, P.lo, P.hi);
-      (void)blo;
+      const uint64_t bhi = clampu(te * P.unit, P.lo, P.hi);
       CountEm d;
       uint64_t ne;
       if (!merge<FMT, 0>(T, w, C, ent[b], nx[j], 0, bhi, 0, d, ne, ovf)) exi[b] = ne;
@@ -597,28 +341,11 @@ static hipError_t launch_one(const ScanParams& P, size_t smem, hipStream_t strea
   return hipGetLastError();
 }
 
-// filter codes with instantiated kernels: NA + NB in {1, 2}, NC in {0, 1, 2} (tables.cpp)
-#define UGPU_FOR_FCODES(X) \
-  X(fcode(1, 0, 0)) X(fcode(2, 0, 0)) X(fcode(0, 1, 0)) X(fcode(0, 1, 1)) X(fcode(0, 1, 2)) X(fcode(1, 1, 0)) \
-  X(fcode(1, 1, 1)) X(fcode(1, 1, 2)) X(fcode(0, 2, 0)) X(fcode(0, 2, 1)) X(fcode(0, 2, 2))
-
-template <bool WRITE>
-static hipError_t launch_byte(const ScanParams& P, int fc, size_t smem, hipStream_t stream)
-{
-  switch (fc) {
-#define X(c) \
-  case c: return launch_one<0, c, WRITE>(P, smem, stream);
-    UGPU_FOR_FCODES(X)
-#undef X
-    default: return launch_one<0, 0, WRITE>(P, smem, stream);
-  }
-}
-
 hipError_t launch_scan(const ScanParams& P, uint32_t format, bool filter, bool write, size_t smem,
                        hipStream_t stream)
 {
-  const int fc = filter ? fcode((int)P.nA, (int)P.nB, (int)P.nC) : 0;
-  if (format == 0) return write ? launch_byte<true>(P, fc, smem, stream) : launch_byte<false>(P, fc, smem, stream);
+  (void)filter;  // prefiltered patterns run sparse_kernel
+  if (format == 0) return write ? launch_one<0, 0, true>(P, smem, stream) : launch_one<0, 0, false>(P, smem, stream);
   return write ? launch_one<1, 0, true>(P, smem, stream) : launch_one<1, 0, false>(P, smem, stream);
 }
 
@@ -649,8 +376,8 @@ static hipError_t occ_one(size_t smem, int* n)
 
 hipError_t scan_occupancy(uint32_t format, bool filter, size_t smem, int* n)
 {
-  // all filter variants share the same resource shape; the common C2 one answers
-  if (format == 0) return filter ? occ_one<0, fcode(0, 1, 2)>(smem, n) : occ_one<0, 0>(smem, n);
+  (void)filter;
+  if (format == 0) return occ_one<0, 0>(smem, n);
   return occ_one<1, 0>(smem, n);
 }
 

@@ -26,8 +26,11 @@ constexpr int kBlock = 256;            // threads per workgroup (4 waves)
 constexpr int kSeg = 64;               // bytes per lane segment
 constexpr int kTile = kBlock * kSeg;   // 16 KiB staged per tile
 constexpr int kHalo = 256;             // bytes staged past the tile end
-constexpr int kMaxGrid = 4096;         // block records fixed by one fix_kernel block
+constexpr int kMaxRec = 8192;          // chain records stitched by one fix_kernel block
 constexpr int kFixThreads = 1024;
+constexpr int kWaveTile = 4096;        // sparse kernel: bytes per wave per iteration
+constexpr int kSpWaves = 4;            // sparse kernel: waves per workgroup
+constexpr int kCandCap = 512;          // sparse kernel: candidate window per wave
 
 struct BlockRec {
   uint64_t entry, exit, cnt, dg, dc, pad0, pad1, pad2;
@@ -48,14 +51,16 @@ struct ScanParams {
   int64_t delta;      // reported start = position + delta
   uint32_t at_eof;    // rend is the end of the stream
   uint32_t ablate;    // benchmarking only (UGPU_ABLATE): 1 = stage tiles only, 2 = + prefilter
-  uint64_t t0, t1, tpb;  // tiles [t0, t1), tiles per block
+  uint64_t t0, t1, tpb;  // tiles [t0, t1), tiles per record
+  uint32_t unit;         // bytes per tile (kTile or kWaveTile)
+  uint32_t nrec;         // chain records (blocks or waves)
+  uint32_t nstates;
   const uint16_t* trans;
   const uint8_t* cls;
   const uint32_t* caps;
   uint32_t ntrans_pad;   // u16 entries, multiple of 8
   uint32_t start, accb, log_row;
-  uint32_t nA, nB, nC;   // prefilter term counts (tables.hpp)
-  uint32_t tm[12], tv[12];  // term masks / values replicated to 4 bytes
+  uint32_t ft[5];        // prefilter lookup tables T0 (lo, hi), T1 (lo, hi), T2 (tables.hpp)
   uint32_t grid;
   BlockRec* recs;
   const uint64_t* entries;   // OFFSETS pass: exact block entries
@@ -79,5 +84,9 @@ hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_e
 hipError_t scan_occupancy(uint32_t format, bool filter, size_t smem, int* blocks_per_cu);
 hipError_t launch_gen(int kind, uint64_t seed, uint64_t off, uint8_t* dbuf, uint64_t len, hipStream_t stream);
 size_t scan_smem_bytes(uint32_t ntrans_pad, uint32_t format);
+// sparse (prefiltered) wave-persistent kernel, sparse_kernel.hip
+hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream_t stream);
+hipError_t sparse_occupancy(const ScanParams& P, size_t smem, int* blocks_per_cu);
+size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates);
 
 }  // namespace ugpu

@@ -32,56 +32,58 @@ struct RawState {
   int64_t target_pc[256];
 };
 
-struct Term {
-  uint8_t m, v;  // byte b matches iff (b & m) == v
-  bool operator<(const Term& o) const { return m != o.m ? m < o.m : v < o.v; }
-  bool operator==(const Term& o) const { return m == o.m && v == o.v; }
+// Bucket approximation used by the GPU prefilter: the bytes whose 3-bit
+// fields (lo3, mid3, hi2) each occur among the members' fields.
+struct Bucket {
+  uint8_t lo = 0, mid = 0, hi = 0;  // bitsets of field values
+  void add(int b)
+  {
+    lo |= (uint8_t)(1u << (b & 7));
+    mid |= (uint8_t)(1u << ((b >> 3) & 7));
+    hi |= (uint8_t)(1u << (b >> 6));
+  }
+  bool has(int b) const { return (lo >> (b & 7) & 1) && (mid >> ((b >> 3) & 7) & 1) && (hi >> (b >> 6) & 1); }
 };
 
-// Exact cover of a byte set by (mask, value) terms: prime implicants by
-// pairwise merging (Quine-McCluskey over 8 bits), then a greedy set cover.
-std::vector<Term> cover_terms(const bool in[256])
+// Split a byte set over two buckets minimising the union of their
+// approximations (exhaustive for small sets, greedy otherwise).
+void split_set(const bool in[256], Bucket& b1, Bucket& b2)
 {
-  std::vector<Term> cur, primes;
+  std::vector<int> mem;
   for (int b = 0; b < 256; ++b)
-    if (in[b]) cur.push_back(Term{0xff, (uint8_t)b});
-  while (!cur.empty()) {
-    std::vector<Term> next;
-    std::vector<bool> used(cur.size(), false);
-    for (size_t i = 0; i < cur.size(); ++i)
-      for (size_t j = i + 1; j < cur.size(); ++j) {
-        if (cur[i].m != cur[j].m) continue;
-        uint8_t d = cur[i].v ^ cur[j].v;
-        if (d && (d & (d - 1)) == 0) {
-          next.push_back(Term{(uint8_t)(cur[i].m & ~d), (uint8_t)(cur[i].v & ~d)});
-          used[i] = used[j] = true;
-        }
-      }
-    for (size_t i = 0; i < cur.size(); ++i)
-      if (!used[i]) primes.push_back(cur[i]);
-    std::sort(next.begin(), next.end());
-    next.erase(std::unique(next.begin(), next.end()), next.end());
-    cur.swap(next);
-  }
-  std::vector<Term> chosen;
-  bool covered[256] = {};
-  for (;;) {
-    int best = -1, best_n = 0;
-    for (size_t i = 0; i < primes.size(); ++i) {
-      int n = 0;
-      for (int b = 0; b < 256; ++b)
-        if (in[b] && !covered[b] && (b & primes[i].m) == primes[i].v) ++n;
-      if (n > best_n) {
-        best_n = n;
-        best = (int)i;
+    if (in[b]) mem.push_back(b);
+  b1 = Bucket();
+  b2 = Bucket();
+  if (mem.empty()) return;
+  auto cost = [](const Bucket& x, const Bucket& y) {
+    int n = 0;
+    for (int b = 0; b < 256; ++b) n += (x.has(b) || y.has(b)) ? 1 : 0;
+    return n;
+  };
+  if (mem.size() <= 12) {
+    int best = 1 << 30;
+    const uint32_t lim = 1u << (mem.size() - 1);
+    for (uint32_t m = 0; m < lim; ++m) {  // member 0 always in bucket 1
+      Bucket x, y;
+      for (size_t i = 0; i < mem.size(); ++i) ((i > 0 && (m >> (i - 1) & 1)) ? y : x).add(mem[i]);
+      const int c = cost(x, y);
+      if (c < best) {
+        best = c;
+        b1 = x;
+        b2 = y;
       }
     }
-    if (best < 0) break;
-    chosen.push_back(primes[best]);
-    for (int b = 0; b < 256; ++b)
-      if ((b & primes[best].m) == primes[best].v) covered[b] = true;
+    return;
   }
-  return chosen;
+  for (int b : mem) {
+    Bucket x = b1, y = b2;
+    x.add(b);
+    y.add(b);
+    if (cost(x, b2) <= cost(b1, y))
+      b1 = x;
+    else
+      b2 = y;
+  }
 }
 
 }  // namespace
@@ -238,35 +240,60 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   t.accepting = S - first_acc;
   t.accb = (t.accepting > 0) ? first_acc * R : 0x10000u;
   // prefilter sets (see tables.hpp): A = first bytes that complete a match,
-  // B = other first bytes, C = bytes that can follow a byte of B
-  bool setA[256] = {}, setB[256] = {}, setC[256] = {};
-  uint32_t nf = 0, nAB = 0;
+  // B = other first bytes, C = bytes that can follow a byte of B, D = bytes
+  // that can follow such a pair; short2 = some 2-byte prefix already accepts
+  bool setA[256] = {}, setB[256] = {}, setC[256] = {}, setD[256] = {};
+  bool short2 = false;
+  uint32_t nf = 0;
   for (int c = 0; c < 256; ++c) {
     const uint32_t s1 = nxt[(size_t)start_sid * 256 + c];
     if (s1 == 0) continue;
     ++nf;
     if (s1 >= first_acc) {
       setA[c] = true;
-    } else {
-      setB[c] = true;
-      for (int d = 0; d < 256; ++d)
-        if (nxt[(size_t)s1 * 256 + d] != 0) setC[d] = true;
+      continue;
+    }
+    setB[c] = true;
+    for (int d = 0; d < 256; ++d) {
+      const uint32_t s2 = nxt[(size_t)s1 * 256 + d];
+      if (s2 == 0) continue;
+      setC[d] = true;
+      if (s2 >= first_acc) short2 = true;
+      for (int e = 0; e < 256; ++e)
+        if (nxt[(size_t)s2 * 256 + e] != 0) setD[e] = true;
     }
   }
   t.first_bytes = nf;
-  std::vector<Term> ta = cover_terms(setA), tb = cover_terms(setB), tc = cover_terms(setC);
-  nAB = (uint32_t)(ta.size() + tb.size());
-  // kernels are instantiated for nA + nB in {1, 2} and nC in {0, 1, 2}
-  // (scan_kernels.hip UGPU_FOR_FCODES); byte-row tables only
-  if (t.format == FMT_BYTE && nf > 0 && nAB <= 2) {
-    t.filter = true;
-    t.nA = (uint32_t)ta.size();
-    t.nB = (uint32_t)tb.size();
-    t.nC = (t.nB > 0 && tc.size() <= 2) ? (uint32_t)tc.size() : 0;  // too wide: no second-byte test
-    for (uint32_t i = 0; i < t.nA; ++i) t.tm[i] = ta[i].m, t.tv[i] = ta[i].v;
-    for (uint32_t i = 0; i < t.nB; ++i) t.tm[4 + i] = tb[i].m, t.tv[4 + i] = tb[i].v;
-    for (uint32_t i = 0; i < t.nC; ++i) t.tm[8 + i] = tc[i].m, t.tv[8 + i] = tc[i].v;
+  Bucket a1, a2, b1, b2, c1, c2, d1, d2;
+  split_set(setA, a1, a2);
+  a1 = Bucket();  // A uses one bucket (bit 0): merge both halves
+  for (int c = 0; c < 256; ++c)
+    if (setA[c]) a1.add(c);
+  split_set(setB, b1, b2);
+  split_set(setC, c1, c2);
+  if (short2) {  // a match may end after 2 bytes: no third-byte test
+    for (int c = 0; c < 256; ++c) setD[c] = true;
   }
+  split_set(setD, d1, d2);
+  const Bucket* bk[7] = {&a1, &b1, &b2, &c1, &c2, &d1, &d2};
+  for (int bit = 0; bit < 7; ++bit) {
+    for (int v = 0; v < 8; ++v) {
+      if (bk[bit]->lo >> v & 1) t.ft[v] |= (uint8_t)(1u << bit);
+      if (bk[bit]->mid >> v & 1) t.ft[8 + v] |= (uint8_t)(1u << bit);
+    }
+    for (int v = 0; v < 4; ++v)
+      if (bk[bit]->hi >> v & 1) t.ft[16 + v] |= (uint8_t)(1u << bit);
+  }
+  // candidate density on printable ASCII + newline, assuming independent bytes
+  auto frac = [](const Bucket& x, const Bucket& y) {
+    int n = 0;
+    for (int b = 0x20; b < 0x7f; ++b) n += (x.has(b) || y.has(b)) ? 1 : 0;
+    return n / 95.0;
+  };
+  const double pa = frac(a1, a1), pb = frac(b1, b2), pc = frac(c1, c2), pd = frac(d1, d2);
+  t.fdensity = pa + (1.0 - pa) * pb * pc * pd;
+  // the sparse kernel pays off when few positions survive the prefilter
+  t.filter = t.format == FMT_BYTE && nf > 0 && t.fdensity <= 0.15;
   out = std::move(t);
   return 0;
 }

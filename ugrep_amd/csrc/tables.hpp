@@ -32,12 +32,16 @@ struct DfaTables {
   uint32_t accepting = 0;
   // Candidate prefilter (replaces the reference's needle/pin prefilters,
   // lib/matcher_avx2.cpp:303-799): a position p can start a match only if
-  //   B[p] in A  (1-byte match possible)  or  B[p] in B and B[p+1] in C.
-  // Each set is an exact cover by (mask, value) terms: b matches a term iff
-  // (b & mask) == value.  filter == false: no prefilter (dense patterns).
-  bool filter = false;
-  uint32_t nA = 0, nB = 0, nC = 0;  // nC == 0: no second-byte test
-  uint8_t tm[12] = {}, tv[12] = {};  // terms: A at [0,nA), B at [4,4+nB), C at [8,8+nC)
+  //   B[p] in A (a 1-byte match)  or  B[p] in B and B[p+1] in C and B[p+2] in D
+  // (C / D = all bytes when a match may end earlier).  The sets are tested
+  // together by three byte-table lookups on the 3-bit fields of a byte
+  // (v_perm_b32 on the GPU): R(b) = T0[b & 7] & T1[(b >> 3) & 7] & T2[b >> 6],
+  // with one bit per bucket: A = bit 0, B = bits 1|2, C = bits 3|4, D = bits
+  // 5|6.  Each bucket over-approximates its members (a superset is safe); each
+  // set is split over two buckets to limit aliasing.
+  bool filter = false;       // false: dense pattern, no prefilter
+  uint8_t ft[20] = {};       // T0[8], T1[8], T2[4]
+  double fdensity = 1.0;     // estimated candidate fraction on printable ASCII
   uint32_t first_bytes = 0;
   std::vector<uint16_t> trans;  // states * row
   std::vector<uint8_t> cls;     // 256

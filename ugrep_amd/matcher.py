@@ -42,6 +42,15 @@ def host_tables(opc):
                 start=start.value, accb=accb.value)
 
 
+def host_prefilter(opc):
+    """(enabled, ft[20]) prefilter lookup tables built on the host (tables.hpp)."""
+    a, p = _as_u32(opc)
+    ft = np.zeros(20, np.uint8)
+    en = ctypes.c_int()
+    check(lib.ugpu_tables_prefilter_host(p, len(a), ft.ctypes.data_as(_lib.c_u8p), ctypes.byref(en)))
+    return bool(en.value), ft
+
+
 class Pattern:
     """Compiled pattern (opcode words) with its device tables."""
 
