@@ -7,13 +7,15 @@
 //
 // Each wave owns a contiguous range of 4 KiB wave-tiles and walks it alone, so
 // the main loop has no workgroup barrier:
-//   1. 4 KiB wave-tiles arrive by coalesced 16 B/lane loads, one tile ahead in
-//      registers, and are stored to the wave's LDS slice;
-//   2. the SWAR prefilter reads chunk k of lane l = bytes [1024k + 16l, +16)
-//      -> 16-bit candidate mask per chunk (walks read the same LDS tile);
-//   3. candidates are compacted in position order (packed DPP scans) into
-//      an LDS list, and up to 64 are walked at once, one per lane: a walk from
-//      c is independent of the chain, so all walks run in parallel;
+//   1. 4 KiB wave-tiles arrive by coalesced 16 B/lane loads into two register
+//      sets used in turn (no LDS staging);
+//   2. the prefilter reads chunk k of lane l = bytes [1024k + 16l, +16) from
+//      registers -> per-byte candidate flags (3 v_perm + 4 ops per dword);
+//   3. chunks with a candidate are ranked by a DPP scan and their candidates
+//      appended in position order to a per-wave LDS list; when 64 are queued they are walked at once, one per
+//      lane, each from its own 32-byte window re-read from global memory (an
+//      L2 hit); a walk from c is independent of the chain, so all walks run
+//      in parallel;
 //   4. the FIND chain over candidates is the greedy rule "keep the match at c
 //      iff c >= end of the last kept match" (Appendix A: a non-candidate
 //      position only steps p+1).  With an exclusive prefix-max of match ends
@@ -26,13 +28,10 @@ namespace ugpu {
 
 namespace {
 
-// 16-bit candidate mask of one 16-byte chunk (bytes 4j..4j+3 = wd[j]); `nx`
-// holds the 4 bytes that follow the chunk; when `nx_known` is false the
-// second-byte test of the chunk's last byte passes (a superset is safe).
-// Prefilter bucket bits of the 4 bytes of x (tables.hpp): three v_perm_b32
-// byte-table lookups on the lo3 / mid3 / hi2 fields of every byte, ANDed;
-// then U = R | R >> 1 folds each set's two buckets (B -> bit 1, C -> bit 3,
-// D -> bit 5; A stays bit 0 of R).
+// Prefilter set bits of the 4 bytes of x (tables.hpp): three v_perm_b32
+// byte-table lookups on the lo3 / mid3 / hi2 fields of every byte, ANDed.
+// Byte i of the result holds B_g(i) at bit g, C_g(i) at bit 2+g, D_g(i) at
+// bit 4+g; bits 6 and 7 are 0.
 struct FTab {
   uint32_t t0lo, t0hi, t1lo, t1hi, t2;
 };
@@ -45,25 +44,21 @@ __device__ __forceinline__ uint32_t bucket_bits(uint32_t x, const FTab& F)
   return r0 & r1 & r2;
 }
 
-// 16-bit candidate mask of one 16-byte chunk: bit i set iff byte i passes
-// A(i) | (B(i) & C(i+1) & D(i+2)).  R[j] = bucket_bits of dword j of the
-// chunk, R[4] = of the 4 bytes after it (all ones when unknown: they pass).
-__device__ __forceinline__ uint32_t chunk_mask(const uint32_t (&R)[5])
+// Candidate flags of one dword: bit g of byte i is set iff group g accepts
+// bytes i, i+1, i+2.  R = set bits of the dword, Rn = of the next 4 bytes
+// (0x3f3f3f3f when unknown: they pass).  alignbit(Rn, R, 10) moves byte
+// i+1's bits 2,3 onto byte i's bits 0,1, alignbit(Rn, R, 20) byte i+2's bits
+// 4,5; since bits 6,7 of every byte of R and Rn are 0, every other bit of the
+// AND is 0.  One v_bitop3 + two v_alignbit per 4 positions.
+__device__ __forceinline__ uint32_t cand_flags(uint32_t R, uint32_t Rn)
 {
-  uint32_t U[5];
-#pragma unroll
-  for (int j = 0; j < 5; ++j) U[j] = R[j] | (R[j] >> 1);
-  uint32_t m = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    // byte i of alignbyte(next, cur, s) = byte i+s of the pair (cur, next);
-    // every term is moved to bit 5 of its byte (no carries cross bytes)
-    const uint32_t bcd = (U[j] << 4) & (__builtin_amdgcn_alignbyte(U[j + 1], U[j], 1) << 2) &
-                         __builtin_amdgcn_alignbyte(U[j + 1], U[j], 2);
-    const uint32_t cand = (bcd | (R[j] << 5)) & 0x20202020u;
-    m |= ((((cand >> 5) * 0x00204081u) >> 21) & 0xfu) << (4 * j);
-  }
-  return m;
+  return R & __builtin_amdgcn_alignbit(Rn, R, 10) & __builtin_amdgcn_alignbit(Rn, R, 20);
+}
+
+// 4-bit mask (bit i = byte i has a flag) of a cand_flags dword.
+__device__ __forceinline__ uint32_t flags4(uint32_t X)
+{
+  return ((((X | (X >> 1)) & 0x01010101u) * 0x01020408u) >> 24);
 }
 
 // Wave-wide inclusive scans by DPP row shifts + row broadcasts (no LDS round
@@ -112,6 +107,197 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t ballot)
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(ballot >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ballot, 0u));
 }
 
+constexpr int kDefer = 64;                          // deferred candidates per wave (one walk batch)
+constexpr int kAux = 2048;                          // per-wave aux LDS bytes
+static_assert(kDefer * 8 <= kAux && 64 * 32 <= kAux && kCandCap * 2 <= kAux, "aux region too small");
+
+// Greedy FIND rule over up to 64 walked candidates held one per lane in
+// position order: keep the match at c iff c >= x, the end of the last kept
+// match (Appendix A: a non-candidate position only steps p+1).  With the
+// exclusive prefix-max of match ends (relative to x) the rule is exact unless
+// two candidate matches overlap; those batches take a 64-step in-wave pass.
+template <bool WRITE>
+__device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, uint32_t le, int lane, const Ctx& C,
+                                        const ScanParams& P, uint64_t& x, CountEm& acc, uint64_t& widx,
+                                        uint32_t& wover)
+{
+  const bool vm = valid && len != 0 && c >= x;
+  const uint64_t endr = vm ? c + len - x : 0;  // > 0 for vm lanes
+  const bool wide = __ballot(endr > 0xffffffffull) != 0;
+  const uint32_t er = (uint32_t)endr, cr = vm ? (uint32_t)(c - x) : 0u;
+  const uint32_t pm = dpp_prev_lane(dpp_scan_max(er));
+  bool kept = vm && cr >= pm;
+  if (wide || __ballot(vm && cr < pm)) {
+    uint64_t xx = x;
+    kept = false;
+    const uint64_t e = vm ? c + len : 0ull;
+    for (int i = 0; i < 64; ++i) {
+      const uint64_t ci = __shfl(c, i, 64), ei = __shfl(e, i, 64);
+      if (ei != 0 && ci >= xx) {
+        if (lane == i) kept = true;
+        xx = ei;
+      }
+    }
+  }
+  const uint64_t kb = __ballot(kept);
+  if (!kb) return;
+  if constexpr (WRITE) {
+    WriteEm we{widx + lanes_below(kb), P.out_capacity, P.out_start, P.out_len, P.out_cap};
+    if (kept) we.put(C, c, len, le, +1);
+    wover |= we.overflow;
+    widx += __popcll(kb);
+  } else {
+    if (kept) acc.put(C, c, len, le, +1);
+  }
+  // kept matches are disjoint and ordered: the last one ends last
+  const int ll = 63 - __builtin_clzll(kb);
+  const uint64_t e = c + len;
+  const uint32_t ehi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(e >> 32), ll);
+  const uint32_t elo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)e, ll);  // readlane is int: no sign extension
+  x = ((uint64_t)ehi << 32) | elo;
+}
+
+// Walk the deferred candidates (one per lane) and resolve them.  The tiles
+// they came from are gone from LDS, so each lane first copies the 32 bytes
+// from c & ~15 into its LDS window; longer walks continue from global memory.
+template <bool WRITE>
+__device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr, uint32_t dn, int lane, const Tab<0>& T,
+                                            const Ctx& C, const ScanParams& P, uint64_t& x, CountEm& acc,
+                                            uint64_t& widx, uint32_t& wover, uint32_t& ovf)
+{
+  wave_lds_sync();
+  const bool valid = (uint32_t)lane < dn;
+  const uint64_t c = valid ? dl[lane] : 0;
+  const uint64_t last16 = (P.rend - 1) & ~uint64_t(15);
+  const uint64_t a = c & ~uint64_t(15);
+  const uint4 v0 = load16(P.g, a, last16), v1 = load16(P.g, a + 16, last16);
+  wave_lds_sync();  // every lane has read its list entry before the windows overwrite it
+  *reinterpret_cast<uint4*>(scr + 32 * lane) = v0;
+  *reinterpret_cast<uint4*>(scr + 32 * lane + 16) = v1;
+  wave_lds_sync();
+  uint64_t len = 0;
+  uint32_t le = 0;
+  if (valid && P.ablate != 3) {
+    Win w;
+    w.lds = scr + 32 * lane;
+    w.base = a;
+    w.lend = a + 32;
+    w.g = P.g;
+    w.rend = P.rend;
+    w.eof = P.at_eof;
+    len = walk<0>(T, w, c, le, ovf);
+  }
+  resolve<WRITE>(valid, c, len, le, lane, C, P, x, acc, widx, wover);
+  wave_lds_sync();  // the aux region is reused
+}
+
+// State of one wave's FIND chain over its tile range.
+struct WaveChain {
+  uint64_t x;      // end of the last kept match (wave-uniform): the chain resumes there
+  uint32_t dn;     // deferred candidates in the list
+  uint64_t widx;   // next output slot (WRITE)
+  uint32_t wover;  // output capacity exceeded
+  uint32_t ovf;    // a walk ran past the read window
+  CountEm acc;
+};
+
+// Prefilter one 4 KiB wave-tile held in registers (v_k = chunk k: bytes
+// [ts + 1024k + 16*lane, +16)) and append its candidates, in position order
+// (chunk, then lane, then byte), to the deferred list; a full list (64, one
+// per lane) is walked and resolved by flush_deferred.
+template <bool WRITE>
+__device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3,
+                                          uint64_t ts, uint64_t wlo, uint64_t whi, int lane, const FTab& F,
+                                          const Tab<0>& T, const Ctx& C, const ScanParams& P, uint64_t* dl,
+                                          uint8_t* scr, WaveChain& w)
+{
+  if (P.ablate == 1) {  // benchmarking only: loads alone
+    w.acc.cnt += v0.x & 1;
+    return;
+  }
+  // the 4 bytes after chunk k of a lane are the next lane's first dword
+  // (DPP wave_shl:1), or lane 0's of chunk k+1 for lane 63; past the tile
+  // they are unknown and pass
+  const uint32_t h0 = bucket_bits(v0.x, F), h1 = bucket_bits(v1.x, F), h2 = bucket_bits(v2.x, F),
+                 h3 = bucket_bits(v3.x, F);
+  // (the DPP moves must run with every lane enabled -- a disabled source lane
+  // reads as 0 -- so they are computed unconditionally, then selected)
+  const uint32_t n0 = __builtin_amdgcn_update_dpp(0, h0, 0x130, 0xf, 0xf, false);
+  const uint32_t n1 = __builtin_amdgcn_update_dpp(0, h1, 0x130, 0xf, 0xf, false);
+  const uint32_t n2 = __builtin_amdgcn_update_dpp(0, h2, 0x130, 0xf, 0xf, false);
+  const uint32_t n3 = __builtin_amdgcn_update_dpp(0, h3, 0x130, 0xf, 0xf, false);
+  const uint32_t s1 = __builtin_amdgcn_readlane(h1, 0), s2 = __builtin_amdgcn_readlane(h2, 0),
+                 s3 = __builtin_amdgcn_readlane(h3, 0);
+  const bool l63 = lane == 63;
+  const uint32_t e0 = l63 ? s1 : n0, e1 = l63 ? s2 : n1, e2 = l63 ? s3 : n2, e3 = l63 ? 0x3f3f3f3fu : n3;
+  uint32_t X[4][4];
+  {
+    const uint32_t y = bucket_bits(v0.y, F), z = bucket_bits(v0.z, F), u = bucket_bits(v0.w, F);
+    X[0][0] = cand_flags(h0, y);
+    X[0][1] = cand_flags(y, z);
+    X[0][2] = cand_flags(z, u);
+    X[0][3] = cand_flags(u, e0);
+  }
+  {
+    const uint32_t y = bucket_bits(v1.y, F), z = bucket_bits(v1.z, F), u = bucket_bits(v1.w, F);
+    X[1][0] = cand_flags(h1, y);
+    X[1][1] = cand_flags(y, z);
+    X[1][2] = cand_flags(z, u);
+    X[1][3] = cand_flags(u, e1);
+  }
+  {
+    const uint32_t y = bucket_bits(v2.y, F), z = bucket_bits(v2.z, F), u = bucket_bits(v2.w, F);
+    X[2][0] = cand_flags(h2, y);
+    X[2][1] = cand_flags(y, z);
+    X[2][2] = cand_flags(z, u);
+    X[2][3] = cand_flags(u, e2);
+  }
+  {
+    const uint32_t y = bucket_bits(v3.y, F), z = bucket_bits(v3.z, F), u = bucket_bits(v3.w, F);
+    X[3][0] = cand_flags(h3, y);
+    X[3][1] = cand_flags(y, z);
+    X[3][2] = cand_flags(z, u);
+    X[3][3] = cand_flags(u, e3);
+  }
+  const bool edge = ts < wlo || ts + kWaveTile > whi;  // first/last tile: clip to [wlo, whi)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (!__ballot((X[k][0] | X[k][1] | X[k][2] | X[k][3]) != 0)) continue;  // the common case
+    uint32_t mk = flags4(X[k][0]) | (flags4(X[k][1]) << 4) | (flags4(X[k][2]) << 8) | (flags4(X[k][3]) << 12);
+    const uint64_t p0 = ts + 1024u * k + 16u * lane;
+    if (edge) {
+      const uint64_t a = wlo > p0 ? (wlo - p0 > 16 ? 16 : wlo - p0) : 0;
+      const uint64_t z = whi > p0 ? (whi - p0 > 16 ? 16 : whi - p0) : 0;
+      mk &= (uint32_t)((lowbits(z) & ~lowbits(a)) & 0xffffu);
+    }
+    if (P.ablate == 2) {  // benchmarking only: loads + prefilter
+      w.acc.cnt += __popc(mk);
+      continue;
+    }
+    // rank this chunk's candidates by a DPP scan of the per-lane counts
+    const uint32_t cnt = __popc(mk);
+    const uint32_t incl = dpp_scan_add(cnt);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+    const uint32_t rank = incl - cnt;
+    for (uint32_t done = 0; done < tot;) {
+      if (w.dn == (uint32_t)kDefer) {
+        flush_deferred<WRITE>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
+        w.dn = 0;
+      }
+      const uint32_t take = tot - done < kDefer - w.dn ? tot - done : kDefer - w.dn;
+      uint32_t m = mk, r = rank;
+      while (m) {
+        const uint32_t bit = __builtin_ctz(m);
+        m &= m - 1;
+        if (r - done < take) dl[w.dn + r - done] = p0 + bit;
+        ++r;
+      }
+      w.dn += take;
+      done += take;
+    }
+  }
+}
+
 }  // namespace
 
 template <bool WRITE>
@@ -120,9 +306,12 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar control flow
-  uint8_t* wt = smem + wid * kWaveTile;
-  uint16_t* cl = reinterpret_cast<uint16_t*>(smem + kSpWaves * kWaveTile) + wid * kCandCap;
-  uint16_t* ltrans = reinterpret_cast<uint16_t*>(smem + kSpWaves * (kWaveTile + 2 * kCandCap));
+  // per-wave aux region, time-multiplexed: the deferred candidate list (u64)
+  // and, while it is walked, the walk windows (32 B per lane)
+  uint8_t* aux = smem + wid * kAux;
+  uint64_t* dl = reinterpret_cast<uint64_t*>(aux);
+  uint8_t* scr = aux;
+  uint16_t* ltrans = reinterpret_cast<uint16_t*>(smem + kSpWaves * kAux);
   uint32_t* lcaps = reinterpret_cast<uint32_t*>(ltrans + P.ntrans_pad);
   {
     const uint4* src = reinterpret_cast<const uint4*>(P.trans);
@@ -141,191 +330,59 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
   if (tb > te) tb = te;
   const uint64_t wlo = clampu(tb * kWaveTile, P.lo, P.hi);
   const uint64_t whi = clampu(te * kWaveTile, P.lo, P.hi);
-  uint64_t x = WRITE ? P.entries[gw] : wlo;  // chain position (wave-uniform)
+  WaveChain w;
+  w.x = WRITE ? P.entries[gw] : wlo;
+  w.dn = 0;
+  w.widx = WRITE ? P.out_base[gw] : 0;
+  w.wover = 0;
+  w.ovf = 0;
 
-  Win w;
-  w.lds = wt;
-  w.g = P.g;
-  w.rend = P.rend;
-  w.eof = P.at_eof;
-  uint32_t ovf = 0, wover = 0;
-  CountEm acc;
-  uint64_t widx = WRITE ? P.out_base[gw] : 0;
-
-  // 1. each tile arrives by coalesced 16 B/lane loads one tile ahead in
-  //    registers; the current tile is stored to the wave's LDS slice, which the
-  //    prefilter and the walks read.
+  // Tiles arrive by coalesced 16 B/lane loads into two register sets used in
+  // turn (a* = tile t, b* = tile t+1): the load of the next tile is in flight
+  // while the current one is filtered, with no register copies between
+  // iterations.  (Unconditional loads into named registers: a conditionally
+  // written array was demoted to scratch by hipcc.)
   const uint64_t last16 = (P.rend - 1) & ~uint64_t(15);  // clamp: bytes >= rend are never consulted
-  // (unconditional loads into named registers: a conditionally written array
-  // captured by a lambda was demoted to scratch by hipcc)
-  // Two tiles in flight per wave (r* = tile t+1, q* = tile t+2 at the top of
-  // iteration t): 24 waves x 8 KiB per CU cover the loaded HBM latency.
-  uint4 r0, r1, r2, r3, q0, q1, q2, q3;
+  uint4 a0, a1, a2, a3, b0, b1, b2, b3;
   {
     const uint64_t p = (tb < te ? tb : 0) * kWaveTile + 16u * lane;
-    r0 = load16(P.g, p, last16);
-    r1 = load16(P.g, p + 1024, last16);
-    r2 = load16(P.g, p + 2048, last16);
-    r3 = load16(P.g, p + 3072, last16);
+    a0 = load16(P.g, p, last16);
+    a1 = load16(P.g, p + 1024, last16);
+    a2 = load16(P.g, p + 2048, last16);
+    a3 = load16(P.g, p + 3072, last16);
     const uint64_t p2 = (tb + 1 < te ? tb + 1 : tb) * kWaveTile + 16u * lane;
-    q0 = load16(P.g, p2, last16);
-    q1 = load16(P.g, p2 + 1024, last16);
-    q2 = load16(P.g, p2 + 2048, last16);
-    q3 = load16(P.g, p2 + 3072, last16);
+    b0 = load16(P.g, p2, last16);
+    b1 = load16(P.g, p2 + 1024, last16);
+    b2 = load16(P.g, p2 + 2048, last16);
+    b3 = load16(P.g, p2 + 3072, last16);
   }
-  for (uint64_t t = tb; t < te; ++t) {
-    const uint64_t ts = t * kWaveTile;
-    *reinterpret_cast<uint4*>(wt + 16 * lane) = r0;
-    *reinterpret_cast<uint4*>(wt + 1024 + 16 * lane) = r1;
-    *reinterpret_cast<uint4*>(wt + 2048 + 16 * lane) = r2;
-    *reinterpret_cast<uint4*>(wt + 3072 + 16 * lane) = r3;
-    w.base = ts;
-    w.lend = ts + kWaveTile;
-
-    // 2. prefilter on the registers: chunk k of this lane = bytes
-    //    [1024k + 16l, +16); the 4 bytes after it are the next lane's first
-    //    dword (DPP wave_shl:1), or lane 0's of chunk k+1 for lane 63.
-    uint32_t m[4];
-    if (P.ablate != 1) {
-      const uint32_t h0 = bucket_bits(r0.x, F), h1 = bucket_bits(r1.x, F), h2 = bucket_bits(r2.x, F),
-                     h3 = bucket_bits(r3.x, F);
-      const uint32_t n0 = __builtin_amdgcn_update_dpp(0, h0, 0x130, 0xf, 0xf, false);
-      const uint32_t n1 = __builtin_amdgcn_update_dpp(0, h1, 0x130, 0xf, 0xf, false);
-      const uint32_t n2 = __builtin_amdgcn_update_dpp(0, h2, 0x130, 0xf, 0xf, false);
-      const uint32_t n3 = __builtin_amdgcn_update_dpp(0, h3, 0x130, 0xf, 0xf, false);
-      const bool l63 = lane == 63;
-      const uint32_t R0[5] = {h0, bucket_bits(r0.y, F), bucket_bits(r0.z, F), bucket_bits(r0.w, F),
-                              l63 ? (uint32_t)__builtin_amdgcn_readlane(h1, 0) : n0};
-      m[0] = chunk_mask(R0);
-      const uint32_t R1[5] = {h1, bucket_bits(r1.y, F), bucket_bits(r1.z, F), bucket_bits(r1.w, F),
-                              l63 ? (uint32_t)__builtin_amdgcn_readlane(h2, 0) : n1};
-      m[1] = chunk_mask(R1);
-      const uint32_t R2[5] = {h2, bucket_bits(r2.y, F), bucket_bits(r2.z, F), bucket_bits(r2.w, F),
-                              l63 ? (uint32_t)__builtin_amdgcn_readlane(h3, 0) : n2};
-      m[2] = chunk_mask(R2);
-      const uint32_t R3[5] = {h3, bucket_bits(r3.y, F), bucket_bits(r3.z, F), bucket_bits(r3.w, F),
-                              l63 ? 0xffffffffu : n3};  // bytes past the wave-tile: unknown, pass
-      m[3] = chunk_mask(R3);
-    }
-    r0 = q0;
-    r1 = q1;
-    r2 = q2;
-    r3 = q3;
+  for (uint64_t t = tb; t < te; t += 2) {
+    tile_pass<WRITE>(a0, a1, a2, a3, t * kWaveTile, wlo, whi, lane, F, T, C, P, dl, scr, w);
     {
       const uint64_t p = (t + 2 < te ? t + 2 : t) * kWaveTile + 16u * lane;  // tail: harmless re-read
-      q0 = load16(P.g, p, last16);
-      q1 = load16(P.g, p + 1024, last16);
-      q2 = load16(P.g, p + 2048, last16);
-      q3 = load16(P.g, p + 3072, last16);
+      a0 = load16(P.g, p, last16);
+      a1 = load16(P.g, p + 1024, last16);
+      a2 = load16(P.g, p + 2048, last16);
+      a3 = load16(P.g, p + 3072, last16);
     }
-    wave_lds_sync();
-    if (P.ablate == 1) {  // benchmarking only: staging alone
-      acc.cnt += wt[lane];
-      x = ts + kWaveTile < whi ? ts + kWaveTile : whi;
-      wave_lds_sync();
-      continue;
+    if (t + 1 >= te) break;
+    tile_pass<WRITE>(b0, b1, b2, b3, (t + 1) * kWaveTile, wlo, whi, lane, F, T, C, P, dl, scr, w);
+    {
+      const uint64_t p = (t + 3 < te ? t + 3 : t + 1) * kWaveTile + 16u * lane;
+      b0 = load16(P.g, p, last16);
+      b1 = load16(P.g, p + 1024, last16);
+      b2 = load16(P.g, p + 2048, last16);
+      b3 = load16(P.g, p + 3072, last16);
     }
-    if (ts < wlo || ts + kWaveTile > whi) {  // first/last tile: clip to [wlo, whi)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint64_t p0 = ts + 1024u * k + 16u * lane;
-        const uint64_t a = wlo > p0 ? (wlo - p0 > 16 ? 16 : wlo - p0) : 0;
-        const uint64_t z = whi > p0 ? (whi - p0 > 16 ? 16 : whi - p0) : 0;
-        m[k] &= (uint32_t)((lowbits(z) & ~lowbits(a)) & 0xffffu);
-      }
-    }
-
-    if (P.ablate == 2) {  // benchmarking only: staging + prefilter
-      acc.cnt += __popc(m[0] | m[1] | m[2] | m[3]);
-      x = ts + kWaveTile < whi ? ts + kWaveTile : whi;
-      wave_lds_sync();
-      continue;
-    }
-    if (__ballot((m[0] | m[1] | m[2] | m[3]) != 0)) {
-      // 3. compact candidates in position order (k-major, then lane, then byte):
-      //    two packed DPP scans of the per-chunk counts (16-bit fields)
-      const uint32_t c01 = __popc(m[0]) | (__popc(m[1]) << 16), c23 = __popc(m[2]) | (__popc(m[3]) << 16);
-      const uint32_t i01 = dpp_scan_add(c01), i23 = dpp_scan_add(c23);
-      const uint32_t t01 = __builtin_amdgcn_readlane(i01, 63), t23 = __builtin_amdgcn_readlane(i23, 63);
-      const uint32_t e01 = i01 - c01, e23 = i23 - c23;
-      const uint32_t tot0 = t01 & 0xffffu, tot1 = t01 >> 16, tot2 = t23 & 0xffffu, tot3 = t23 >> 16;
-      const uint32_t base[4] = {e01 & 0xffffu, tot0 + (e01 >> 16), tot0 + tot1 + (e23 & 0xffffu),
-                                tot0 + tot1 + tot2 + (e23 >> 16)};
-      const uint32_t ncand = tot0 + tot1 + tot2 + tot3;
-      for (uint32_t win = 0; win < ncand; win += kCandCap) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          uint32_t mk = m[k], rank = base[k];
-          while (mk) {
-            const uint32_t bit = __builtin_ctz(mk);
-            mk &= mk - 1;
-            if (rank - win < (uint32_t)kCandCap) cl[rank - win] = (uint16_t)(1024 * k + 16 * lane + bit);
-            ++rank;
-          }
-        }
-        wave_lds_sync();
-        const uint32_t nwin = ncand - win < (uint32_t)kCandCap ? ncand - win : (uint32_t)kCandCap;
-        // 4. walk up to 64 candidates at once, then apply the greedy chain rule
-        for (uint32_t i0 = 0; i0 < nwin; i0 += 64) {
-          const uint32_t j = i0 + lane;
-          uint32_t coff = 0, le = 0;
-          uint64_t len = 0;
-          if (j < nwin) {
-            coff = cl[j];
-            if (P.ablate != 3) len = walk<0>(T, w, ts + coff, le, ovf);  // 3: benchmarking, no walks
-          }
-          const uint64_t c = ts + coff;
-          const bool vm = len != 0 && c >= x;
-          // match ends relative to the tile start (clamped; only order matters)
-          const uint64_t endr = c + len - ts;
-          const uint32_t er = vm ? (endr > 0xffffffffull ? 0xffffffffu : (uint32_t)endr) : 0u;
-          const uint32_t xr = x > ts ? (x - ts > 0xffffffffull ? 0xffffffffu : (uint32_t)(x - ts)) : 0u;
-          const uint32_t pm = umax32(dpp_prev_lane(dpp_scan_max(er)), xr);
-          bool kept = vm && coff >= pm;
-          if (__ballot(vm && coff < pm)) {
-            // overlapping candidate matches: exact sequential greedy pass
-            uint64_t xx = x;
-            kept = false;
-            for (int i = 0; i < 64; ++i) {
-              const uint64_t ci = __shfl(c, i, 64);
-              const uint64_t ei = __shfl(vm ? c + len : 0ull, i, 64);
-              if (ei != 0 && ci >= xx) {
-                if (lane == i) kept = true;
-                xx = ei;
-              }
-            }
-          }
-          const uint64_t kb = __ballot(kept);
-          if (kb) {
-            if constexpr (WRITE) {
-              WriteEm we{widx + lanes_below(kb), P.out_capacity, P.out_start, P.out_len, P.out_cap};
-              if (kept) we.put(C, c, len, le, +1);
-              wover |= we.overflow;
-              widx += __popcll(kb);
-            } else {
-              if (kept) acc.put(C, c, len, le, +1);
-            }
-            // kept matches are disjoint and ordered: the last one ends last
-            const int ll = 63 - __builtin_clzll(kb);
-            const uint64_t e = c + len;
-            const uint32_t ehi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(e >> 32), ll);
-            const uint32_t elo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)e, ll);  // readlane is int: no sign extension
-            x = ((uint64_t)ehi << 32) | elo;
-          }
-        }
-        wave_lds_sync();  // the list is rewritten by the next window
-      }
-    }
-    const uint64_t tend = ts + kWaveTile < whi ? ts + kWaveTile : whi;
-    x = x > tend ? x : tend;
-    wave_lds_sync();  // reads of this tile precede the next tile's stores
   }
+  if (w.dn) flush_deferred<WRITE>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
+  uint64_t x = w.x > whi ? w.x : whi;  // chain exit: the last kept match end or the range end
   if (tb == te) x = wlo;
 
-  if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
-  if (wover) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+  if (w.ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
+  if (w.wover) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
   if constexpr (!WRITE) {
-    const uint64_t c = wave_sum(acc.cnt), d = wave_sum(acc.dg), dc = wave_sum(acc.dc);
+    const uint64_t c = wave_sum(w.acc.cnt), d = wave_sum(w.acc.dg), dc = wave_sum(w.acc.dc);
     if (lane == 0) {
       BlockRec rec;
       rec.entry = wlo;
@@ -342,7 +399,7 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
 // ---------------------------------------------------------------- launchers
 size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates)
 {
-  size_t b = (size_t)kSpWaves * (kWaveTile + 2 * kCandCap) + 2 * (size_t)ntrans_pad + 4 * (size_t)nstates;
+  size_t b = (size_t)kSpWaves * kAux + 2 * (size_t)ntrans_pad + 4 * (size_t)nstates;
   return (b + 15) & ~size_t(15);
 }
 

@@ -43,47 +43,76 @@ struct Bucket {
     hi |= (uint8_t)(1u << (b >> 6));
   }
   bool has(int b) const { return (lo >> (b & 7) & 1) && (mid >> ((b >> 3) & 7) & 1) && (hi >> (b >> 6) & 1); }
+  static Bucket all()
+  {
+    Bucket x;
+    x.lo = x.mid = 0xff;
+    x.hi = 0x0f;
+    return x;
+  }
+  Bucket& operator|=(const Bucket& o)
+  {
+    lo |= o.lo;
+    mid |= o.mid;
+    hi |= o.hi;
+    return *this;
+  }
+  // fraction of text bytes (printable ASCII and '\n') in the approximation
+  double text_frac() const
+  {
+    int n = has('\n') ? 1 : 0;
+    for (int b = 0x20; b < 0x7f; ++b) n += has(b) ? 1 : 0;
+    return n / 96.0;
+  }
 };
 
-// Split a byte set over two buckets minimising the union of their
-// approximations (exhaustive for small sets, greedy otherwise).
-void split_set(const bool in[256], Bucket& b1, Bucket& b2)
+// First bytes of a term group with the bytes that may follow them.
+struct Lead {
+  Bucket b, c, d;
+  Lead& operator|=(const Lead& o)
+  {
+    b |= o.b;
+    c |= o.c;
+    d |= o.d;
+    return *this;
+  }
+  double density() const { return b.text_frac() * c.text_frac() * d.text_frac(); }
+};
+
+// Partition the leads (one per first byte) into the two prefilter groups,
+// minimising the summed candidate density of the group approximations:
+// exhaustive up to 14 leads, greedy beyond.  Returns that density (<= 1).
+double group_leads(const std::vector<Lead>& leads, Lead (&g)[2])
 {
-  std::vector<int> mem;
-  for (int b = 0; b < 256; ++b)
-    if (in[b]) mem.push_back(b);
-  b1 = Bucket();
-  b2 = Bucket();
-  if (mem.empty()) return;
-  auto cost = [](const Bucket& x, const Bucket& y) {
-    int n = 0;
-    for (int b = 0; b < 256; ++b) n += (x.has(b) || y.has(b)) ? 1 : 0;
-    return n;
-  };
-  if (mem.size() <= 12) {
-    int best = 1 << 30;
-    const uint32_t lim = 1u << (mem.size() - 1);
-    for (uint32_t m = 0; m < lim; ++m) {  // member 0 always in bucket 1
-      Bucket x, y;
-      for (size_t i = 0; i < mem.size(); ++i) ((i > 0 && (m >> (i - 1) & 1)) ? y : x).add(mem[i]);
-      const int c = cost(x, y);
+  g[0] = Lead();
+  g[1] = Lead();
+  const size_t n = leads.size();
+  double best = 2.0;
+  if (n <= 14) {
+    const uint32_t lim = n ? 1u << (n - 1) : 1u;
+    for (uint32_t m = 0; m < lim; ++m) {  // lead 0 always in group 0
+      Lead x, y;
+      for (size_t i = 0; i < n; ++i) ((i > 0 && (m >> (i - 1) & 1)) ? y : x) |= leads[i];
+      const double c = x.density() + y.density();
       if (c < best) {
         best = c;
-        b1 = x;
-        b2 = y;
+        g[0] = x;
+        g[1] = y;
       }
     }
-    return;
+  } else {
+    for (const Lead& l : leads) {
+      Lead x = g[0], y = g[1];
+      x |= l;
+      y |= l;
+      if (x.density() + g[1].density() <= g[0].density() + y.density())
+        g[0] = x;
+      else
+        g[1] = y;
+    }
+    best = g[0].density() + g[1].density();
   }
-  for (int b : mem) {
-    Bucket x = b1, y = b2;
-    x.add(b);
-    y.add(b);
-    if (cost(x, b2) <= cost(b1, y))
-      b1 = x;
-    else
-      b2 = y;
-  }
+  return n ? (best < 1.0 ? best : 1.0) : 0.0;
 }
 
 }  // namespace
@@ -239,61 +268,49 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   t.start = start_sid * R;
   t.accepting = S - first_acc;
   t.accb = (t.accepting > 0) ? first_acc * R : 0x10000u;
-  // prefilter sets (see tables.hpp): A = first bytes that complete a match,
-  // B = other first bytes, C = bytes that can follow a byte of B, D = bytes
-  // that can follow such a pair; short2 = some 2-byte prefix already accepts
-  bool setA[256] = {}, setB[256] = {}, setC[256] = {}, setD[256] = {};
-  bool short2 = false;
-  uint32_t nf = 0;
+  // prefilter (see tables.hpp): per first byte c, the bytes that can follow
+  // it (second) and follow those (third); "all" once a prefix accepts
+  std::vector<Lead> leads;
   for (int c = 0; c < 256; ++c) {
     const uint32_t s1 = nxt[(size_t)start_sid * 256 + c];
     if (s1 == 0) continue;
-    ++nf;
-    if (s1 >= first_acc) {
-      setA[c] = true;
+    Lead l;
+    l.b.add(c);
+    if (s1 >= first_acc) {  // 1-byte match: no follow-up test
+      l.c = Bucket::all();
+      l.d = Bucket::all();
+      leads.push_back(l);
       continue;
     }
-    setB[c] = true;
+    bool short2 = false;
     for (int d = 0; d < 256; ++d) {
       const uint32_t s2 = nxt[(size_t)s1 * 256 + d];
       if (s2 == 0) continue;
-      setC[d] = true;
+      l.c.add(d);
       if (s2 >= first_acc) short2 = true;
       for (int e = 0; e < 256; ++e)
-        if (nxt[(size_t)s2 * 256 + e] != 0) setD[e] = true;
+        if (nxt[(size_t)s2 * 256 + e] != 0) l.d.add(e);
+    }
+    if (short2) l.d = Bucket::all();  // a match may end after 2 bytes
+    leads.push_back(l);
+  }
+  t.first_bytes = (uint32_t)leads.size();
+  Lead g[2];
+  t.fdensity = group_leads(leads, g);
+  for (int k = 0; k < 2; ++k) {
+    const Bucket* bk[3] = {&g[k].b, &g[k].c, &g[k].d};
+    for (int s = 0; s < 3; ++s) {
+      const uint8_t bit = (uint8_t)(1u << (2 * s + k));
+      for (int v = 0; v < 8; ++v) {
+        if (bk[s]->lo >> v & 1) t.ft[v] |= bit;
+        if (bk[s]->mid >> v & 1) t.ft[8 + v] |= bit;
+      }
+      for (int v = 0; v < 4; ++v)
+        if (bk[s]->hi >> v & 1) t.ft[16 + v] |= bit;
     }
   }
-  t.first_bytes = nf;
-  Bucket a1, a2, b1, b2, c1, c2, d1, d2;
-  split_set(setA, a1, a2);
-  a1 = Bucket();  // A uses one bucket (bit 0): merge both halves
-  for (int c = 0; c < 256; ++c)
-    if (setA[c]) a1.add(c);
-  split_set(setB, b1, b2);
-  split_set(setC, c1, c2);
-  if (short2) {  // a match may end after 2 bytes: no third-byte test
-    for (int c = 0; c < 256; ++c) setD[c] = true;
-  }
-  split_set(setD, d1, d2);
-  const Bucket* bk[7] = {&a1, &b1, &b2, &c1, &c2, &d1, &d2};
-  for (int bit = 0; bit < 7; ++bit) {
-    for (int v = 0; v < 8; ++v) {
-      if (bk[bit]->lo >> v & 1) t.ft[v] |= (uint8_t)(1u << bit);
-      if (bk[bit]->mid >> v & 1) t.ft[8 + v] |= (uint8_t)(1u << bit);
-    }
-    for (int v = 0; v < 4; ++v)
-      if (bk[bit]->hi >> v & 1) t.ft[16 + v] |= (uint8_t)(1u << bit);
-  }
-  // candidate density on printable ASCII + newline, assuming independent bytes
-  auto frac = [](const Bucket& x, const Bucket& y) {
-    int n = 0;
-    for (int b = 0x20; b < 0x7f; ++b) n += (x.has(b) || y.has(b)) ? 1 : 0;
-    return n / 95.0;
-  };
-  const double pa = frac(a1, a1), pb = frac(b1, b2), pc = frac(c1, c2), pd = frac(d1, d2);
-  t.fdensity = pa + (1.0 - pa) * pb * pc * pd;
   // the sparse kernel pays off when few positions survive the prefilter
-  t.filter = t.format == FMT_BYTE && nf > 0 && t.fdensity <= 0.15;
+  t.filter = t.format == FMT_BYTE && !leads.empty() && t.fdensity <= 0.15;
   out = std::move(t);
   return 0;
 }

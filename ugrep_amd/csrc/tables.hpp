@@ -31,14 +31,15 @@ struct DfaTables {
   uint32_t accb = 0;     // first accepting entry (A * R)
   uint32_t accepting = 0;
   // Candidate prefilter (replaces the reference's needle/pin prefilters,
-  // lib/matcher_avx2.cpp:303-799): a position p can start a match only if
-  //   B[p] in A (a 1-byte match)  or  B[p] in B and B[p+1] in C and B[p+2] in D
-  // (C / D = all bytes when a match may end earlier).  The sets are tested
-  // together by three byte-table lookups on the 3-bit fields of a byte
-  // (v_perm_b32 on the GPU): R(b) = T0[b & 7] & T1[(b >> 3) & 7] & T2[b >> 6],
-  // with one bit per bucket: A = bit 0, B = bits 1|2, C = bits 3|4, D = bits
-  // 5|6.  Each bucket over-approximates its members (a superset is safe); each
-  // set is split over two buckets to limit aliasing.
+  // lib/matcher_avx2.cpp:303-799): the first bytes of the pattern are split
+  // into two groups g; a position p can start a match only if for some g
+  //   B[p] in B_g  and  B[p+1] in C_g  and  B[p+2] in D_g
+  // (B_g = the group's first bytes, C_g / D_g = the bytes that may follow;
+  // all bytes once a prefix accepts).  All six sets are tested at once by
+  // three byte-table lookups on the 3-bit fields of a byte (v_perm_b32 on the
+  // GPU): R(b) = T0[b & 7] & T1[(b >> 3) & 7] & T2[b >> 6], with B_g = bit g,
+  // C_g = bit 2+g, D_g = bit 4+g (bits 6, 7 stay 0).  Each set's
+  // approximation is a superset of it (safe: it only adds candidates).
   bool filter = false;       // false: dense pattern, no prefilter
   uint8_t ft[20] = {};       // T0[8], T1[8], T2[4]
   double fdensity = 1.0;     // estimated candidate fraction on printable ASCII
