@@ -7,7 +7,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libugrep_amd.so")
+# UGPU_LIB selects an in-tree build variant (benchmarking experiments only)
+LIB_PATH = os.path.join(HERE, os.path.basename(os.environ.get("UGPU_LIB", "libugrep_amd.so")))
 HEADER = os.path.join(os.path.dirname(HERE), "include", "ugpu.h")
 
 UGPU_OK = 0
