@@ -87,6 +87,20 @@ def cpu_baseline(cfg, sample, threads):
                 sample="%d MiB, oracle restatement (dense-table walker), %d threads" % (sample >> 20, threads))
 
 
+def measured_traffic(cfg, nbytes):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    PMC summary (profiles/traffic.json, written from tools/profile.sh runs:
+    FETCH_SIZE x 1024 x 2 on gfx950), when it was taken on this config and size."""
+    try:
+        with open(os.path.join(REPO, "profiles", "traffic.json")) as f:
+            t = json.load(f).get(cfg)
+    except (OSError, ValueError):
+        return None
+    if not t or t.get("algorithmic_bytes_per_launch") != nbytes:
+        return None
+    return t
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -191,10 +205,15 @@ def main():
         "matches": res["count"],
         "matches_per_s": round(matches_per_s, 1),
         "digest": res["digest"],
-        "roofline": {"bound": "hbm", "kernel": "scan_kernel", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "sparse_kernel" if info["prefilter_ppm"] else "scan_kernel",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel_ms": round(k_avg, 4), "algorithmic_bytes_per_launch": hi - lo},
     }
+    tr = measured_traffic(args.config, hi - lo)
+    if tr:
+        out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+        out["roofline"]["traffic_source"] = tr["source"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, len(os.sched_getaffinity(0)))
         sample = min(args.cpu_sample_mib << 20, per_gpu)

@@ -95,12 +95,21 @@ __device__ __forceinline__ uint4 load16(const uint8_t* g, uint64_t pos, uint64_t
   return *reinterpret_cast<const uint4*>(g + (pos < last16 ? pos : last16));
 }
 
-// Streaming tile loads: each byte is read once from HBM, so the loads carry
-// the non-temporal hint (global_load ... nt): C2 16 GiB 2.93 -> 2.71 ms.
-__device__ __forceinline__ uint4 stream16(const uint8_t* g, uint64_t pos, uint64_t last16)
+// Streaming tile loads.  Each byte is read once from HBM, so the loads carry
+// the non-temporal hint (C2 16 GiB 2.93 -> 2.71 ms).  They go through a
+// per-tile buffer resource (scalar base = tile start, num_records = readable
+// bytes of the tile rounded up to 16): lane offsets are loop-invariant, there
+// is no 64-bit address or clamp arithmetic per load, and 16-byte granules
+// wholly past the readable end read as 0 (positions there are clipped, and a
+// zero byte only ever fails or passes a prefilter test -- see tile_pass).
+struct TileLoad {
+  __amdgpu_buffer_rsrc_t rs;
+};
+
+__device__ __forceinline__ uint4 stream16(const TileLoad& L, uint32_t off)
 {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(g + (pos < last16 ? pos : last16)));
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(L.rs, (int)off, 0, 2 /* nt */);
   return uint4{v.x, v.y, v.z, v.w};
 }
 
@@ -166,10 +175,10 @@ __device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, ui
   x = ((uint64_t)ehi << 32) | elo;
 }
 
-// Walk the deferred candidates (one per lane) and resolve them.  The tiles
-// they came from are gone from LDS, so each lane first copies the 32 bytes
-// from c & ~15 into its LDS window; longer walks continue from global memory.
-template <bool WRITE>
+// Walk the deferred candidates (one per lane) and resolve them.  Each lane
+// copies the 32 bytes from c & ~15 into its LDS window (the tiles are gone
+// from registers); longer walks continue from global memory.
+template <bool WRITE, int ABL>
 __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr, uint32_t dn, int lane, const Tab<0>& T,
                                             const Ctx& C, const ScanParams& P, uint64_t& x, CountEm& acc,
                                             uint64_t& widx, uint32_t& wover, uint32_t& ovf)
@@ -186,7 +195,7 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
   wave_lds_sync();
   uint64_t len = 0;
   uint32_t le = 0;
-  if (valid && P.ablate != 3) {
+  if (valid && ABL != 3) {
     Win w;
     w.lds = scr + 32 * lane;
     w.base = a;
@@ -213,15 +222,18 @@ struct WaveChain {
 // Prefilter one 4 KiB wave-tile held in registers (v_k = chunk k: bytes
 // [ts + 1024k + 16*lane, +16)) and append its candidates, in position order
 // (chunk, then lane, then byte), to the deferred list; a full list (64, one
-// per lane) is walked and resolved by flush_deferred.
-template <bool WRITE>
+// per lane) is walked and resolved by flush_deferred.  edge: the tile is cut
+// by the wave's range [wlo, whi).
+// ABL (benchmarking only; results are not matches): 1 loads alone, 2 loads +
+// prefilter, 3 everything but the walks.
+template <bool WRITE, int ABL>
 __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3,
-                                          uint64_t ts, uint64_t wlo, uint64_t whi, int lane, const FTab& F,
-                                          const Tab<0>& T, const Ctx& C, const ScanParams& P, uint64_t* dl,
-                                          uint8_t* scr, WaveChain& w)
+                                          uint64_t ts, bool edge, uint64_t wlo, uint64_t whi, int lane,
+                                          const FTab& F, const Tab<0>& T, const Ctx& C, const ScanParams& P,
+                                          uint64_t* dl, uint8_t* scr, WaveChain& w)
 {
-  if (P.ablate == 1) {  // benchmarking only: loads alone
-    w.acc.cnt += v0.x & 1;
+  if constexpr (ABL == 1) {
+    w.acc.cnt += (v0.x ^ v1.y ^ v2.z ^ v3.w) & 1;
     return;
   }
   // the 4 bytes after chunk k of a lane are the next lane's first dword
@@ -268,10 +280,13 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
     X[3][2] = cand_flags(z, u);
     X[3][3] = cand_flags(u, e3);
   }
-  const bool edge = ts < wlo || ts + kWaveTile > whi;  // first/last tile: clip to [wlo, whi)
+  const uint32_t any0 = X[0][0] | X[0][1] | X[0][2] | X[0][3], any1 = X[1][0] | X[1][1] | X[1][2] | X[1][3];
+  const uint32_t any2 = X[2][0] | X[2][1] | X[2][2] | X[2][3], any3 = X[3][0] | X[3][1] | X[3][2] | X[3][3];
+  if (!__ballot((any0 | any1 | any2 | any3) != 0)) return;  // the common case: no candidate in the tile
+  const uint32_t anyk[4] = {any0, any1, any2, any3};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    if (!__ballot((X[k][0] | X[k][1] | X[k][2] | X[k][3]) != 0)) continue;  // the common case
+    if (!__ballot(anyk[k] != 0)) continue;
     uint32_t mk = flags4(X[k][0]) | (flags4(X[k][1]) << 4) | (flags4(X[k][2]) << 8) | (flags4(X[k][3]) << 12);
     const uint64_t p0 = ts + 1024u * k + 16u * lane;
     if (edge) {
@@ -279,7 +294,7 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
       const uint64_t z = whi > p0 ? (whi - p0 > 16 ? 16 : whi - p0) : 0;
       mk &= (uint32_t)((lowbits(z) & ~lowbits(a)) & 0xffffu);
     }
-    if (P.ablate == 2) {  // benchmarking only: loads + prefilter
+    if constexpr (ABL == 2) {
       w.acc.cnt += __popc(mk);
       continue;
     }
@@ -290,7 +305,7 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
     const uint32_t rank = incl - cnt;
     for (uint32_t done = 0; done < tot;) {
       if (w.dn == (uint32_t)kDefer) {
-        flush_deferred<WRITE>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
+        flush_deferred<WRITE, ABL>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
         w.dn = 0;
       }
       const uint32_t take = tot - done < kDefer - w.dn ? tot - done : kDefer - w.dn;
@@ -307,9 +322,21 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
   }
 }
 
+// Buffer resource of tile i of a wave (base = the wave's first tile, rel =
+// readable bytes from there rounded up to 16, < 2^32).
+__device__ __forceinline__ TileLoad wave_tile(const uint8_t* wbase, uint32_t i, uint32_t rel)
+{
+  const uint32_t off = i * (uint32_t)kWaveTile;
+  const uint32_t n = rel > off ? rel - off : 0u;
+  // readfirstlane: the value is uniform, but without it hipcc computes it on
+  // the VALU and wraps every load in a waterfall loop
+  const int nr = __builtin_amdgcn_readfirstlane((int)(n < (uint32_t)kWaveTile ? n : (uint32_t)kWaveTile));
+  return TileLoad{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(wbase + off), (short)0, nr, 0x00020000)};
+}
+
 }  // namespace
 
-template <bool WRITE>
+template <bool WRITE, int ABL>
 __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -347,44 +374,60 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
   w.ovf = 0;
 
   // Tiles arrive by coalesced 16 B/lane loads into two register sets used in
-  // turn (a* = tile t, b* = tile t+1): the load of the next tile is in flight
+  // turn (a* = tile i, b* = tile i+1): the load of the next tile is in flight
   // while the current one is filtered, with no register copies between
-  // iterations.  (Unconditional loads into named registers: a conditionally
-  // written array was demoted to scratch by hipcc.)
-  const uint64_t last16 = (P.rend - 1) & ~uint64_t(15);  // clamp: bytes >= rend are never consulted
+  // iterations.  All loop control is 32-bit scalar (tile index i < n, the
+  // engine keeps n * 4 KiB < 4 GiB); past n the resource is empty (no access).
+  const uint32_t n = (uint32_t)(te - tb);
+  const uint8_t* wbase = P.g + tb * kWaveTile;
+  const uint64_t rend16 = (P.rend + 15) & ~uint64_t(15), wb = tb * kWaveTile;
+  const uint64_t relw = rend16 > wb ? rend16 - wb : 0;
+  const uint32_t rel = (uint32_t)(relw < (uint64_t)n * kWaveTile ? relw : (uint64_t)n * kWaveTile);
+  const bool clip_lo = wlo != wb, clip_hi = whi != te * kWaveTile;
+  const uint32_t lo16 = 16u * lane;
   uint4 a0, a1, a2, a3, b0, b1, b2, b3;
   {
-    const uint64_t p = (tb < te ? tb : 0) * kWaveTile + 16u * lane;
-    a0 = stream16(P.g, p, last16);
-    a1 = stream16(P.g, p + 1024, last16);
-    a2 = stream16(P.g, p + 2048, last16);
-    a3 = stream16(P.g, p + 3072, last16);
-    const uint64_t p2 = (tb + 1 < te ? tb + 1 : tb) * kWaveTile + 16u * lane;
-    b0 = stream16(P.g, p2, last16);
-    b1 = stream16(P.g, p2 + 1024, last16);
-    b2 = stream16(P.g, p2 + 2048, last16);
-    b3 = stream16(P.g, p2 + 3072, last16);
+    const TileLoad La = wave_tile(wbase, 0, rel);
+    a0 = stream16(La, lo16);
+    a1 = stream16(La, lo16 + 1024);
+    a2 = stream16(La, lo16 + 2048);
+    a3 = stream16(La, lo16 + 3072);
+    const TileLoad Lb = wave_tile(wbase, 1, rel);
+    b0 = stream16(Lb, lo16);
+    b1 = stream16(Lb, lo16 + 1024);
+    b2 = stream16(Lb, lo16 + 2048);
+    b3 = stream16(Lb, lo16 + 3072);
   }
-  for (uint64_t t = tb; t < te; t += 2) {
-    tile_pass<WRITE>(a0, a1, a2, a3, t * kWaveTile, wlo, whi, lane, F, T, C, P, dl, scr, w);
-    {
-      const uint64_t p = (t + 2 < te ? t + 2 : t) * kWaveTile + 16u * lane;  // tail: harmless re-read
-      a0 = stream16(P.g, p, last16);
-      a1 = stream16(P.g, p + 1024, last16);
-      a2 = stream16(P.g, p + 2048, last16);
-      a3 = stream16(P.g, p + 3072, last16);
-    }
-    if (t + 1 >= te) break;
-    tile_pass<WRITE>(b0, b1, b2, b3, (t + 1) * kWaveTile, wlo, whi, lane, F, T, C, P, dl, scr, w);
-    {
-      const uint64_t p = (t + 3 < te ? t + 3 : t + 1) * kWaveTile + 16u * lane;
-      b0 = stream16(P.g, p, last16);
-      b1 = stream16(P.g, p + 1024, last16);
-      b2 = stream16(P.g, p + 2048, last16);
-      b3 = stream16(P.g, p + 3072, last16);
-    }
+  // one exit at the bottom (a mid-loop break let hipcc rotate the loop so that
+  // its header waited on the loads just issued); an odd last tile follows
+  uint32_t i = 0;
+  if (n >= 2) {
+    do {
+      tile_pass<WRITE, ABL>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, i == 0 && clip_lo, wlo, whi, lane, F, T, C,
+                            P, dl, scr, w);
+      {
+        const TileLoad L = wave_tile(wbase, i + 2, rel);
+        a0 = stream16(L, lo16);
+        a1 = stream16(L, lo16 + 1024);
+        a2 = stream16(L, lo16 + 2048);
+        a3 = stream16(L, lo16 + 3072);
+      }
+      tile_pass<WRITE, ABL>(b0, b1, b2, b3, wb + (uint64_t)(i + 1) * kWaveTile, i + 2 == n && clip_hi, wlo, whi,
+                            lane, F, T, C, P, dl, scr, w);
+      {
+        const TileLoad L = wave_tile(wbase, i + 3, rel);
+        b0 = stream16(L, lo16);
+        b1 = stream16(L, lo16 + 1024);
+        b2 = stream16(L, lo16 + 2048);
+        b3 = stream16(L, lo16 + 3072);
+      }
+      i += 2;
+    } while (i + 1 < n);
   }
-  if (w.dn) flush_deferred<WRITE>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
+  if (i < n)  // a* holds tile i = n - 1
+    tile_pass<WRITE, ABL>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, (i == 0 && clip_lo) || clip_hi, wlo, whi,
+                          lane, F, T, C, P, dl, scr, w);
+  if (w.dn) flush_deferred<WRITE, ABL>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
   uint64_t x = w.x > whi ? w.x : whi;  // chain exit: the last kept match end or the range end
   if (tb == te) x = wlo;
 
@@ -414,17 +457,17 @@ size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates)
 
 namespace {
 
-template <bool WRITE>
+template <bool WRITE, int ABL>
 hipError_t sparse_one(const ScanParams& P, size_t smem, hipStream_t stream)
 {
   static size_t attr_smem = 65536;
   if (smem > attr_smem) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE, ABL>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_smem = smem;
   }
-  hipLaunchKernelGGL((sparse_kernel<WRITE>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream, P);
+  hipLaunchKernelGGL((sparse_kernel<WRITE, ABL>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream, P);
   return hipGetLastError();
 }
 
@@ -432,13 +475,19 @@ hipError_t sparse_one(const ScanParams& P, size_t smem, hipStream_t stream)
 
 hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream_t stream)
 {
-  return write ? sparse_one<true>(P, smem, stream) : sparse_one<false>(P, smem, stream);
+  if (write) return sparse_one<true, 0>(P, smem, stream);
+  switch (P.ablate) {  // benchmarking knob (UGPU_ABLATE): count pass only
+    case 1: return sparse_one<false, 1>(P, smem, stream);
+    case 2: return sparse_one<false, 2>(P, smem, stream);
+    case 3: return sparse_one<false, 3>(P, smem, stream);
+    default: return sparse_one<false, 0>(P, smem, stream);
+  }
 }
 
 hipError_t sparse_occupancy(const ScanParams& P, size_t smem, int* n)
 {
   (void)P;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, sparse_kernel<false>, kSpWaves * 64, smem);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, sparse_kernel<false, 0>, kSpWaves * 64, smem);
 }
 
 }  // namespace ugpu
