@@ -26,10 +26,10 @@ def main(d):
                 "select name, total_calls, total_duration, average, percentage from top_kernels"):
             kernels.append({"name": name, "calls": calls, "total_us": round(total, 3), "avg_us": round(avg, 3),
                             "pct": round(pct, 3)})
-    scan = [k for k in kernels if "sparse_kernel" in k["name"] or "scan_kernel" in k["name"]]
+    scan = [k for k in kernels if any(n in k["name"] for n in ("sparse_kernel", "dense_kernel", "scan_kernel"))]
     dom = max(scan, key=lambda k: k["total_us"]) if scan else None
     counters = {}
-    for sub in ("pmc1", "pmc2"):
+    for sub in ("pmc1", "pmc2", "pmc3"):
         c = db(d, sub)
         if not c or not dom:
             continue

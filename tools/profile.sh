@@ -18,6 +18,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$out/pmc1" -o ru
     python3 "$root/bench.py" "${args[@]}" > /dev/null 2> "$out/pmc1.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$out/pmc2" -o run -- \
     python3 "$root/bench.py" "${args[@]}" > /dev/null 2> "$out/pmc2.err"
+if [ -n "$PMC3" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY -d "$out/pmc3" -o run -- \
+      python3 "$root/bench.py" "${args[@]}" > /dev/null 2> "$out/pmc3.err"
+fi
 cd "$root"
 python3 tools/pmc_summary.py "$out" > "$out/summary.json"
 cat "$out/summary.json"

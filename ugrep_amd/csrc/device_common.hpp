@@ -1,6 +1,6 @@
 // device_common.hpp -- device building blocks shared by the scan kernels:
-// flattened DFA table lookup, the exact FIND walk, match emitters, the chain
-// step/merge used to stitch speculative segments, and the SWAR prefilter.
+// flattened DFA table lookup, the exact FIND walk, match emitters, and the
+// chain step/merge used to stitch speculative pieces.
 #pragma once
 #include "scan_kernels.hpp"
 
@@ -110,45 +110,26 @@ struct WriteEm {
   }
 };
 
-// One step of the FIND chain from p (< e).  With the prefilter (FILT), positions
-// whose byte cannot start a match are skipped via the candidate mask of the
-// lane's 64-byte segment [sa, sa+64): their step is p+1 with no match.
-template <int FMT, bool FILT, class Em>
-__device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t p,
-                                               uint64_t sa, uint64_t e, uint64_t mask, Em& em, int sign,
-                                               uint32_t& ovf)
+// One step of the FIND chain from p: the longest match at p (emitted with
+// `sign`, then the chain continues at its end) or p+1.
+template <int FMT, class Em>
+__device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t p, Em& em,
+                                               int sign, uint32_t& ovf)
 {
-  uint64_t c0 = p;
-  if constexpr (FILT) {
-    uint64_t off = p - sa;
-    uint64_t m = off < 64 ? (mask & (~0ull << off)) : 0ull;
-    if (m == 0) return e;
-    c0 = sa + (uint64_t)__builtin_ctzll(m);
-  }
   uint32_t le;
-  uint64_t len = walk<FMT>(T, w, c0, le, ovf);
+  const uint64_t len = walk<FMT>(T, w, p, le, ovf);
   if (len) {
-    em.put(c, c0, len, le, sign);
-    return c0 + len;
+    em.put(c, p, len, le, sign);
+    return p + len;
   }
-  return c0 + 1;
-}
-
-template <int FMT, bool FILT, class Em>
-__device__ __forceinline__ uint64_t run_seg(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t x, uint64_t sa,
-                                            uint64_t e, uint64_t mask, Em& em, uint32_t& ovf)
-{
-  uint64_t p = x;
-  while (p < e) p = chain_step<FMT, FILT>(T, w, c, p, sa, e, mask, em, +1, ovf);
-  return p;
+  return p + 1;
 }
 
 // Re-enter [.., e) at xn instead of xo.  Adds (true - speculative) matches to em.
 // Returns true if the chains met (exit unchanged), else sets nexit.
-template <int FMT, bool FILT>
+template <int FMT>
 __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t xo, uint64_t xn,
-                                      uint64_t sa, uint64_t e, uint64_t mask, CountEm& em, uint64_t& nexit,
-                                      uint32_t& ovf)
+                                      uint64_t e, CountEm& em, uint64_t& nexit, uint32_t& ovf)
 {
   uint64_t po = xo, pn = xn;
   for (;;) {
@@ -158,53 +139,15 @@ __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx
       return false;
     }
     if (po < pn)
-      po = chain_step<FMT, FILT>(T, w, c, po, sa, e, mask, em, -1, ovf);
+      po = chain_step<FMT>(T, w, c, po, em, -1, ovf);
     else
-      pn = chain_step<FMT, FILT>(T, w, c, pn, sa, e, mask, em, +1, ovf);
+      pn = chain_step<FMT>(T, w, c, pn, em, +1, ovf);
   }
-}
-
-// SWAR prefilter terms (tables.hpp): a set test is an OR over (mask, value)
-// terms, each an exact per-byte zero test ((t & 0x7f..) + 0x7f..) | t (bit 7
-// = byte nonzero, no borrow leakage).  Term counts are compile-time, packed in
-// the filter code FC = fcode(nA, nB, nC, nD).
-constexpr int fcode(int na, int nb, int nc, int nd) { return 1 + na * 27 + nb * 9 + nc * 3 + nd; }
-constexpr int fc_na(int fc) { return (fc - 1) / 27; }
-constexpr int fc_nb(int fc) { return ((fc - 1) / 9) % 3; }
-constexpr int fc_nc(int fc) { return ((fc - 1) / 3) % 3; }
-constexpr int fc_nd(int fc) { return (fc - 1) % 3; }
-
-struct Filter {
-  uint32_t tm[16], tv[16];
-};
-
-__device__ __forceinline__ uint32_t nz_bytes(uint32_t t) { return ((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t; }
-
-// bit 7 of each byte set iff the byte matches NO term of the set [o, o+N)
-template <int N>
-__device__ __forceinline__ uint32_t no_match(const Filter& F, int o, uint32_t x)
-{
-  uint32_t r = 0xffffffffu;
-#pragma unroll
-  for (int i = 0; i < N; ++i) r &= nz_bytes((x & F.tm[o + i]) ^ F.tv[o + i]);
-  return r;
 }
 
 __device__ __forceinline__ uint64_t lowbits(uint64_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }
 
 __device__ __forceinline__ uint64_t clampu(uint64_t v, uint64_t a, uint64_t b) { return v < a ? a : (v > b ? b : v); }
-
-__device__ __forceinline__ uint4 load_chunk(const uint8_t* g, uint64_t pos, uint64_t rend)
-{
-  // A 16-byte aligned chunk holding at least one readable byte lies in a mapped
-  // page, so it is loaded whole; bytes >= rend are never consulted.
-  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-  if (pos < rend) {
-    v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(g + pos));
-    return make_uint4(v.x, v.y, v.z, v.w);
-  }
-  return make_uint4(0, 0, 0, 0);
-}
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v)
 {

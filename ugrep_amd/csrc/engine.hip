@@ -84,6 +84,7 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.accb = d->t.accb;
   P.log_row = d->t.log_row;
   P.nstates = d->t.states;
+  P.cap1 = d->t.cap1;
   for (int i = 0; i < 5; ++i)
     P.ft[i] = (uint32_t)d->t.ft[4 * i] | ((uint32_t)d->t.ft[4 * i + 1] << 8) | ((uint32_t)d->t.ft[4 * i + 2] << 16) |
               ((uint32_t)d->t.ft[4 * i + 3] << 24);
@@ -106,6 +107,9 @@ void geometry(ScanParams& P, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint
   const uint64_t nt = t1 - t0;
   uint64_t nrec = nt < (uint64_t)max_rec ? nt : (uint64_t)max_rec;
   if (nrec == 0) nrec = 1;
+  // the kernels address a record's bytes with 32-bit offsets
+  const uint64_t min_rec = (nt * unit + kMaxRecBytes - 1) / kMaxRecBytes;
+  if (nrec < min_rec) nrec = min_rec < nt ? min_rec : nt;
   const uint64_t tpr = (nt + nrec - 1) / nrec;
   nrec = (nt + tpr - 1) / tpr;
   const uint64_t grid = (nrec + per - 1) / per;
@@ -123,13 +127,13 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
   if (s->sparse)
     geometry(P, dbuf, lo, hi, read_end, s->max_rec, kWaveTile, kSpWaves, off);
   else
-    geometry(P, dbuf, lo, hi, read_end, s->max_rec, kTile, 1, off);
+    geometry(P, dbuf, lo, hi, read_end, s->max_rec, dense_unit(s->dfa->t.format), kDWaves, off);
 }
 
 hipError_t launch_main(const ugpu_scanner* s, const ScanParams& P, bool write, hipStream_t st)
 {
   if (s->sparse) return launch_sparse(P, write, s->smem, st);
-  return launch_scan(P, s->dfa->t.format, s->dfa->t.filter, write, s->smem, st);
+  return launch_dense(P, s->dfa->t.format, write, s->smem, st);
 }
 
 bool is_device_ptr(const void* p)
@@ -262,7 +266,7 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   HIP_TRY(hipGetDevice(&s->device));
   s->sparse = dfa->t.filter && dfa->t.format == FMT_BYTE;
   s->smem = s->sparse ? sparse_smem_bytes(dfa->ntrans_pad, dfa->t.states)
-                      : scan_smem_bytes(dfa->ntrans_pad, dfa->t.format);
+                      : dense_smem_bytes(dfa->t.format, dfa->ntrans_pad, dfa->t.states);
   if (s->smem > 160 * 1024) {
     delete s;
     return fail(UGPU_UNSUPPORTED, "tables do not fit in LDS");
@@ -272,12 +276,12 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
     ScanParams probe{};
     HIP_TRY(sparse_occupancy(probe, s->smem, &per_cu));
   } else {
-    HIP_TRY(scan_occupancy(dfa->t.format, dfa->t.filter, s->smem, &per_cu));
+    HIP_TRY(dense_occupancy(dfa->t.format, dfa->t.cap1 != 0, s->smem, &per_cu));
   }
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, s->device));
   if (per_cu < 1) per_cu = 1;
-  int g = prop.multiProcessorCount * per_cu * (s->sparse ? kSpWaves : 1);
+  int g = prop.multiProcessorCount * per_cu * (s->sparse ? kSpWaves : kDWaves);
   if (g > kMaxRec) g = kMaxRec;
   s->max_rec = g;
   if (const char* env = std::getenv("UGPU_MAX_GRID")) {

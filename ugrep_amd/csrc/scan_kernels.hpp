@@ -4,33 +4,34 @@
 // (lib/matcher.cpp:42-750): at position p walk the DFA,
 // remember the last accepting state, emit the longest non-empty match and jump
 // to its end, else move to p+1.  The chain is sequential; the GPU cuts the
-// input into lane SEGMENTS (64 B), runs every segment's chain speculatively
-// from the segment start, and stitches the true chain back together:
+// input into pieces (lane segments, wave ranges, GPU shards), runs every
+// piece's chain speculatively from the piece start, and stitches the true chain
+// back together:
 //
-//   * the true chain enters segment k at the exit x of segment k-1 (x >= start);
-//   * if x differs from the speculative entry, the lane re-walks both chains in
+//   * the true chain enters piece k at the exit x of piece k-1 (x >= start);
+//   * if x differs from the speculative entry, both chains are re-walked in
 //     lock step, subtracting the speculative matches and adding the true ones,
-//     until the two chains meet (then everything after is identical) or both
-//     leave the segment (then the exit changed and the next lane repeats this).
+//     until they meet (then everything after is identical) or both leave the
+//     piece (then the exit changed and the next piece repeats this).
 //
-// Within a 16 KiB tile the lanes resolve this in LDS rounds; tiles of one block
-// are processed in order so a block's chain is exact from its entry; block
-// entries are fixed by fix_kernel the same way (rarely more than one round).
+// Lanes of a wave resolve this with DPP rounds inside the scan kernels
+// (dense_kernel.hip; sparse_kernel.hip has no lane pieces: its candidates are
+// resolved in order), waves are stitched by fix_kernel, GPU shards by
+// chain_fix_kernel (ugrep_amd/dist.py).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
 namespace ugpu {
 
-constexpr int kBlock = 256;            // threads per workgroup (4 waves)
-constexpr int kSeg = 64;               // bytes per lane segment
-constexpr int kTile = kBlock * kSeg;   // 16 KiB staged per tile
-constexpr int kHalo = 256;             // bytes staged past the tile end
 constexpr int kMaxRec = 8192;          // chain records stitched by one fix_kernel block
 constexpr int kFixThreads = 1024;
 constexpr int kWaveTile = 4096;        // sparse kernel: bytes per wave per iteration
 constexpr int kSpWaves = 4;            // sparse kernel: waves per workgroup
-constexpr int kCandCap = 512;          // sparse kernel: candidate window per wave
+constexpr int kDWaves = 4;             // dense kernel: waves per workgroup
+constexpr int kDSegByte = 124;         // dense kernel: lane segment bytes, 256-column tables (31 dwords: odd)
+constexpr int kDSegClass = 60;         // dense kernel: lane segment bytes, class tables (15 dwords: odd)
+constexpr uint64_t kMaxRecBytes = 1ull << 30;  // bytes per chain record (32-bit wave-relative offsets)
 
 struct BlockRec {
   uint64_t entry, exit, cnt, dg, dc, pad0, pad1, pad2;
@@ -50,9 +51,9 @@ struct ScanParams {
   uint64_t rend;      // walks may read bytes < rend
   int64_t delta;      // reported start = position + delta
   uint32_t at_eof;    // rend is the end of the stream
-  uint32_t ablate;    // benchmarking only (UGPU_ABLATE): 1 = stage tiles only, 2 = + prefilter
+  uint32_t ablate;    // benchmarking only (UGPU_ABLATE, sparse kernel): 1 loads, 2 + prefilter, 3 no walks
   uint64_t t0, t1, tpb;  // tiles [t0, t1), tiles per record
-  uint32_t unit;         // bytes per tile (kTile or kWaveTile)
+  uint32_t unit;         // bytes per tile (kWaveTile, or dense_unit())
   uint32_t nrec;         // chain records (blocks or waves)
   uint32_t nstates;
   const uint16_t* trans;
@@ -61,6 +62,7 @@ struct ScanParams {
   uint32_t ntrans_pad;   // u16 entries, multiple of 8
   uint32_t start, accb, log_row;
   uint32_t ft[5];        // prefilter lookup tables T0 (lo, hi), T1 (lo, hi), T2 (tables.hpp)
+  uint32_t cap1;         // the accept index when all accepting states share it, else 0
   uint32_t grid;
   BlockRec* recs;
   const uint64_t* entries;   // OFFSETS pass: exact block entries
@@ -75,18 +77,19 @@ struct ScanParams {
   uint64_t* out_base_out;    // fix_kernel: exclusive scan of block counts
 };
 
-// launchers (scan_kernels.hip)
-hipError_t launch_scan(const ScanParams& P, uint32_t format, bool filter, bool write, size_t smem,
-                       hipStream_t stream);
+// launchers (scan_kernels.hip, gen.hip)
 hipError_t launch_fix(const ScanParams& P, uint32_t format, hipStream_t stream);
 hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_entry, uint64_t new_entry,
                             hipStream_t stream);
-hipError_t scan_occupancy(uint32_t format, bool filter, size_t smem, int* blocks_per_cu);
 hipError_t launch_gen(int kind, uint64_t seed, uint64_t off, uint8_t* dbuf, uint64_t len, hipStream_t stream);
-size_t scan_smem_bytes(uint32_t ntrans_pad, uint32_t format);
 // sparse (prefiltered) wave-persistent kernel, sparse_kernel.hip
 hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream_t stream);
 hipError_t sparse_occupancy(const ScanParams& P, size_t smem, int* blocks_per_cu);
 size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates);
+// dense wave-persistent kernel, dense_kernel.hip
+hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);
+hipError_t dense_occupancy(uint32_t format, bool cap1, size_t smem, int* blocks_per_cu);
+size_t dense_smem_bytes(uint32_t format, uint32_t ntrans_pad, uint32_t nstates);
+uint32_t dense_unit(uint32_t format);
 
 }  // namespace ugpu

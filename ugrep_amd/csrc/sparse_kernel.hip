@@ -127,7 +127,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t ballot)
 
 constexpr int kDefer = 64;                          // deferred candidates per wave (one walk batch)
 constexpr int kAux = 2048;                          // per-wave aux LDS bytes
-static_assert(kDefer * 8 <= kAux && 64 * 32 <= kAux && kCandCap * 2 <= kAux, "aux region too small");
+static_assert(kDefer * 8 <= kAux && 64 * 32 <= kAux, "aux region too small");
 
 // Greedy FIND rule over up to 64 walked candidates held one per lane in
 // position order: keep the match at c iff c >= x, the end of the last kept

@@ -268,6 +268,12 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   t.start = start_sid * R;
   t.accepting = S - first_acc;
   t.accb = (t.accepting > 0) ? first_acc * R : 0x10000u;
+  for (uint32_t s = first_acc; s < S; ++s) {
+    if (s == first_acc)
+      t.cap1 = caps[s];
+    else if (caps[s] != t.cap1)
+      t.cap1 = 0;
+  }
   // prefilter (see tables.hpp): per first byte c, the bytes that can follow
   // it (second) and follow those (third); "all" once a prefix accepts
   std::vector<Lead> leads;
