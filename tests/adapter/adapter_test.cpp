@@ -1,0 +1,177 @@
+// adapter_test.cpp -- TEST INFRASTRUCTURE (GPU box): the drop-in adapter
+// reflex::GpuMatcher (integration/reflex_gpu_matcher.h) against the reference
+// reflex::Matcher, both linked in one binary (the reference libreflex compiled
+// from its sources by oracle/Makefile into oracle/_ref/).
+//
+// For every case line "MODE<TAB>REGEX<TAB>INPUT" of the spec file:
+//   1. plain loop   : while (m.find()) -> (first, size, accept) sequences equal
+//   2. -c loop      : while (m.find()) { ++n; m.skip('\n'); }  (src/ugrep.cpp:10583)
+//   3. skip(' ')    : cur_ moved to arbitrary positions between finds
+//   4. state        : after each hit lineno(), columno(), and after exhaustion
+//                     at_end() agree
+// INPUT as in oracle/ref_harness.cpp (file:, gen:, hex:).  Prints one line
+// per case; exit status 1 if any case differs.
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <fstream>
+#include <string>
+#include <vector>
+
+// The opcode words are Pattern's private opc_ (reflex::Matcher is its friend);
+// INTEGRATION.md proposes a public accessor.  This test reads them directly.
+#define private public
+#include <reflex/pattern.h>
+#undef private
+#include <reflex/matcher.h>
+
+#include "gen.h"
+#include "reflex_gpu_matcher.h"
+
+static std::string build_regex(const std::string& mode, const std::string& rx)
+{
+  // as src/ugrep.cpp:8574-8604, :8849 (see oracle/ref_harness.cpp)
+  std::string regex = rx;
+  if (mode == "F" && !regex.empty())
+  {
+    size_t from = 0, to;
+    while ((to = regex.find("\\E", from)) != std::string::npos)
+    {
+      regex.insert(to + 2, "\\\\E\\Q");
+      from = to + 7;
+    }
+    regex.insert(0, "\\Q").append("\\E");
+  }
+  regex.insert(0, "(?m)");
+  return reflex::Matcher::convert(regex, reflex::convert_flag::notnewline | reflex::convert_flag::unicode);
+}
+
+static std::vector<char> load_input(const std::string& spec)
+{
+  std::vector<char> buf;
+  if (spec.compare(0, 5, "file:") == 0)
+  {
+    std::string rest = spec.substr(5);
+    size_t total = 0;
+    size_t c = rest.rfind(':');
+    if (c != std::string::npos && c > 0 && rest.find_first_not_of("0123456789", c + 1) == std::string::npos)
+    {
+      total = strtoull(rest.c_str() + c + 1, NULL, 10);
+      rest = rest.substr(0, c);
+    }
+    std::ifstream f(rest.c_str(), std::ios::binary);
+    std::vector<char> data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (total == 0)
+      total = data.size();
+    buf.resize(total);
+    for (size_t i = 0; i < total && !data.empty(); ++i)
+      buf[i] = data[i % data.size()];
+  }
+  else if (spec.compare(0, 4, "gen:") == 0)
+  {
+    int kind;
+    unsigned long long seed, off, len;
+    if (sscanf(spec.c_str() + 4, "%d:%llu:%llu:%llu", &kind, &seed, &off, &len) == 4)
+    {
+      buf.resize(len);
+      gen_fill(kind, seed, off, reinterpret_cast<uint8_t*>(buf.data()), len);
+    }
+  }
+  else if (spec.compare(0, 4, "hex:") == 0)
+  {
+    std::string h = spec.substr(4);
+    for (size_t i = 0; i + 1 < h.size(); i += 2)
+      buf.push_back(static_cast<char>(strtoul(h.substr(i, 2).c_str(), NULL, 16)));
+  }
+  buf.push_back('\0');  // ugrep passes size+1 (src/ugrep.cpp:3939)
+  return buf;
+}
+
+struct Hit {
+  size_t first, size, accept, lineno, columno;
+  bool operator!=(const Hit& o) const
+  {
+    return first != o.first || size != o.size || accept != o.accept || lineno != o.lineno || columno != o.columno;
+  }
+};
+
+// loop kind: 0 plain, 1 skip('\n') after each hit, 2 skip(' ') after every other hit
+template <class M>
+static std::vector<Hit> run(M& m, std::vector<char>& buf, int kind, bool& at_end)
+{
+  std::vector<Hit> out;
+  m.buffer(buf.data(), buf.size());
+  while (m.find())
+  {
+    out.push_back(Hit{m.first(), m.size(), m.accept(), m.lineno(), m.columno()});
+    if (kind == 1)
+      m.skip('\n');
+    else if (kind == 2 && (out.size() & 1))
+      m.skip(' ');
+  }
+  at_end = m.at_end();
+  return out;
+}
+
+int main(int argc, char** argv)
+{
+  if (argc < 2)
+  {
+    fprintf(stderr, "usage: adapter_test SPECFILE\n");
+    return 2;
+  }
+  std::ifstream spec(argv[1]);
+  std::string line;
+  int bad = 0, n = 0;
+  while (std::getline(spec, line))
+  {
+    if (line.empty() || line[0] == '#')
+      continue;
+    size_t t1 = line.find('\t'), t2 = line.find('\t', t1 + 1);
+    const std::string mode = line.substr(0, t1), rx = line.substr(t1 + 1, t2 - t1 - 1), in = line.substr(t2 + 1);
+    reflex::Pattern pat(build_regex(mode, rx), "r");
+    ugpu_dfa* dfa = NULL;
+    const int rc = ugpu_dfa_create(pat.opc_, static_cast<uint32_t>(pat.nop_), 0, &dfa);
+    if (rc != UGPU_OK && rc != UGPU_UNSUPPORTED)
+    {
+      printf("FAIL /%s/: ugpu_dfa_create: %d %s\n", rx.c_str(), rc, ugpu_last_error());
+      ++bad;
+      continue;
+    }
+    std::vector<char> a = load_input(in), b = a;
+    for (int kind = 0; kind < 3; ++kind)
+    {
+      reflex::Matcher cpu(pat);
+      reflex::GpuMatcher gpu(pat, rc == UGPU_OK ? dfa : NULL);
+      bool ea = false, eb = false;
+      std::vector<Hit> ra = run(cpu, a, kind, ea), rb = run(gpu, b, kind, eb);
+      size_t diff = 0;
+      while (diff < ra.size() && diff < rb.size() && !(ra[diff] != rb[diff]))
+        ++diff;
+      const bool ok = ra.size() == rb.size() && diff == ra.size() && ea == eb;
+      printf("%s %s kind=%d /%s/ %s: cpu %zu gpu %zu matches, gpu scans %zu%s\n", ok ? "ok" : "FAIL",
+             rc == UGPU_OK ? "gpu" : "cpu-only", kind, rx.c_str(), in.substr(0, 40).c_str(), ra.size(), rb.size(),
+             gpu.gpu_scans(), rc == UGPU_OK ? "" : " (engine: unsupported table)");
+      if (!ok)
+      {
+        ++bad;
+        if (diff < ra.size() && diff < rb.size())
+          printf("  first difference at #%zu: cpu (%zu,%zu,%zu,%zu) gpu (%zu,%zu,%zu,%zu)\n", diff, ra[diff].first,
+                 ra[diff].size, ra[diff].accept, ra[diff].lineno, rb[diff].first, rb[diff].size, rb[diff].accept,
+                 rb[diff].lineno);
+      }
+      // the GPU path must actually have served supported tables
+      if (rc == UGPU_OK && gpu.gpu_scans() == 0 && !ra.empty())
+      {
+        printf("FAIL gpu matcher fell back to the CPU for /%s/\n", rx.c_str());
+        ++bad;
+      }
+      ++n;
+    }
+    ugpu_dfa_destroy(dfa);
+  }
+  printf("%d cases, %d failed\n", n, bad);
+  return bad ? 1 : 0;
+}
