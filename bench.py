@@ -101,6 +101,27 @@ def measured_traffic(cfg, nbytes):
     return t
 
 
+def verify_whole(args, kind, total, pat, res, rank, dev, sptr):
+    """Scan the whole logical stream [0, total) as one buffer on this GPU and
+    compare count/digest/dcap with the stitched multi-shard result."""
+    whole = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    if kind == 0:
+        data = open(os.path.join(REPO, "tests", "golden", "lorem.utf8.txt"), "rb").read()
+        tile = np.frombuffer(data, np.uint8)
+        whole[:total].copy_(torch.from_numpy(tile[np.arange(total, dtype=np.int64) % tile.size]))
+    else:
+        ugrep_amd.gen(kind, 1, 0, whole.data_ptr(), total, sptr)
+    sc = ugrep_amd.Scanner(pat)
+    sc.scan(whole.data_ptr(), 0, total, total, True, 0, sptr)
+    t = sc.totals()
+    ok = (t.count, t.digest, t.dcap) == (res["count"], res["digest"], res["dcap"])
+    log("verify: whole-stream count %d digest %d dcap %d; stitched %d %d %d -> %s"
+        % (t.count, t.digest, t.dcap, res["count"], res["digest"], res["dcap"], "OK" if ok else "MISMATCH"))
+    del whole
+    torch.cuda.empty_cache()
+    return ok
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,6 +132,8 @@ def main():
     ap.add_argument("--halo", type=int, default=1 << 20, help="readable bytes past a shard end")
     ap.add_argument("--cpu-sample-mib", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 also scans the whole logical stream alone and checks the stitched totals")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,10 +141,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    # rehearsal knobs for a one-GPU box: UGPU_BENCH_BACKEND=gloo puts every rank
+    # on UGPU_BENCH_DEVICE (default 0) and stitches over gloo on the host
+    backend = os.environ.get("UGPU_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = int(os.environ.get("UGPU_BENCH_DEVICE", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    xdev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     pkey, mode, rx, kind, size, desc = CONFIGS[args.config]
     per_gpu = args.bytes or size
@@ -161,7 +193,7 @@ def main():
         kms.append(sc.kernel_ms())
         rec = dict(entry=t.entry + lo, exit=t.exit + lo, count=t.count, digest=t.digest, dcap=t.dcap)
         if world > 1:
-            rec = stitch(rec, fix_fn, device=dev)
+            rec = stitch(rec, fix_fn, device=xdev)
         return rec
 
     for _ in range(args.warmup):
@@ -178,9 +210,19 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    verified = None
+    if args.verify:
+        del buf
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        if world > 1:
+            dist.barrier()  # every shard buffer is released before rank 0 allocates the whole stream
+        verified = verify_whole(args, kind, total, pat, res, rank, dev, sptr) if rank == 0 else None
+        if world > 1:
+            dist.barrier()
 
     k_avg = float(np.mean(kms)) if kms else float("nan")
     achieved = (hi - lo) / (k_avg * 1e-3) / 1e9
@@ -210,6 +252,8 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel_ms": round(k_avg, 4), "algorithmic_bytes_per_launch": hi - lo},
     }
+    if verified is not None:
+        out["verified_whole_stream"] = verified
     tr = measured_traffic(args.config, hi - lo)
     if tr:
         out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
