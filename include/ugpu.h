@@ -111,6 +111,13 @@ int ugpu_tables_build_host(const uint32_t *opc, uint32_t nop, ugpu_dfa_info *inf
    when the sparse (prefiltered) kernel is used for this table. */
 int ugpu_tables_prefilter_host(const uint32_t *opc, uint32_t nop, uint8_t *ft, int *enabled);
 
+/* Host-only: the FIND transducer table of a restart-local DFA (see
+   ugrep_amd/csrc/tables.hpp: entries = row | XT_DEAD(1) | XT_LIVE(2)), same
+   shape as trans.  *local = 0 (and nothing written) when the table is not
+   restart-local; then the dense kernel uses its general walk. */
+int ugpu_tables_transducer_host(const uint32_t *opc, uint32_t nop, uint16_t *xtrans, uint32_t xtrans_cap,
+                                int *local);
+
 /* --- whole-buffer FIND (Matcher::buffer(); while (find()) ...) --- */
 
 /* buf may be host or device memory, len bytes, search starts at `start`

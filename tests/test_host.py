@@ -136,3 +136,44 @@ def test_prefilter_selectivity_c2():
 def test_result_struct_layout():
     assert ctypes.sizeof(_lib.Totals) == 48
     assert ctypes.sizeof(_lib.DfaInfo) == 32
+
+
+def _xt_find(t, x, data):
+    """FIND over `data` with the transducer table x, one lookup per byte, the
+    way dense_kernel.hip's lockstep loop runs it (no re-reads)."""
+    R, start, accb, fmt = t["info"]["row"], t["start"], t["accb"], t["info"]["format"]
+    cls, caps, lr = t["cls"].tolist(), t["caps"].tolist(), R.bit_length() - 1
+    x = x.tolist()
+    m, p, last, le, out = start, 0, 0, 0, []
+    for q, b in enumerate(data):
+        e = x[(m & ~(R - 1)) + (b if fmt == 0 else cls[b])]
+        if e & 1:  # XT_DEAD: emit [p, last), restart at this byte
+            if last > p:
+                out.append([p, last - p, caps[le >> lr]])
+            p = last = q if e & 2 else q + 1
+        if e >= accb:
+            last, le = q + 1, e & ~(R - 1)
+        m = e
+    if last > p:  # end of input cuts the walk
+        out.append([p, last - p, caps[le >> lr]])
+    return out
+
+
+def test_transducer_reproduces_reference_matches(patterns, cases):
+    """Restart-local tables: the one-lookup-per-byte transducer gives the
+    reference's match lists (dense_kernel.hip lockstep path)."""
+    local = {}
+    for name, p in patterns.items():
+        if name not in UNSUPPORTED:
+            local[name] = ugrep_amd.host_transducer(p["opc"])
+    assert local["c3_ident"] is not None and local["c4_word"] is not None
+    assert any(v is None for v in local.values())  # backtracking tables exist and are detected
+    done = 0
+    for c in cases:
+        if c["input"]["type"] != "hex" or c["pattern"] in UNSUPPORTED or local.get(c["pattern"]) is None:
+            continue
+        t = ugrep_amd.host_tables(patterns[c["pattern"]]["opc"])
+        data = case_input(c["input"]).tolist()
+        assert _xt_find(t, local[c["pattern"]], data) == c["matches"], (c["pattern"], c["input"]["name"])
+        done += 1
+    assert done > 100

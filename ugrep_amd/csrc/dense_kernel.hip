@@ -22,6 +22,8 @@
 // Per-wave chain records (entry, exit, counts) are stitched by fix_kernel.
 #include "device_common.hpp"
 
+#include <type_traits>
+
 namespace ugpu {
 
 namespace {
@@ -108,8 +110,8 @@ struct DWin {
 // Longest match from p (tile-relative), the reference walk (lib/matcher.cpp:
 // 207-217 TAKE, :528-541 HALT, :460-465 EOF).  Used by the fix-up and OFFSETS
 // passes; the main pass inlines the same step into run_lane.
-template <int FMT>
-__device__ __forceinline__ uint32_t walk_rel(const Tab<FMT>& T, const DWin& w, uint32_t p, uint32_t& le, uint32_t& ovf)
+template <class TT>
+__device__ __forceinline__ uint32_t walk_rel(const TT& T, const DWin& w, uint32_t p, uint32_t& le, uint32_t& ovf)
 {
   uint32_t s = T.start, q = p, last = p;
   le = 0;
@@ -130,11 +132,11 @@ __device__ __forceinline__ uint32_t walk_rel(const Tab<FMT>& T, const DWin& w, u
   return last - p;
 }
 
-template <int FMT, class Em>
-__device__ __forceinline__ uint32_t step_rel(const Tab<FMT>& T, const DWin& w, uint32_t p, Em& em, int sign, uint32_t& ovf)
+template <class TT, class Em>
+__device__ __forceinline__ uint32_t step_rel(const TT& T, const DWin& w, uint32_t p, Em& em, int sign, uint32_t& ovf)
 {
   uint32_t le;
-  const uint32_t len = walk_rel<FMT>(T, w, p, le, ovf);
+  const uint32_t len = walk_rel(T, w, p, le, ovf);
   if (len) {
     em.put(p, len, le, sign);
     return p + len;
@@ -156,8 +158,8 @@ struct LaneWalk {
 // parked lanes with GLOBAL = true.  Keeping global loads out of the main loop
 // matters: hipcc would otherwise wait for every outstanding load (the next
 // tile's prefetch included) at each byte.
-template <int FMT, bool CAP1, bool GLOBAL>
-__device__ __forceinline__ void run_lane(const Tab<FMT>& T, const DWin& w, LaneWalk& L, uint32_t b, RelEm<CAP1>& em,
+template <bool CAP1, bool GLOBAL, class TT>
+__device__ __forceinline__ void run_lane(const TT& T, const DWin& w, LaneWalk& L, uint32_t b, RelEm<CAP1>& em,
                                          bool& hit_end)
 {
   uint32_t p = L.p, q = L.q, s = L.s, last = L.last, le = L.le;
@@ -213,8 +215,8 @@ __device__ __forceinline__ void run_lane(const Tab<FMT>& T, const DWin& w, LaneW
 // (old) and the true (new) chains in lock step, subtracting the old matches and
 // adding the new ones, until they meet (true: the exit is unchanged) or both
 // leave the segment (false: nexit = the new exit).
-template <int FMT, class Em>
-__device__ __forceinline__ bool merge_rel(const Tab<FMT>& T, const DWin& w, uint32_t xo, uint32_t xn, uint32_t b, Em& em,
+template <class TT, class Em>
+__device__ __forceinline__ bool merge_rel(const TT& T, const DWin& w, uint32_t xo, uint32_t xn, uint32_t b, Em& em,
                                           uint32_t& nexit, uint32_t& ovf)
 {
   uint32_t po = xo, pn = xn;
@@ -225,9 +227,9 @@ __device__ __forceinline__ bool merge_rel(const Tab<FMT>& T, const DWin& w, uint
       return false;
     }
     if (po < pn)
-      po = step_rel<FMT>(T, w, po, em, -1, ovf);
+      po = step_rel(T, w, po, em, -1, ovf);
     else
-      pn = step_rel<FMT>(T, w, pn, em, +1, ovf);
+      pn = step_rel(T, w, pn, em, +1, ovf);
   }
 }
 
@@ -270,12 +272,154 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t dtile_rsrc(const uint8_t* wbas
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(wbase + off), (short)0, nr, 0x00020000);
 }
 
+// FIND transducer entries (tables.hpp xtrans): row offset | flags.
+constexpr uint32_t kXtDead = 1;  // XT_DEAD: the walk died here; the row is the restart state
+constexpr uint32_t kXtLive = 2;  // XT_LIVE: the restart at this byte begins a walk
+
+// The transducer table seen as a plain DFA table by the general walks
+// (fix-up, parked lanes, edge tiles, OFFSETS): a DEAD entry is the dead state.
+template <int FMT>
+struct XTab {
+  const uint16_t* trans;
+  const uint8_t* cls;
+  uint32_t start, accb;
+  __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t b) const
+  {
+    const uint32_t e = FMT == 0 ? trans[s | b] : trans[s + cls[b]];
+    return (e & kXtDead) ? 0u : e;
+  }
+};
+
+// Lockstep FIND over one full lane segment [0, S) (lane-relative positions)
+// for restart-local tables: one transducer lookup per byte for every lane,
+// bytes read four at a time, no per-lane control flow (SURVEY Appendix A,
+// restated for tables.hpp xtrans):
+//   dead entry: emit [p, last) if last > p; the chain restarts at this byte
+//               (p = last = q, or q + 1 when no walk begins here);
+//   accepting entry: last = q + 1.
+// Walks still alive at the segment end continue byte by byte (other lanes
+// masked) until they die; a walk that reaches the staged window end `wend`
+// parks for the general global-memory path.  cnt / sp / sl = number, sum of
+// starts and sum of ends of the emitted matches (lane-relative).  Returns the
+// lane's exit (first chain position >= S) unless parked.
+template <int FMT, int S>
+__device__ __forceinline__ uint32_t lockstep_lane(const uint16_t* xt, const uint8_t* lcls, const uint8_t* seg,
+                                                  uint32_t wend, uint32_t start, uint32_t accb, uint32_t rowmask,
+                                                  uint32_t& cnt, uint32_t& sp, uint32_t& sl, LaneWalk& park,
+                                                  bool& parked, bool ablate_tail)
+{
+  uint32_t m = start, p = 0, last = 0;
+#pragma unroll 2
+  for (uint32_t i = 0; i < (uint32_t)S; i += 4) {
+    const uint32_t x = *reinterpret_cast<const uint32_t*>(seg + i);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t b = (x >> (8 * k)) & 0xffu;
+      const uint32_t col = FMT == 0 ? b : (uint32_t)lcls[b];
+      const uint32_t e = xt[(m & rowmask) | col];
+      const uint32_t q = i + k;
+      const bool dead = (e & kXtDead) != 0;
+      const bool em = dead && last > p;
+      cnt += em ? 1u : 0u;
+      sp += em ? p : 0u;
+      sl += em ? last : 0u;
+      const uint32_t pn = (e & kXtLive) ? q : q + 1;
+      p = dead ? pn : p;
+      last = e >= accb ? q + 1 : (dead ? pn : last);
+      m = e;
+    }
+  }
+  uint32_t ex = p;  // == S when no walk is open at the segment end
+  bool act = p < (uint32_t)S && !ablate_tail;
+  for (uint32_t q = S; __ballot(act); ++q) {
+    if (act) {
+      if (q >= wend) {
+        park = LaneWalk{p, q, m & rowmask, last, 0};
+        parked = true;
+        act = false;
+      } else {
+        const uint32_t b = seg[q];
+        const uint32_t e = xt[(m & rowmask) | (FMT == 0 ? b : (uint32_t)lcls[b])];
+        if (e & kXtDead) {
+          if (last > p) {
+            cnt += 1;
+            sp += p;
+            sl += last;
+          }
+          const uint32_t c = last > p ? last : p + 1;  // the chain runs on from here to q
+          ex = c > (uint32_t)S ? c : (uint32_t)S;
+          act = false;
+        } else {
+          if (e >= accb) last = q + 1;
+          m = e;
+        }
+      }
+    }
+  }
+  return ex;
+}
+
+// Fix-up of one lane for restart-local tables: the speculative chain entered
+// at `a` but the true chain enters at x (a < x).  A FIND chain passes through
+// every position not strictly inside one of its matches, so when x is not
+// inside a speculative match the two chains coincide from x on and the
+// correction is just "drop the speculative matches starting before x"; they
+// are found by re-running the transducer from a until the chain reaches x.
+// Returns false when x lies strictly inside a speculative match (or the walk
+// leaves the staged window): the caller falls back to merge_rel.
+// All lanes with `act` run together, one byte per iteration, with selects
+// only (a divergent loop with early exits cost more SALU exec-mask work than
+// the walk itself).  ok = the shortcut held; the sums go to cnt/sst/dsum.
+template <int FMT>
+__device__ __forceinline__ bool xt_correct(const uint16_t* xt, const uint8_t* lcls, const uint8_t* lds, uint32_t wlen,
+                                           uint32_t a, uint32_t x, bool act, uint32_t start, uint32_t accb,
+                                           uint32_t rowmask, uint32_t& cnt, uint32_t& sst, uint32_t& dsum)
+{
+  uint32_t m = start, p = a, last = a, q = a;
+  bool ok = true;
+  uint32_t dc = 0, ds = 0, dd = 0;
+  while (__ballot(act)) {
+    // state at the top: chain position p (walk start) <= q
+    const bool at = p >= x;        // the chain reached x: it passes through x iff p == x
+    const bool out = q >= wlen;    // left the staged window
+    const bool fin = act && (at || out);
+    ok = fin ? (ok && at && p == x) : ok;
+    act = act && !fin;
+    const uint32_t b = lds[q < wlen ? q : 0u];
+    const uint32_t e = xt[(m & rowmask) | (FMT == 0 ? b : (uint32_t)lcls[b])];
+    const bool dead = act && (e & kXtDead) != 0;
+    const bool em = dead && last > p;
+    const bool inside = em && last > x;  // x strictly inside the match [p, last)
+    const bool sub = em && !inside;
+    dc += sub ? 1u : 0u;
+    ds += sub ? p : 0u;
+    dd += sub ? __umul24(p, 30u) + last : 0u;
+    const bool passed = dead && q >= x;  // x lies in [last, q]: the chain runs through it
+    ok = inside ? false : ok;
+    act = act && !inside && !passed;
+    const uint32_t pn = (e & kXtLive) ? q : q + 1;
+    p = dead ? pn : p;
+    last = (e >= accb) ? q + 1 : (dead ? pn : last);
+    m = e;
+    ++q;
+  }
+  if (ok) {
+    cnt -= dc;
+    sst -= ds;
+    dsum -= dd;
+  }
+  return ok;
+}
+
 }  // namespace
 
-template <int FMT, int S, bool CAP1, bool WRITE>
-__global__ __launch_bounds__(kDWaves * 64) void dense_kernel(ScanParams P)
+template <int FMT, int S, bool CAP1, bool XT, bool WRITE>
+__global__ __launch_bounds__((FMT == 0 ? kDWavesByte : kDWavesClass) * 64) void dense_kernel(ScanParams P)
 {
+  constexpr int kDWaves = FMT == 0 ? kDWavesByte : kDWavesClass;
+  static_assert(!XT || CAP1, "the lockstep path sums matches for a single accept index");
   using G = DGeo<S>;
+  using TT = typename std::conditional<XT, XTab<FMT>, Tab<FMT> >::type;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -284,7 +428,7 @@ __global__ __launch_bounds__(kDWaves * 64) void dense_kernel(ScanParams P)
   uint32_t* lcaps = reinterpret_cast<uint32_t*>(ltrans + P.ntrans_pad);
   uint8_t* lcls = reinterpret_cast<uint8_t*>(lcaps + ((P.nstates + 3) & ~3u));
   {
-    const uint4* src = reinterpret_cast<const uint4*>(P.trans);
+    const uint4* src = reinterpret_cast<const uint4*>(XT ? P.xtrans : P.trans);
     uint4* dst = reinterpret_cast<uint4*>(ltrans);
     for (uint32_t i = tid; i < P.ntrans_pad / 8; i += kDWaves * 64) dst[i] = src[i];
     for (uint32_t i = tid; i < P.nstates; i += kDWaves * 64) lcaps[i] = P.caps[i];
@@ -293,7 +437,8 @@ __global__ __launch_bounds__(kDWaves * 64) void dense_kernel(ScanParams P)
     }
   }
   __syncthreads();  // the only workgroup barrier: tables staged
-  const Tab<FMT> T{ltrans, lcls, P.start, P.accb};
+  const TT T{ltrans, lcls, P.start, P.accb};
+  const uint32_t rowmask = ~((1u << P.log_row) - 1u);
 
   const uint64_t gw = (uint64_t)blockIdx.x * kDWaves + wid;
   uint64_t tb = P.t0 + gw * P.tpb;
@@ -308,6 +453,7 @@ __global__ __launch_bounds__(kDWaves * 64) void dense_kernel(ScanParams P)
   const uint64_t relw = rend16 > wb ? rend16 - wb : 0;
   const uint64_t span = (uint64_t)n * G::kTileB + kDHalo;
   const uint32_t rel = (uint32_t)(relw < span ? relw : span);
+  const bool clip_lo = wlo != wb, clip_hi = whi != te * G::kTileB;
 
   uint64_t x = WRITE ? P.entries[gw] : wlo;  // true chain position (wave-uniform)
   uint64_t widx = WRITE ? P.out_base[gw] : 0;
@@ -353,24 +499,65 @@ __global__ __launch_bounds__(kDWaves * 64) void dense_kernel(ScanParams P)
     RelEm<CAP1> em;
     em.caps = lcaps;
     em.log_row = P.log_row;
-    uint32_t ent = a;
-    LaneWalk L{a, a, T.start, a, 0};
+    uint32_t ent = a, ex;
     bool hit_end = false;
-    run_lane<FMT, CAP1, false>(T, w, L, b, em, hit_end);
-    if (__ballot(L.p < b)) run_lane<FMT, CAP1, true>(T, w, L, b, em, hit_end);  // parked lanes
+    // interior tile: every segment whole and the staged window readable
+    const bool interior = !((i == 0 && clip_lo) || (i + 1 == n && clip_hi)) && w.rlim >= w.wlen;
+    if (XT && interior) {
+      const uint32_t lb = (uint32_t)lane * S;
+      uint32_t cnt = 0, sp = 0, sl = 0;
+      LaneWalk park{};
+      bool parked = false;
+      ex = lb + lockstep_lane<FMT, S>(ltrans, lcls, buf + lb, w.wlen - lb, P.start, P.accb, rowmask, cnt, sp, sl, park,
+                                      parked, P.ablate == 5);
+      // lane-relative sums -> tile-relative: start = lb + p, 31 start + len = 30 p + end + 31 lb
+      em.r.cnt = cnt;
+      em.r.sst = sp + cnt * lb;
+      em.r.dsum = 30u * sp + sl + 31u * lb * cnt;
+      if (__ballot(parked)) {
+        if (parked) {
+          LaneWalk L{park.p + lb, park.q + lb, park.s, park.last + lb, 0};
+          run_lane<CAP1, true>(T, w, L, b, em, hit_end);
+          ex = L.p;
+        }
+      }
+    } else {
+      LaneWalk L{a, a, T.start, a, 0};
+      run_lane<CAP1, false>(T, w, L, b, em, hit_end);
+      if (__ballot(L.p < b)) run_lane<CAP1, true>(T, w, L, b, em, hit_end);  // parked lanes
+      ex = L.p;
+    }
     if (hit_end && !w.eof) ovf = 1;  // a live walk ran into the end of the readable bytes
-    uint32_t ex = L.p;
     // fix-up rounds: lane l's true entry is lane l-1's exit
     for (;;) {
+      if (P.ablate == 4) break;  // benchmarking only: no fix-up (results are not matches)
       const uint32_t pv = dprev_lane(ex);
       const uint32_t nx = lane == 0 ? x0 : pv;
       const bool ch = nx != ent;
       if (!__ballot(ch)) break;
-      if (ch) {
-        uint32_t ne;
-        if (!merge_rel<FMT>(T, w, ent, nx, b, em, ne, ovf)) ex = ne;
-        ent = nx;
+      bool done = false;
+      if constexpr (XT) {
+        const bool skip = ch && nx >= b;  // the true chain skips the whole segment
+        if (skip) {
+          em.r = RelSums();
+          ex = nx;
+        }
+        const bool need = ch && !skip;
+        uint32_t c2 = em.r.cnt, s2 = em.r.sst, d2 = em.r.dsum;
+        const bool ok = xt_correct<FMT>(ltrans, lcls, buf, w.wlen < w.rlim ? w.wlen : w.rlim, ent, nx, need, P.start,
+                                        P.accb, rowmask, c2, s2, d2);
+        if (need && ok) {
+          em.r.cnt = c2;
+          em.r.sst = s2;
+          em.r.dsum = d2;
+        }
+        done = skip || (need && ok);
       }
+      if (ch && !done) {
+        uint32_t ne;
+        if (!merge_rel(T, w, ent, nx, b, em, ne, ovf)) ex = ne;
+      }
+      if (ch) ent = nx;
     }
     const uint32_t ex63 = (uint32_t)__builtin_amdgcn_readlane(ex, 63);
     x = (x >= tend) ? x : ts + ex63;
@@ -382,7 +569,7 @@ __global__ __launch_bounds__(kDWaves * 64) void dense_kernel(ScanParams P)
       const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
       AbsWriteEm we{base, widx + (incl - cl), P.out_capacity, P.out_start, P.out_len, P.out_cap, lcaps, P.log_row};
       uint32_t p = ent;
-      while (p < b) p = step_rel<FMT>(T, w, p, we, +1, ovf);
+      while (p < b) p = step_rel(T, w, p, we, +1, ovf);
       wover |= we.overflow;
       widx += tot;
     } else {
@@ -421,10 +608,10 @@ namespace {
 template <int FMT>
 constexpr int seg_for() { return FMT == 0 ? kDSegByte : kDSegClass; }
 
-template <int FMT, bool CAP1, bool WRITE>
+template <int FMT, bool CAP1, bool XT, bool WRITE>
 hipError_t dense_one(const ScanParams& P, size_t smem, hipStream_t stream)
 {
-  auto kern = dense_kernel<FMT, seg_for<FMT>(), CAP1, WRITE>;
+  auto kern = dense_kernel<FMT, seg_for<FMT>(), CAP1, XT, WRITE>;
   static size_t attr_smem = 65536;
   if (smem > attr_smem) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -432,16 +619,16 @@ hipError_t dense_one(const ScanParams& P, size_t smem, hipStream_t stream)
     if (e != hipSuccess) return e;
     attr_smem = smem;
   }
-  hipLaunchKernelGGL(kern, dim3(P.grid), dim3(kDWaves * 64), smem, stream, P);
+  hipLaunchKernelGGL(kern, dim3(P.grid), dim3(dense_waves(FMT) * 64), smem, stream, P);
   return hipGetLastError();
 }
 
-template <int FMT>
-hipError_t dense_fmt(const ScanParams& P, bool write, size_t smem, hipStream_t stream)
+template <int FMT, bool WRITE>
+hipError_t dense_fmt(const ScanParams& P, size_t smem, hipStream_t stream)
 {
-  const bool cap1 = P.cap1 != 0;
-  if (write) return cap1 ? dense_one<FMT, true, true>(P, smem, stream) : dense_one<FMT, false, true>(P, smem, stream);
-  return cap1 ? dense_one<FMT, true, false>(P, smem, stream) : dense_one<FMT, false, false>(P, smem, stream);
+  if (P.cap1 == 0) return dense_one<FMT, false, false, WRITE>(P, smem, stream);
+  if (P.xtrans) return dense_one<FMT, true, true, WRITE>(P, smem, stream);
+  return dense_one<FMT, true, false, WRITE>(P, smem, stream);
 }
 
 }  // namespace
@@ -451,22 +638,26 @@ uint32_t dense_unit(uint32_t format) { return 64u * (uint32_t)(format == 0 ? kDS
 size_t dense_smem_bytes(uint32_t format, uint32_t ntrans_pad, uint32_t nstates)
 {
   const size_t bufb = format == 0 ? DGeo<kDSegByte>::kBuf : DGeo<kDSegClass>::kBuf;
-  size_t b = kDWaves * bufb + 2 * (size_t)ntrans_pad + 4 * (size_t)((nstates + 3) & ~3u) + 256;
+  size_t b = dense_waves(format) * bufb + 2 * (size_t)ntrans_pad + 4 * (size_t)((nstates + 3) & ~3u) + 256;
   return (b + 15) & ~size_t(15);
 }
 
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream)
 {
-  return format == 0 ? dense_fmt<0>(P, write, smem, stream) : dense_fmt<1>(P, write, smem, stream);
+  if (format == 0) return write ? dense_fmt<0, true>(P, smem, stream) : dense_fmt<0, false>(P, smem, stream);
+  return write ? dense_fmt<1, true>(P, smem, stream) : dense_fmt<1, false>(P, smem, stream);
 }
 
-hipError_t dense_occupancy(uint32_t format, bool cap1, size_t smem, int* n)
+hipError_t dense_occupancy(uint32_t format, bool cap1, bool xt, size_t smem, int* n)
 {
+#define UGPU_DENSE_OCC(F, SEG, C, X) \
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(n, dense_kernel<F, SEG, C, X, false>, dense_waves(F) * 64, smem)
   if (format == 0)
-    return cap1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(n, dense_kernel<0, kDSegByte, true, false>, kDWaves * 64, smem)
-                : hipOccupancyMaxActiveBlocksPerMultiprocessor(n, dense_kernel<0, kDSegByte, false, false>, kDWaves * 64, smem);
-  return cap1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(n, dense_kernel<1, kDSegClass, true, false>, kDWaves * 64, smem)
-              : hipOccupancyMaxActiveBlocksPerMultiprocessor(n, dense_kernel<1, kDSegClass, false, false>, kDWaves * 64, smem);
+    return !cap1 ? UGPU_DENSE_OCC(0, kDSegByte, false, false)
+                 : (xt ? UGPU_DENSE_OCC(0, kDSegByte, true, true) : UGPU_DENSE_OCC(0, kDSegByte, true, false));
+  return !cap1 ? UGPU_DENSE_OCC(1, kDSegClass, false, false)
+               : (xt ? UGPU_DENSE_OCC(1, kDSegClass, true, true) : UGPU_DENSE_OCC(1, kDSegClass, true, false));
+#undef UGPU_DENSE_OCC
 }
 
 }  // namespace ugpu

@@ -28,6 +28,7 @@ struct ugpu_dfa {
   int device = 0;
   uint32_t ntrans_pad = 0;
   uint16_t* d_trans = nullptr;
+  uint16_t* d_xtrans = nullptr;  // FIND transducer (restart-local tables on the dense path)
   uint8_t* d_cls = nullptr;
   uint32_t* d_caps = nullptr;
 };
@@ -77,6 +78,7 @@ int hip_fail(hipError_t e, const char* what)
 void fill_tables(ScanParams& P, const ugpu_dfa* d)
 {
   P.trans = d->d_trans;
+  P.xtrans = d->d_xtrans;
   P.cls = d->d_cls;
   P.caps = d->d_caps;
   P.ntrans_pad = d->ntrans_pad;
@@ -127,7 +129,7 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
   if (s->sparse)
     geometry(P, dbuf, lo, hi, read_end, s->max_rec, kWaveTile, kSpWaves, off);
   else
-    geometry(P, dbuf, lo, hi, read_end, s->max_rec, dense_unit(s->dfa->t.format), kDWaves, off);
+    geometry(P, dbuf, lo, hi, read_end, s->max_rec, dense_unit(s->dfa->t.format), dense_waves(s->dfa->t.format), off);
 }
 
 hipError_t launch_main(const ugpu_scanner* s, const ScanParams& P, bool write, hipStream_t st)
@@ -185,6 +187,15 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     ugpu_dfa_destroy(d);
     return hip_fail(e, "table upload");
   }
+  if (d->t.restart_local && !d->t.filter && d->t.cap1 != 0) {
+    std::vector<uint16_t> xt(d->ntrans_pad, 0);
+    std::copy(d->t.xtrans.begin(), d->t.xtrans.end(), xt.begin());
+    if ((e = hipMalloc(&d->d_xtrans, xt.size() * 2)) != hipSuccess ||
+        (e = hipMemcpy(d->d_xtrans, xt.data(), xt.size() * 2, hipMemcpyHostToDevice)) != hipSuccess) {
+      ugpu_dfa_destroy(d);
+      return hip_fail(e, "transducer table upload");
+    }
+  }
   *out = d;
   return UGPU_OK;
 }
@@ -193,6 +204,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
 {
   if (!d) return UGPU_OK;
   if (d->d_trans) (void)hipFree(d->d_trans);
+  if (d->d_xtrans) (void)hipFree(d->d_xtrans);
   if (d->d_cls) (void)hipFree(d->d_cls);
   if (d->d_caps) (void)hipFree(d->d_caps);
   delete d;
@@ -256,6 +268,20 @@ int ugpu_tables_prefilter_host(const uint32_t* opc, uint32_t nop, uint8_t* ft, i
   return UGPU_OK;
 }
 
+int ugpu_tables_transducer_host(const uint32_t* opc, uint32_t nop, uint16_t* xtrans, uint32_t xtrans_cap, int* local)
+{
+  if (!local) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *local = t.restart_local ? 1 : 0;
+  if (!t.restart_local) return UGPU_OK;
+  if (!xtrans || xtrans_cap < t.xtrans.size()) return fail(UGPU_INVAL, "xtrans capacity too small");
+  std::copy(t.xtrans.begin(), t.xtrans.end(), xtrans);
+  return UGPU_OK;
+}
+
 int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
 {
   if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
@@ -276,12 +302,12 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
     ScanParams probe{};
     HIP_TRY(sparse_occupancy(probe, s->smem, &per_cu));
   } else {
-    HIP_TRY(dense_occupancy(dfa->t.format, dfa->t.cap1 != 0, s->smem, &per_cu));
+    HIP_TRY(dense_occupancy(dfa->t.format, dfa->t.cap1 != 0, dfa->d_xtrans != nullptr, s->smem, &per_cu));
   }
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, s->device));
   if (per_cu < 1) per_cu = 1;
-  int g = prop.multiProcessorCount * per_cu * (s->sparse ? kSpWaves : kDWaves);
+  int g = prop.multiProcessorCount * per_cu * (s->sparse ? kSpWaves : dense_waves(dfa->t.format));
   if (g > kMaxRec) g = kMaxRec;
   s->max_rec = g;
   if (const char* env = std::getenv("UGPU_MAX_GRID")) {

@@ -28,7 +28,11 @@ constexpr int kMaxRec = 8192;          // chain records stitched by one fix_kern
 constexpr int kFixThreads = 1024;
 constexpr int kWaveTile = 4096;        // sparse kernel: bytes per wave per iteration
 constexpr int kSpWaves = 4;            // sparse kernel: waves per workgroup
-constexpr int kDWaves = 4;             // dense kernel: waves per workgroup
+// dense kernel: waves per workgroup (one staged table per workgroup: the big
+// class tables share theirs among more waves)
+constexpr int kDWavesByte = 4;
+constexpr int kDWavesClass = 8;
+constexpr int dense_waves(uint32_t format) { return format == 0 ? kDWavesByte : kDWavesClass; }
 constexpr int kDSegByte = 124;         // dense kernel: lane segment bytes, 256-column tables (31 dwords: odd)
 constexpr int kDSegClass = 60;         // dense kernel: lane segment bytes, class tables (15 dwords: odd)
 constexpr uint64_t kMaxRecBytes = 1ull << 30;  // bytes per chain record (32-bit wave-relative offsets)
@@ -57,6 +61,7 @@ struct ScanParams {
   uint32_t nrec;         // chain records (blocks or waves)
   uint32_t nstates;
   const uint16_t* trans;
+  const uint16_t* xtrans;  // FIND transducer table or NULL (dense kernel, tables.hpp)
   const uint8_t* cls;
   const uint32_t* caps;
   uint32_t ntrans_pad;   // u16 entries, multiple of 8
@@ -88,7 +93,7 @@ hipError_t sparse_occupancy(const ScanParams& P, size_t smem, int* blocks_per_cu
 size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates);
 // dense wave-persistent kernel, dense_kernel.hip
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);
-hipError_t dense_occupancy(uint32_t format, bool cap1, size_t smem, int* blocks_per_cu);
+hipError_t dense_occupancy(uint32_t format, bool cap1, bool xt, size_t smem, int* blocks_per_cu);
 size_t dense_smem_bytes(uint32_t format, uint32_t ntrans_pad, uint32_t nstates);
 uint32_t dense_unit(uint32_t format);
 

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <map>
+#include <set>
 #include <unordered_map>
 
 namespace ugpu {
@@ -113,6 +114,60 @@ double group_leads(const std::vector<Lead>& leads, Lead (&g)[2])
     best = g[0].density() + g[1].density();
   }
   return n ? (best < 1.0 ? best : 1.0) : 0.0;
+}
+
+// Restart-locality (tables.hpp): breadth-first over the configurations a FIND
+// walk can be in -- main walk state m, the live "shadow" walks the chain would
+// start at every position after the current anchor (p+1, or the end of the
+// last accept), and whether the next byte is the walk's first -- over one
+// representative byte per column class.  The table is restart-local iff no
+// shadow ever accepts while the main walk is alive and not accepting, and
+// every shadow dies on the byte that kills the main walk.
+bool restart_local(const std::vector<uint32_t>& nxt, uint32_t start, uint32_t first_acc,
+                   const std::vector<int>& reps)
+{
+  typedef std::pair<std::pair<uint32_t, bool>, std::vector<uint32_t> > Cfg;
+  std::set<Cfg> seen;
+  std::vector<Cfg> work;
+  work.push_back(Cfg(std::make_pair(start, true), std::vector<uint32_t>()));
+  seen.insert(work.back());
+  while (!work.empty()) {
+    const Cfg cfg = work.back();
+    work.pop_back();
+    const uint32_t m = cfg.first.first;
+    const bool first = cfg.first.second;
+    for (int c : reps) {
+      const uint32_t m2 = nxt[(size_t)m * 256 + c];
+      std::vector<uint32_t> r2;
+      for (uint32_t r : cfg.second) {
+        const uint32_t t = nxt[(size_t)r * 256 + c];
+        if (t) r2.push_back(t);
+      }
+      Cfg next;
+      if (m2 == 0) {
+        if (!r2.empty()) return false;  // a shadow walk outlives the main walk
+        continue;
+      } else if (m2 >= first_acc) {
+        next = Cfg(std::make_pair(m2, false), std::vector<uint32_t>());  // shadows lie inside the match
+      } else {
+        for (uint32_t t : r2)
+          if (t >= first_acc) return false;  // a match would start inside the walk
+        if (!first) {
+          const uint32_t t = nxt[(size_t)start * 256 + c];
+          if (t >= first_acc) return false;
+          if (t) r2.push_back(t);
+        }
+        std::sort(r2.begin(), r2.end());
+        r2.erase(std::unique(r2.begin(), r2.end()), r2.end());
+        next = Cfg(std::make_pair(m2, false), r2);
+      }
+      if (seen.insert(next).second) {
+        if (seen.size() > 200000) return false;  // too many configurations: treat as not local
+        work.push_back(next);
+      }
+    }
+  }
+  return true;
 }
 
 }  // namespace
@@ -265,6 +320,38 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   }
   t.caps = caps;
   const uint32_t start_sid = sid[0];
+  // FIND transducer for restart-local tables (tables.hpp)
+  if (R >= 4) {
+    std::vector<int> reps;  // one byte per column class
+    {
+      std::vector<bool> seen_cls(256, false);
+      for (int c = 0; c < 256; ++c)
+        if (!seen_cls[cls[c]]) {
+          seen_cls[cls[c]] = true;
+          reps.push_back(c);
+        }
+    }
+    if (restart_local(nxt, start_sid, first_acc, reps)) {
+      t.restart_local = true;
+      t.xtrans.assign((size_t)S * R, 0);
+      for (uint32_t s = 0; s < S; ++s)
+        for (int c : reps) {
+          const uint32_t col = t.format == FMT_BYTE ? (uint32_t)c : cls[c];
+          const uint32_t nx = nxt[(size_t)s * 256 + c], r = nxt[(size_t)start_sid * 256 + c];
+          uint32_t x;
+          if (nx)
+            x = nx * R;
+          else
+            x = (r ? r : start_sid) * R | XT_DEAD | (r ? XT_LIVE : 0);
+          if (t.format == FMT_BYTE) {
+            for (int b = 0; b < 256; ++b)  // every byte of the class
+              if (cls[b] == cls[c]) t.xtrans[(size_t)s * R + b] = (uint16_t)x;
+          } else {
+            t.xtrans[(size_t)s * R + col] = (uint16_t)x;
+          }
+        }
+    }
+  }
   t.start = start_sid * R;
   t.accepting = S - first_acc;
   t.accb = (t.accepting > 0) ? first_acc * R : 0x10000u;

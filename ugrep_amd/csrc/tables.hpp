@@ -48,7 +48,22 @@ struct DfaTables {
   std::vector<uint16_t> trans;  // states * row
   std::vector<uint8_t> cls;     // 256
   std::vector<uint32_t> caps;   // states
+  // FIND transducer (dense_kernel.hip lockstep path), valid when the table is
+  // restart-local: whenever a walk dies at byte q, every walk the FIND chain
+  // would start between the end of the emitted match (or p+1) and q dies by q
+  // without accepting, so the chain never has to re-read bytes before q.  Then
+  //   xtrans[s*R + col] = trans[..]                                   (alive)
+  //                     = r | XT_DEAD | (trans[start][col] ? XT_LIVE : 0)  (dead)
+  // with r = the row of trans[start][col] (the start row when that is dead):
+  // one lookup per byte both continues the walk and restarts it at the dying
+  // byte.  Flags sit below the row offset (R >= 4), so "entry >= accb" still
+  // tests acceptance.
+  bool restart_local = false;
+  std::vector<uint16_t> xtrans;  // states * row (empty unless restart_local)
 };
+
+constexpr uint16_t XT_DEAD = 1;  // the walk died on this byte; the row is the restart state
+constexpr uint16_t XT_LIVE = 2;  // the restart at this byte is alive (a walk begins here)
 
 // Returns 0 (UGPU_OK), 1 (UNSUPPORTED) or 2 (INVAL); err gets a message.
 int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string& err);

@@ -51,6 +51,17 @@ def host_prefilter(opc):
     return bool(en.value), ft
 
 
+def host_transducer(opc):
+    """FIND transducer table (u16 numpy array, tables.hpp) or None when the DFA
+    is not restart-local."""
+    a, p = _as_u32(opc)
+    t = host_tables(opc)
+    x = np.zeros(t["info"]["states"] * t["info"]["row"], np.uint16)
+    loc = ctypes.c_int()
+    check(lib.ugpu_tables_transducer_host(p, len(a), x.ctypes.data_as(_lib.c_u16p), len(x), ctypes.byref(loc)))
+    return x if loc.value else None
+
+
 class Pattern:
     """Compiled pattern (opcode words) with its device tables."""
 
