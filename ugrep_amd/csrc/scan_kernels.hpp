@@ -28,13 +28,30 @@ constexpr int kMaxRec = 8192;          // chain records stitched by one fix_kern
 constexpr int kFixThreads = 1024;
 constexpr int kWaveTile = 4096;        // sparse kernel: bytes per wave per iteration
 constexpr int kSpWaves = 4;            // sparse kernel: waves per workgroup
-// dense kernel: waves per workgroup (one staged table per workgroup: the big
-// class tables share theirs among more waves)
-constexpr int kDWavesByte = 4;
-constexpr int kDWavesClass = 8;
+// Dense kernel geometry (overridable for variant builds, ugrep_amd/Makefile):
+// lane segment bytes (S/4 odd) and waves per workgroup.  One staged table per
+// workgroup: the big class tables share theirs among more waves.  Measured
+// (16 GiB C3 / 8 GiB C4): byte S = 60/92/124/188/252 -> 29.2/22.1/20.7/18.7/
+// 20.7 ms; class S = 28/44/60/92 (16/12/8/8 waves) -> 20.7/17.8/18.9/14.8 ms:
+// per-segment costs (walk tails, fix-ups) favour long segments until the
+// LDS buffers cut occupancy.
+#ifndef UGPU_DSEG_BYTE
+#define UGPU_DSEG_BYTE 188
+#endif
+#ifndef UGPU_DSEG_CLASS
+#define UGPU_DSEG_CLASS 92
+#endif
+#ifndef UGPU_DWAVES_BYTE
+#define UGPU_DWAVES_BYTE 4
+#endif
+#ifndef UGPU_DWAVES_CLASS
+#define UGPU_DWAVES_CLASS 8
+#endif
+constexpr int kDSegByte = UGPU_DSEG_BYTE;    // 256-column tables
+constexpr int kDSegClass = UGPU_DSEG_CLASS;  // class tables
+constexpr int kDWavesByte = UGPU_DWAVES_BYTE;
+constexpr int kDWavesClass = UGPU_DWAVES_CLASS;
 constexpr int dense_waves(uint32_t format) { return format == 0 ? kDWavesByte : kDWavesClass; }
-constexpr int kDSegByte = 124;         // dense kernel: lane segment bytes, 256-column tables (31 dwords: odd)
-constexpr int kDSegClass = 60;         // dense kernel: lane segment bytes, class tables (15 dwords: odd)
 constexpr uint64_t kMaxRecBytes = 1ull << 30;  // bytes per chain record (32-bit wave-relative offsets)
 
 struct BlockRec {
