@@ -12,11 +12,16 @@
 //      the wave's LDS buffer afterwards (S/4 odd: lanes at the same offset of
 //      their segments read distinct banks);
 //   2. every lane runs the FIND chain of its segment speculatively from the
-//      segment start: one byte per loop iteration for every lane, restarts
-//      folded in with selects, so lanes stay busy while their walks diverge;
-//   3. fix-up rounds: the true chain enters lane l at lane l-1's exit (DPP);
-//      lanes whose entry differs re-walk old and new chains in lock step until
-//      they meet (or both leave the segment: the exit changed, another round);
+//      segment start.  Restart-local tables (tables.hpp: C3, C4) use the FIND
+//      transducer: all lanes in lockstep, bytes read a dword at a time, one
+//      table lookup per byte that both continues and restarts walks
+//      (lockstep_lane).  Other tables run the general walk with restarts
+//      folded into selects (run_lane);
+//   3. fix-up rounds: the true chain enters lane l at lane l-1's exit (DPP).
+//      For restart-local tables a lane whose entry differs just drops the
+//      speculative matches that start before the true entry (xt_correct);
+//      otherwise both chains are re-walked in lock step until they meet
+//      (merge_rel);
 //   4. match counts and digests are summed tile-relative in 32 bits and folded
 //      into 64-bit totals once per tile.
 // Per-wave chain records (entry, exit, counts) are stitched by fix_kernel.

@@ -2,11 +2,15 @@
 //
 // Pipeline of one whole-buffer FIND (what Matcher::find() computes lazily, one
 // match per call, lib/matcher.cpp:42-750):
-//   scan_kernel<.., WRITE=false>  persistent grid, speculative per-block chains,
-//                                 per-block (entry, exit, count, digests)
-//   fix_kernel                    stitch block entries, totals, output bases
-//   scan_kernel<.., WRITE=true>   (OFFSETS only) re-walk from exact entries and
+//   sparse_kernel / dense_kernel <WRITE=false>
+//                                 wave-persistent grid, speculative per-wave chains,
+//                                 per-wave (entry, exit, count, digests)
+//   fix_kernel                    stitch wave entries, totals, output bases
+//   sparse_kernel / dense_kernel <WRITE=true>
+//                                 (OFFSETS only) re-walk from exact entries and
 //                                 store (start, len, cap) records
+// The prefiltered sparse kernel serves tables with a selective three-byte
+// prefilter (tables.hpp); every other table runs the dense kernel.
 // Tables are uploaded once per ugpu_dfa (one Pattern), shared by all scanners.
 #include <hip/hip_runtime.h>
 
