@@ -153,6 +153,32 @@ int ugpu_chain_fix(ugpu_scanner *sc, const uint8_t *dbuf, uint64_t lo, uint64_t 
    recorded on the scan stream around that launch. */
 int ugpu_scan_kernel_ms(ugpu_scanner *sc, float *ms);
 
+/* --- streaming FIND ---
+   Input fed in chunks (what AbstractMatcher::input() + grow()/peek_more()
+   provide to Matcher::match, absmatcher.h:1417-1536, :1582-1593; ugrep streams
+   stdin, decompressed data and files it does not mmap, src/ugrep.cpp:3936-3944).
+   Each ugpu_stream_feed() scans the unsettled tail of the previous chunks plus
+   the new chunk on the device and returns the matches that are final: the
+   FIND chain is settled up to a point `keep` bytes before the end (or the end
+   when `final`), the rest is carried to the next call.  Offsets are absolute
+   (from the first byte ever fed); a match may span any number of chunks.  The
+   concatenation of all results equals ugpu_find_all over the whole input. */
+typedef struct ugpu_stream ugpu_stream;
+
+/* keep: bytes held back from each non-final scan (a match that is still open
+   that close to the end is re-scanned with the next chunk; 0 = 64 KiB). */
+int ugpu_stream_create(const ugpu_dfa *dfa, uint64_t keep, ugpu_stream **out);
+int ugpu_stream_destroy(ugpu_stream *st);
+
+/* Feed host bytes; *out (free with ugpu_result_free) gets the newly final
+   matches (records in OFFSETS mode) and their count/digest/dcap. */
+int ugpu_stream_feed(ugpu_stream *st, const uint8_t *chunk, uint64_t len, int final, uint32_t mode,
+                     ugpu_result **out);
+
+/* Absolute offset up to which the FIND chain is settled (bytes before it will
+   not be scanned again). */
+uint64_t ugpu_stream_settled(const ugpu_stream *st);
+
 /* --- synthetic corpora, generated on device --- */
 #define UGPU_GEN_WORDS 1
 #define UGPU_GEN_PLANTED 2

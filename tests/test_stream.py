@@ -1,0 +1,87 @@
+"""GPU: streaming FIND (ugpu_stream).  Feeding any chunking
+of an input -- one byte at a time, ragged sizes, chunks that split matches,
+matches longer than the carry margin -- yields exactly the whole-buffer FIND
+result (ugpu_find_all), which the other GPU tests pin to the reference."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def U():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd
+    return ugrep_amd
+
+
+def _stream(U, pat, data, sizes, keep, offsets=True):
+    st = U.Stream(pat, keep=keep)
+    trip, cnt, dg, dc, i = [], 0, 0, 0, 0
+    k = 0
+    while True:
+        n = sizes[k % len(sizes)]
+        k += 1
+        chunk = data[i:i + n]
+        i += len(chunk)
+        final = i >= len(data)
+        r = st.feed(chunk.tobytes(), final=final, offsets=offsets)
+        if offsets:
+            trip += r.triples()
+        cnt += r.count
+        dg = (dg + r.digest) % (1 << 64)
+        dc = (dc + r.dcap) % (1 << 64)
+        if final:
+            break
+    return trip, cnt, dg, dc
+
+
+def _whole(U, pat, data):
+    r = U.find_all(pat, data.tobytes(), offsets=True)
+    return r.triples(), r.count, r.digest, r.dcap
+
+
+@pytest.mark.parametrize("pname,kind", [("c2_foobarbaz", 1), ("c3_ident", 3), ("c4_word", 4)])
+def test_stream_equals_whole_buffer(U, patterns, pname, kind):
+    from oracle_lib import gen
+    data = gen(kind, 11, 0, 3 << 20)
+    pat = U.Pattern(patterns[pname]["opc"])
+    want = _whole(U, pat, data)
+    rng = np.random.default_rng(kind)
+    for sizes, keep in (([1 << 20], 0), ([int(x) for x in rng.integers(1, 70000, 50)], 4096),
+                        ([int(x) for x in rng.integers(1, 300, 50)] + [500000], 64)):
+        got = _stream(U, pat, data, sizes, keep)
+        assert got == want, (pname, keep)
+
+
+def test_stream_small_chunks_and_long_matches(U, patterns):
+    # 'aa' over a long run of a's: every match spans chunk ends, the open walk
+    # is longer than the carry margin (retries), and one-byte chunks
+    pat = U.Pattern(patterns["aa"]["opc"])
+    data = np.frombuffer(b"b" + b"a" * 20001 + b"\nab aaab aab\n" + b"a" * 7, np.uint8)
+    want = _whole(U, pat, data)
+    for sizes, keep in (([1], 16), ([3, 1, 4, 1, 5, 9, 2, 6], 16), ([997], 64)):
+        assert _stream(U, pat, data, sizes, keep) == want
+    # identifier runs much longer than the margin
+    pat = U.Pattern(patterns["c3_ident"]["opc"])
+    data = np.frombuffer((b"x" * 100000 + b" 9a_b " + b"y" * 3000) * 3, np.uint8)
+    want = _whole(U, pat, data)
+    assert _stream(U, pat, data, [12345, 777], 256) == want
+
+
+def test_stream_count_mode_and_settled(U, patterns):
+    from oracle_lib import gen
+    data = gen(3, 5, 0, 1 << 20)
+    pat = U.Pattern(patterns["c3_ident"]["opc"])
+    want = _whole(U, pat, data)
+    got = _stream(U, pat, data, [65536], 0, offsets=False)
+    assert got[1:] == want[1:]
+    st = U.Stream(pat, keep=1024)
+    st.feed(data[:200000].tobytes())
+    assert 200000 - 1024 <= st.settled() <= 200000
+    r = st.feed(b"", final=True)
+    assert st.settled() == 200000
+    with pytest.raises(U.UgpuError):
+        st.feed(b"x")

@@ -6,8 +6,8 @@ holds the multi-GPU shard stitching (dist.py).
 """
 from ._lib import (GEN_CODE, GEN_PLANTED, GEN_UTF8, GEN_WORDS, MODE_COUNT, MODE_OFFSETS, UgpuError,  # noqa: F401
                    Unsupported, lib)
-from .matcher import (Matcher, Pattern, Scanner, find_all, gen, host_prefilter, host_tables,  # noqa: F401
-                      host_transducer)
+from .matcher import (Matcher, Pattern, Scanner, Stream, find_all, gen, host_prefilter,  # noqa: F401
+                      host_tables, host_transducer)
 
-__all__ = ["Pattern", "Matcher", "Scanner", "find_all", "gen", "host_tables", "host_prefilter", "Unsupported",
+__all__ = ["Pattern", "Matcher", "Scanner", "Stream", "find_all", "gen", "host_tables", "host_prefilter", "Unsupported",
            "UgpuError"]

@@ -84,6 +84,10 @@ def _load():
                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, P(Totals), V]),
         "ugpu_scan_kernel_ms": (ctypes.c_int, [V, P(ctypes.c_float)]),
         "ugpu_gen": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, V, ctypes.c_uint64, V]),
+        "ugpu_stream_create": (ctypes.c_int, [V, ctypes.c_uint64, P(V)]),
+        "ugpu_stream_destroy": (ctypes.c_int, [V]),
+        "ugpu_stream_feed": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, P(P(Result))]),
+        "ugpu_stream_settled": (ctypes.c_uint64, [V]),
         "ugpu_last_error": (ctypes.c_char_p, []),
         "ugpu_version": (ctypes.c_char_p, []),
     }

@@ -538,6 +538,149 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
   return UGPU_OK;
 }
 
+// ---------------------------------------------------------------- streaming
+// Device buffer holds the unsettled carry followed by the new chunk; each feed
+// scans [0, hi) of it with the chain entering at 0 (the previous settled
+// exit), readable to the end, and carries [exit, n) into the other buffer.
+struct ugpu_stream {
+  const ugpu_dfa* dfa = nullptr;
+  ugpu_scanner* sc = nullptr;
+  uint64_t keep = 0;
+  uint8_t* buf[2] = {nullptr, nullptr};
+  uint64_t cap = 0;    // capacity of each buffer (bytes, + 16 padding allocated)
+  int cur = 0;         // buffer holding the carry
+  uint64_t carry = 0;  // unsettled bytes at buf[cur][0..carry)
+  uint64_t base = 0;   // absolute offset of buf[cur][0] = the settled chain position
+  bool done = false;
+};
+
+namespace {
+
+int stream_grow(ugpu_stream* st, uint64_t need)
+{
+  if (need <= st->cap) return UGPU_OK;
+  uint64_t c = st->cap ? st->cap : (1ull << 20);
+  while (c < need) c *= 2;
+  uint8_t* nb[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; ++i) {
+    hipError_t e = hipMalloc(&nb[i], c + 16);
+    if (e != hipSuccess) {
+      if (nb[0]) (void)hipFree(nb[0]);
+      return hip_fail(e, "stream buffer");
+    }
+  }
+  if (st->carry) HIP_TRY(hipMemcpy(nb[0], st->buf[st->cur], st->carry, hipMemcpyDeviceToDevice));
+  for (int i = 0; i < 2; ++i)
+    if (st->buf[i]) (void)hipFree(st->buf[i]);
+  st->buf[0] = nb[0];
+  st->buf[1] = nb[1];
+  st->cur = 0;
+  st->cap = c;
+  return UGPU_OK;
+}
+
+}  // namespace
+
+int ugpu_stream_create(const ugpu_dfa* dfa, uint64_t keep, ugpu_stream** out)
+{
+  if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
+  *out = nullptr;
+  ugpu_stream* st = new (std::nothrow) ugpu_stream();
+  if (!st) return fail(UGPU_NOMEM, "host allocation");
+  st->dfa = dfa;
+  st->keep = keep ? keep : (64ull << 10);
+  int rc = ugpu_scanner_create(dfa, &st->sc);
+  if (rc) {
+    delete st;
+    return rc;
+  }
+  *out = st;
+  return UGPU_OK;
+}
+
+int ugpu_stream_destroy(ugpu_stream* st)
+{
+  if (!st) return UGPU_OK;
+  ugpu_scanner_destroy(st->sc);
+  for (int i = 0; i < 2; ++i)
+    if (st->buf[i]) (void)hipFree(st->buf[i]);
+  delete st;
+  return UGPU_OK;
+}
+
+uint64_t ugpu_stream_settled(const ugpu_stream* st) { return st ? st->base : 0; }
+
+int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int final, uint32_t mode, ugpu_result** out)
+{
+  if (!st || !out || (!chunk && len)) return fail(UGPU_INVAL, "NULL argument");
+  if (st->done) return fail(UGPU_INVAL, "stream already ended (final chunk fed)");
+  *out = nullptr;
+  const uint64_t n = st->carry + len;
+  int rc = stream_grow(st, n);
+  if (rc) return rc;
+  uint8_t* b = st->buf[st->cur];
+  if (len) HIP_TRY(hipMemcpy(b + st->carry, chunk, len, hipMemcpyHostToDevice));
+  ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
+  if (!r) return fail(UGPU_NOMEM, "host allocation");
+  // settle the chain up to `keep` bytes before the end (all of it when final);
+  // a walk still open at the end of the bytes so far means hi was too close
+  uint64_t hi = final ? n : (n > st->keep ? n - st->keep : 0);
+  uint64_t exit = 0;
+  ugpu_totals tot{};
+  while (hi > 0) {
+    rc = ugpu_scan(st->sc, b, 0, hi, n, final ? 1 : 0, st->base, nullptr);
+    if (!rc) rc = ugpu_scan_totals(st->sc, &tot);
+    if (rc == UGPU_HALO && !final) {
+      hi /= 2;
+      continue;
+    }
+    if (rc) {
+      std::free(r);
+      return rc;
+    }
+    exit = final ? n : tot.exit;
+    break;
+  }
+  if (hi > 0) {
+    r->count = tot.count;
+    r->digest = tot.digest;
+    r->dcap = tot.dcap;
+    if (mode == UGPU_MODE_OFFSETS && tot.count > 0) {
+      const uint64_t m = tot.count;
+      uint64_t* d_start = nullptr;
+      uint32_t *d_len = nullptr, *d_cap = nullptr;
+      r->start = static_cast<uint64_t*>(std::malloc(m * 8));
+      r->len = static_cast<uint32_t*>(std::malloc(m * 4));
+      r->cap = static_cast<uint32_t*>(std::malloc(m * 4));
+      hipError_t e = hipSuccess;
+      if (!r->start || !r->len || !r->cap || (e = hipMalloc(&d_start, m * 8)) != hipSuccess ||
+          (e = hipMalloc(&d_len, m * 4)) != hipSuccess || (e = hipMalloc(&d_cap, m * 4)) != hipSuccess)
+        rc = e != hipSuccess ? hip_fail(e, "stream match list") : fail(UGPU_NOMEM, "stream match list");
+      if (!rc) rc = ugpu_scan_offsets(st->sc, d_start, d_len, d_cap, m, nullptr);
+      if (!rc && ((e = hipMemcpy(r->start, d_start, m * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
+                  (e = hipMemcpy(r->len, d_len, m * 4, hipMemcpyDeviceToHost)) != hipSuccess ||
+                  (e = hipMemcpy(r->cap, d_cap, m * 4, hipMemcpyDeviceToHost)) != hipSuccess))
+        rc = hip_fail(e, "stream match list copy");
+      (void)hipFree(d_start);
+      (void)hipFree(d_len);
+      (void)hipFree(d_cap);
+      if (rc) {
+        ugpu_result_free(r);
+        return rc;
+      }
+    }
+  }
+  // carry [exit, n) to the other buffer; the chain resumes at its first byte
+  const uint64_t keep_n = n - exit;
+  if (keep_n) HIP_TRY(hipMemcpy(st->buf[1 - st->cur], b + exit, keep_n, hipMemcpyDeviceToDevice));
+  st->cur = 1 - st->cur;
+  st->carry = keep_n;
+  st->base += exit;
+  if (final) st->done = true;
+  *out = r;
+  return UGPU_OK;
+}
+
 int ugpu_result_free(ugpu_result* r)
 {
   if (!r) return UGPU_OK;

@@ -115,12 +115,7 @@ class FindResult:
         return [[int(s), int(l), int(c)] for s, l, c in zip(self.start, self.length, self.cap)]
 
 
-def find_all(pattern, data, start=0, offsets=True):
-    """ugpu_find_all: every FIND match of `data` from position `start`."""
-    ptr, n, keep = _buffer_ptr(data)
-    res = ctypes.POINTER(_lib.Result)()
-    check(lib.ugpu_find_all(pattern.handle, ctypes.c_void_p(ptr), n, start,
-                            _lib.MODE_OFFSETS if offsets else _lib.MODE_COUNT, ctypes.byref(res)))
+def _take_result(res, offsets):
     try:
         r = res.contents
         if offsets and r.count:
@@ -131,11 +126,54 @@ def find_all(pattern, data, start=0, offsets=True):
             st = np.zeros(0, np.uint64)
             ln = np.zeros(0, np.uint32)
             cp = np.zeros(0, np.uint32)
-        out = FindResult(r.count, r.digest, r.dcap, st, ln, cp)
+        return FindResult(r.count, r.digest, r.dcap, st, ln, cp)
     finally:
         lib.ugpu_result_free(res)
+
+
+def find_all(pattern, data, start=0, offsets=True):
+    """ugpu_find_all: every FIND match of `data` from position `start`."""
+    ptr, n, keep = _buffer_ptr(data)
+    res = ctypes.POINTER(_lib.Result)()
+    check(lib.ugpu_find_all(pattern.handle, ctypes.c_void_p(ptr), n, start,
+                            _lib.MODE_OFFSETS if offsets else _lib.MODE_COUNT, ctypes.byref(res)))
+    out = _take_result(res, offsets)
     del keep
     return out
+
+
+class Stream:
+    """Streaming FIND over input fed in chunks (ugpu_stream):
+    feed() returns the matches that became final, with absolute offsets."""
+
+    def __init__(self, pattern, keep=0):
+        self.pattern = pattern
+        h = ctypes.c_void_p()
+        check(lib.ugpu_stream_create(pattern.handle, keep, ctypes.byref(h)))
+        self._h = h
+
+    def feed(self, chunk, final=False, offsets=True):
+        ptr, n, keep = _buffer_ptr(chunk)
+        res = ctypes.POINTER(_lib.Result)()
+        check(lib.ugpu_stream_feed(self._h, ctypes.c_void_p(ptr), n, 1 if final else 0,
+                                   _lib.MODE_OFFSETS if offsets else _lib.MODE_COUNT, ctypes.byref(res)))
+        out = _take_result(res, offsets)
+        del keep
+        return out
+
+    def settled(self):
+        return lib.ugpu_stream_settled(self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.ugpu_stream_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Matcher:
