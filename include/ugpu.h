@@ -179,6 +179,19 @@ int ugpu_stream_feed(ugpu_stream *st, const uint8_t *chunk, uint64_t len, int fi
    not be scanned again). */
 uint64_t ugpu_stream_settled(const ugpu_stream *st);
 
+/* --- line-level consumers ---
+   For a device-resident buffer (16-byte aligned; the kernels load whole
+   16-byte granules, so the last granule is read up to its end and the bytes
+   past len are ignored) and its sorted match starts
+   (e.g. from ugpu_scan_offsets): *newlines = number of '\n' bytes in [0, len)
+   (simd nlcount, lib/simd.cpp:62-166), d_line[i] = 1-based line of
+   d_start[i] (AbstractMatcher::lineno(), absmatcher.h:695-766; d_line may be
+   NULL), *matching_lines = number of distinct lines holding a match start
+   (ugrep -c with skip('\n') after each hit, src/ugrep.cpp:10567-10586; equal
+   to ugrep -c whenever matches cannot contain '\n').  Synchronous. */
+int ugpu_lines(const uint8_t *dbuf, uint64_t len, const uint64_t *d_start, uint64_t n, uint64_t *d_line,
+               uint64_t *newlines, uint64_t *matching_lines, void *stream);
+
 /* --- synthetic corpora, generated on device --- */
 #define UGPU_GEN_WORDS 1
 #define UGPU_GEN_PLANTED 2

@@ -146,23 +146,38 @@ def main():
     with open(os.path.join(HERE, "cases.json"), "w") as f:
         json.dump(cases, f)
 
-    # the reference's own goldens (tests/verify.sh:262-271): -U -ounkbT byte offsets
+    write_refgold()
+    print("patterns", len(pats), "cases", len(cases))
+
+
+def write_refgold():
+    """The reference's own goldens (tests/verify.sh:262-271): -U -ounkbT gives
+    line, column and byte offset of every match; -c the matching-line count."""
     refgold = {}
     strip = re.compile(r"\x1b\[[0-9;]*[mK]")
     for pname, fn in (("hello", "Hello_Hello-ounkbT.out"), ("hello_wnhS", "Hello_wnhS-ounkbT.out")):
-        offs = []
+        offs, lines = [], []
         for ln in open(os.path.join(REFTESTS, "out", fn), encoding="latin-1"):
             ln = strip.sub("", ln)
-            m = re.match(r"Hello\.java:\s*\d+:\s*\d+:\s*(\d+):", ln)
+            m = re.match(r"Hello\.java:\s*(\d+):\s*\d+:\s*(\d+):", ln)
             if m:
-                offs.append(int(m.group(1)))
-        refgold[pname] = dict(file="Hello.java", source="tests/out/" + fn, starts=offs)
+                lines.append(int(m.group(1)))
+                offs.append(int(m.group(2)))
+        refgold[pname] = dict(file="Hello.java", source="tests/out/" + fn, starts=offs, lines=lines)
+    for ln in open(os.path.join(REFTESTS, "out", "Hello_Hello-c.out"), encoding="latin-1"):
+        m = re.match(r"Hello\.java:(\d+)", strip.sub("", ln))
+        if m:
+            refgold["hello"]["c_count"] = int(m.group(1))
+            refgold["hello"]["c_source"] = "tests/out/Hello_Hello-c.out"
     cnt = open(os.path.join(REFTESTS, "out", "lorem.utf8-iwco.out"), encoding="latin-1").read()
     refgold["lorem_iwco_count"] = int(strip.sub("", cnt).strip())
     with open(os.path.join(HERE, "refgold.json"), "w") as f:
         json.dump(refgold, f, indent=1)
-    print("patterns", len(pats), "cases", len(cases))
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    if sys.argv[1:] == ["--refgold-only"]:
+        write_refgold()
+    else:
+        main()

@@ -3,6 +3,7 @@ builder (opcode words -> dense device tables) reproduces the reference's
 matches when walked on the CPU with the exact FIND chain."""
 import ctypes
 
+import numpy as np
 import pytest
 
 import ugrep_amd
@@ -177,3 +178,17 @@ def test_transducer_reproduces_reference_matches(patterns, cases):
         assert _xt_find(t, local[c["pattern"]], data) == c["matches"], (c["pattern"], c["input"]["name"])
         done += 1
     assert done > 100
+
+
+def test_line_goldens_restated(refgold):
+    """The line-number rule the ugpu_lines tests check against (1 + newlines
+    before the start; -c = distinct lines of the starts) reproduces the
+    reference's -n and -c outputs for Hello.java."""
+    import os
+    data = np.frombuffer(open(os.path.join(os.path.dirname(__file__), "golden", "Hello.java"), "rb").read(), np.uint8)
+    nlpos = np.flatnonzero(data == 10)
+    for key in ("hello", "hello_wnhS"):
+        g = refgold[key]
+        lines = 1 + np.searchsorted(nlpos, np.asarray(g["starts"]), side="left")
+        assert lines.tolist() == g["lines"]
+    assert len(np.unique(1 + np.searchsorted(nlpos, np.asarray(refgold["hello"]["starts"])))) == refgold["hello"]["c_count"]

@@ -7,7 +7,7 @@ holds the multi-GPU shard stitching (dist.py).
 from ._lib import (GEN_CODE, GEN_PLANTED, GEN_UTF8, GEN_WORDS, MODE_COUNT, MODE_OFFSETS, UgpuError,  # noqa: F401
                    Unsupported, lib)
 from .matcher import (Matcher, Pattern, Scanner, Stream, find_all, gen, host_prefilter,  # noqa: F401
-                      host_tables, host_transducer)
+                      host_tables, host_transducer, lines)
 
 __all__ = ["Pattern", "Matcher", "Scanner", "Stream", "find_all", "gen", "host_tables", "host_prefilter", "Unsupported",
            "UgpuError"]

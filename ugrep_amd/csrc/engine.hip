@@ -538,6 +538,88 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
   return UGPU_OK;
 }
 
+// ---------------------------------------------------------------- lines
+int ugpu_lines(const uint8_t* dbuf, uint64_t len, const uint64_t* d_start, uint64_t n, uint64_t* d_line,
+               uint64_t* newlines, uint64_t* matching_lines, void* stream)
+{
+  if (!dbuf || (n && !d_start)) return fail(UGPU_INVAL, "NULL argument");
+  if (reinterpret_cast<uintptr_t>(dbuf) & 15u) return fail(UGPU_INVAL, "buffer must be 16-byte aligned");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t tile = lines_tile();
+  int dev = 0, cus = 256;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  // wave ranges: whole tiles, about 16 waves per CU, at most kMaxRec records
+  const uint64_t tiles = (len + tile - 1) / tile;
+  uint64_t want = (uint64_t)cus * 16;
+  if (want > (uint64_t)kMaxRec) want = kMaxRec;
+  uint64_t tpw = tiles ? (tiles + want - 1) / want : 1;
+  while (tpw * tile > kMaxRecBytes) --tpw;  // (never for sane sizes; 32-bit offsets)
+  if (tpw == 0) tpw = 1;
+  const uint64_t nw = tiles ? (tiles + tpw - 1) / tpw : 1;
+  LinesParams L{};
+  L.g = dbuf;
+  L.len = len;
+  L.per = tpw * tile;
+  L.nwaves = nw;
+  L.starts = d_start;
+  L.nmatch = n;
+  L.lines = d_line;
+  std::vector<uint64_t> cnt(nw), pre(nw);
+  std::vector<LineRec> recs(nw);
+  uint64_t* d_cnt = nullptr;
+  uint64_t* d_pre = nullptr;
+  LineRec* d_rec = nullptr;
+  auto cleanup = [&]() {
+    if (d_cnt) (void)hipFree(d_cnt);
+    if (d_pre) (void)hipFree(d_pre);
+    if (d_rec) (void)hipFree(d_rec);
+  };
+  hipError_t e;
+  if ((e = hipMalloc(&d_cnt, nw * 8)) != hipSuccess || (e = hipMalloc(&d_pre, nw * 8)) != hipSuccess ||
+      (e = hipMalloc(&d_rec, nw * sizeof(LineRec))) != hipSuccess) {
+    cleanup();
+    return hip_fail(e, "lines buffers");
+  }
+  L.counts = d_cnt;
+  L.prefix = d_pre;
+  L.recs = d_rec;
+  if ((e = launch_nl_count(L, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(cnt.data(), d_cnt, nw * 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+      (e = hipStreamSynchronize(st)) != hipSuccess) {
+    cleanup();
+    return hip_fail(e, "newline count");
+  }
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < nw; ++i) {
+    pre[i] = total;
+    total += cnt[i];
+  }
+  if (newlines) *newlines = total;
+  if (n > 0 || matching_lines) {
+    if ((e = hipMemcpyAsync(d_pre, pre.data(), nw * 8, hipMemcpyHostToDevice, st)) != hipSuccess ||
+        (e = launch_nl_assign(L, st)) != hipSuccess ||
+        (e = hipMemcpyAsync(recs.data(), d_rec, nw * sizeof(LineRec), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess) {
+      cleanup();
+      return hip_fail(e, "line assignment");
+    }
+    // lines of consecutive matches in different waves may coincide
+    uint64_t lines = 0, last = 0;
+    bool any = false;
+    for (uint64_t i = 0; i < nw; ++i) {
+      if (!recs[i].nmatch) continue;
+      lines += recs[i].trans;
+      if (any && recs[i].first_line == last) --lines;
+      last = recs[i].last_line;
+      any = true;
+    }
+    if (matching_lines) *matching_lines = lines;
+  }
+  cleanup();
+  return UGPU_OK;
+}
+
 // ---------------------------------------------------------------- streaming
 // Device buffer holds the unsettled carry followed by the new chunk; each feed
 // scans [0, hi) of it with the chain entering at 0 (the previous settled

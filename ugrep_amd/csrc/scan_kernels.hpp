@@ -108,6 +108,27 @@ hipError_t launch_gen(int kind, uint64_t seed, uint64_t off, uint8_t* dbuf, uint
 hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream_t stream);
 hipError_t sparse_occupancy(const ScanParams& P, size_t smem, int* blocks_per_cu);
 size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates);
+// line-level consumers, lines.hip
+struct LineRec {
+  uint64_t first_line, last_line;  // lines of the wave's first / last match start (0: none)
+  uint64_t trans;                  // matches whose line differs from the previous match's (first included)
+  uint64_t nmatch;
+};
+struct LinesParams {
+  const uint8_t* g;         // 16-byte aligned buffer
+  uint64_t len;             // bytes
+  uint64_t per;             // bytes per wave range (multiple of 4 KiB)
+  uint64_t nwaves;
+  const uint64_t* starts;   // sorted match starts (offsets into g)
+  uint64_t nmatch;
+  uint64_t* counts;         // out (count pass): newlines per wave range
+  const uint64_t* prefix;   // in (assign pass): newlines before each wave range
+  uint64_t* lines;          // out: line of each match start (1-based), may be NULL
+  LineRec* recs;            // out: per-wave line transitions
+};
+hipError_t launch_nl_count(const LinesParams& L, hipStream_t stream);
+hipError_t launch_nl_assign(const LinesParams& L, hipStream_t stream);
+uint32_t lines_tile();
 // dense wave-persistent kernel, dense_kernel.hip
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);
 hipError_t dense_occupancy(uint32_t format, bool cap1, bool xt, size_t smem, int* blocks_per_cu);

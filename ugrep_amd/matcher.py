@@ -285,6 +285,16 @@ class Scanner:
             pass
 
 
+def lines(dptr, length, d_start=0, n=0, d_line=0, stream=0):
+    """ugpu_lines over a 16-byte aligned device buffer: (newlines, matching_lines);
+    fills d_line[i] with the 1-based line of d_start[i] when d_line is given."""
+    nl = ctypes.c_uint64()
+    ml = ctypes.c_uint64()
+    check(lib.ugpu_lines(ctypes.c_void_p(dptr), length, ctypes.c_void_p(d_start), n, ctypes.c_void_p(d_line),
+                         ctypes.byref(nl), ctypes.byref(ml), ctypes.c_void_p(stream)))
+    return nl.value, ml.value
+
+
 def gen(kind, seed, off, dptr, length, stream=0):
     """Generate corpus bytes [off, off+length) on the device (ugpu_gen)."""
     check(lib.ugpu_gen(kind, seed, off, ctypes.c_void_p(dptr), length, ctypes.c_void_p(stream)))
