@@ -247,7 +247,7 @@ def main():
         "matches": res["count"],
         "matches_per_s": round(matches_per_s, 1),
         "digest": res["digest"],
-        "roofline": {"bound": "hbm", "kernel": "sparse_kernel" if info["prefilter_ppm"] else "scan_kernel",
+        "roofline": {"bound": "hbm", "kernel": "sparse_kernel" if info["prefilter_ppm"] else "dense_kernel",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel_ms": round(k_avg, 4), "algorithmic_bytes_per_launch": hi - lo},

@@ -54,8 +54,13 @@ def test_reference_goldens(U, patterns, refgold):
     assert nl == int(np.count_nonzero(data == 10))
 
 
+MODES = ["0", "1", "2"]  # UGPU_LINES_MODE: auto, dense assign pass, sparse (quarter) assign pass
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("pname,kind", [("c2_foobarbaz", 1), ("c3_ident", 3), ("c4_word", 4)])
-def test_corpus_lines(U, patterns, pname, kind):
+def test_corpus_lines(U, patterns, pname, kind, mode, monkeypatch):
+    monkeypatch.setenv("UGPU_LINES_MODE", mode)
     from oracle_lib import gen
     data = gen(kind, 21, 0, 16 << 20)
     r = U.find_all(U.Pattern(patterns[pname]["opc"]), data.tobytes(), offsets=True)
@@ -66,7 +71,9 @@ def test_corpus_lines(U, patterns, pname, kind):
     assert np.array_equal(got[2], want[2])
 
 
-def test_edge_buffers(U):
+@pytest.mark.parametrize("mode", MODES)
+def test_edge_buffers(U, mode, monkeypatch):
+    monkeypatch.setenv("UGPU_LINES_MODE", mode)
     rng = np.random.default_rng(3)
     cases = []
     # newlines on and around 4 KiB tile and 16-byte granule borders, next to 0x0b/0x09
@@ -80,6 +87,11 @@ def test_edge_buffers(U):
     cases.append(np.frombuffer(b"no newline at all" * 500, np.uint8))
     cases.append((rng.integers(0, 4, 1 << 20) * 3 + 7).astype(np.uint8))  # 7, 10, 13, 16: 1/4 newlines
     for d in cases:
+        for nst in (1, 7, 5000):  # sparse to dense match lists
+            starts = np.sort(rng.choice(len(d), size=min(len(d), nst), replace=False))
+            got = _run(U, d, starts)
+            want = _np(d, starts)
+            assert got[0] == want[0] and got[1] == want[1] and np.array_equal(got[2], want[2])
         starts = np.sort(rng.choice(len(d), size=min(len(d), 5000), replace=False))
         got = _run(U, d, starts)
         want = _np(d, starts)
@@ -89,3 +101,19 @@ def test_edge_buffers(U):
     # newline count without matches
     d = cases[3]
     assert _run(U, d, [])[0] == int(np.count_nonzero(d == 10))
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_many_waves_clusters(U, mode, monkeypatch):
+    """64 MiB (thousands of wave ranges): match clusters of > 64 starts inside
+    one quarter and one tile, runs of empty ranges, starts on range borders."""
+    monkeypatch.setenv("UGPU_LINES_MODE", mode)
+    rng = np.random.default_rng(11)
+    n = (64 << 20) + 123
+    d = np.where(rng.random(n) < 0.02, 10, 97).astype(np.uint8)
+    parts = [np.arange(5000, 5300), np.arange(1 << 20, (1 << 20) + 4096, 3),
+             rng.choice(n, 2000, replace=False), np.array([0, 4095, 4096, n - 1])]
+    starts = np.unique(np.concatenate(parts)).astype(np.int64)
+    got = _run(U, d, starts)
+    want = _np(d, starts)
+    assert got[0] == want[0] and got[1] == want[1] and np.array_equal(got[2], want[2])

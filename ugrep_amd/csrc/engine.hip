@@ -20,6 +20,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/ugpu.h"
 #include "scan_kernels.hpp"
@@ -539,6 +540,88 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
 }
 
 // ---------------------------------------------------------------- lines
+namespace {
+
+// Per-call scratch of ugpu_lines, pooled per device so that repeated calls do
+// no hipMalloc/hipFree (hipFree synchronises the device): per-wave counts and
+// prefixes, per-wave -c records, quarter counts (sparse mode) and pinned host
+// copies of the counts and records.
+struct LinesWs {
+  int dev = -1;
+  uint64_t nw_cap = 0, q_cap = 0;
+  uint64_t* d_cnt = nullptr;
+  uint64_t* d_pre = nullptr;
+  LineRec* d_rec = nullptr;
+  uint16_t* d_qc = nullptr;
+  uint64_t* h_cnt = nullptr;
+  uint64_t* h_pre = nullptr;
+  LineRec* h_rec = nullptr;
+
+  void release_wave_arrays()
+  {
+    (void)hipFree(d_cnt);
+    (void)hipFree(d_pre);
+    (void)hipFree(d_rec);
+    (void)hipHostFree(h_cnt);
+    (void)hipHostFree(h_pre);
+    (void)hipHostFree(h_rec);
+    d_cnt = d_pre = nullptr;
+    d_rec = nullptr;
+    h_cnt = h_pre = nullptr;
+    h_rec = nullptr;
+    nw_cap = 0;
+  }
+
+  hipError_t reserve(uint64_t nw, uint64_t quarters)
+  {
+    hipError_t e = hipSuccess;
+    if (nw > nw_cap) {
+      release_wave_arrays();
+      if ((e = hipMalloc(&d_cnt, nw * 8)) != hipSuccess || (e = hipMalloc(&d_pre, nw * 8)) != hipSuccess ||
+          (e = hipMalloc(&d_rec, nw * sizeof(LineRec))) != hipSuccess ||
+          (e = hipHostMalloc(&h_cnt, nw * 8)) != hipSuccess || (e = hipHostMalloc(&h_pre, nw * 8)) != hipSuccess ||
+          (e = hipHostMalloc(&h_rec, nw * sizeof(LineRec))) != hipSuccess) {
+        release_wave_arrays();
+        return e;
+      }
+      nw_cap = nw;
+    }
+    if (quarters > q_cap) {
+      (void)hipFree(d_qc);
+      d_qc = nullptr;
+      q_cap = 0;
+      if ((e = hipMalloc(&d_qc, quarters * 2)) != hipSuccess) return e;
+      q_cap = quarters;
+    }
+    return e;
+  }
+};
+
+std::mutex g_lines_mu;
+std::vector<LinesWs*> g_lines_pool;  // idle workspaces (kept for the process lifetime)
+
+LinesWs* lines_ws_acquire(int dev)
+{
+  std::lock_guard<std::mutex> lk(g_lines_mu);
+  for (size_t i = 0; i < g_lines_pool.size(); ++i)
+    if (g_lines_pool[i]->dev == dev) {
+      LinesWs* w = g_lines_pool[i];
+      g_lines_pool.erase(g_lines_pool.begin() + (long)i);
+      return w;
+    }
+  LinesWs* w = new (std::nothrow) LinesWs;
+  if (w) w->dev = dev;
+  return w;
+}
+
+void lines_ws_release(LinesWs* w)
+{
+  std::lock_guard<std::mutex> lk(g_lines_mu);
+  g_lines_pool.push_back(w);
+}
+
+}  // namespace
+
 int ugpu_lines(const uint8_t* dbuf, uint64_t len, const uint64_t* d_start, uint64_t n, uint64_t* d_line,
                uint64_t* newlines, uint64_t* matching_lines, void* stream)
 {
@@ -557,6 +640,21 @@ int ugpu_lines(const uint8_t* dbuf, uint64_t len, const uint64_t* d_start, uint6
   while (tpw * tile > kMaxRecBytes) --tpw;  // (never for sane sizes; 32-bit offsets)
   if (tpw == 0) tpw = 1;
   const uint64_t nw = tiles ? (tiles + tpw - 1) / tpw : 1;
+  // sparse assign pass when matches are rarer than one per two quarters
+  // (UGPU_LINES_MODE=1/2 forces dense/sparse, for tests)
+  const uint64_t quarters = tiles * (tile / kLinesQuarter);
+  bool sparse = n > 0 && n * 2 < quarters;
+  if (const char* mo = getenv("UGPU_LINES_MODE")) {
+    if (mo[0] == '1') sparse = false;
+    if (mo[0] == '2') sparse = n > 0;
+  }
+  LinesWs* ws = lines_ws_acquire(dev);
+  if (!ws) return fail(UGPU_NOMEM, "lines workspace");
+  hipError_t e = ws->reserve(nw, sparse ? quarters : 0);
+  if (e != hipSuccess) {
+    lines_ws_release(ws);
+    return hip_fail(e, "lines buffers");
+  }
   LinesParams L{};
   L.g = dbuf;
   L.len = len;
@@ -565,59 +663,47 @@ int ugpu_lines(const uint8_t* dbuf, uint64_t len, const uint64_t* d_start, uint6
   L.starts = d_start;
   L.nmatch = n;
   L.lines = d_line;
-  std::vector<uint64_t> cnt(nw), pre(nw);
-  std::vector<LineRec> recs(nw);
-  uint64_t* d_cnt = nullptr;
-  uint64_t* d_pre = nullptr;
-  LineRec* d_rec = nullptr;
-  auto cleanup = [&]() {
-    if (d_cnt) (void)hipFree(d_cnt);
-    if (d_pre) (void)hipFree(d_pre);
-    if (d_rec) (void)hipFree(d_rec);
-  };
-  hipError_t e;
-  if ((e = hipMalloc(&d_cnt, nw * 8)) != hipSuccess || (e = hipMalloc(&d_pre, nw * 8)) != hipSuccess ||
-      (e = hipMalloc(&d_rec, nw * sizeof(LineRec))) != hipSuccess) {
-    cleanup();
-    return hip_fail(e, "lines buffers");
-  }
-  L.counts = d_cnt;
-  L.prefix = d_pre;
-  L.recs = d_rec;
-  if ((e = launch_nl_count(L, st)) != hipSuccess ||
-      (e = hipMemcpyAsync(cnt.data(), d_cnt, nw * 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+  L.counts = ws->d_cnt;
+  L.prefix = ws->d_pre;
+  L.recs = ws->d_rec;
+  L.qcount = sparse ? ws->d_qc : nullptr;
+  int rc = UGPU_OK;
+  if ((e = launch_nl_count(L, sparse, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(ws->h_cnt, ws->d_cnt, nw * 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
       (e = hipStreamSynchronize(st)) != hipSuccess) {
-    cleanup();
-    return hip_fail(e, "newline count");
-  }
-  uint64_t total = 0;
-  for (uint64_t i = 0; i < nw; ++i) {
-    pre[i] = total;
-    total += cnt[i];
-  }
-  if (newlines) *newlines = total;
-  if (n > 0 || matching_lines) {
-    if ((e = hipMemcpyAsync(d_pre, pre.data(), nw * 8, hipMemcpyHostToDevice, st)) != hipSuccess ||
-        (e = launch_nl_assign(L, st)) != hipSuccess ||
-        (e = hipMemcpyAsync(recs.data(), d_rec, nw * sizeof(LineRec), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipStreamSynchronize(st)) != hipSuccess) {
-      cleanup();
-      return hip_fail(e, "line assignment");
-    }
-    // lines of consecutive matches in different waves may coincide
-    uint64_t lines = 0, last = 0;
-    bool any = false;
+    rc = hip_fail(e, "newline count");
+  } else {
+    uint64_t total = 0;
     for (uint64_t i = 0; i < nw; ++i) {
-      if (!recs[i].nmatch) continue;
-      lines += recs[i].trans;
-      if (any && recs[i].first_line == last) --lines;
-      last = recs[i].last_line;
-      any = true;
+      ws->h_pre[i] = total;
+      total += ws->h_cnt[i];
     }
-    if (matching_lines) *matching_lines = lines;
+    if (newlines) *newlines = total;
+    if (n > 0 || matching_lines) {
+      if ((e = hipMemcpyAsync(ws->d_pre, ws->h_pre, nw * 8, hipMemcpyHostToDevice, st)) != hipSuccess ||
+          (e = launch_nl_assign(L, sparse, st)) != hipSuccess ||
+          (e = hipMemcpyAsync(ws->h_rec, ws->d_rec, nw * sizeof(LineRec), hipMemcpyDeviceToHost, st)) !=
+              hipSuccess ||
+          (e = hipStreamSynchronize(st)) != hipSuccess) {
+        rc = hip_fail(e, "line assignment");
+      } else {
+        // lines of consecutive matches in different waves may coincide
+        uint64_t lines = 0, last = 0;
+        bool any = false;
+        for (uint64_t i = 0; i < nw; ++i) {
+          const LineRec& r = ws->h_rec[i];
+          if (!r.nmatch) continue;
+          lines += r.trans;
+          if (any && r.first_line == last) --lines;
+          last = r.last_line;
+          any = true;
+        }
+        if (matching_lines) *matching_lines = lines;
+      }
+    }
   }
-  cleanup();
-  return UGPU_OK;
+  lines_ws_release(ws);
+  return rc;
 }
 
 // ---------------------------------------------------------------- streaming

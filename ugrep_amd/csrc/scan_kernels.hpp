@@ -125,10 +125,14 @@ struct LinesParams {
   const uint64_t* prefix;   // in (assign pass): newlines before each wave range
   uint64_t* lines;          // out: line of each match start (1-based), may be NULL
   LineRec* recs;            // out: per-wave line transitions
+  uint16_t* qcount;         // sparse mode: newlines per 1 KiB quarter (count pass out, assign pass in)
 };
-hipError_t launch_nl_count(const LinesParams& L, hipStream_t stream);
-hipError_t launch_nl_assign(const LinesParams& L, hipStream_t stream);
+// sparse = the assign pass loads only the 1 KiB quarters holding match starts
+// (the count pass also writes qcount); dense = it reloads the whole buffer
+hipError_t launch_nl_count(const LinesParams& L, bool sparse, hipStream_t stream);
+hipError_t launch_nl_assign(const LinesParams& L, bool sparse, hipStream_t stream);
 uint32_t lines_tile();
+constexpr uint32_t kLinesQuarter = 1024;
 // dense wave-persistent kernel, dense_kernel.hip
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);
 hipError_t dense_occupancy(uint32_t format, bool cap1, bool xt, size_t smem, int* blocks_per_cu);
