@@ -26,7 +26,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import ugrep_amd  # noqa: E402
-from ugrep_amd.dist import shard_bounds, stitch  # noqa: E402
+from ugrep_amd.dist import gather_offsets, shard_bounds, stitch  # noqa: E402
 
 METRIC = "GB/s scanned + matches/s, 16 GiB synthetic buffer, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
@@ -132,6 +132,9 @@ def main():
     ap.add_argument("--halo", type=int, default=1 << 20, help="readable bytes past a shard end")
     ap.add_argument("--cpu-sample-mib", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--offsets", action="store_true",
+                    help="each step also materialises the match records (start, len, accept) in HBM and, "
+                         "for N > 1, all-gathers them to every rank (SURVEY.md §8e step 4)")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also scans the whole logical stream alone and checks the stitched totals")
     args = ap.parse_args()
@@ -187,6 +190,21 @@ def main():
         return dict(count=t.count, digest=t.digest, dcap=t.dcap,
                     exit=None if t.exit == (1 << 64) - 1 else t.exit + lo)
 
+    recs_dev = {}  # --offsets: device record arrays, grown outside the timed steps when possible
+
+    def records(count):
+        if recs_dev.get("cap", -1) < count:
+            cap = count + count // 8 + 1024
+            recs_dev.update(cap=cap, start=torch.empty(cap, dtype=torch.int64, device=dev),
+                            len=torch.empty(cap, dtype=torch.int32, device=dev),
+                            acc=torch.empty(cap, dtype=torch.int32, device=dev))
+        sc.offsets(recs_dev["start"].data_ptr(), recs_dev["len"].data_ptr(), recs_dev["acc"].data_ptr(), count,
+                   sptr)
+        st, ln, ac = recs_dev["start"][:count], recs_dev["len"][:count], recs_dev["acc"][:count]
+        if world > 1:
+            st, ln, ac = gather_offsets(st.to(xdev), ln.to(xdev), ac.to(xdev))
+        return st, ln, ac
+
     def step():
         sc.scan(ptr, 0, hi - lo, n_read, eof, lo, sptr)
         t = sc.totals()
@@ -194,6 +212,12 @@ def main():
         rec = dict(entry=t.entry + lo, exit=t.exit + lo, count=t.count, digest=t.digest, dcap=t.dcap)
         if world > 1:
             rec = stitch(rec, fix_fn, device=xdev)
+        if args.offsets:
+            count = t.count
+            if world > 1 and rec["entries"][rank] != lo:  # chain re-entered this shard: re-scan from there
+                sc.scan(ptr, rec["entries"][rank] - lo, hi - lo, n_read, eof, lo, sptr)
+                count = sc.totals().count
+            rec["records"] = records(count)
         return rec
 
     for _ in range(args.warmup):
@@ -254,6 +278,13 @@ def main():
     }
     if verified is not None:
         out["verified_whole_stream"] = verified
+    if args.offsets:
+        st, ln, _ = res["records"]
+        m64 = (1 << 64) - 1
+        dg = int((st * 31 + ln.to(torch.int64)).sum().item()) & m64  # int64 sums wrap like the u64 digest
+        out["offsets"] = {"records": int(st.numel()), "bytes_per_record": 16,
+                          "gathered_to": "all ranks" if world > 1 else "local",
+                          "digest_matches_totals": int(st.numel()) == res["count"] and dg == res["digest"]}
     tr = measured_traffic(args.config, hi - lo)
     if tr:
         out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]

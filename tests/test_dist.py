@@ -90,3 +90,50 @@ def test_stitch_nonsynchronising(patterns):
     cnt, dg, dc, _ = OracleDfa(opc).find(data)
     assert (out["count"], out["digest"], out["dcap"]) == (cnt, dg, dc)
     assert out["fixes"] == 1
+
+
+def _gather_worker(rank, world, port, recs, dst, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        from ugrep_amd.dist import gather_offsets
+        mine = np.asarray(recs[rank], dtype=np.int64).reshape(-1, 3)
+        out = gather_offsets(torch.from_numpy(mine[:, 0].copy()), torch.from_numpy(mine[:, 1].astype(np.int32)),
+                             torch.from_numpy(mine[:, 2].astype(np.int32)), dst=dst)
+        q.put((rank, None if out is None else [t.tolist() for t in out]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,dst", [(2, None), (3, None), (3, 1)])
+def test_gather_offsets(patterns, world, dst):
+    """Per-shard records of the true chain, exchanged, equal one sequential scan's list."""
+    from oracle_lib import OracleDfa, gen
+    from ugrep_amd.dist import shard_bounds
+    data = gen(3, 5, 0, 50021)
+    opc = patterns["c3_ident"]["opc"]
+    _, _, _, lst = OracleDfa(opc).find(data, want_list=True)
+    recs = []
+    for r in range(world):
+        lo, hi, _, _ = shard_bounds(len(data), world, r, 0)
+        recs.append([m for m in lst if lo <= m[0] < hi])
+    recs[1] = []  # an empty shard on the way
+    want = [m for r in recs for m in r]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, recs, dst, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        if dst is not None and r != dst:
+            assert res[r] is None
+            continue
+        s, ln, cp = res[r]
+        assert [list(t) for t in zip(s, ln, cp)] == [list(m) for m in want]

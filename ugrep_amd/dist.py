@@ -39,7 +39,9 @@ def stitch(rec, fix_fn, device="cpu", group=None):
     rec    : dict(entry, exit, count, digest, dcap) of this rank's shard, positions global.
     fix_fn : fix_fn(old_entry, new_entry) -> dict(count, digest, dcap, exit) correction for
              THIS rank's shard (exit None if unchanged); only called on the rank that owns it.
-    Returns dict(count, digest, dcap, exit, fixes) identical on every rank.
+    Returns dict(count, digest, dcap, exit, fixes, entries, counts) identical on every
+    rank; entries[r] / counts[r] are shard r's true chain entry and match count (a
+    rank whose entry moved re-scans from it to materialise its records).
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -69,7 +71,8 @@ def stitch(rec, fix_fn, device="cpu", group=None):
             if v[3]:
                 recs[r]["exit"] = v[4]
         prev_exit = recs[r]["exit"]
-    out = dict(count=0, digest=0, dcap=0, exit=prev_exit, fixes=fixes)
+    out = dict(count=0, digest=0, dcap=0, exit=prev_exit, fixes=fixes,
+               entries=[r["entry"] for r in recs], counts=[r["count"] for r in recs])
     for r in recs:
         out["count"] = (out["count"] + r["count"]) & MASK64
         out["digest"] = (out["digest"] + r["digest"]) & MASK64
@@ -84,3 +87,41 @@ def shard_bounds(total, world, rank, halo):
     hi = total if rank == world - 1 else lo + per
     read_end = min(total, hi + halo)
     return lo, hi, read_end, read_end == total
+
+
+def gather_offsets(start, length, cap, group=None, dst=None):
+    """Exchange the final match records of every shard.
+
+    start (int64, global byte offsets), length and cap (int32) are this rank's
+    records in chain order, on the collective's device.  The records are
+    packed 16 B each ((start, len << 32 | cap)), padded to the largest shard's
+    count and exchanged with one all_gather (dst None: every rank gets the
+    whole list) or one gather to rank dst (others get None); the result is the
+    concatenation in rank order, which is global chain order because shards
+    are contiguous and ordered.  RCCL has no all_gatherv; padding costs at most
+    (world - 1) x the count spread, and the counts travel first in one
+    8-byte all_gather.
+    """
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = start.device
+    n = torch.tensor([start.numel()], dtype=torch.int64, device=dev)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    counts = [int(x.item()) for x in ns]
+    m = max(max(counts), 1)
+    pack = torch.zeros((m, 2), dtype=torch.int64, device=dev)
+    k = counts[rank]
+    if k:
+        pack[:k, 0] = start[:k].to(torch.int64)
+        pack[:k, 1] = (length[:k].to(torch.int64) << 32) | (cap[:k].to(torch.int64) & 0xFFFFFFFF)
+    if dst is None:
+        parts = [torch.empty_like(pack) for _ in range(world)]
+        dist.all_gather(parts, pack, group=group)
+    else:
+        parts = [torch.empty_like(pack) for _ in range(world)] if rank == dst else None
+        dist.gather(pack, parts, dst=dst, group=group)
+        if rank != dst:
+            return None
+    allp = torch.cat([parts[r][:counts[r]] for r in range(world)])
+    return allp[:, 0].clone(), (allp[:, 1] >> 32).to(torch.int32), (allp[:, 1] & 0xFFFFFFFF).to(torch.int32)
