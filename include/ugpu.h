@@ -192,6 +192,30 @@ uint64_t ugpu_stream_settled(const ugpu_stream *st);
 int ugpu_lines(const uint8_t *dbuf, uint64_t len, const uint64_t *d_start, uint64_t n, uint64_t *d_line,
                uint64_t *newlines, uint64_t *matching_lines, void *stream);
 
+/* --- binary-file detection ---
+   Device buffers of any alignment (the kernel reads the enclosing 16-byte
+   granules).  Synchronous. */
+
+/* reflex::isutf8(s, s + len) (lib/simd.cpp:169-421): *first_bad = UINT64_MAX
+   when the bytes are valid UTF-8 without NUL (as the reference defines it:
+   surrogates and 3/4-byte overlongs pass), else the offset of the first byte
+   that fails (len for a sequence cut off by the end). */
+int ugpu_check_utf8(const uint8_t *dbuf, uint64_t len, uint64_t *first_bad, void *stream);
+
+/* memchr(s, '\0', len): *pos = offset of the first NUL or UINT64_MAX. */
+int ugpu_find_nul(const uint8_t *dbuf, uint64_t len, uint64_t *pos, void *stream);
+
+/* ugrep's is_binary(s, n) (src/ugrep.cpp:699-711) and, with
+   UGPU_BIN_INIT_WINDOW, GrepWorker::init_is_binary() (:3998-4015) over a
+   window of len bytes (a trailing UTF-8 sequence is not judged).
+   flags: UGPU_BIN_NULL_DATA = --null-data (never binary by content);
+   UGPU_BIN_NUL_ONLY = -a/-U without -W (binary iff it holds a NUL);
+   otherwise binary iff not isutf8. */
+#define UGPU_BIN_NULL_DATA 1u
+#define UGPU_BIN_NUL_ONLY 2u
+#define UGPU_BIN_INIT_WINDOW 4u
+int ugpu_is_binary(const uint8_t *dbuf, uint64_t len, uint32_t flags, int *binary, void *stream);
+
 /* --- synthetic corpora, generated on device --- */
 #define UGPU_GEN_WORDS 1
 #define UGPU_GEN_PLANTED 2

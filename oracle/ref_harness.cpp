@@ -41,6 +41,7 @@
 #define private public
 #define protected public
 #include <reflex/matcher.h>
+#include <reflex/simd.h>
 #undef private
 #undef protected
 
@@ -148,10 +149,26 @@ static Tally scan(const reflex::Pattern& pat, char *base, size_t n, size_t bias,
 
 int main(int argc, char **argv)
 {
-  if (argc < 4)
+  if (argc < 4 && !(argc == 2 && std::string(argv[1]) == "isutf8"))
   {
-    fprintf(stderr, "usage: ref_harness dump|find|bench re|F PATTERN ...\n");
+    fprintf(stderr, "usage: ref_harness dump|find|bench re|F PATTERN ... | isutf8 < specs\n");
     return 2;
+  }
+  if (std::string(argv[1]) == "isutf8")
+  {
+    // reflex::isutf8 (lib/simd.cpp:169) on each input spec read from stdin,
+    // one per line; prints 1/0 per line (tests/golden/make_utf8_golden.py)
+    char line[1 << 16];
+    while (fgets(line, sizeof(line), stdin))
+    {
+      std::string spec(line);
+      while (!spec.empty() && (spec.back() == '\n' || spec.back() == '\r'))
+        spec.pop_back();
+      std::vector<char> b = load_input(spec.c_str());
+      size_t n = b.size() - 1;
+      printf("%d\n", reflex::isutf8(b.data(), b.data() + n) ? 1 : 0);
+    }
+    return 0;
   }
   std::string cmd = argv[1], mode = argv[2], rx = argv[3];
   std::string conv = build_regex(mode, rx);

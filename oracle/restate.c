@@ -317,3 +317,72 @@ void orc_gen(int kind, uint64_t seed, uint64_t off, uint8_t *buf, uint64_t len)
 {
   gen_fill(kind, seed, off, buf, len);
 }
+
+/*
+ * Binary-file detection.
+ *
+ * orc_isutf8 -- reflex::isutf8(s, s + n), restated from the reference's scalar
+ *   loop (lib/simd.cpp:391-418): skip ASCII > 0; a lead must be c2..f4 and is
+ *   followed by 1, 2 or 3 continuation bytes (80..bf) by its range (c2, e0,
+ *   f0); NUL and everything else fail.  The SIMD paths (simd.cpp:174-300,
+ *   simd_avx2.cpp:82-150) accept the same language; tests/test_oracle.py pins
+ *   this against the compiled reference on the golden cases.
+ * orc_utf8_first_bad -- the first failing position under the same language,
+ *   in the local form the GPU kernel uses (a byte needs a continuation iff one
+ *   of the 3 bytes before it is a lead announcing one; the end needs none):
+ *   n + 1 when valid, n for a sequence cut off by the end.
+ * orc_init_window -- GrepWorker::init_is_binary's trim of a trailing UTF-8
+ *   sequence (src/ugrep.cpp:3998-4015): returns -1 for "binary", else the
+ *   number of bytes to judge.
+ */
+int orc_isutf8(const uint8_t *s, uint64_t n)
+{
+  const uint8_t *e = s + n;
+  while (s < e)
+  {
+    int8_t c = 0;
+    while (s < e && (c = (int8_t)*s) > 0)
+      ++s;
+    if (s++ >= e)
+      break;
+    if (c < -62 || c > -12 || s >= e || (*s++ & 0xc0) != 0x80)
+      return 0;
+    if (c >= -32 && (s >= e || (*s++ & 0xc0) != 0x80))
+      return 0;
+    if (c >= -16 && (s >= e || (*s++ & 0xc0) != 0x80))
+      return 0;
+  }
+  return 1;
+}
+
+uint64_t orc_utf8_first_bad(const uint8_t *s, uint64_t n)
+{
+  uint64_t i;
+  for (i = 0; i <= n; ++i)
+  {
+    int need = (i >= 1 && s[i - 1] >= 0xc0) || (i >= 2 && s[i - 2] >= 0xe0) || (i >= 3 && s[i - 3] >= 0xf0);
+    if (i == n)
+      return need ? n : n + 1;
+    uint8_t c = s[i];
+    int cont = (c & 0xc0) == 0x80;
+    int valid = (c >= 0x01 && c <= 0x7f) || cont || (c >= 0xc2 && c <= 0xf4);
+    if (!valid || need != cont)
+      return i;
+  }
+  return n + 1;
+}
+
+int64_t orc_init_window(const uint8_t *buf, uint64_t avail)
+{
+  if (avail == 0)
+    return 0;
+  if ((buf[avail - 1] & 0x80) == 0x80)
+  {
+    uint64_t k = avail < 4 ? avail : 4;
+    while (k > 0 && (buf[--avail] & 0xc0) == 0x80)
+      --k;
+    if ((buf[avail] & 0xc0) != 0xc0)
+      return -1;
+  }
+  return (int64_t)avail;
+}

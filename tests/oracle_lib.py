@@ -33,6 +33,12 @@ def _load():
     L.orc_chain_exit.argtypes = [V, V, U64, U64, U64]
     L.orc_chain_exit.restype = U64
     L.orc_gen.argtypes = [ctypes.c_int, U64, U64, V, U64]
+    L.orc_isutf8.argtypes = [V, U64]
+    L.orc_isutf8.restype = ctypes.c_int
+    L.orc_utf8_first_bad.argtypes = [V, U64]
+    L.orc_utf8_first_bad.restype = U64
+    L.orc_init_window.argtypes = [V, U64]
+    L.orc_init_window.restype = ctypes.c_int64
     return L
 
 
@@ -81,6 +87,46 @@ def gen(kind, seed, off, length):
     buf = np.zeros(length, np.uint8)
     L.orc_gen(kind, seed, off, buf.ctypes.data, length)
     return buf
+
+
+def _u8(data):
+    return np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
+
+
+def isutf8(data):
+    """reflex::isutf8 restated (lib/simd.cpp:391-418)."""
+    b = _u8(data)
+    return bool(L.orc_isutf8(b.ctypes.data, b.size))
+
+
+def utf8_first_bad(data):
+    """First failing position (len for a cut-off sequence) or None when valid."""
+    b = _u8(data)
+    r = L.orc_utf8_first_bad(b.ctypes.data, b.size)
+    return None if r == b.size + 1 else int(r)
+
+
+def first_nul(data):
+    b = _u8(data)
+    z = np.flatnonzero(b == 0)
+    return int(z[0]) if z.size else None
+
+
+def is_binary(data, null_data=False, nul_only=False, init_window=False):
+    """ugrep's is_binary (src/ugrep.cpp:699-711), with init_is_binary's trim
+    (:3998-4015) when init_window."""
+    b = _u8(data)
+    n = b.size
+    if init_window:
+        w = L.orc_init_window(b.ctypes.data, n)
+        if w < 0:
+            return True
+        n = int(w)
+    if null_data:
+        return False
+    if nul_only:
+        return first_nul(b[:n]) is not None
+    return not isutf8(b[:n])
 
 
 def case_input(inp):

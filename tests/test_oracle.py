@@ -84,3 +84,36 @@ def test_generator_cells_are_independent():
         full = gen(kind, 42, 0, 1 << 16)
         part = gen(kind, 42, 777, 5000)
         assert np.array_equal(full[777:5777], part)
+
+
+def test_isutf8_restatement_pinned_to_reference():
+    """orc_isutf8 (restated scalar loop) and orc_utf8_first_bad (the kernel's
+    local rule) both agree with the compiled reference's reflex::isutf8 on every
+    golden case (tests/golden/make_utf8_golden.py)."""
+    import json
+    import os
+    import oracle_lib as O
+    with open(os.path.join(os.path.dirname(__file__), "golden", "utf8.json")) as f:
+        gold = json.load(f)
+    assert len(gold["cases"]) > 3000
+    for h, ref in gold["cases"]:
+        b = bytes.fromhex(h)
+        assert O.isutf8(b) == ref, h
+        assert (O.utf8_first_bad(b) is None) == ref, h
+    for inp in gold["inputs"]:
+        assert O.isutf8(case_input(inp)) == inp["isutf8"]
+
+
+def test_init_window_trim():
+    """GrepWorker::init_is_binary's trailing-sequence rule (src/ugrep.cpp:3998-4015)."""
+    import oracle_lib as O
+    assert O.is_binary(b"", init_window=True) is False
+    assert O.is_binary(b"abc\xc3", init_window=True) is False  # cut-off lead ignored
+    assert O.is_binary(b"abc\xc3") is True
+    assert O.is_binary(b"abc\xe2\x82", init_window=True) is False
+    assert O.is_binary(b"ab\x80", init_window=True) is True  # continuation after ASCII
+    assert O.is_binary(b"a\x80\x80\x80\x80", init_window=True) is True  # 4 continuations back
+    assert O.is_binary(b"\xc3\xa9", init_window=True) is False
+    assert O.is_binary(b"a\x00b", nul_only=True) is True
+    assert O.is_binary(b"a\xffb", nul_only=True) is False
+    assert O.is_binary(b"a\x00b", null_data=True) is False

@@ -18,7 +18,7 @@ def db(d, sub):
     return sqlite3.connect(f[0]) if f else None
 
 
-def main(d):
+def main(d, match=("sparse_kernel", "dense_kernel", "scan_kernel")):
     kernels = []
     c = db(d, "trace")
     if c:
@@ -26,7 +26,7 @@ def main(d):
                 "select name, total_calls, total_duration, average, percentage from top_kernels"):
             kernels.append({"name": name, "calls": calls, "total_us": round(total, 3), "avg_us": round(avg, 3),
                             "pct": round(pct, 3)})
-    scan = [k for k in kernels if any(n in k["name"] for n in ("sparse_kernel", "dense_kernel", "scan_kernel"))]
+    scan = [k for k in kernels if any(n in k["name"] for n in match)]
     dom = max(scan, key=lambda k: k["total_us"]) if scan else None
     counters = {}
     for sub in ("pmc1", "pmc2", "pmc3"):
@@ -47,10 +47,11 @@ def main(d):
         pass
     res = {"kernels": kernels, "dominant": dom, "counters_last_dispatch": counters}
     if bench:
-        res["bench"] = {k: bench[k] for k in ("value", "ms_per_step", "matches", "roofline", "config")}
+        res["bench"] = {k: bench[k] for k in ("value", "ms_per_step", "matches", "roofline", "config") if k in bench} \
+            if "roofline" in bench else bench
     if "FETCH_SIZE" in counters:
         res["hbm_bytes_per_launch"] = int(counters["FETCH_SIZE"] * 1024 * 2)
-        if bench:
+        if bench and "roofline" in bench:
             alg = bench["roofline"]["algorithmic_bytes_per_launch"]
             res["algorithmic_bytes_per_launch"] = alg
             res["traffic_over_algorithmic"] = round(res["hbm_bytes_per_launch"] / alg, 4)
@@ -60,4 +61,5 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    # usage: pmc_summary.py DIR [kernel-name-substring ...]
+    main(sys.argv[1], tuple(sys.argv[2:]) or ("sparse_kernel", "dense_kernel", "scan_kernel"))

@@ -24,6 +24,8 @@ MODE_OFFSETS = 1
 
 GEN_WORDS, GEN_PLANTED, GEN_CODE, GEN_UTF8 = 1, 2, 3, 4
 
+BIN_NULL_DATA, BIN_NUL_ONLY, BIN_INIT_WINDOW = 1, 2, 4
+
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u16p = ctypes.POINTER(ctypes.c_uint16)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -90,6 +92,9 @@ def _load():
         "ugpu_stream_settled": (ctypes.c_uint64, [V]),
         "ugpu_lines": (ctypes.c_int, [V, ctypes.c_uint64, V, ctypes.c_uint64, V, P(ctypes.c_uint64),
                                       P(ctypes.c_uint64), V]),
+        "ugpu_check_utf8": (ctypes.c_int, [V, ctypes.c_uint64, P(ctypes.c_uint64), V]),
+        "ugpu_find_nul": (ctypes.c_int, [V, ctypes.c_uint64, P(ctypes.c_uint64), V]),
+        "ugpu_is_binary": (ctypes.c_int, [V, ctypes.c_uint64, ctypes.c_uint32, P(ctypes.c_int), V]),
         "ugpu_last_error": (ctypes.c_char_p, []),
         "ugpu_version": (ctypes.c_char_p, []),
     }

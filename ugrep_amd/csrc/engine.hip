@@ -706,6 +706,128 @@ int ugpu_lines(const uint8_t* dbuf, uint64_t len, const uint64_t* d_start, uint6
   return rc;
 }
 
+// ---------------------------------------------------------------- binary detection
+namespace {
+
+// One device result slot and its pinned host copy, pooled per device.
+struct SlotWs {
+  int dev = -1;
+  uint64_t* d = nullptr;
+  uint64_t* h = nullptr;
+};
+std::mutex g_slot_mu;
+std::vector<SlotWs*> g_slot_pool;
+
+SlotWs* slot_acquire(int dev)
+{
+  {
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    for (size_t i = 0; i < g_slot_pool.size(); ++i)
+      if (g_slot_pool[i]->dev == dev) {
+        SlotWs* w = g_slot_pool[i];
+        g_slot_pool.erase(g_slot_pool.begin() + (long)i);
+        return w;
+      }
+  }
+  SlotWs* w = new (std::nothrow) SlotWs;
+  if (!w) return nullptr;
+  w->dev = dev;
+  if (hipMalloc(&w->d, 8) != hipSuccess || hipHostMalloc(&w->h, 8) != hipSuccess) {
+    (void)hipFree(w->d);
+    delete w;
+    return nullptr;
+  }
+  return w;
+}
+
+void slot_release(SlotWs* w)
+{
+  std::lock_guard<std::mutex> lk(g_slot_mu);
+  g_slot_pool.push_back(w);
+}
+
+// First failing byte of dbuf[0, len) (isutf8, or NUL with nul) or ~0.
+int utf8_scan(const uint8_t* dbuf, uint64_t len, bool nul, uint64_t* pos, void* stream)
+{
+  if (!dbuf && len) return fail(UGPU_INVAL, "NULL buffer");
+  if (!pos) return fail(UGPU_INVAL, "NULL result pointer");
+  *pos = ~0ull;
+  if (len == 0) return UGPU_OK;
+  if (!is_device_ptr(dbuf)) return fail(UGPU_INVAL, "buffer must be device memory");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int dev = 0, cus = 256;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  Utf8Params U{};
+  U.head = reinterpret_cast<uintptr_t>(dbuf) & 15u;
+  U.g = dbuf - U.head;
+  U.len = len;
+  U.span = (U.head + len + 15u) & ~15ull;
+  const uint64_t tile = utf8_tile();
+  const uint64_t tiles = (U.span + tile - 1) / tile;
+  const uint64_t want = (uint64_t)cus * 16;  // about 16 waves per CU
+  const uint64_t tpw = (tiles + want - 1) / want;
+  U.per = tpw * tile;
+  U.nwaves = (tiles + tpw - 1) / tpw;
+  SlotWs* w = slot_acquire(dev);
+  if (!w) return fail(UGPU_NOMEM, "result slot");
+  U.out = w->d;
+  hipError_t e;
+  int rc = UGPU_OK;
+  if ((e = hipMemsetAsync(w->d, 0xff, 8, st)) != hipSuccess || (e = launch_utf8(U, nul, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(w->h, w->d, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+      (e = hipStreamSynchronize(st)) != hipSuccess) {
+    rc = hip_fail(e, nul ? "NUL scan" : "UTF-8 check");
+  } else {
+    *pos = *w->h == ~0ull ? ~0ull : *w->h - U.head;
+  }
+  slot_release(w);
+  return rc;
+}
+
+}  // namespace
+
+int ugpu_check_utf8(const uint8_t* dbuf, uint64_t len, uint64_t* first_bad, void* stream)
+{
+  return utf8_scan(dbuf, len, false, first_bad, stream);
+}
+
+int ugpu_find_nul(const uint8_t* dbuf, uint64_t len, uint64_t* pos, void* stream)
+{
+  return utf8_scan(dbuf, len, true, pos, stream);
+}
+
+int ugpu_is_binary(const uint8_t* dbuf, uint64_t len, uint32_t flags, int* binary, void* stream)
+{
+  if (!binary) return fail(UGPU_INVAL, "NULL result pointer");
+  *binary = 0;
+  if (flags & UGPU_BIN_INIT_WINDOW) {
+    // GrepWorker::init_is_binary (src/ugrep.cpp:3998-4015): do not judge a
+    // UTF-8 sequence cut off by the window end
+    if (len == 0) return UGPU_OK;
+    uint8_t tail[4] = {0, 0, 0, 0};
+    const uint64_t nt = len < 4 ? len : 4;
+    HIP_TRY(hipMemcpy(tail + (4 - nt), dbuf + len - nt, nt, hipMemcpyDeviceToHost));
+    const uint8_t* t = tail + 4;  // t[-1] = last byte
+    uint64_t avail = len;
+    if ((t[-1] & 0x80) == 0x80) {
+      uint64_t n = nt;
+      while (n > 0 && (t[(int64_t)(--avail) - (int64_t)len] & 0xc0) == 0x80) --n;
+      if ((t[(int64_t)avail - (int64_t)len] & 0xc0) != 0xc0) {
+        *binary = 1;
+        return UGPU_OK;
+      }
+    }
+    len = avail;
+  }
+  // is_binary (src/ugrep.cpp:699-711)
+  if (flags & UGPU_BIN_NULL_DATA) return UGPU_OK;
+  uint64_t pos = ~0ull;
+  const int rc = utf8_scan(dbuf, len, (flags & UGPU_BIN_NUL_ONLY) != 0, &pos, stream);
+  if (rc == UGPU_OK) *binary = pos != ~0ull;
+  return rc;
+}
+
 // ---------------------------------------------------------------- streaming
 // Device buffer holds the unsettled carry followed by the new chunk; each feed
 // scans [0, hi) of it with the chain entering at 0 (the previous settled

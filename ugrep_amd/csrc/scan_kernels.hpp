@@ -133,6 +133,20 @@ hipError_t launch_nl_count(const LinesParams& L, bool sparse, hipStream_t stream
 hipError_t launch_nl_assign(const LinesParams& L, bool sparse, hipStream_t stream);
 uint32_t lines_tile();
 constexpr uint32_t kLinesQuarter = 1024;
+// binary-file detection, utf8.hip: first byte failing reflex::isutf8 (or, with
+// nul, the first 0x00) of the data bytes [head, head + len) of the 16-byte
+// aligned span g[0, span), atomically min'ed into *out (preset to ~0)
+struct Utf8Params {
+  const uint8_t* g;  // 16-byte aligned
+  uint64_t head;     // data start within the span (< 16)
+  uint64_t len;      // data bytes
+  uint64_t span;     // head + len rounded up to 16
+  uint64_t per;      // bytes per wave range (multiple of the 4 KiB tile)
+  uint64_t nwaves;
+  uint64_t* out;     // span offset of the first failing byte (head + len: truncated sequence)
+};
+hipError_t launch_utf8(const Utf8Params& U, bool nul, hipStream_t stream);
+uint32_t utf8_tile();
 // dense wave-persistent kernel, dense_kernel.hip
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);
 hipError_t dense_occupancy(uint32_t format, bool cap1, bool xt, size_t smem, int* blocks_per_cu);

@@ -17,7 +17,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import check, lib
+from ._lib import BIN_INIT_WINDOW, BIN_NUL_ONLY, BIN_NULL_DATA, check, lib
 
 
 def _as_u32(opc):
@@ -293,6 +293,36 @@ def lines(dptr, length, d_start=0, n=0, d_line=0, stream=0):
     check(lib.ugpu_lines(ctypes.c_void_p(dptr), length, ctypes.c_void_p(d_start), n, ctypes.c_void_p(d_line),
                          ctypes.byref(nl), ctypes.byref(ml), ctypes.c_void_p(stream)))
     return nl.value, ml.value
+
+
+def check_utf8(dptr, length, stream=0):
+    """reflex::isutf8 over device bytes (ugpu_check_utf8): None when valid,
+    else the offset of the first failing byte (length for a cut-off sequence)."""
+    r = ctypes.c_uint64()
+    check(lib.ugpu_check_utf8(ctypes.c_void_p(dptr), length, ctypes.byref(r), ctypes.c_void_p(stream)))
+    return None if r.value == 0xFFFFFFFFFFFFFFFF else r.value
+
+
+def isutf8(dptr, length, stream=0):
+    """reflex::isutf8(s, s + length) (lib/simd.cpp:169) on a device buffer."""
+    return check_utf8(dptr, length, stream) is None
+
+
+def find_nul(dptr, length, stream=0):
+    """memchr(s, '\\0', length) on a device buffer: offset or None."""
+    r = ctypes.c_uint64()
+    check(lib.ugpu_find_nul(ctypes.c_void_p(dptr), length, ctypes.byref(r), ctypes.c_void_p(stream)))
+    return None if r.value == 0xFFFFFFFFFFFFFFFF else r.value
+
+
+def is_binary(dptr, length, null_data=False, nul_only=False, init_window=False, stream=0):
+    """ugrep's is_binary (src/ugrep.cpp:699-711); init_window adds
+    init_is_binary's trailing-sequence trim (:3998-4015)."""
+    flags = (BIN_NULL_DATA if null_data else 0) | (BIN_NUL_ONLY if nul_only else 0) | \
+        (BIN_INIT_WINDOW if init_window else 0)
+    r = ctypes.c_int()
+    check(lib.ugpu_is_binary(ctypes.c_void_p(dptr), length, flags, ctypes.byref(r), ctypes.c_void_p(stream)))
+    return bool(r.value)
 
 
 def gen(kind, seed, off, dptr, length, stream=0):
