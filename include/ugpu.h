@@ -118,6 +118,14 @@ int ugpu_tables_prefilter_host(const uint32_t *opc, uint32_t nop, uint8_t *ft, i
 int ugpu_tables_transducer_host(const uint32_t *opc, uint32_t nop, uint16_t *xtrans, uint32_t xtrans_cap,
                                 int *local);
 
+/* Host-only: the immediate FIND transducer of xi_kernel (ugrep_amd/csrc/
+   tables.hpp): for restart-local tables whose walks accept on every byte,
+   u8 ids (walk state << 3 | SYNC 4 | IN 2 | START 1), rows*256 bytes of
+   next ids.  *immediate = 0 (nothing written) when the table does not qualify;
+   pass xid = NULL to query *rows first. */
+int ugpu_tables_immediate_host(const uint32_t *opc, uint32_t nop, uint8_t *xid, uint32_t xid_cap, uint32_t *rows,
+                               uint8_t *sync_byte, int *immediate);
+
 /* --- whole-buffer FIND (Matcher::buffer(); while (find()) ...) --- */
 
 /* buf may be host or device memory, len bytes, search starts at `start`

@@ -192,3 +192,32 @@ def test_line_goldens_restated(refgold):
         lines = 1 + np.searchsorted(nlpos, np.asarray(g["starts"]), side="left")
         assert lines.tolist() == g["lines"]
     assert len(np.unique(1 + np.searchsorted(nlpos, np.asarray(refgold["hello"]["starts"])))) == refgold["hello"]["c_count"]
+
+
+@pytest.mark.parametrize("pname", ["c3_ident", "digits", "dot"])
+def test_immediate_transducer_semantics(patterns, cases, pname):
+    """The byte-id table of xi_kernel (tables.hpp 'immediate'): one walk over the
+    ids gives count = #START, sum start = sum of START positions and sum len =
+    #IN bytes; digest / dcap must equal the oracle's on seeded corpora and on
+    the golden small cases.  Non-immediate tables are refused."""
+    from oracle_lib import OracleDfa, gen
+    from ugrep_amd.matcher import host_immediate
+    opc = patterns[pname]["opc"]
+    x, sync = host_immediate(opc)
+    assert all(x[0, sync] == x[r, sync] for r in range(x.shape[0]))  # a sync byte resets every walk
+    assert x[0, sync] & 4 and not x[0, sync] & 3
+    M = (1 << 64) - 1
+    inputs = [gen(kind, 5, 0, 40000) for kind in (1, 3, 4)]
+    inputs += [case_input(c["input"]) for c in cases if c["pattern"] == pname]
+    for buf in inputs:
+        ids = np.zeros(buf.size, np.uint8)
+        s = 0
+        for i, b in enumerate(buf.tolist()):
+            s = x[s, b]
+            ids[i] = s
+        st = np.flatnonzero(ids & 1)
+        cnt, ss, ln = st.size, int(st.sum()), int(np.count_nonzero(ids & 2))
+        o = OracleDfa(opc).find(buf)
+        assert (cnt, (31 * ss + ln) & M) == (o[0], o[1])
+    for other in ("c2_foobarbaz", "c4_word", "s_plus", "float"):
+        assert host_immediate(patterns[other]["opc"]) is None

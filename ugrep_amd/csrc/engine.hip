@@ -34,6 +34,7 @@ struct ugpu_dfa {
   uint32_t ntrans_pad = 0;
   uint16_t* d_trans = nullptr;
   uint16_t* d_xtrans = nullptr;  // FIND transducer (restart-local tables on the dense path)
+  uint8_t* d_xid = nullptr;      // immediate transducer ids (xi_kernel), COUNT scans
   uint8_t* d_cls = nullptr;
   uint32_t* d_caps = nullptr;
 };
@@ -43,7 +44,13 @@ struct ugpu_scanner {
   int device = 0;
   int max_rec = 0;       // chain records per scan (blocks or waves)
   bool sparse = false;   // prefiltered wave-persistent kernel (sparse_kernel.hip)
-  size_t smem = 0;
+  bool xi = false;       // COUNT scans run xi_kernel (immediate tables); OFFSETS use the dense kernel
+  size_t smem = 0;       // sparse / dense kernel
+  size_t xi_smem = 0;
+  int xi_rec = 0;        // chain records of an xi scan
+  bool last_xi = false;  // the last ugpu_scan ran xi_kernel
+  const uint8_t* last_buf = nullptr;
+  uint64_t last_args[5] = {0, 0, 0, 0, 0};  // lo, hi, read_end, at_eof, bias of the last scan
   BlockRec* d_recs = nullptr;
   uint64_t* d_entries = nullptr;
   uint64_t* d_obase = nullptr;
@@ -84,6 +91,8 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
 {
   P.trans = d->d_trans;
   P.xtrans = d->d_xtrans;
+  P.xid = d->d_xid;
+  P.xid_rows = d->t.xid_rows;
   P.cls = d->d_cls;
   P.caps = d->d_caps;
   P.ntrans_pad = d->ntrans_pad;
@@ -129,16 +138,19 @@ void geometry(ScanParams& P, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint
 }
 
 void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi,
-                  uint64_t read_end, uint64_t& off)
+                  uint64_t read_end, uint64_t& off, bool xi = false)
 {
-  if (s->sparse)
+  if (xi)
+    geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xi_unit(), xi_waves(), off);
+  else if (s->sparse)
     geometry(P, dbuf, lo, hi, read_end, s->max_rec, kWaveTile, kSpWaves, off);
   else
     geometry(P, dbuf, lo, hi, read_end, s->max_rec, dense_unit(s->dfa->t.format), dense_waves(s->dfa->t.format), off);
 }
 
-hipError_t launch_main(const ugpu_scanner* s, const ScanParams& P, bool write, hipStream_t st)
+hipError_t launch_main(const ugpu_scanner* s, const ScanParams& P, bool write, hipStream_t st, bool xi = false)
 {
+  if (xi) return launch_xi(P, s->xi_smem, st);
   if (s->sparse) return launch_sparse(P, write, s->smem, st);
   return launch_dense(P, s->dfa->t.format, write, s->smem, st);
 }
@@ -201,6 +213,13 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       return hip_fail(e, "transducer table upload");
     }
   }
+  if (d->t.immediate && !d->t.filter && d->t.cap1 != 0) {
+    if ((e = hipMalloc(&d->d_xid, d->t.xid.size())) != hipSuccess ||
+        (e = hipMemcpy(d->d_xid, d->t.xid.data(), d->t.xid.size(), hipMemcpyHostToDevice)) != hipSuccess) {
+      ugpu_dfa_destroy(d);
+      return hip_fail(e, "immediate transducer upload");
+    }
+  }
   *out = d;
   return UGPU_OK;
 }
@@ -210,6 +229,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   if (!d) return UGPU_OK;
   if (d->d_trans) (void)hipFree(d->d_trans);
   if (d->d_xtrans) (void)hipFree(d->d_xtrans);
+  if (d->d_xid) (void)hipFree(d->d_xid);
   if (d->d_cls) (void)hipFree(d->d_cls);
   if (d->d_caps) (void)hipFree(d->d_caps);
   delete d;
@@ -287,6 +307,23 @@ int ugpu_tables_transducer_host(const uint32_t* opc, uint32_t nop, uint16_t* xtr
   return UGPU_OK;
 }
 
+int ugpu_tables_immediate_host(const uint32_t* opc, uint32_t nop, uint8_t* xid, uint32_t xid_cap, uint32_t* rows,
+                               uint8_t* sync_byte, int* immediate)
+{
+  if (!immediate || !rows) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *immediate = t.immediate ? 1 : 0;
+  *rows = t.xid_rows;
+  if (sync_byte) *sync_byte = t.sync_byte;
+  if (!t.immediate || !xid) return UGPU_OK;
+  if (xid_cap < t.xid.size()) return fail(UGPU_INVAL, "xid capacity too small");
+  std::copy(t.xid.begin(), t.xid.end(), xid);
+  return UGPU_OK;
+}
+
 int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
 {
   if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
@@ -318,6 +355,22 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   if (const char* env = std::getenv("UGPU_MAX_GRID")) {
     int v = std::atoi(env);
     if (v >= 1 && v <= kMaxRec) s->max_rec = v;
+  }
+  // immediate tables: COUNT scans on xi_kernel (UGPU_XI=0 keeps the dense kernel)
+  const char* xenv = std::getenv("UGPU_XI");
+  if (!s->sparse && dfa->d_xid && !(xenv && xenv[0] == '0')) {
+    s->xi_smem = (size_t)dfa->t.xid_rows * 256;
+    int xpc = 0;
+    HIP_TRY(xi_occupancy(s->xi_smem, &xpc));
+    if (xpc >= 1) {
+      s->xi = true;
+      int xg = prop.multiProcessorCount * xpc * (int)xi_waves();
+      s->xi_rec = xg > kMaxRec ? kMaxRec : xg;
+      if (const char* env = std::getenv("UGPU_MAX_GRID")) {
+        int v = std::atoi(env);
+        if (v >= 1 && v <= kMaxRec) s->xi_rec = v;
+      }
+    }
   }
   HIP_TRY(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
   HIP_TRY(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
@@ -356,7 +409,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P{};
   fill_tables(P, s->dfa);
-  geometry_for(P, s, dbuf, lo, hi, read_end, s->off);
+  geometry_for(P, s, dbuf, lo, hi, read_end, s->off, s->xi);
   P.delta = (int64_t)bias - (int64_t)s->off;
   P.at_eof = at_eof ? 1u : 0u;
   if (const char* ab = std::getenv("UGPU_ABLATE")) P.ablate = (uint32_t)std::atoi(ab);
@@ -367,12 +420,19 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   P.out_base_out = s->d_obase;
   HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
   HIP_TRY(hipEventRecord(s->ev0, st));
-  HIP_TRY(launch_main(s, P, false, st));
+  HIP_TRY(launch_main(s, P, false, st, s->xi));
   HIP_TRY(hipEventRecord(s->ev1, st));
   HIP_TRY(launch_fix(P, s->dfa->t.format, st));
   HIP_TRY(hipMemcpyAsync(s->h_tot, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   s->last = P;
+  s->last_xi = s->xi;
+  s->last_buf = dbuf;
+  s->last_args[0] = lo;
+  s->last_args[1] = hi;
+  s->last_args[2] = read_end;
+  s->last_args[3] = at_eof ? 1u : 0u;
+  s->last_args[4] = bias;
   s->stream = st;
   s->have_scan = true;
   return UGPU_OK;
@@ -409,6 +469,23 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
   if (!s || !s->have_scan) return fail(UGPU_INVAL, "no scan issued");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P = s->last;
+  if (s->last_xi) {
+    // xi_kernel has no record-writing pass: redo the chain records with the
+    // dense kernel's geometry (COUNT + fix), then its WRITE pass
+    P = ScanParams{};
+    fill_tables(P, s->dfa);
+    uint64_t off = 0;
+    geometry_for(P, s, s->last_buf, s->last_args[0], s->last_args[1], s->last_args[2], off, false);
+    P.delta = (int64_t)s->last_args[4] - (int64_t)off;
+    P.at_eof = (uint32_t)s->last_args[3];
+    P.recs = s->d_recs;
+    P.flags = s->d_flags;
+    P.totals = s->d_tot;
+    P.entries_out = s->d_entries;
+    P.out_base_out = s->d_obase;
+    HIP_TRY(launch_main(s, P, false, st));
+    HIP_TRY(launch_fix(P, s->dfa->t.format, st));
+  }
   P.entries = s->d_entries;
   P.out_base = s->d_obase;
   P.out_start = d_start;

@@ -79,6 +79,8 @@ struct ScanParams {
   uint32_t nstates;
   const uint16_t* trans;
   const uint16_t* xtrans;  // FIND transducer table or NULL (dense kernel, tables.hpp)
+  const uint8_t* xid;      // immediate transducer byte ids (xi_kernel, tables.hpp) or NULL
+  uint32_t xid_rows;
   const uint8_t* cls;
   const uint32_t* caps;
   uint32_t ntrans_pad;   // u16 entries, multiple of 8
@@ -147,6 +149,11 @@ struct Utf8Params {
 };
 hipError_t launch_utf8(const Utf8Params& U, bool nul, hipStream_t stream);
 uint32_t utf8_tile();
+// immediate-transducer kernel, xi_kernel.hip (COUNT mode only)
+hipError_t launch_xi(const ScanParams& P, size_t smem, hipStream_t stream);
+hipError_t xi_occupancy(size_t smem, int* blocks_per_cu);
+uint32_t xi_unit();
+uint32_t xi_waves();
 // dense wave-persistent kernel, dense_kernel.hip
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);
 hipError_t dense_occupancy(uint32_t format, bool cap1, bool xt, size_t smem, int* blocks_per_cu);

@@ -352,6 +352,57 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
         }
     }
   }
+  // immediate transducer (tables.hpp, xi_kernel.hip)
+  if (t.restart_local && start_sid < first_acc) {
+    std::vector<int> sig(S, -1);  // walk states reachable from start -> sigma
+    std::vector<uint32_t> order;
+    sig[start_sid] = 0;
+    order.push_back(start_sid);
+    bool ok = true;
+    for (size_t i = 0; i < order.size() && ok; ++i)
+      for (int c = 0; c < 256 && ok; ++c) {
+        const uint32_t n = nxt[(size_t)order[i] * 256 + c];
+        if (n == 0) continue;
+        if (n == start_sid || n < first_acc) ok = false;  // re-enters start, or a walk state that does not accept
+        if (ok && sig[n] < 0) {
+          sig[n] = (int)order.size();
+          order.push_back(n);
+        }
+      }
+    std::vector<bool> sync(256, false);
+    int first_sync = -1;
+    for (int c = 0; ok && c < 256; ++c) {
+      bool y = nxt[(size_t)start_sid * 256 + c] == 0;
+      for (size_t i = 1; i < order.size() && y; ++i) y = nxt[(size_t)order[i] * 256 + c] == 0;
+      sync[c] = y;
+      if (y && first_sync < 0) first_sync = c;
+    }
+    if (ok && order.size() <= 32 && first_sync >= 0) {
+      t.immediate = true;
+      t.sync_byte = (uint8_t)first_sync;
+      t.xid_rows = (uint32_t)order.size() * 8;
+      t.xid.assign((size_t)t.xid_rows * 256, 0);
+      for (uint32_t id = 0; id < t.xid_rows; ++id) {
+        const uint32_t sg = id >> 3, s = order[sg];
+        for (int c = 0; c < 256; ++c) {
+          const uint32_t nx = nxt[(size_t)s * 256 + c];
+          uint32_t to = 0, st = 0;
+          if (nx) {
+            to = (uint32_t)sig[nx];
+            st = sg == 0 ? 1u : 0u;  // leaving start begins a match
+          } else {
+            const uint32_t r = nxt[(size_t)start_sid * 256 + c];  // the walk dies (or none runs): restart here
+            if (r) {
+              to = (uint32_t)sig[r];
+              st = 1;
+            }
+          }
+          t.xid[(size_t)id * 256 + c] =
+              (uint8_t)(to << 3 | (sync[c] ? XI_Y : 0u) | (to ? XI_IN : 0u) | (st ? XI_ST : 0u));
+        }
+      }
+    }
+  }
   t.start = start_sid * R;
   t.accepting = S - first_acc;
   t.accb = (t.accepting > 0) ? first_acc * R : 0x10000u;

@@ -60,7 +60,24 @@ struct DfaTables {
   // tests acceptance.
   bool restart_local = false;
   std::vector<uint16_t> xtrans;  // states * row (empty unless restart_local)
+  // Immediate FIND transducer (xi_kernel.hip), for restart-local tables whose
+  // walks accept on every byte (every live state other than start accepts,
+  // nothing re-enters start): a match is then exactly one walk, it starts at
+  // the byte that leaves the start state and ends where the walk dies.  Byte
+  // ids (u8) carry the walk state and the events of the byte just read:
+  //   id = sigma << 3 | Y << 2 | IN << 1 | ST
+  //   ST  a match starts at this byte      IN  this byte lies inside a match
+  //   Y   this is a sync byte: it kills every walk and starts none, so every
+  //       FIND chain is in the start state after it
+  // and xid[id * 256 + byte] = next id (rows of ids sharing sigma are equal).
+  // Needs sigma < 32 and at least one sync byte.
+  bool immediate = false;
+  uint32_t xid_rows = 0;        // ids (table rows)
+  uint8_t sync_byte = 0;        // smallest sync byte
+  std::vector<uint8_t> xid;     // xid_rows * 256
 };
+
+constexpr uint8_t XI_ST = 1, XI_IN = 2, XI_Y = 4;
 
 constexpr uint16_t XT_DEAD = 1;  // the walk died on this byte; the row is the restart state
 constexpr uint16_t XT_LIVE = 2;  // the restart at this byte is alive (a walk begins here)

@@ -62,6 +62,19 @@ def host_transducer(opc):
     return x if loc.value else None
 
 
+def host_immediate(opc):
+    """Immediate transducer of xi_kernel: (xid table as uint8[rows, 256], sync byte) or None."""
+    a, p = _as_u32(opc)
+    rows, sb, imm = ctypes.c_uint32(), ctypes.c_uint8(), ctypes.c_int()
+    check(lib.ugpu_tables_immediate_host(p, len(a), None, 0, ctypes.byref(rows), ctypes.byref(sb), ctypes.byref(imm)))
+    if not imm.value:
+        return None
+    x = np.zeros(rows.value * 256, np.uint8)
+    check(lib.ugpu_tables_immediate_host(p, len(a), x.ctypes.data_as(_lib.c_u8p), x.size, ctypes.byref(rows),
+                                         ctypes.byref(sb), ctypes.byref(imm)))
+    return x.reshape(rows.value, 256), sb.value
+
+
 class Pattern:
     """Compiled pattern (opcode words) with its device tables."""
 
