@@ -87,7 +87,10 @@ def cpu_baseline(cfg, sample, threads):
                 sample="%d MiB, oracle restatement (dense-table walker), %d threads" % (sample >> 20, threads))
 
 
-def measured_traffic(cfg, nbytes):
+KERNELS = {0: "sparse_kernel", 1: "dense_kernel", 2: "xi_kernel"}
+
+
+def measured_traffic(cfg, nbytes, kernel):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
     PMC summary (profiles/traffic.json, written from tools/profile.sh runs:
     FETCH_SIZE x 1024 x 2 on gfx950), when it was taken on this config and size."""
@@ -96,7 +99,7 @@ def measured_traffic(cfg, nbytes):
             t = json.load(f).get(cfg)
     except (OSError, ValueError):
         return None
-    if not t or t.get("algorithmic_bytes_per_launch") != nbytes:
+    if not t or t.get("algorithmic_bytes_per_launch") != nbytes or kernel not in t.get("kernel", ""):
         return None
     return t
 
@@ -271,7 +274,7 @@ def main():
         "matches": res["count"],
         "matches_per_s": round(matches_per_s, 1),
         "digest": res["digest"],
-        "roofline": {"bound": "hbm", "kernel": "sparse_kernel" if info["prefilter_ppm"] else "dense_kernel",
+        "roofline": {"bound": "hbm", "kernel": KERNELS[info["kernel"]],
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel_ms": round(k_avg, 4), "algorithmic_bytes_per_launch": hi - lo},
@@ -285,7 +288,7 @@ def main():
         out["offsets"] = {"records": int(st.numel()), "bytes_per_record": 16,
                           "gathered_to": "all ranks" if world > 1 else "local",
                           "digest_matches_totals": int(st.numel()) == res["count"] and dg == res["digest"]}
-    tr = measured_traffic(args.config, hi - lo)
+    tr = measured_traffic(args.config, hi - lo, KERNELS[info["kernel"]])
     if tr:
         out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
         out["roofline"]["traffic_source"] = tr["source"]

@@ -34,7 +34,8 @@ c_u64p = ctypes.POINTER(ctypes.c_uint64)
 
 class DfaInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in
-                ("states", "classes", "row", "format", "table_bytes", "prefilter_ppm", "first_bytes", "accepting")]
+                ("states", "classes", "row", "format", "table_bytes", "prefilter_ppm", "first_bytes", "accepting",
+                 "kernel")]
 
 
 class Totals(ctypes.Structure):

@@ -247,6 +247,8 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->prefilter_ppm = d->t.filter ? (uint32_t)(d->t.fdensity * 1e6) + 1 : 0;
   info->first_bytes = d->t.first_bytes;
   info->accepting = d->t.accepting;
+  const char* xenv = std::getenv("UGPU_XI");
+  info->kernel = (d->t.filter && d->t.format == FMT_BYTE) ? 0u : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u : 1u;
   return UGPU_OK;
 }
 
@@ -267,6 +269,7 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
+  info->kernel = (t.filter && t.format == FMT_BYTE) ? 0u : (t.immediate && t.cap1 != 0) ? 2u : 1u;
   if (start) *start = t.start;
   if (accb) *accb = t.accb;
   if (trans) {

@@ -72,7 +72,9 @@ struct ScanParams {
   uint64_t rend;      // walks may read bytes < rend
   int64_t delta;      // reported start = position + delta
   uint32_t at_eof;    // rend is the end of the stream
-  uint32_t ablate;    // benchmarking only (UGPU_ABLATE, sparse kernel): 1 loads, 2 + prefilter, 3 no walks
+  uint32_t ablate;    // benchmarking only (UGPU_ABLATE; sparse kernel: 1 loads, 2 + prefilter, 3 no walks;
+                      // dense: 4 no fix-up, 5 no tails; xi: 6 loads only)
+  uint32_t zero;      // always 0 (keeps prefetch loads alive in xi_kernel)
   uint64_t t0, t1, tpb;  // tiles [t0, t1), tiles per record
   uint32_t unit;         // bytes per tile (kWaveTile, or dense_unit())
   uint32_t nrec;         // chain records (blocks or waves)

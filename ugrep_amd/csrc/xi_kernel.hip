@@ -38,17 +38,63 @@ namespace ugpu {
 
 namespace {
 
-constexpr int kXS = 1024;          // lane segment bytes
+#ifndef UGPU_XI_SEG
+#define UGPU_XI_SEG 1024
+#endif
+#ifndef UGPU_XI_PADLDS
+// Extra LDS per workgroup, capping xi_kernel at 3 workgroups (12 waves) per CU:
+// measured on C3 16 GiB, 3 waves per SIMD beat 4 (4.49 vs 5.39 ms) and 2 (5.64):
+// more waves keep more lane lines (64 per wave, 1 KiB apart) in flight.
+#define UGPU_XI_PADLDS 49152
+#endif
+constexpr int kXS = UGPU_XI_SEG;   // lane segment bytes
 constexpr int kXTile = 64 * kXS;   // wave tile
-constexpr int kXBlk = 64;          // bytes per block (4 x 16 B per lane)
+#ifndef UGPU_XI_BLK
+#define UGPU_XI_BLK 64
+#endif
+#ifndef UGPU_XI_STAGE
+#define UGPU_XI_STAGE 0  // 1: coalesced loads staged through LDS rows
+#endif
+constexpr int kXBlk = UGPU_XI_BLK;  // bytes per block: one 128-byte line per lane, read by back-to-back loads
+constexpr int kXLd = kXBlk / 16;    // 16-byte loads per lane per block
+// Staging: per block the wave loads 64 segments x kXBlk bytes coalesced --
+// load j, lane l reads bytes [16 (l % G), +16) of segment (64 / kXLd) j + l / G,
+// G = kXLd lanes per line -- and writes them to its LDS rows (pitch kXPitch,
+// 34 dwords: two lanes share a bank at most when reading their rows).
+constexpr int kXG = kXLd;                  // lanes sharing one segment line in a load
+constexpr int kXPitch = kXBlk + 8;         // LDS row bytes per segment
+constexpr int kXBuf = 64 * kXPitch;        // LDS bytes per wave
 constexpr int kXBlocks = kXS / kXBlk;
 constexpr int kXWaves = 4;         // waves per workgroup (one staged table)
+
+#ifndef UGPU_XI_NT
+#define UGPU_XI_NT 0  // 1: non-temporal main-loop loads
+#endif
 
 __device__ __forceinline__ uint4 xload16(__amdgpu_buffer_rsrc_t rs, uint32_t off)
 {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
   return uint4{v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ uint4 xload16m(__amdgpu_buffer_rsrc_t rs, uint32_t off)  // main loop
+{
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, UGPU_XI_NT ? 2 : 0);
+  return uint4{v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ void xsync()
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t xload4(__amdgpu_buffer_rsrc_t rs, uint32_t off)
+{
+  return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t xrsrc(const uint8_t* base, uint64_t readable)
@@ -99,18 +145,21 @@ __device__ __forceinline__ void xdword(const uint8_t* T, uint32_t w, uint32_t& i
   cI = __builtin_amdgcn_udot4(Q & 0x02020202u, 0x01010101u, cI, false);
 }
 
-// 16 dwords (one 64-byte block); bb = block byte offset in the segment
-template <bool MASK>
-__device__ __forceinline__ void xblock(const uint8_t* T, const uint4 (&v)[4], uint32_t& id, XSum& a, bool& synced,
+// One block (kXBlk bytes of the lane's segment; dot4 position weights
+// 0..kXBlk-1); bb = block byte offset in the segment.  The bytes come from the
+// lane's LDS row (staged loads) or from registers (direct loads).
+template <bool MASK, class SRC>
+__device__ __forceinline__ void xblock(const uint8_t* T, const SRC& src, uint32_t& id, XSum& a, bool& synced,
                                        uint32_t& fs, uint32_t bb)
 {
   uint32_t cS = 0, wS = 0, cI = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+  for (int k = 0; k < kXBlk / 8; ++k) {
+    const uint2 v = src(k);
+    const uint32_t w[2] = {v.x, v.y};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t d = (uint32_t)(4 * k + j);  // dword index in the block
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t d = (uint32_t)(2 * k + j);  // dword index in the block
       const uint32_t wj = (4 * d) | ((4 * d + 1) << 8) | ((4 * d + 2) << 16) | ((4 * d + 3) << 24);
       xdword<MASK>(T, w[j], id, wj, cS, wS, cI, synced, fs, bb + 4 * d);
     }
@@ -119,6 +168,19 @@ __device__ __forceinline__ void xblock(const uint8_t* T, const uint4 (&v)[4], ui
   a.pos += wS + bb * cS;
   a.ins2 += cI;
 }
+
+struct XRow {  // staged: the lane's LDS row
+  const uint2* row;
+  __device__ __forceinline__ uint2 operator()(int k) const { return row[k]; }
+};
+
+struct XRegs {  // direct: registers
+  const uint4* v;
+  __device__ __forceinline__ uint2 operator()(int k) const
+  {
+    return (k & 1) ? uint2{v[k >> 1].z, v[k >> 1].w} : uint2{v[k >> 1].x, v[k >> 1].y};
+  }
+};
 
 // Per-byte walk of one lane (tails and the edge tiles): returns the next id and
 // adds the byte's events when counting.
@@ -137,6 +199,11 @@ __device__ __forceinline__ uint32_t xsel4(const uint4& v, uint32_t j)
 // Past the range end hi only the walk crossing hi goes on.  Returns the chain
 // position where the lane's coverage ends: after the sync byte, the first
 // chain position >= hi, or the readable end; ~0 for lanes not active.
+__device__ __forceinline__ uint32_t xdist(uint64_t lim, uint64_t base)  // lim - base clamped to [0, 64]
+{
+  return lim > base ? (lim - base < 64 ? (uint32_t)(lim - base) : 64u) : 0u;
+}
+
 __device__ __forceinline__ uint64_t xtail(const uint8_t* T, const uint8_t* g, uint64_t ts, uint32_t o,
                                           uint32_t seg, uint32_t& id, XSum& a, uint64_t hi, uint64_t rend,
                                           uint32_t at_eof, uint32_t& ovf, bool act)
@@ -144,48 +211,54 @@ __device__ __forceinline__ uint64_t xtail(const uint8_t* T, const uint8_t* g, ui
   uint64_t xit = ~0ull;
   const uint64_t rend16 = (rend + 15) & ~uint64_t(15);
   // (the resource moves with c: tails may be longer than 32-bit offsets; the
-  // next 16 bytes load while these are walked)
+  // next 16 bytes load while these are walked; per-byte work is 32-bit,
+  // relative to the chunk)
   uint4 vn = xload16(xrsrc(g + ts, rend16 > ts ? rend16 - ts : 0), o);
   for (uint64_t c = 0; __ballot(act); c += 16) {
     const uint4 v = vn;
     const uint64_t cb = ts + c + 16;
     vn = xload16(xrsrc(g + cb, rend16 > cb ? rend16 - cb : 0), o);
+    const uint64_t base = ts + o + c;  // position of byte 0 of this chunk
+    const uint32_t dh = xdist(hi, base), dr = xdist(rend, base);
+    uint32_t cn = 0, ps = 0, in2 = 0, stop = 0xffffffffu;
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
-      const uint64_t r = o + c + k;  // tile-relative position
-      const uint64_t q = ts + r;
       bool go = act;
-      if (go && q >= hi && !(id & XI_IN)) {  // no walk crosses into q: the chain is at q
-        xit = q;
+      if (go && k >= dh && !(id & XI_IN)) {  // no walk crosses into this byte: the chain is here
+        stop = k;
         act = go = false;
       }
-      if (go && q >= rend) {  // readable end: at EOF the walk ends there
+      if (go && k >= dr) {  // readable end: at EOF the walk ends there
         if (!at_eof && (id & XI_IN)) ovf |= 1;
-        xit = q;
+        stop = k;
         act = go = false;
       }
       const uint32_t e = xbyte(T, id, xsel4(v, k >> 2), k & 3);
       if (go) {
-        if (q >= hi) {
-          if ((e & XI_ST) || !(e & XI_IN)) {  // the walk crossing hi ended at q
-            xit = q;
+        if (k >= dh) {
+          if ((e & XI_ST) || !(e & XI_IN)) {  // the walk crossing hi ended here
+            stop = k;
             act = false;
           } else {
-            a.ins2 += XI_IN;
+            in2 += XI_IN;
           }
         } else {
           const uint32_t st = e & XI_ST;
-          a.cnt += st;
-          a.pos += st ? r - seg : 0ull;
-          a.ins2 += e & XI_IN;
+          cn += st;
+          ps += st ? k : 0u;
+          in2 += e & XI_IN;
           if (e & XI_Y) {
-            xit = q + 1;
+            stop = k + 1;
             act = false;
           }
         }
         id = e;
       }
     }
+    a.cnt += cn;
+    a.pos += (uint64_t)cn * (o + c - seg) + ps;
+    a.ins2 += in2;
+    if (stop != 0xffffffffu) xit = base + stop;
   }
   return xit;
 }
@@ -210,52 +283,60 @@ __device__ __forceinline__ uint64_t xslow_lane(const uint8_t* T, const uint8_t* 
     const uint4 v = vn;
     const uint64_t cb = ts + c + 16;
     vn = xload16(xrsrc(g + cb, rend16 > cb ? rend16 - cb : 0), seg);
+    const uint64_t base = ts + seg + c;  // position of byte 0 of this chunk
+    const uint32_t dh = xdist(hi, base), dr = xdist(rend, base), dl = xdist(wlo, base);
+    const uint32_t df = fresh >= base && fresh - base < 16 ? (uint32_t)(fresh - base) : 0xffffffffu;
+    const uint32_t dseg = c >= (uint64_t)kXS ? 0u : (uint32_t)(kXS - c);  // bytes left in the segment
+    uint32_t cn = 0, ps = 0, in2 = 0, stop = 0xffffffffu, fsk = 0xffffffffu;
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
-      const uint64_t r = c + k;  // segment-relative position
-      const uint64_t q = ts + seg + r;
-      bool go = act && q >= wlo;
-      if (go && q == fresh) {
+      bool go = act && k >= dl;
+      if (go && k == df) {
         id = 0;
         synced = true;
       }
-      if (go && !synced && r >= (uint64_t)kXS) act = go = false;  // no sync in the segment: covered by a tail
-      if (go && q >= hi && !(synced && (id & XI_IN))) {
-        if (synced) xit = q;
+      if (go && !synced && k >= dseg) act = go = false;  // no sync in the segment: covered by a tail
+      if (go && k >= dh && !(synced && (id & XI_IN))) {
+        if (synced) stop = k;
         act = go = false;
       }
-      if (go && q >= rend) {
+      if (go && k >= dr) {
         if (synced) {
           if (!at_eof && (id & XI_IN)) ovf |= 1;
-          xit = q;
+          stop = k;
         }
         act = go = false;
       }
       const uint32_t e = xbyte(T, id, xsel4(v, k >> 2), k & 3);
       if (go) {
-        if (q >= hi) {
+        if (k >= dh) {
           if ((e & XI_ST) || !(e & XI_IN)) {
-            xit = q;
+            stop = k;
             act = false;
           } else {
-            a.ins2 += XI_IN;
+            in2 += XI_IN;
           }
         } else if (synced) {
           const uint32_t st = e & XI_ST;
-          a.cnt += st;
-          a.pos += st ? r : 0ull;
-          a.ins2 += e & XI_IN;
-          if ((e & XI_Y) && r >= (uint64_t)kXS) {  // the tail ends at a sync byte
-            xit = q + 1;
+          cn += st;
+          ps += st ? k : 0u;
+          in2 += e & XI_IN;
+          if ((e & XI_Y) && k >= dseg) {  // the tail ends at a sync byte
+            stop = k + 1;
             act = false;
           }
         } else if (e & XI_Y) {
           synced = true;
-          fs = q;
+          fsk = k;
         }
         id = e;
       }
     }
+    a.cnt += cn;
+    a.pos += (uint64_t)cn * c + ps;
+    a.ins2 += in2;
+    if (stop != 0xffffffffu) xit = base + stop;
+    if (fsk != 0xffffffffu) fs = base + fsk;
   }
   return xit;
 }
@@ -291,9 +372,22 @@ __device__ __forceinline__ void xfold(const XSum& a, uint64_t base, uint64_t& cn
 
 }  // namespace
 
-__global__ __launch_bounds__(kXWaves * 64) void xi_kernel(ScanParams P)
+// ROWS = table capacity (ids); a static LDS array lets the table address fold
+// into the ds_read offset field (an extern array costs an add per byte)
+#ifndef UGPU_XI_MINW
+#define UGPU_XI_MINW 4  // waves per SIMD the register budget must allow (4: 128 VGPRs, no spills)
+#endif
+template <int ROWS>
+__global__ __launch_bounds__(kXWaves * 64, UGPU_XI_MINW) void xi_kernel(ScanParams P)
 {
-  extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
+  __shared__ __attribute__((aligned(16))) uint8_t xsm[ROWS * 256];
+#if UGPU_XI_STAGE
+  __shared__ __attribute__((aligned(16))) uint8_t xbuf[kXWaves * kXBuf];
+#endif
+#if UGPU_XI_PADLDS
+  __shared__ uint8_t xpad[UGPU_XI_PADLDS];
+  if (P.zero) xpad[threadIdx.x] = 0;
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   {
@@ -317,6 +411,7 @@ __global__ __launch_bounds__(kXWaves * 64) void xi_kernel(ScanParams P)
   uint64_t cnt = 0, sst = 0, len = 0;  // lane totals (absolute positions)
   uint64_t entry = first_wave ? wlo : ~0ull, exit = whi;
   uint32_t ovf = 0;
+  bool has_edge = false;
 
   for (uint32_t i = 0; i < n; ++i) {
     const uint64_t ts = (tb + i) * (uint64_t)kXTile;
@@ -329,30 +424,60 @@ __global__ __launch_bounds__(kXWaves * 64) void xi_kernel(ScanParams P)
     const uint64_t fresh = first_wave && i == 0 ? wlo : ~0ull;
     XSum a;
     uint64_t xit, f;
-    if (edge_lo || edge_hi) {
-      uint64_t fs = ~0ull;
-      xit = xslow_lane(T, P.g, ts, seg, wlo, P.hi, fresh, P.rend, P.at_eof, a, fs, ovf);
-      f = fs;
+    if (edge_lo || edge_hi) {  // xi_edge_kernel completes this wave's record
+      has_edge = true;
+      continue;
     } else {
       // ---- fast tile: every lane segment lies inside [wlo, whi) ----
       bool synced = fresh == ts && lane == 0;  // fresh entry at the tile start
       uint32_t fs = ~0u, id = 0;
-      uint4 cur[4], nxt[4];
+#if UGPU_XI_STAGE
+      // Blocks are staged through the wave's LDS rows: coalesced loads (kXG
+      // lanes per 128-byte line) of block b+1 are in flight while block b is
+      // walked from LDS.
+      uint8_t* wbuf = xbuf + wid * kXBuf;
+      const XRow src{reinterpret_cast<const uint2*>(wbuf + lane * kXPitch)};
+      const uint32_t ls = (uint32_t)lane / kXG, lo16 = 16u * ((uint32_t)lane % kXG);
+      uint4 st[kXLd];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) cur[k] = xload16(rs, seg + 16u * k);
+      for (int j = 0; j < kXLd; ++j) st[j] = xload16(rs, (ls + (64 / kXLd) * j) * kXS + lo16);
+      for (uint32_t b = 0; b < (uint32_t)kXBlocks; ++b) {
+        xsync();  // the previous block's rows are read
+#pragma unroll
+        for (int j = 0; j < kXLd; ++j) {
+          uint2* dst = reinterpret_cast<uint2*>(wbuf + (ls + (64 / kXLd) * j) * kXPitch + lo16);
+          dst[0] = uint2{st[j].x, st[j].y};
+          dst[1] = uint2{st[j].z, st[j].w};
+        }
+        xsync();
+        if (b + 1 < (uint32_t)kXBlocks) {
+#pragma unroll
+          for (int j = 0; j < kXLd; ++j)
+            st[j] = xload16(rs, (ls + (64 / kXLd) * j) * kXS + (b + 1) * kXBlk + lo16);
+        }
+#else
+      // Direct loads: lane l reads its own segment, 16 bytes per load, block
+      // b+1 in flight while block b is walked.
+      uint4 cur[kXLd], nxt[kXLd];
+      const XRegs src{cur};
+#pragma unroll
+      for (int k = 0; k < kXLd; ++k) cur[k] = xload16m(rs, seg + 16u * k);
       for (uint32_t b = 0; b < (uint32_t)kXBlocks; ++b) {
         const uint32_t nb = b + 1 < (uint32_t)kXBlocks ? b + 1 : b;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) nxt[k] = xload16(rs, seg + nb * kXBlk + 16u * k);
+        for (int k = 0; k < kXLd; ++k) nxt[k] = xload16m(rs, seg + nb * kXBlk + 16u * k);
+#endif
         if (P.ablate == 6) {
-          id ^= cur[0].x ^ cur[1].y ^ cur[2].z ^ cur[3].w;  // loads only (benchmarking; wrong counts)
+          id ^= src(0).x ^ src(3).y;  // loads only (benchmarking; wrong counts)
         } else if (__ballot(!synced)) {
-          xblock<true>(T, cur, id, a, synced, fs, b * kXBlk);
+          xblock<true>(T, src, id, a, synced, fs, b * kXBlk);
         } else {
-          xblock<false>(T, cur, id, a, synced, fs, b * kXBlk);
+          xblock<false>(T, src, id, a, synced, fs, b * kXBlk);
         }
+#if !UGPU_XI_STAGE
 #pragma unroll
-        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+        for (int k = 0; k < kXLd; ++k) cur[k] = nxt[k];
+#endif
       }
       // a lane that never met a sync byte counts nothing: an earlier tail covers it
       if (!synced) a = XSum();
@@ -367,7 +492,11 @@ __global__ __launch_bounds__(kXWaves * 64) void xi_kernel(ScanParams P)
     if (mx) exit = mx;
     xfold(a, ts + seg, cnt, sst, len);
   }
-  if (entry == ~0ull) entry = exit;  // no sync byte in the whole range: the previous tail covers it
+  if (entry == ~0ull && !has_edge) entry = exit;  // no sync byte in the range: the previous tail covers it
+  if (P.ablate == 6) {  // loads-only benchmark: keep the records chained
+    entry = wlo;
+    exit = whi;
+  }
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
   const uint64_t c = wave_sum(cnt), s = wave_sum(sst), l = wave_sum(len);
   if (lane == 0) {
@@ -383,15 +512,95 @@ __global__ __launch_bounds__(kXWaves * 64) void xi_kernel(ScanParams P)
   }
 }
 
+// The tiles holding the range edges (P.lo unaligned, P.hi), done by one wave
+// after xi_kernel with the exact per-byte rules of xslow_lane; each completes
+// its wave's record (sums added, exit and a missing entry set).  Kept out of
+// xi_kernel: the per-byte edge code needs many more registers than the main loop.
+struct XEdges {
+  uint64_t tile[2], wave[2];
+  uint32_t n;
+};
+
+template <int ROWS>
+__global__ __launch_bounds__(64) void xi_edge_kernel(ScanParams P, XEdges E)
+{
+  __shared__ __attribute__((aligned(16))) uint8_t xsm[ROWS * 256];
+  const int lane = threadIdx.x;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(P.xid);
+    uint4* dst = reinterpret_cast<uint4*>(xsm);
+    for (uint32_t i = lane; i < P.xid_rows * 16; i += 64) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint8_t* T = xsm;
+  const uint32_t seg = (uint32_t)lane * kXS;
+  uint32_t ovf = 0;
+  for (uint32_t k = 0; k < E.n; ++k) {
+    const uint64_t gw = E.wave[k];
+    uint64_t tb = P.t0 + gw * P.tpb;
+    uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
+    if (tb > te) tb = te;
+    const uint64_t wlo = clampu(tb * kXTile, P.lo, P.hi);
+    const uint64_t whi = clampu(te * kXTile, P.lo, P.hi);
+    const uint64_t t = E.tile[k], ts = t * (uint64_t)kXTile;
+    const uint64_t fresh = wlo == P.lo && t == tb ? wlo : ~0ull;
+    XSum a;
+    uint64_t fs = ~0ull;
+    const uint64_t xit = xslow_lane(T, P.g, ts, seg, wlo, P.hi, fresh, P.rend, P.at_eof, a, fs, ovf);
+    uint64_t cnt = 0, sst = 0, len = 0;
+    xfold(a, ts + seg, cnt, sst, len);
+    const uint64_t c = wave_sum(cnt), sm = wave_sum(sst), l = wave_sum(len);
+    const uint64_t mx = wave_max_set(xit), mf = wave_min64(fs);
+    if (lane == 0) {
+      BlockRec r = P.recs[gw];
+      const uint64_t s_rep = sm + c * (uint64_t)P.delta;
+      r.cnt += c;
+      r.dg += 31 * s_rep + l;
+      r.dc += (uint64_t)P.cap1 * (s_rep + c);
+      if (t + 1 == te && mx) r.exit = mx;  // the wave's last tile: its coverage end is the exit
+      if (r.entry == ~0ull) r.entry = mf != ~0ull ? mf + 1 : r.exit;
+      P.recs[gw] = r;
+    }
+    __syncthreads();
+  }
+  if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
+}
+
 hipError_t launch_xi(const ScanParams& P, size_t smem, hipStream_t stream)
 {
-  hipLaunchKernelGGL(xi_kernel, dim3(P.grid), dim3(kXWaves * 64), smem, stream, P);
+  (void)smem;
+  // edge tiles: the first tile when lo is not tile aligned, the last tile
+  XEdges E{};
+  const uint64_t unit = kXTile;
+  if (P.lo % unit != 0) {
+    E.tile[E.n] = P.t0;
+    E.wave[E.n] = 0;
+    ++E.n;
+  }
+  if (P.t1 > P.t0 && !(E.n == 1 && E.tile[0] == P.t1 - 1)) {
+    E.tile[E.n] = P.t1 - 1;
+    E.wave[E.n] = (P.t1 - 1 - P.t0) / P.tpb;
+    ++E.n;
+  }
+  if (P.xid_rows <= 16) {
+    hipLaunchKernelGGL(xi_kernel<16>, dim3(P.grid), dim3(kXWaves * 64), 0, stream, P);
+    hipLaunchKernelGGL(xi_edge_kernel<16>, dim3(1), dim3(64), 0, stream, P, E);
+  } else if (P.xid_rows <= 64) {
+    hipLaunchKernelGGL(xi_kernel<64>, dim3(P.grid), dim3(kXWaves * 64), 0, stream, P);
+    hipLaunchKernelGGL(xi_edge_kernel<64>, dim3(1), dim3(64), 0, stream, P, E);
+  } else {
+    hipLaunchKernelGGL(xi_kernel<256>, dim3(P.grid), dim3(kXWaves * 64), 0, stream, P);
+    hipLaunchKernelGGL(xi_edge_kernel<256>, dim3(1), dim3(64), 0, stream, P, E);
+  }
   return hipGetLastError();
 }
 
 hipError_t xi_occupancy(size_t smem, int* n)
 {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xi_kernel, kXWaves * 64, smem);
+  const uint32_t rows = (uint32_t)(smem / 256);
+  if (rows <= 16) return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xi_kernel<16>, kXWaves * 64, 0);
+  if (rows <= 64) return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xi_kernel<64>, kXWaves * 64, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xi_kernel<256>, kXWaves * 64, 0);
 }
 
 uint32_t xi_unit() { return kXTile; }
