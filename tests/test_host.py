@@ -136,7 +136,7 @@ def test_prefilter_selectivity_c2():
 
 def test_result_struct_layout():
     assert ctypes.sizeof(_lib.Totals) == 48
-    assert ctypes.sizeof(_lib.DfaInfo) == 32
+    assert ctypes.sizeof(_lib.DfaInfo) == 36
 
 
 def _xt_find(t, x, data):
