@@ -87,7 +87,7 @@ def cpu_baseline(cfg, sample, threads):
                 sample="%d MiB, oracle restatement (dense-table walker), %d threads" % (sample >> 20, threads))
 
 
-KERNELS = {0: "sparse_kernel", 1: "dense_kernel", 2: "xi_kernel"}
+KERNELS = {0: "sparse_kernel", 1: "dense_kernel", 2: "xi_kernel", 3: "xg_kernel"}
 
 
 def measured_traffic(cfg, nbytes, kernel):

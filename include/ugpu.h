@@ -64,7 +64,7 @@ typedef struct ugpu_dfa_info
   uint32_t first_bytes; /* number of bytes that can start a match (|fst_|) */
   uint32_t accepting;   /* accepting states */
   uint32_t kernel;      /* kernel of a COUNT scan: 0 sparse (prefiltered), 1 dense, 2 xi (immediate
-                           transducer; UGPU_XI=0 selects dense) */
+                           transducer; UGPU_XI=0 selects dense), 3 xg (gap transducer; UGPU_XG=0) */
 } ugpu_dfa_info;
 
 /* Totals of one scan.  digest = sum(start*31 + len), dcap = sum((start+1)*cap),
@@ -127,6 +127,12 @@ int ugpu_tables_transducer_host(const uint32_t *opc, uint32_t nop, uint16_t *xtr
    pass xid = NULL to query *rows first. */
 int ugpu_tables_immediate_host(const uint32_t *opc, uint32_t nop, uint8_t *xid, uint32_t xid_cap, uint32_t *rows,
                                uint8_t *sync_byte, int *immediate);
+
+/* Host-only: the gap transducer of xg_kernel (ugrep_amd/csrc/tables.hpp):
+   xtrans entries plus XG_A (4, the new state accepts) and the accept's
+   gap + 1 in bits 3-5, same shape as trans; sync[256] = sync-byte flags.
+   *gap = 0 (nothing written) when the table does not qualify. */
+int ugpu_tables_gap_host(const uint32_t *opc, uint32_t nop, uint16_t *xg, uint32_t xg_cap, uint8_t *sync, int *gap);
 
 /* --- whole-buffer FIND (Matcher::buffer(); while (find()) ...) --- */
 

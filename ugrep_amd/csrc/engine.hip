@@ -35,6 +35,8 @@ struct ugpu_dfa {
   uint16_t* d_trans = nullptr;
   uint16_t* d_xtrans = nullptr;  // FIND transducer (restart-local tables on the dense path)
   uint8_t* d_xid = nullptr;      // immediate transducer ids (xi_kernel), COUNT scans
+  uint16_t* d_xg = nullptr;      // gap transducer (xg_kernel), COUNT scans
+  uint8_t* d_xg_sync = nullptr;
   uint8_t* d_cls = nullptr;
   uint32_t* d_caps = nullptr;
 };
@@ -45,6 +47,7 @@ struct ugpu_scanner {
   int max_rec = 0;       // chain records per scan (blocks or waves)
   bool sparse = false;   // prefiltered wave-persistent kernel (sparse_kernel.hip)
   bool xi = false;       // COUNT scans run xi_kernel (immediate tables); OFFSETS use the dense kernel
+  bool xg = false;       // COUNT scans run xg_kernel (gap tables); OFFSETS use the dense kernel
   size_t smem = 0;       // sparse / dense kernel
   size_t xi_smem = 0;
   int xi_rec = 0;        // chain records of an xi scan
@@ -93,6 +96,8 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.xtrans = d->d_xtrans;
   P.xid = d->d_xid;
   P.xid_rows = d->t.xid_rows;
+  P.xg = d->d_xg;
+  P.xg_sync = d->d_xg_sync;
   P.cls = d->d_cls;
   P.caps = d->d_caps;
   P.ntrans_pad = d->ntrans_pad;
@@ -140,7 +145,9 @@ void geometry(ScanParams& P, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint
 void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi,
                   uint64_t read_end, uint64_t& off, bool xi = false)
 {
-  if (xi)
+  if (xi && s->xg)
+    geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xg_unit(), xg_waves(), off);
+  else if (xi)
     geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xi_unit(), xi_waves(), off);
   else if (s->sparse)
     geometry(P, dbuf, lo, hi, read_end, s->max_rec, kWaveTile, kSpWaves, off);
@@ -150,6 +157,7 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
 
 hipError_t launch_main(const ugpu_scanner* s, const ScanParams& P, bool write, hipStream_t st, bool xi = false)
 {
+  if (xi && s->xg) return launch_xg(P, st);
   if (xi) return launch_xi(P, s->xi_smem, st);
   if (s->sparse) return launch_sparse(P, write, s->smem, st);
   return launch_dense(P, s->dfa->t.format, write, s->smem, st);
@@ -220,6 +228,17 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       return hip_fail(e, "immediate transducer upload");
     }
   }
+  if (d->t.gap && !d->t.filter && d->t.cap1 != 0) {
+    std::vector<uint16_t> xg(d->ntrans_pad, 0);
+    std::copy(d->t.xg.begin(), d->t.xg.end(), xg.begin());
+    if ((e = hipMalloc(&d->d_xg, xg.size() * 2)) != hipSuccess ||
+        (e = hipMemcpy(d->d_xg, xg.data(), xg.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMalloc(&d->d_xg_sync, 256)) != hipSuccess ||
+        (e = hipMemcpy(d->d_xg_sync, d->t.xg_sync.data(), 256, hipMemcpyHostToDevice)) != hipSuccess) {
+      ugpu_dfa_destroy(d);
+      return hip_fail(e, "gap transducer upload");
+    }
+  }
   *out = d;
   return UGPU_OK;
 }
@@ -230,6 +249,8 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   if (d->d_trans) (void)hipFree(d->d_trans);
   if (d->d_xtrans) (void)hipFree(d->d_xtrans);
   if (d->d_xid) (void)hipFree(d->d_xid);
+  if (d->d_xg) (void)hipFree(d->d_xg);
+  if (d->d_xg_sync) (void)hipFree(d->d_xg_sync);
   if (d->d_cls) (void)hipFree(d->d_cls);
   if (d->d_caps) (void)hipFree(d->d_caps);
   delete d;
@@ -248,7 +269,11 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->first_bytes = d->t.first_bytes;
   info->accepting = d->t.accepting;
   const char* xenv = std::getenv("UGPU_XI");
-  info->kernel = (d->t.filter && d->t.format == FMT_BYTE) ? 0u : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u : 1u;
+  const char* genv = std::getenv("UGPU_XG");
+  info->kernel = (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
+                 : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u
+                 : (d->d_xg && !(genv && genv[0] == '0'))  ? 3u
+                                                           : 1u;
   return UGPU_OK;
 }
 
@@ -269,7 +294,10 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
-  info->kernel = (t.filter && t.format == FMT_BYTE) ? 0u : (t.immediate && t.cap1 != 0) ? 2u : 1u;
+  info->kernel = (t.filter && t.format == FMT_BYTE) ? 0u
+                 : (t.immediate && t.cap1 != 0)      ? 2u
+                 : (t.gap && t.cap1 != 0)            ? 3u
+                                                     : 1u;
   if (start) *start = t.start;
   if (accb) *accb = t.accb;
   if (trans) {
@@ -327,6 +355,21 @@ int ugpu_tables_immediate_host(const uint32_t* opc, uint32_t nop, uint8_t* xid, 
   return UGPU_OK;
 }
 
+int ugpu_tables_gap_host(const uint32_t* opc, uint32_t nop, uint16_t* xg, uint32_t xg_cap, uint8_t* sync, int* gap)
+{
+  if (!gap) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *gap = t.gap ? 1 : 0;
+  if (!t.gap) return UGPU_OK;
+  if (!xg || xg_cap < t.xg.size()) return fail(UGPU_INVAL, "xg capacity too small");
+  std::copy(t.xg.begin(), t.xg.end(), xg);
+  if (sync) std::copy(t.xg_sync.begin(), t.xg_sync.end(), sync);
+  return UGPU_OK;
+}
+
 int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
 {
   if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
@@ -359,8 +402,23 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
     int v = std::atoi(env);
     if (v >= 1 && v <= kMaxRec) s->max_rec = v;
   }
-  // immediate tables: COUNT scans on xi_kernel (UGPU_XI=0 keeps the dense kernel)
+  // immediate tables: COUNT scans on xi_kernel (UGPU_XI=0 keeps the dense kernel);
+  // gap tables: xg_kernel (UGPU_XG=0 keeps the dense kernel)
   const char* xenv = std::getenv("UGPU_XI");
+  const char* genv = std::getenv("UGPU_XG");
+  if (!s->sparse && !(dfa->d_xid && !(xenv && xenv[0] == '0')) && dfa->d_xg && !(genv && genv[0] == '0')) {
+    int gpc = 0;
+    HIP_TRY(xg_occupancy(dfa->t.format, &gpc));
+    if (gpc >= 1) {
+      s->xg = true;
+      int gg = prop.multiProcessorCount * gpc * (int)xg_waves();
+      s->xi_rec = gg > kMaxRec ? kMaxRec : gg;
+      if (const char* env = std::getenv("UGPU_MAX_GRID")) {
+        int v = std::atoi(env);
+        if (v >= 1 && v <= kMaxRec) s->xi_rec = v;
+      }
+    }
+  }
   if (!s->sparse && dfa->d_xid && !(xenv && xenv[0] == '0')) {
     s->xi_smem = (size_t)dfa->t.xid_rows * 256;
     int xpc = 0;
@@ -412,7 +470,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P{};
   fill_tables(P, s->dfa);
-  geometry_for(P, s, dbuf, lo, hi, read_end, s->off, s->xi);
+  geometry_for(P, s, dbuf, lo, hi, read_end, s->off, s->xi || s->xg);
   P.delta = (int64_t)bias - (int64_t)s->off;
   P.at_eof = at_eof ? 1u : 0u;
   if (const char* ab = std::getenv("UGPU_ABLATE")) P.ablate = (uint32_t)std::atoi(ab);
@@ -423,13 +481,13 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   P.out_base_out = s->d_obase;
   HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
   HIP_TRY(hipEventRecord(s->ev0, st));
-  HIP_TRY(launch_main(s, P, false, st, s->xi));
+  HIP_TRY(launch_main(s, P, false, st, s->xi || s->xg));
   HIP_TRY(hipEventRecord(s->ev1, st));
   HIP_TRY(launch_fix(P, s->dfa->t.format, st));
   HIP_TRY(hipMemcpyAsync(s->h_tot, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   s->last = P;
-  s->last_xi = s->xi;
+  s->last_xi = s->xi || s->xg;
   s->last_buf = dbuf;
   s->last_args[0] = lo;
   s->last_args[1] = hi;

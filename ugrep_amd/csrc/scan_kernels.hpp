@@ -83,6 +83,8 @@ struct ScanParams {
   const uint16_t* xtrans;  // FIND transducer table or NULL (dense kernel, tables.hpp)
   const uint8_t* xid;      // immediate transducer byte ids (xi_kernel, tables.hpp) or NULL
   uint32_t xid_rows;
+  const uint16_t* xg;      // gap transducer (xg_kernel, tables.hpp) or NULL
+  const uint8_t* xg_sync;  // its sync-byte flags
   const uint8_t* cls;
   const uint32_t* caps;
   uint32_t ntrans_pad;   // u16 entries, multiple of 8
@@ -156,6 +158,11 @@ hipError_t launch_xi(const ScanParams& P, size_t smem, hipStream_t stream);
 hipError_t xi_occupancy(size_t smem, int* blocks_per_cu);
 uint32_t xi_unit();
 uint32_t xi_waves();
+// gap-transducer kernel, xg_kernel.hip (COUNT mode only)
+hipError_t launch_xg(const ScanParams& P, hipStream_t stream);
+hipError_t xg_occupancy(uint32_t format, int* blocks_per_cu);
+uint32_t xg_unit();
+uint32_t xg_waves();
 // dense wave-persistent kernel, dense_kernel.hip
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);
 hipError_t dense_occupancy(uint32_t format, bool cap1, bool xt, size_t smem, int* blocks_per_cu);

@@ -403,6 +403,56 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       }
     }
   }
+  // gap transducer (tables.hpp, xg_kernel.hip)
+  if (t.restart_local && R >= 64 && start_sid < first_acc) {
+    std::vector<int> gap(S, -1);
+    std::vector<std::pair<uint32_t, int> > work;  // (state, gap) pairs, BFS over walks from start
+    std::set<std::pair<uint32_t, int> > seen;
+    work.push_back(std::make_pair(start_sid, 0));
+    seen.insert(work.back());
+    bool ok = true;
+    while (!work.empty() && ok) {
+      const std::pair<uint32_t, int> cur = work.back();
+      work.pop_back();
+      if (gap[cur.first] >= 0 && gap[cur.first] != cur.second) ok = false;
+      gap[cur.first] = cur.second;
+      for (int c = 0; c < 256 && ok; ++c) {
+        const uint32_t n = nxt[(size_t)cur.first * 256 + c];
+        if (n == 0) continue;
+        const std::pair<uint32_t, int> nx(n, n >= first_acc ? 0 : cur.second + 1);
+        if (nx.second > 6) ok = false;
+        if (seen.insert(nx).second) work.push_back(nx);
+      }
+    }
+    std::vector<uint8_t> sync(256, 0);
+    bool any_sync = false;
+    for (int c = 0; ok && c < 256; ++c) {
+      bool y = nxt[(size_t)start_sid * 256 + c] == 0;
+      for (uint32_t s2 = 1; s2 < S && y; ++s2)
+        if (gap[s2] >= 0 && s2 != start_sid) y = nxt[(size_t)s2 * 256 + c] == 0;
+      sync[c] = y ? 1 : 0;
+      any_sync |= y;
+    }
+    if (ok && any_sync) {
+      t.gap = true;
+      t.xg_sync = sync;
+      t.xg.assign((size_t)S * R, 0);
+      for (uint32_t s2 = 0; s2 < S; ++s2)
+        for (int c = 0; c < 256; ++c) {
+          const uint32_t col = t.format == FMT_BYTE ? (uint32_t)c : cls[c];
+          const uint32_t nx = nxt[(size_t)s2 * 256 + c], r = nxt[(size_t)start_sid * 256 + c];
+          uint32_t x;
+          if (nx) {
+            x = nx * R;
+            if (nx >= first_acc) x |= XG_A | (uint32_t)((gap[s2] < 0 ? 0 : gap[s2]) + 1) << XG_LSHIFT;
+          } else {
+            x = (r ? r : start_sid) * R | XT_DEAD | (r ? XT_LIVE : 0);
+            if (r && r >= first_acc) x |= XG_A | 1u << XG_LSHIFT;
+          }
+          t.xg[(size_t)s2 * R + col] = (uint16_t)x;
+        }
+    }
+  }
   t.start = start_sid * R;
   t.accepting = S - first_acc;
   t.accb = (t.accepting > 0) ? first_acc * R : 0x10000u;

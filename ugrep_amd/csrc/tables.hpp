@@ -75,9 +75,27 @@ struct DfaTables {
   uint32_t xid_rows = 0;        // ids (table rows)
   uint8_t sync_byte = 0;        // smallest sync byte
   std::vector<uint8_t> xid;     // xid_rows * 256
+  bool gap = false;             // xg table valid
+  std::vector<uint16_t> xg;     // states * row
+  std::vector<uint8_t> xg_sync; // 256
 };
 
 constexpr uint8_t XI_ST = 1, XI_IN = 2, XI_Y = 4;
+
+// Gap transducer (xg_kernel.hip), for restart-local tables in which the
+// number of bytes a walk has read since its start or its last accept (its
+// "gap") is a function of the DFA state (true for UTF-8 word patterns such as
+// \w+, \S+, where states sit at fixed depths of a UTF-8 sequence).  Then every
+// accept adds gap + 1 bytes to the current match and the first accept of a
+// walk starts a match at q + 1 - (gap + 1), so a walk needs no (p, last)
+// registers: only one bit "this walk has accepted" per lane.  Entries are the
+// xtrans entries (row | XT_DEAD | XT_LIVE) plus
+//   XG_A   the new state accepts (after a death: the restart state does)
+//   L      bits 3-5: gap + 1 of that accept (0 when XG_A is clear)
+// which needs row >= 64.  xg_sync[byte] = 1 for sync bytes (kill every walk,
+// start none).
+constexpr uint16_t XG_A = 4;
+constexpr uint32_t XG_LSHIFT = 3;
 
 constexpr uint16_t XT_DEAD = 1;  // the walk died on this byte; the row is the restart state
 constexpr uint16_t XT_LIVE = 2;  // the restart at this byte is alive (a walk begins here)

@@ -75,6 +75,18 @@ def host_immediate(opc):
     return x.reshape(rows.value, 256), sb.value
 
 
+def host_gap(opc):
+    """Gap transducer of xg_kernel: (xg table uint16[states*row], sync uint8[256]) or None."""
+    a, p = _as_u32(opc)
+    info = host_tables(opc)["info"]
+    x = np.zeros(info["states"] * info["row"], np.uint16)
+    sy = np.zeros(256, np.uint8)
+    ok = ctypes.c_int()
+    check(lib.ugpu_tables_gap_host(p, len(a), x.ctypes.data_as(_lib.c_u16p), x.size, sy.ctypes.data_as(_lib.c_u8p),
+                                   ctypes.byref(ok)))
+    return (x, sy) if ok.value else None
+
+
 class Pattern:
     """Compiled pattern (opcode words) with its device tables."""
 
