@@ -28,7 +28,10 @@ constexpr int kGTile = 64 * kGS;   // wave tile
 constexpr int kGBlk = 64;          // bytes per block (4 x 16 B per lane, double buffered)
 constexpr int kGLd = kGBlk / 16;
 constexpr int kGBlocks = kGS / kGBlk;
-constexpr int kGWaves = 16;        // waves per workgroup: one staged table per CU
+#ifndef UGPU_XG_WAVES
+#define UGPU_XG_WAVES 16
+#endif
+constexpr int kGWaves = UGPU_XG_WAVES;  // waves per workgroup: one staged table per CU
 constexpr int kGMaxEntries = 65536;  // u16 table entries (128 KB)
 
 __device__ __forceinline__ uint4 gload16(__amdgpu_buffer_rsrc_t rs, uint32_t off)
@@ -93,9 +96,10 @@ __device__ __forceinline__ void gbyte(const GTab<FMT>& T, uint32_t w, uint32_t& 
                                       uint32_t rp1, bool& synced, uint32_t& fs)
 {
   const uint32_t e = T.template step<K>(m, w);
-  const uint32_t t = e >> 2;                      // bit 0: the new state accepts; bits 1-3: L
-  uint32_t f = t & (e | ~acc) & 1u;               // first accept of the walk (a death restarts it)
-  acc = t | (acc & ~e);                           // bit 0: the walk has accepted
+  // bit 2 (XG_A): the new state accepts; d2 bit 2: the walk died here
+  const uint32_t d2 = e << 2;
+  uint32_t f = e & (d2 | ~acc) & XG_A;  // first accept of the walk (XG_A or 0; a death restarts it)
+  acc = e | (acc & ~d2);                // bit 2: the walk has accepted
   uint32_t L = (e >> XG_LSHIFT) & 7u;
   if constexpr (MASK) {
     const uint32_t y = T.sy[(w >> (8 * K)) & 0xffu];
@@ -106,17 +110,19 @@ __device__ __forceinline__ void gbyte(const GTab<FMT>& T, uint32_t w, uint32_t& 
     }
     synced = synced || y != 0;
   }
-  s.cnt += f;
-  s.sq += f * rp1;
-  s.sfl += f * L;
+  s.cnt += f;                     // (sums of f are 4x: XG_A == 4)
+  s.sq += __umul24(f, rp1);
+  s.sfl += __umul24(f, L);
   s.sl += L;
   m = e;
 }
 
+// acc: bit 2 = the walk has accepted (main-loop form; the tail's form is bit 0)
 template <int FMT, bool MASK>
 __device__ __forceinline__ void gblock(const GTab<FMT>& T, const uint4 (&v)[kGLd], uint32_t& m, uint32_t& acc,
-                                       GSum& s, bool& synced, uint32_t& fs, uint32_t bb)
+                                       GSum& s4, bool& synced, uint32_t& fs, uint32_t bb)
 {
+  GSum& s = s4;  // sums of f are scaled by 4 (f = XG_A or 0), sl is exact
 #pragma unroll
   for (int k = 0; k < kGLd; ++k) {
     const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
@@ -176,8 +182,8 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
           act = false;
         } else {
           s.cnt += f;
-          s.sq += f * (r0 + k + 1);
-          s.sfl += f * L;
+          s.sq += __umul24(f, r0 + k + 1);
+          s.sfl += __umul24(f, L);
           s.sl += L;
           if (t & 1u) last = base + k + 1;
           acc = t | (acc & ~e);
@@ -199,10 +205,10 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
 // byte; past hi only the crossing walk).
 template <int FMT>
 __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t* g, uint64_t ts, uint32_t seg,
-                                               uint64_t wlo, uint64_t hi, uint64_t fresh, uint64_t rend,
-                                               uint32_t at_eof, GSum& s, uint64_t& fs, uint32_t& ovf)
+                                               uint32_t slen, uint64_t wlo, uint64_t hi, uint64_t fresh,
+                                               uint64_t rend, uint32_t at_eof, GSum& s, uint64_t& fs, uint32_t& ovf)
 {
-  bool act = ts + seg + kGS > wlo && ts + seg < hi;
+  bool act = ts + seg + slen > wlo && ts + seg < hi;
   bool synced = false;
   uint32_t m = T.start_row, acc = 0;
   uint64_t xit = ~0ull, last = 0;
@@ -215,7 +221,7 @@ __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t
     const uint64_t base = ts + seg + c;
     const uint32_t dh = gdist(hi, base), dr = gdist(rend, base), dl = gdist(wlo, base);
     const uint32_t df = fresh >= base && fresh - base < 16 ? (uint32_t)(fresh - base) : 0xffffffffu;
-    const uint32_t dseg = c >= (uint64_t)kGS ? 0u : (uint32_t)(kGS - c);
+    const uint32_t dseg = c >= (uint64_t)slen ? 0u : (uint32_t)(slen - c);
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
       bool go = act && k >= dl;
@@ -248,8 +254,8 @@ __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t
           act = false;
         } else if (synced) {
           s.cnt += f;
-          s.sq += f * (uint32_t)(c + k + 1);
-          s.sfl += f * L;
+          s.sq += __umul24(f, (uint32_t)(c + k + 1));
+          s.sfl += __umul24(f, L);
           s.sl += L;
           if (t & 1u) last = base + k + 1;
           if (k < dh && T.sy[b] && k >= dseg) {  // the tail ends at a sync byte
@@ -356,7 +362,7 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
     }
     bool synced = first_wave && i == 0 && lane == 0 && ts == wlo;  // fresh entry at the tile start
     uint32_t fs = ~0u, m = T.start_row, acc = 0;
-    GSum s;
+    GSum s4;  // main loop: f-weighted sums x4
     uint4 cur[kGLd], nxt[kGLd];
 #pragma unroll
     for (int k = 0; k < kGLd; ++k) cur[k] = gload16(rs, seg + 16u * k);
@@ -365,13 +371,19 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
 #pragma unroll
       for (int k = 0; k < kGLd; ++k) nxt[k] = gload16(rs, seg + nb * kGBlk + 16u * k);
       if (__ballot(!synced))
-        gblock<FMT, true>(T, cur, m, acc, s, synced, fs, b * kGBlk);
+        gblock<FMT, true>(T, cur, m, acc, s4, synced, fs, b * kGBlk);
       else
-        gblock<FMT, false>(T, cur, m, acc, s, synced, fs, b * kGBlk);
+        gblock<FMT, false>(T, cur, m, acc, s4, synced, fs, b * kGBlk);
 #pragma unroll
       for (int k = 0; k < kGLd; ++k) cur[k] = nxt[k];
     }
+    GSum s;
+    s.cnt = s4.cnt >> 2;
+    s.sq = s4.sq >> 2;
+    s.sfl = s4.sfl >> 2;
+    s.sl = s4.sl;
     if (!synced) s = GSum();  // covered by an earlier tail
+    acc = (acc >> 2) & 1u;    // the tail keeps the accepted bit in bit 0
     const uint64_t xit = gtail<FMT>(T, P.g, ts, seg + kGS, seg, m, acc, s, P.hi, P.rend, P.at_eof, ovf, synced);
     const uint64_t f = synced && fs != ~0u ? ts + seg + fs : ~0ull;
     if (entry == ~0ull) {
@@ -403,14 +415,23 @@ struct GEdges {
   uint32_t n;
 };
 
+// Edge tiles: 1024 lanes of 64-byte segments (see xi_kernel.hip).
+constexpr int kGEdgeThreads = 1024;
+constexpr uint32_t kGEdgeSeg = kGTile / kGEdgeThreads;
+
+struct GBlockRed {
+  uint64_t v[kGEdgeThreads / 64][5];
+};
+
 template <int FMT>
-__global__ __launch_bounds__(64) void xg_edge_kernel(ScanParams P, GEdges E)
+__global__ __launch_bounds__(kGEdgeThreads) void xg_edge_kernel(ScanParams P, GEdges E)
 {
   __shared__ __attribute__((aligned(16))) uint16_t gxg[kGMaxEntries];
   __shared__ uint8_t gc2[256], gsy[256];
-  const int lane = threadIdx.x;
-  const GTab<FMT> T = gstage<FMT>(P, gxg, gc2, gsy, lane, 64);
-  const uint32_t seg = (uint32_t)lane * kGS;
+  __shared__ GBlockRed R;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const GTab<FMT> T = gstage<FMT>(P, gxg, gc2, gsy, tid, kGEdgeThreads);
+  const uint32_t seg = (uint32_t)tid * kGEdgeSeg;
   uint32_t ovf = 0;
   for (uint32_t k = 0; k < E.n; ++k) {
     const uint64_t gw = E.wave[k];
@@ -422,19 +443,36 @@ __global__ __launch_bounds__(64) void xg_edge_kernel(ScanParams P, GEdges E)
     const uint64_t fresh = wlo == P.lo && t == tb ? wlo : ~0ull;
     GSum s;
     uint64_t fs = ~0ull;
-    const uint64_t xit = gslow_lane<FMT>(T, P.g, ts, seg, wlo, P.hi, fresh, P.rend, P.at_eof, s, fs, ovf);
+    const uint64_t xit =
+        gslow_lane<FMT>(T, P.g, ts, seg, kGEdgeSeg, wlo, P.hi, fresh, P.rend, P.at_eof, s, fs, ovf);
     uint64_t cnt = 0, sst = 0, len = 0;
     gfold(s, ts + seg, cnt, sst, len);
     const uint64_t c = wave_sum(cnt), sm = wave_sum(sst), l = wave_sum(len);
     const uint64_t mx = gwave_max_set(xit), mf = gwave_min64(fs);
     if (lane == 0) {
+      R.v[wid][0] = c;
+      R.v[wid][1] = sm;
+      R.v[wid][2] = l;
+      R.v[wid][3] = mf;
+      R.v[wid][4] = mx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint64_t rc = 0, rs = 0, rl = 0, rf = ~0ull, rx = 0;
+      for (int w = 0; w < kGEdgeThreads / 64; ++w) {
+        rc += R.v[w][0];
+        rs += R.v[w][1];
+        rl += R.v[w][2];
+        rf = R.v[w][3] < rf ? R.v[w][3] : rf;
+        rx = R.v[w][4] > rx ? R.v[w][4] : rx;
+      }
       BlockRec r = P.recs[gw];
-      const uint64_t s_rep = sm + c * (uint64_t)P.delta;
-      r.cnt += c;
-      r.dg += 31 * s_rep + l;
-      r.dc += (uint64_t)P.cap1 * (s_rep + c);
-      if (t + 1 == te && mx) r.exit = mx;
-      if (r.entry == ~0ull) r.entry = mf != ~0ull ? mf + 1 : r.exit;
+      const uint64_t s_rep = rs + rc * (uint64_t)P.delta;
+      r.cnt += rc;
+      r.dg += 31 * s_rep + rl;
+      r.dc += (uint64_t)P.cap1 * (s_rep + rc);
+      if (t + 1 == te && rx) r.exit = rx;
+      if (r.entry == ~0ull) r.entry = rf != ~0ull ? rf + 1 : r.exit;
       P.recs[gw] = r;
     }
     __syncthreads();
@@ -458,10 +496,10 @@ hipError_t launch_xg(const ScanParams& P, hipStream_t stream)
   }
   if (P.log_row == 8) {
     hipLaunchKernelGGL(xg_kernel<0>, dim3(P.grid), dim3(kGWaves * 64), 0, stream, P);
-    hipLaunchKernelGGL(xg_edge_kernel<0>, dim3(1), dim3(64), 0, stream, P, E);
+    hipLaunchKernelGGL(xg_edge_kernel<0>, dim3(1), dim3(kGEdgeThreads), 0, stream, P, E);
   } else {
     hipLaunchKernelGGL(xg_kernel<1>, dim3(P.grid), dim3(kGWaves * 64), 0, stream, P);
-    hipLaunchKernelGGL(xg_edge_kernel<1>, dim3(1), dim3(64), 0, stream, P, E);
+    hipLaunchKernelGGL(xg_edge_kernel<1>, dim3(1), dim3(kGEdgeThreads), 0, stream, P, E);
   }
   return hipGetLastError();
 }

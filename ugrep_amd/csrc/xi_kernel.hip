@@ -270,10 +270,10 @@ __device__ __forceinline__ uint64_t xtail(const uint8_t* T, const uint8_t* g, ui
 // sync byte, past hi only the walk crossing hi.  Returns the lane's coverage
 // end as xtail does (~0: the lane covers nothing) and its first sync byte in fs.
 __device__ __forceinline__ uint64_t xslow_lane(const uint8_t* T, const uint8_t* g, uint64_t ts, uint32_t seg,
-                                               uint64_t wlo, uint64_t hi, uint64_t fresh, uint64_t rend,
-                                               uint32_t at_eof, XSum& a, uint64_t& fs, uint32_t& ovf)
+                                               uint32_t slen, uint64_t wlo, uint64_t hi, uint64_t fresh,
+                                               uint64_t rend, uint32_t at_eof, XSum& a, uint64_t& fs, uint32_t& ovf)
 {
-  bool act = ts + seg + kXS > wlo && ts + seg < hi;
+  bool act = ts + seg + slen > wlo && ts + seg < hi;
   bool synced = false;
   uint32_t id = 0;
   uint64_t xit = ~0ull;
@@ -286,7 +286,7 @@ __device__ __forceinline__ uint64_t xslow_lane(const uint8_t* T, const uint8_t* 
     const uint64_t base = ts + seg + c;  // position of byte 0 of this chunk
     const uint32_t dh = xdist(hi, base), dr = xdist(rend, base), dl = xdist(wlo, base);
     const uint32_t df = fresh >= base && fresh - base < 16 ? (uint32_t)(fresh - base) : 0xffffffffu;
-    const uint32_t dseg = c >= (uint64_t)kXS ? 0u : (uint32_t)(kXS - c);  // bytes left in the segment
+    const uint32_t dseg = c >= (uint64_t)slen ? 0u : (uint32_t)(slen - c);  // bytes left in the segment
     uint32_t cn = 0, ps = 0, in2 = 0, stop = 0xffffffffu, fsk = 0xffffffffu;
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
@@ -521,19 +521,62 @@ struct XEdges {
   uint32_t n;
 };
 
+// Edge tiles run with 1024 lanes of 64-byte segments (the segment length only
+// matters inside the tile: lanes still count after their first sync byte and
+// their tails end at the next one), so the per-byte walk is 16x shorter than
+// with the main kernel's 1 KiB segments.
+constexpr int kEdgeThreads = 1024;
+constexpr uint32_t kEdgeSeg = kXTile / kEdgeThreads;
+
+// block-wide sums / min / max (16 waves)
+struct XBlockRed {
+  uint64_t v[kEdgeThreads / 64][5];
+};
+
+__device__ __forceinline__ void xblock_reduce(XBlockRed& R, uint64_t c, uint64_t s, uint64_t l, uint64_t fsmin,
+                                              uint64_t xmax, uint64_t out[5])
+{
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  c = wave_sum(c);
+  s = wave_sum(s);
+  l = wave_sum(l);
+  if (lane == 0) {
+    R.v[wid][0] = c;
+    R.v[wid][1] = s;
+    R.v[wid][2] = l;
+    R.v[wid][3] = fsmin;
+    R.v[wid][4] = xmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[0] = out[1] = out[2] = 0;
+    out[3] = ~0ull;
+    out[4] = 0;
+    for (int w = 0; w < kEdgeThreads / 64; ++w) {
+      out[0] += R.v[w][0];
+      out[1] += R.v[w][1];
+      out[2] += R.v[w][2];
+      out[3] = R.v[w][3] < out[3] ? R.v[w][3] : out[3];
+      out[4] = R.v[w][4] > out[4] ? R.v[w][4] : out[4];
+    }
+  }
+  __syncthreads();
+}
+
 template <int ROWS>
-__global__ __launch_bounds__(64) void xi_edge_kernel(ScanParams P, XEdges E)
+__global__ __launch_bounds__(kEdgeThreads) void xi_edge_kernel(ScanParams P, XEdges E)
 {
   __shared__ __attribute__((aligned(16))) uint8_t xsm[ROWS * 256];
-  const int lane = threadIdx.x;
+  __shared__ XBlockRed R;
+  const int tid = threadIdx.x;
   {
     const uint4* src = reinterpret_cast<const uint4*>(P.xid);
     uint4* dst = reinterpret_cast<uint4*>(xsm);
-    for (uint32_t i = lane; i < P.xid_rows * 16; i += 64) dst[i] = src[i];
+    for (uint32_t i = tid; i < P.xid_rows * 16; i += kEdgeThreads) dst[i] = src[i];
   }
   __syncthreads();
   const uint8_t* T = xsm;
-  const uint32_t seg = (uint32_t)lane * kXS;
+  const uint32_t seg = (uint32_t)tid * kEdgeSeg;
   uint32_t ovf = 0;
   for (uint32_t k = 0; k < E.n; ++k) {
     const uint64_t gw = E.wave[k];
@@ -541,25 +584,24 @@ __global__ __launch_bounds__(64) void xi_edge_kernel(ScanParams P, XEdges E)
     uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
     if (tb > te) tb = te;
     const uint64_t wlo = clampu(tb * kXTile, P.lo, P.hi);
-    const uint64_t whi = clampu(te * kXTile, P.lo, P.hi);
     const uint64_t t = E.tile[k], ts = t * (uint64_t)kXTile;
     const uint64_t fresh = wlo == P.lo && t == tb ? wlo : ~0ull;
     XSum a;
     uint64_t fs = ~0ull;
-    const uint64_t xit = xslow_lane(T, P.g, ts, seg, wlo, P.hi, fresh, P.rend, P.at_eof, a, fs, ovf);
+    const uint64_t xit = xslow_lane(T, P.g, ts, seg, kEdgeSeg, wlo, P.hi, fresh, P.rend, P.at_eof, a, fs, ovf);
     uint64_t cnt = 0, sst = 0, len = 0;
     xfold(a, ts + seg, cnt, sst, len);
-    const uint64_t c = wave_sum(cnt), sm = wave_sum(sst), l = wave_sum(len);
-    const uint64_t mx = wave_max_set(xit), mf = wave_min64(fs);
-    if (lane == 0) {
-      BlockRec r = P.recs[gw];
-      const uint64_t s_rep = sm + c * (uint64_t)P.delta;
-      r.cnt += c;
-      r.dg += 31 * s_rep + l;
-      r.dc += (uint64_t)P.cap1 * (s_rep + c);
-      if (t + 1 == te && mx) r.exit = mx;  // the wave's last tile: its coverage end is the exit
-      if (r.entry == ~0ull) r.entry = mf != ~0ull ? mf + 1 : r.exit;
-      P.recs[gw] = r;
+    uint64_t r[5];
+    xblock_reduce(R, cnt, sst, len, wave_min64(fs), wave_max_set(xit), r);
+    if (tid == 0) {
+      BlockRec rec = P.recs[gw];
+      const uint64_t s_rep = r[1] + r[0] * (uint64_t)P.delta;
+      rec.cnt += r[0];
+      rec.dg += 31 * s_rep + r[2];
+      rec.dc += (uint64_t)P.cap1 * (s_rep + r[0]);
+      if (t + 1 == te && r[4]) rec.exit = r[4];  // the wave's last tile: its coverage end is the exit
+      if (rec.entry == ~0ull) rec.entry = r[3] != ~0ull ? r[3] + 1 : rec.exit;
+      P.recs[gw] = rec;
     }
     __syncthreads();
   }
@@ -584,13 +626,13 @@ hipError_t launch_xi(const ScanParams& P, size_t smem, hipStream_t stream)
   }
   if (P.xid_rows <= 16) {
     hipLaunchKernelGGL(xi_kernel<16>, dim3(P.grid), dim3(kXWaves * 64), 0, stream, P);
-    hipLaunchKernelGGL(xi_edge_kernel<16>, dim3(1), dim3(64), 0, stream, P, E);
+    hipLaunchKernelGGL(xi_edge_kernel<16>, dim3(1), dim3(kEdgeThreads), 0, stream, P, E);
   } else if (P.xid_rows <= 64) {
     hipLaunchKernelGGL(xi_kernel<64>, dim3(P.grid), dim3(kXWaves * 64), 0, stream, P);
-    hipLaunchKernelGGL(xi_edge_kernel<64>, dim3(1), dim3(64), 0, stream, P, E);
+    hipLaunchKernelGGL(xi_edge_kernel<64>, dim3(1), dim3(kEdgeThreads), 0, stream, P, E);
   } else {
     hipLaunchKernelGGL(xi_kernel<256>, dim3(P.grid), dim3(kXWaves * 64), 0, stream, P);
-    hipLaunchKernelGGL(xi_edge_kernel<256>, dim3(1), dim3(64), 0, stream, P, E);
+    hipLaunchKernelGGL(xi_edge_kernel<256>, dim3(1), dim3(kEdgeThreads), 0, stream, P, E);
   }
   return hipGetLastError();
 }
