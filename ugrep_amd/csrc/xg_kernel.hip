@@ -28,6 +28,9 @@ constexpr int kGTile = 64 * kGS;   // wave tile
 constexpr int kGBlk = 64;          // bytes per block (4 x 16 B per lane, double buffered)
 constexpr int kGLd = kGBlk / 16;
 constexpr int kGBlocks = kGS / kGBlk;
+#ifndef UGPU_XG_SELECT
+#define UGPU_XG_SELECT 0
+#endif
 #ifndef UGPU_XG_WAVES
 #define UGPU_XG_WAVES 16
 #endif
@@ -111,7 +114,11 @@ __device__ __forceinline__ void gbyte(const GTab<FMT>& T, uint32_t w, uint32_t& 
     synced = synced || y != 0;
   }
   s.cnt += f;                     // (sums of f are 4x: XG_A == 4)
-  s.sq += __umul24(f, rp1);
+#if UGPU_XG_SELECT
+  s.sq += f ? rp1 : 0u;                 // (a select: not scaled)
+#else
+  s.sq += __umul24(f, rp1) >> 2;        // f = XG_A or 0
+#endif
   s.sfl += __umul24(f, L);
   s.sl += L;
   m = e;
@@ -122,7 +129,7 @@ template <int FMT, bool MASK>
 __device__ __forceinline__ void gblock(const GTab<FMT>& T, const uint4 (&v)[kGLd], uint32_t& m, uint32_t& acc,
                                        GSum& s4, bool& synced, uint32_t& fs, uint32_t bb)
 {
-  GSum& s = s4;  // sums of f are scaled by 4 (f = XG_A or 0), sl is exact
+  GSum& s = s4;  // cnt and sfl are scaled by 4 (f = XG_A or 0); sq and sl are exact
 #pragma unroll
   for (int k = 0; k < kGLd; ++k) {
     const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
@@ -362,7 +369,7 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
     }
     bool synced = first_wave && i == 0 && lane == 0 && ts == wlo;  // fresh entry at the tile start
     uint32_t fs = ~0u, m = T.start_row, acc = 0;
-    GSum s4;  // main loop: f-weighted sums x4
+    GSum s4;  // main loop: cnt and sfl x4
     uint4 cur[kGLd], nxt[kGLd];
 #pragma unroll
     for (int k = 0; k < kGLd; ++k) cur[k] = gload16(rs, seg + 16u * k);
@@ -379,7 +386,7 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
     }
     GSum s;
     s.cnt = s4.cnt >> 2;
-    s.sq = s4.sq >> 2;
+    s.sq = s4.sq;
     s.sfl = s4.sfl >> 2;
     s.sl = s4.sl;
     if (!synced) s = GSum();  // covered by an earlier tail
