@@ -28,9 +28,6 @@ constexpr int kGTile = 64 * kGS;   // wave tile
 constexpr int kGBlk = 64;          // bytes per block (4 x 16 B per lane, double buffered)
 constexpr int kGLd = kGBlk / 16;
 constexpr int kGBlocks = kGS / kGBlk;
-#ifndef UGPU_XG_SELECT
-#define UGPU_XG_SELECT 0
-#endif
 #ifndef UGPU_XG_WAVES
 #define UGPU_XG_WAVES 16
 #endif
@@ -93,10 +90,11 @@ struct GSum {
 };
 
 // One byte of the main loop.  MASK: events of the lane's head (up to and
-// including its first sync byte) are dropped.
+// including its first sync byte) are dropped.  off1 = the byte's offset in its
+// block + 1 (a constant once unrolled): sq gets f (off1) here and f bb per block.
 template <int FMT, int K, bool MASK>
 __device__ __forceinline__ void gbyte(const GTab<FMT>& T, uint32_t w, uint32_t& m, uint32_t& acc, GSum& s,
-                                      uint32_t rp1, bool& synced, uint32_t& fs)
+                                      uint32_t bb, uint32_t off1, bool& synced, uint32_t& fs)
 {
   const uint32_t e = T.template step<K>(m, w);
   // bit 2 (XG_A): the new state accepts; d2 bit 2: the walk died here
@@ -109,16 +107,12 @@ __device__ __forceinline__ void gbyte(const GTab<FMT>& T, uint32_t w, uint32_t& 
     if (!synced) {
       f = 0;
       L = 0;
-      if (y) fs = rp1 - 1;
+      if (y) fs = bb + off1 - 1;
     }
     synced = synced || y != 0;
   }
-  s.cnt += f;                     // (sums of f are 4x: XG_A == 4)
-#if UGPU_XG_SELECT
-  s.sq += f ? rp1 : 0u;                 // (a select: not scaled)
-#else
-  s.sq += __umul24(f, rp1) >> 2;        // f = XG_A or 0
-#endif
+  s.cnt += f;  // (sums of f are 4x: XG_A == 4)
+  s.sq += __umul24(f, off1);
   s.sfl += __umul24(f, L);
   s.sl += L;
   m = e;
@@ -129,19 +123,21 @@ template <int FMT, bool MASK>
 __device__ __forceinline__ void gblock(const GTab<FMT>& T, const uint4 (&v)[kGLd], uint32_t& m, uint32_t& acc,
                                        GSum& s4, bool& synced, uint32_t& fs, uint32_t bb)
 {
-  GSum& s = s4;  // cnt and sfl are scaled by 4 (f = XG_A or 0); sq and sl are exact
+  GSum& s = s4;  // cnt, sq and sfl are scaled by 4 (f = XG_A or 0); sl is exact
+  const uint32_t c0 = s.cnt;
 #pragma unroll
   for (int k = 0; k < kGLd; ++k) {
     const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t q1 = bb + 16u * k + 4u * j + 1u;
-      gbyte<FMT, 0, MASK>(T, w[j], m, acc, s, q1, synced, fs);
-      gbyte<FMT, 1, MASK>(T, w[j], m, acc, s, q1 + 1, synced, fs);
-      gbyte<FMT, 2, MASK>(T, w[j], m, acc, s, q1 + 2, synced, fs);
-      gbyte<FMT, 3, MASK>(T, w[j], m, acc, s, q1 + 3, synced, fs);
+      const uint32_t o1 = 16u * k + 4u * j + 1u;
+      gbyte<FMT, 0, MASK>(T, w[j], m, acc, s, bb, o1, synced, fs);
+      gbyte<FMT, 1, MASK>(T, w[j], m, acc, s, bb, o1 + 1, synced, fs);
+      gbyte<FMT, 2, MASK>(T, w[j], m, acc, s, bb, o1 + 2, synced, fs);
+      gbyte<FMT, 3, MASK>(T, w[j], m, acc, s, bb, o1 + 3, synced, fs);
     }
   }
+  s.sq += __umul24(s.cnt - c0, bb);  // the block's starts at offset bb
 }
 
 __device__ __forceinline__ uint32_t gdist(uint64_t lim, uint64_t base)  // lim - base clamped to [0, 64]
@@ -369,7 +365,7 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
     }
     bool synced = first_wave && i == 0 && lane == 0 && ts == wlo;  // fresh entry at the tile start
     uint32_t fs = ~0u, m = T.start_row, acc = 0;
-    GSum s4;  // main loop: cnt and sfl x4
+    GSum s4;  // main loop: cnt, sq and sfl x4
     uint4 cur[kGLd], nxt[kGLd];
 #pragma unroll
     for (int k = 0; k < kGLd; ++k) cur[k] = gload16(rs, seg + 16u * k);
@@ -386,7 +382,7 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
     }
     GSum s;
     s.cnt = s4.cnt >> 2;
-    s.sq = s4.sq;
+    s.sq = s4.sq >> 2;
     s.sfl = s4.sfl >> 2;
     s.sl = s4.sl;
     if (!synced) s = GSum();  // covered by an earlier tail

@@ -41,60 +41,27 @@ namespace {
 #ifndef UGPU_XI_SEG
 #define UGPU_XI_SEG 1024
 #endif
-#ifndef UGPU_XI_PADLDS
-// Extra LDS per workgroup, capping xi_kernel at 3 workgroups (12 waves) per CU:
-// measured on C3 16 GiB, 3 waves per SIMD beat 4 (4.49 vs 5.39 ms) and 2 (5.64):
-// more waves keep more lane lines (64 per wave, 1 KiB apart) in flight.
-#define UGPU_XI_PADLDS 49152
+#ifndef UGPU_XI_WGLDS
+// LDS per workgroup (table + padding), capping xi_kernel at 3 workgroups (12
+// waves) per CU: measured on C3 16 GiB, 3 waves per SIMD beat 4 (4.49 vs 5.39
+// ms) and 2 (5.64).  Tables above 208 rows exceed it (2 workgroups per CU).
+#define UGPU_XI_WGLDS 53248
 #endif
 constexpr int kXS = UGPU_XI_SEG;   // lane segment bytes
 constexpr int kXTile = 64 * kXS;   // wave tile
 #ifndef UGPU_XI_BLK
 #define UGPU_XI_BLK 64
 #endif
-#ifndef UGPU_XI_STAGE
-#define UGPU_XI_STAGE 0  // 1: coalesced loads staged through LDS rows
-#endif
-constexpr int kXBlk = UGPU_XI_BLK;  // bytes per block: one 128-byte line per lane, read by back-to-back loads
+constexpr int kXBlk = UGPU_XI_BLK;  // bytes per block, read by back-to-back 16-byte loads
 constexpr int kXLd = kXBlk / 16;    // 16-byte loads per lane per block
-// Staging: per block the wave loads 64 segments x kXBlk bytes coalesced --
-// load j, lane l reads bytes [16 (l % G), +16) of segment (64 / kXLd) j + l / G,
-// G = kXLd lanes per line -- and writes them to its LDS rows (pitch kXPitch,
-// 34 dwords: two lanes share a bank at most when reading their rows).
-constexpr int kXG = kXLd;                  // lanes sharing one segment line in a load
-constexpr int kXPitch = kXBlk + 8;         // LDS row bytes per segment
-constexpr int kXBuf = 64 * kXPitch;        // LDS bytes per wave
 constexpr int kXBlocks = kXS / kXBlk;
 constexpr int kXWaves = 4;         // waves per workgroup (one staged table)
-
-#ifndef UGPU_XI_NT
-#define UGPU_XI_NT 0  // 1: non-temporal main-loop loads
-#endif
 
 __device__ __forceinline__ uint4 xload16(__amdgpu_buffer_rsrc_t rs, uint32_t off)
 {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
   return uint4{v.x, v.y, v.z, v.w};
-}
-
-__device__ __forceinline__ uint4 xload16m(__amdgpu_buffer_rsrc_t rs, uint32_t off)  // main loop
-{
-  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, UGPU_XI_NT ? 2 : 0);
-  return uint4{v.x, v.y, v.z, v.w};
-}
-
-__device__ __forceinline__ void xsync()
-{
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ uint32_t xload4(__amdgpu_buffer_rsrc_t rs, uint32_t off)
-{
-  return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t xrsrc(const uint8_t* base, uint64_t readable)
@@ -147,7 +114,7 @@ __device__ __forceinline__ void xdword(const uint8_t* T, uint32_t w, uint32_t& i
 
 // One block (kXBlk bytes of the lane's segment; dot4 position weights
 // 0..kXBlk-1); bb = block byte offset in the segment.  The bytes come from the
-// lane's LDS row (staged loads) or from registers (direct loads).
+// lane's registers.
 template <bool MASK, class SRC>
 __device__ __forceinline__ void xblock(const uint8_t* T, const SRC& src, uint32_t& id, XSum& a, bool& synced,
                                        uint32_t& fs, uint32_t bb)
@@ -169,12 +136,7 @@ __device__ __forceinline__ void xblock(const uint8_t* T, const SRC& src, uint32_
   a.ins2 += cI;
 }
 
-struct XRow {  // staged: the lane's LDS row
-  const uint2* row;
-  __device__ __forceinline__ uint2 operator()(int k) const { return row[k]; }
-};
-
-struct XRegs {  // direct: registers
+struct XRegs {  // the block's bytes in registers
   const uint4* v;
   __device__ __forceinline__ uint2 operator()(int k) const
   {
@@ -381,13 +343,9 @@ template <int ROWS>
 __global__ __launch_bounds__(kXWaves * 64, UGPU_XI_MINW) void xi_kernel(ScanParams P)
 {
   __shared__ __attribute__((aligned(16))) uint8_t xsm[ROWS * 256];
-#if UGPU_XI_STAGE
-  __shared__ __attribute__((aligned(16))) uint8_t xbuf[kXWaves * kXBuf];
-#endif
-#if UGPU_XI_PADLDS
-  __shared__ uint8_t xpad[UGPU_XI_PADLDS];
-  if (P.zero) xpad[threadIdx.x] = 0;
-#endif
+  constexpr int kPad = UGPU_XI_WGLDS - ROWS * 256 > 64 ? UGPU_XI_WGLDS - ROWS * 256 : 64;
+  __shared__ uint8_t xpad[kPad];
+  if (P.zero) xpad[threadIdx.x & 63] = 0;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   {
@@ -431,42 +389,16 @@ __global__ __launch_bounds__(kXWaves * 64, UGPU_XI_MINW) void xi_kernel(ScanPara
       // ---- fast tile: every lane segment lies inside [wlo, whi) ----
       bool synced = fresh == ts && lane == 0;  // fresh entry at the tile start
       uint32_t fs = ~0u, id = 0;
-#if UGPU_XI_STAGE
-      // Blocks are staged through the wave's LDS rows: coalesced loads (kXG
-      // lanes per 128-byte line) of block b+1 are in flight while block b is
-      // walked from LDS.
-      uint8_t* wbuf = xbuf + wid * kXBuf;
-      const XRow src{reinterpret_cast<const uint2*>(wbuf + lane * kXPitch)};
-      const uint32_t ls = (uint32_t)lane / kXG, lo16 = 16u * ((uint32_t)lane % kXG);
-      uint4 st[kXLd];
-#pragma unroll
-      for (int j = 0; j < kXLd; ++j) st[j] = xload16(rs, (ls + (64 / kXLd) * j) * kXS + lo16);
-      for (uint32_t b = 0; b < (uint32_t)kXBlocks; ++b) {
-        xsync();  // the previous block's rows are read
-#pragma unroll
-        for (int j = 0; j < kXLd; ++j) {
-          uint2* dst = reinterpret_cast<uint2*>(wbuf + (ls + (64 / kXLd) * j) * kXPitch + lo16);
-          dst[0] = uint2{st[j].x, st[j].y};
-          dst[1] = uint2{st[j].z, st[j].w};
-        }
-        xsync();
-        if (b + 1 < (uint32_t)kXBlocks) {
-#pragma unroll
-          for (int j = 0; j < kXLd; ++j)
-            st[j] = xload16(rs, (ls + (64 / kXLd) * j) * kXS + (b + 1) * kXBlk + lo16);
-        }
-#else
       // Direct loads: lane l reads its own segment, 16 bytes per load, block
       // b+1 in flight while block b is walked.
       uint4 cur[kXLd], nxt[kXLd];
       const XRegs src{cur};
 #pragma unroll
-      for (int k = 0; k < kXLd; ++k) cur[k] = xload16m(rs, seg + 16u * k);
+      for (int k = 0; k < kXLd; ++k) cur[k] = xload16(rs, seg + 16u * k);
       for (uint32_t b = 0; b < (uint32_t)kXBlocks; ++b) {
         const uint32_t nb = b + 1 < (uint32_t)kXBlocks ? b + 1 : b;
 #pragma unroll
-        for (int k = 0; k < kXLd; ++k) nxt[k] = xload16m(rs, seg + nb * kXBlk + 16u * k);
-#endif
+        for (int k = 0; k < kXLd; ++k) nxt[k] = xload16(rs, seg + nb * kXBlk + 16u * k);
         if (P.ablate == 6) {
           id ^= src(0).x ^ src(3).y;  // loads only (benchmarking; wrong counts)
         } else if (__ballot(!synced)) {
@@ -474,10 +406,8 @@ __global__ __launch_bounds__(kXWaves * 64, UGPU_XI_MINW) void xi_kernel(ScanPara
         } else {
           xblock<false>(T, src, id, a, synced, fs, b * kXBlk);
         }
-#if !UGPU_XI_STAGE
 #pragma unroll
         for (int k = 0; k < kXLd; ++k) cur[k] = nxt[k];
-#endif
       }
       // a lane that never met a sync byte counts nothing: an earlier tail covers it
       if (!synced) a = XSum();
