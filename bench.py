@@ -140,6 +140,9 @@ def main():
                          "for N > 1, all-gathers them to every rank (SURVEY.md §8e step 4)")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also scans the whole logical stream alone and checks the stitched totals")
+    ap.add_argument("--compile", action="store_true",
+                    help="tables from the native regex compiler (ugpu_compile) instead of the reference's "
+                         "dumped opcode words")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,6 +171,8 @@ def main():
     n_read = read_end - lo
     with open(os.path.join(REPO, "ugrep_amd", "data", "config_patterns.json")) as f:
         opc = json.load(f)[pkey]["opc"]
+    if args.compile:
+        opc = ugrep_amd.compile_regex(rx, fixed=(mode == "F"))
     pat = ugrep_amd.Pattern(opc)
     info = pat.info()
 
@@ -270,7 +275,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc, "config": args.config, "pattern": rx, "bytes_per_gpu": per_gpu,
                    "total_bytes": total, "corpus_kind": kind, "parallelism": "shard%d" % world,
-                   "dfa_states": info["states"], "dfa_row": info["row"], "prefilter_ppm": info["prefilter_ppm"]},
+                   "tables": "compiled" if args.compile else "reference", "dfa_states": info["states"], "dfa_row": info["row"], "prefilter_ppm": info["prefilter_ppm"]},
         "matches": res["count"],
         "matches_per_s": round(matches_per_s, 1),
         "digest": res["digest"],

@@ -240,6 +240,24 @@ int ugpu_is_binary(const uint8_t *dbuf, uint64_t len, uint32_t flags, int *binar
 /* Write bytes [off, off+len) of corpus `kind` with `seed` into dbuf. */
 int ugpu_gen(int kind, uint64_t seed, uint64_t off, uint8_t *dbuf, uint64_t len, void *stream);
 
+/* --- regex -> opcode words (replaces Matcher::convert + Pattern(conv, "r"),
+   lib/convert.cpp and lib/pattern.cpp:171-3063, for FIND tables) ---
+
+   Compiles `regex` (len bytes, ugrep's default ERE syntax in Unicode mode with
+   notnewline, src/ugrep.cpp:8574-8578) into opcode words in the reference's
+   format (include/reflex/pattern.h:1155-1247), language-equivalent per accept
+   index to the reference's Pattern; feed them to ugpu_dfa_create().  *opc is
+   malloc'd, free it with ugpu_opc_free().  Returns UGPU_INVAL on a syntax error
+   (the reference throws regex_error, lib/pattern.cpp:162-169) and
+   UGPU_UNSUPPORTED for constructs the GPU tables do not cover (anchors, word
+   boundaries, lazy quantifiers, lookaround, \p{..}, POSIX [:class:]); the
+   message is in ugpu_compile_error(). */
+#define UGPU_RX_FIXED 1u /* -F: the pattern is a literal string (src/cnf.hpp:147-165) */
+#define UGPU_RX_ICASE 2u /* -i, ASCII letters only */
+int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, uint32_t *nop);
+void ugpu_opc_free(uint32_t *opc);
+const char *ugpu_compile_error(void);
+
 const char *ugpu_last_error(void);
 const char *ugpu_version(void);
 

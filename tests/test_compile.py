@@ -1,0 +1,148 @@
+"""Regex -> opcode compiler (ugpu_compile, ugrep_amd/csrc/regex_compile.cpp)
+against the reference's own compiled tables.
+
+The fixture tests/golden/compile_cases.npz holds, per case, the opcode words
+the reference Pattern produced (tools/gen_compile_golden.py, libreflex built
+from /root/reference; empty = the reference throws regex_error).  Parity is
+language equivalence per accept index (tests/dfa_equiv.py), which is exactly
+"identical FIND results on every input" (SURVEY Appendix A).  The GPU test
+runs compiled tables through the HIP engine and checks every match record
+against the oracle restatement driven by the reference's table.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from dfa_equiv import counterexample
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _cases():
+    z = np.load(os.path.join(HERE, "golden", "compile_cases.npz"))
+    offs, words = z["offsets"], z["words"]
+    out = []
+    for i, (mode, pat) in enumerate(zip(z["modes"], z["patterns"])):
+        ref = words[offs[i]:offs[i + 1]]
+        out.append((str(mode), bytes(pat).decode("utf-8"), ref if len(ref) else None))
+    return out
+
+
+CASES = _cases()
+
+
+def _compile(U, mode, rx):
+    return U.compile_regex(rx, fixed=(mode == "F"), icase=(mode == "i"))
+
+
+def test_fixture_covers_configs():
+    pats = {(m, p) for m, p, _ in CASES}
+    for key in (("re", "foo|bar|baz"), ("re", "[A-Za-z_][A-Za-z0-9_]*"), ("re", r"\w+"), ("F", "lorem")):
+        assert key in pats
+    assert len(CASES) > 200
+
+
+@pytest.mark.parametrize("chunk", range(4))
+def test_compile_equivalent_to_reference(chunk):
+    import ugrep_amd as U
+    bad = []
+    for mode, rx, ref in CASES[chunk::4]:
+        if ref is None:
+            with pytest.raises(U.UgpuError) as e:
+                _compile(U, mode, rx)
+            assert not isinstance(e.value, U.Unsupported), (mode, rx)
+            continue
+        mine = _compile(U, mode, rx)
+        ce = counterexample(mine, ref)
+        if ce is not None:
+            bad.append((mode, rx, ce))
+    assert not bad, bad[:5]
+
+
+def test_config_tables_are_loadable():
+    """Compiled tables pass the device-table builder (host side) and pick the
+    same kernel class as the reference's tables for the BASELINE configs."""
+    import ugrep_amd as U
+    ref = {(m, p): r for m, p, r in CASES}
+    for mode, rx in (("re", "foo|bar|baz"), ("re", "[A-Za-z_][A-Za-z0-9_]*"), ("re", r"\w+"), ("F", "lorem")):
+        a = U.host_tables(_compile(U, mode, rx))["info"]
+        b = U.host_tables(ref[(mode, rx)])["info"]
+        assert a["kernel"] == b["kernel"], (rx, a, b)
+        assert a["states"] <= b["states"]
+
+
+@pytest.mark.parametrize("rx", ["^a", "a$", r"\bfoo", r"\<x", "a*?", "a+?", r"(a)\1", r"\p{L}", "[[:alpha:]]",
+                                "(?=x)", r"\Qa\E", "é"])
+def test_unsupported_constructs(rx):
+    import ugrep_amd as U
+    with pytest.raises(U.Unsupported):
+        U.compile_regex(rx, icase=(rx == "é"))
+
+
+def test_long_gotos():
+    """Tables past 0xFFFE words use LONG gotos (lib/pattern.cpp:2877-2939) and
+    stay equivalent: a large alternation of distinct words."""
+    import ugrep_amd as U
+    import random
+    rng = random.Random(5)
+    words = sorted({"".join(rng.choice("abcdefghij") for _ in range(10)) for _ in range(5000)})
+    opc = U.compile_regex("|".join(words))
+    assert len(opc) > 0xFFFE
+    assert any((w & 0xFFFF) == 0xFFFE for w in opc[:64])
+    from dfa_equiv import _parse_opc
+    nxt, caps = _parse_opc(opc)
+    # walk each word: accepts with its 1-based alternative index
+    for k in (0, 1, len(words) // 2, len(words) - 1):
+        s = 1
+        for ch in words[k].encode():
+            s = nxt[s][ch]
+        assert caps[s] == k + 1
+
+
+@pytest.mark.gpu
+def test_compiled_tables_on_gpu():
+    """Compiled tables through the HIP engine == the oracle driven by the
+    reference's tables, record by record, on a mixed UTF-8/code corpus."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd as U
+    from oracle_lib import OracleDfa, gen
+    host = np.concatenate([gen(4, 7, 0, 1 << 20), gen(3, 7, 0, 1 << 20), gen(1, 7, 0, 1 << 19)])
+    dev = torch.from_numpy(host).to("cuda")
+    torch.cuda.synchronize()
+    checked = 0
+    for mode, rx, ref in CASES[::3]:
+        if ref is None:
+            continue
+        try:
+            pat = U.Pattern(_compile(U, mode, rx))
+        except U.Unsupported:
+            continue  # table too large for the 16-bit device tables
+        res = U.find_all(pat, dev, offsets=True)
+        cnt, dg, dc, lst = OracleDfa(ref).find(host, want_list=True)
+        assert (res.count, res.digest, res.dcap) == (cnt, dg, dc), (mode, rx)
+        assert res.triples() == lst, (mode, rx)
+        checked += 1
+    assert checked > 40
+
+
+@pytest.mark.gpu
+def test_rare_sync_bytes_long_tails():
+    """\\D over UTF-8 words: only digits are sync bytes, so xg_kernel lanes
+    walk tails across the whole buffer (64-bit tail sums; a 32-bit lane sum
+    wrapped here before).  Whole-buffer totals == oracle."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd as U
+    from oracle_lib import OracleDfa, gen
+    host = gen(4, 11, 0, 48 << 20)
+    dev = torch.from_numpy(host).to("cuda")
+    torch.cuda.synchronize()
+    for rx in (r"\D", r"\D\D", r"[^0-9]+"):
+        opc = U.compile_regex(rx)
+        pat = U.Pattern(opc)
+        res = U.find_all(pat, dev)
+        assert (res.count, res.digest, res.dcap) == OracleDfa(opc).find(host)[:3], rx

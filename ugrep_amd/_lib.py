@@ -100,6 +100,10 @@ def _load():
         "ugpu_check_utf8": (ctypes.c_int, [V, ctypes.c_uint64, P(ctypes.c_uint64), V]),
         "ugpu_find_nul": (ctypes.c_int, [V, ctypes.c_uint64, P(ctypes.c_uint64), V]),
         "ugpu_is_binary": (ctypes.c_int, [V, ctypes.c_uint64, ctypes.c_uint32, P(ctypes.c_int), V]),
+        "ugpu_compile": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, P(c_u32p),
+                                        P(ctypes.c_uint32)]),
+        "ugpu_opc_free": (None, [c_u32p]),
+        "ugpu_compile_error": (ctypes.c_char_p, []),
         "ugpu_last_error": (ctypes.c_char_p, []),
         "ugpu_version": (ctypes.c_char_p, []),
     }

@@ -1,0 +1,1190 @@
+// regex_compile.cpp -- host-side regex -> DFA -> opcode-word compiler.
+//
+// Replaces, for the FIND hot path, the reference's pattern pipeline
+//   Matcher::convert(rx, notnewline|unicode)   (lib/convert.cpp, src/ugrep.cpp:8574-8578)
+//   Pattern(conv, "r") -> parse/compile/encode_dfa  (lib/pattern.cpp:171-3063)
+// with a from-scratch construction:
+//   parse (ugrep's default ERE syntax, Unicode mode)  -> byte-level syntax tree
+//   Unicode code point sets -> valid UTF-8 byte-range sequences (strict, like
+//     lib/utf8.cpp utf8(a, b, .., strict=true) as called by convert.cpp:124-171)
+//   Glushkov positions + subset construction -> DFA over bytes
+//   Moore minimisation -> opcode words in the reference's format
+//     (include/reflex/pattern.h:1155-1247; Appendix B of SURVEY.md in reverse),
+// so ugpu_dfa_create() consumes the result exactly like a table dumped from a
+// reference Pattern.  Parity is language equivalence with the reference's DFA
+// per accept index (tests/test_compile.py), which implies identical FIND
+// results on every input.
+//
+// Supported: literals (UTF-8), escapes \t\n\r\f\v\a\e \xHH \x{H..} \0ooo and
+// escaped punctuation, '.', bracket expressions (ranges, negation, escapes,
+// \w\d\s\h inside), \w \W \d \D \s \S \h \H, groups ( ) (?: ), alternation,
+// * + ? {n} {n,} {n,m}, -F literal mode, and ASCII -i case folding.
+// Returns UGPU_UNSUPPORTED for what the GPU tables cannot express or this
+// compiler does not cover (anchors, word boundaries, lazy quantifiers,
+// lookaround, backreferences, \p{..}, POSIX [:class:]): the caller keeps the
+// CPU matcher for those, as for any unsupported opcode table.
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <bitset>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ugpu.h"
+
+namespace {
+
+#include "unicode_ranges.inc"
+
+typedef std::vector<std::pair<uint32_t, uint32_t>> CpSet;  // sorted, disjoint, inclusive
+typedef std::bitset<256> ByteSet;
+
+const uint32_t kMaxCp = 0x10FFFF;
+const size_t kMaxPositions = 1u << 16;  // expansion guard ({n,m} of large subtrees)
+const size_t kMaxStates = 1u << 16;
+
+struct CompileError
+{
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string &msg)
+{
+  throw CompileError{code, msg};
+}
+
+// ---------------------------------------------------------------- code point sets
+
+CpSet normalize(CpSet s)
+{
+  std::sort(s.begin(), s.end());
+  CpSet out;
+  for (auto &r : s)
+  {
+    if (!out.empty() && r.first <= out.back().second + 1)
+      out.back().second = std::max(out.back().second, r.second);
+    else
+      out.push_back(r);
+  }
+  return out;
+}
+
+// complement over [0, hi], surrogates included
+CpSet complement_upto(const CpSet &s, uint32_t hi)
+{
+  CpSet out;
+  uint32_t next = 0;
+  for (auto &r : s)
+  {
+    if (r.first > hi)
+      break;
+    if (r.first > next)
+      out.push_back({next, r.first - 1});
+    next = r.second + 1;
+  }
+  if (next <= hi)
+    out.push_back({next, hi});
+  return out;
+}
+
+CpSet no_surrogates(const CpSet &s);
+
+// complement over the Unicode scalar values (surrogates never match, as
+// convert.cpp:124-162 skips D800-DFFF)
+CpSet complement(const CpSet &s)
+{
+  return no_surrogates(complement_upto(s, kMaxCp));
+}
+
+CpSet minus(const CpSet &a, const CpSet &b)
+{
+  CpSet out;
+  for (auto r : a)
+  {
+    uint32_t lo = r.first;
+    for (auto &x : b)
+    {
+      if (x.second < lo || x.first > r.second)
+        continue;
+      if (x.first > lo)
+        out.push_back({lo, x.first - 1});
+      lo = x.second + 1;
+      if (lo > r.second || x.second == kMaxCp)
+        break;
+    }
+    if (lo <= r.second && lo != 0x110000)
+      out.push_back({lo, r.second});
+  }
+  return out;
+}
+
+CpSet no_surrogates(const CpSet &s)
+{
+  return minus(s, CpSet{{0xD800, 0xDFFF}});
+}
+
+template <size_t N>
+CpSet table_set(const uint32_t (&t)[N][2])
+{
+  CpSet s;
+  for (size_t i = 0; i < N; ++i)
+    s.push_back({t[i][0], t[i][1]});
+  return s;
+}
+
+CpSet word_set() { return table_set(k_word_ranges); }
+CpSet digit_set() { return table_set(k_digit_ranges); }
+CpSet space_set() { return table_set(k_space_ranges); }
+CpSet hspace_set() { return CpSet{{'\t', '\t'}, {' ', ' '}}; }
+
+void add_ascii_case(CpSet &s)
+{
+  CpSet extra;
+  for (auto &r : s)
+    for (uint32_t c = r.first; c <= r.second && c < 0x80; ++c)
+    {
+      if (c >= 'a' && c <= 'z')
+        extra.push_back({c - 32, c - 32});
+      else if (c >= 'A' && c <= 'Z')
+        extra.push_back({c + 32, c + 32});
+    }
+  s.insert(s.end(), extra.begin(), extra.end());
+  s = normalize(s);
+}
+
+// ---------------------------------------------------------------- syntax tree
+
+enum Kind
+{
+  LEAF,  // one byte from `bytes`
+  CAT,
+  ALT,
+  STAR,
+  PLUS,
+  OPT,
+  EMPTY
+};
+
+struct Node
+{
+  Kind kind;
+  ByteSet bytes;
+  std::vector<int> kids;
+};
+
+struct Tree
+{
+  std::vector<Node> nodes;
+  size_t leaves = 0;
+
+  int add(Kind k, std::vector<int> kids = {})
+  {
+    nodes.push_back(Node{k, ByteSet(), std::move(kids)});
+    return static_cast<int>(nodes.size() - 1);
+  }
+  int leaf(const ByteSet &b)
+  {
+    if (++leaves > kMaxPositions)
+      fail(UGPU_UNSUPPORTED, "pattern expands to too many positions");
+    int n = add(LEAF);
+    nodes[n].bytes = b;
+    return n;
+  }
+  int leaf_range(unsigned lo, unsigned hi)
+  {
+    ByteSet b;
+    for (unsigned c = lo; c <= hi; ++c)
+      b.set(c);
+    return leaf(b);
+  }
+  int clone(int n)
+  {
+    Node copy = nodes[n];
+    if (copy.kind == LEAF)
+      return leaf(copy.bytes);
+    std::vector<int> kids;
+    for (int k : copy.kids)
+      kids.push_back(clone(k));
+    return add(copy.kind, kids);
+  }
+
+  // UTF-8 byte-range sequences of [lo, hi] (same encoded length, split so that
+  // each sequence is a product of byte ranges)
+  void utf8_split(uint32_t lo, uint32_t hi, std::vector<std::vector<std::pair<uint8_t, uint8_t>>> &out)
+  {
+    static const uint32_t len_max[3] = {0x7F, 0x7FF, 0xFFFF};
+    for (uint32_t m : len_max)
+      if (lo <= m && hi > m)
+      {
+        utf8_split(lo, m, out);
+        utf8_split(m + 1, hi, out);
+        return;
+      }
+    if (hi <= 0x7F)
+    {
+      out.push_back({{static_cast<uint8_t>(lo), static_cast<uint8_t>(hi)}});
+      return;
+    }
+    for (int i = 1; i < 4; ++i)
+    {
+      uint32_t m = (1u << (6 * i)) - 1;
+      if ((lo & ~m) != (hi & ~m))
+      {
+        if ((lo & m) != 0)
+        {
+          utf8_split(lo, lo | m, out);
+          utf8_split((lo | m) + 1, hi, out);
+          return;
+        }
+        if ((hi & m) != m)
+        {
+          utf8_split(lo, (hi & ~m) - 1, out);
+          utf8_split(hi & ~m, hi, out);
+          return;
+        }
+      }
+    }
+    uint8_t a[4], b[4];
+    int n = encode(lo, a);
+    encode(hi, b);
+    std::vector<std::pair<uint8_t, uint8_t>> seq;
+    for (int i = 0; i < n; ++i)
+      seq.push_back({a[i], b[i]});
+    out.push_back(seq);
+  }
+
+  static int encode(uint32_t c, uint8_t *o)
+  {
+    if (c < 0x80)
+    {
+      o[0] = static_cast<uint8_t>(c);
+      return 1;
+    }
+    if (c < 0x800)
+    {
+      o[0] = static_cast<uint8_t>(0xC0 | (c >> 6));
+      o[1] = static_cast<uint8_t>(0x80 | (c & 0x3F));
+      return 2;
+    }
+    if (c < 0x10000)
+    {
+      o[0] = static_cast<uint8_t>(0xE0 | (c >> 12));
+      o[1] = static_cast<uint8_t>(0x80 | ((c >> 6) & 0x3F));
+      o[2] = static_cast<uint8_t>(0x80 | (c & 0x3F));
+      return 3;
+    }
+    o[0] = static_cast<uint8_t>(0xF0 | (c >> 18));
+    o[1] = static_cast<uint8_t>(0x80 | ((c >> 12) & 0x3F));
+    o[2] = static_cast<uint8_t>(0x80 | ((c >> 6) & 0x3F));
+    o[3] = static_cast<uint8_t>(0x80 | (c & 0x3F));
+    return 4;
+  }
+
+  // subtree matching exactly the valid UTF-8 encodings of the code points in s
+  int cpset(const CpSet &s0)
+  {
+    CpSet s = normalize(s0);
+    ByteSet ascii;
+    std::vector<std::vector<std::pair<uint8_t, uint8_t>>> seqs;
+    for (auto &r : s)
+    {
+      if (r.first < 0x80)
+        for (uint32_t c = r.first; c <= std::min<uint32_t>(r.second, 0x7F); ++c)
+          ascii.set(c);
+      if (r.second >= 0x80)
+        utf8_split(std::max<uint32_t>(r.first, 0x80), r.second, seqs);
+    }
+    std::vector<int> alts;
+    if (ascii.any())
+      alts.push_back(leaf(ascii));
+    // share leading byte ranges: group sequences by their first range
+    std::map<std::pair<uint8_t, uint8_t>, std::vector<std::vector<std::pair<uint8_t, uint8_t>>>> groups;
+    for (auto &q : seqs)
+      groups[q[0]].push_back(std::vector<std::pair<uint8_t, uint8_t>>(q.begin() + 1, q.end()));
+    for (auto &g : groups)
+      alts.push_back(add(CAT, {leaf_range(g.first.first, g.first.second), suffixes(g.second)}));
+    if (alts.empty())
+      fail(UGPU_INVAL, "empty character class");
+    return alts.size() == 1 ? alts[0] : add(ALT, alts);
+  }
+
+  int suffixes(std::vector<std::vector<std::pair<uint8_t, uint8_t>>> &tails)
+  {
+    std::map<std::pair<uint8_t, uint8_t>, std::vector<std::vector<std::pair<uint8_t, uint8_t>>>> groups;
+    for (auto &q : tails)
+      groups[q[0]].push_back(std::vector<std::pair<uint8_t, uint8_t>>(q.begin() + 1, q.end()));
+    std::vector<int> alts;
+    for (auto &g : groups)
+    {
+      int head = leaf_range(g.first.first, g.first.second);
+      if (g.second[0].empty())
+        alts.push_back(head);
+      else
+        alts.push_back(add(CAT, {head, suffixes(g.second)}));
+    }
+    return alts.size() == 1 ? alts[0] : add(ALT, alts);
+  }
+};
+
+// ---------------------------------------------------------------- parser
+
+class Parser
+{
+ public:
+  Parser(const std::string &rx, uint32_t flags, Tree &t) : s_(rx), flags_(flags), t_(t) {}
+
+  // top-level alternatives (each gets its own accept index, as the reference's
+  // Pattern numbers top-level choices: SURVEY Appendix D, foo|bar|baz -> TAKE 1/2/3)
+  std::vector<int> parse_top()
+  {
+    std::vector<int> alts;
+    if (flags_ & UGPU_RX_FIXED)
+    {
+      std::vector<int> seq;
+      for (size_t i = 0; i < s_.size(); ++i)
+        seq.push_back(literal_byte(static_cast<uint8_t>(s_[i])));
+      alts.push_back(seq.empty() ? t_.add(EMPTY) : t_.add(CAT, seq));
+      return alts;
+    }
+    if (!s_.empty() && s_[0] == '|')
+      fail(UGPU_INVAL, "empty first alternative");  // the reference rejects "|a" (but not "a|")
+    alts.push_back(parse_concat());
+    while (p_ < s_.size() && s_[p_] == '|')
+    {
+      ++p_;
+      alts.push_back(parse_concat());
+    }
+    if (p_ != s_.size())
+      fail(UGPU_INVAL, "unbalanced ')'");
+    return alts;
+  }
+
+ private:
+  const std::string &s_;
+  uint32_t flags_;
+  Tree &t_;
+  size_t p_ = 0;
+
+  bool icase() const { return flags_ & UGPU_RX_ICASE; }
+
+  int literal_byte(uint8_t c)
+  {
+    ByteSet b;
+    b.set(c);
+    if (icase() && ((c | 0x20) >= 'a' && (c | 0x20) <= 'z'))
+      b.set(c ^ 0x20);
+    return t_.leaf(b);
+  }
+
+  int parse_alt()
+  {
+    // an empty alternative inside a group is a regex_error in the reference
+    // (only top-level alternatives may be empty)
+    auto branch = [&]() {
+      if (p_ >= s_.size() || s_[p_] == '|' || s_[p_] == ')')
+        fail(UGPU_INVAL, "empty alternative in group");
+      return parse_concat();
+    };
+    std::vector<int> alts{branch()};
+    while (p_ < s_.size() && s_[p_] == '|')
+    {
+      ++p_;
+      alts.push_back(branch());
+    }
+    return alts.size() == 1 ? alts[0] : t_.add(ALT, alts);
+  }
+
+  int parse_concat()
+  {
+    std::vector<int> seq;
+    while (p_ < s_.size() && s_[p_] != '|' && s_[p_] != ')')
+      seq.push_back(parse_repeat());
+    if (seq.empty())
+      return t_.add(EMPTY);
+    return seq.size() == 1 ? seq[0] : t_.add(CAT, seq);
+  }
+
+  bool parse_braces(int &lo, int &hi)
+  {
+    // {n}, {n,}, {n,m} at p_ (p_ on '{'); returns false when not a quantifier
+    size_t q = p_ + 1;
+    auto num = [&](int &v) {
+      size_t st = q;
+      v = 0;
+      while (q < s_.size() && s_[q] >= '0' && s_[q] <= '9')
+      {
+        v = v * 10 + (s_[q++] - '0');
+        if (v > 1000)
+          fail(UGPU_UNSUPPORTED, "repeat count too large");
+      }
+      return q > st;
+    };
+    if (!num(lo))
+      return false;
+    hi = lo;
+    if (q < s_.size() && s_[q] == ',')
+    {
+      ++q;
+      if (!num(hi))
+        hi = -1;
+    }
+    if (q >= s_.size() || s_[q] != '}')
+      return false;
+    if (hi >= 0 && hi < lo)
+      fail(UGPU_INVAL, "bad repeat range");
+    p_ = q + 1;
+    return true;
+  }
+
+  int repeat(int a, int lo, int hi)
+  {
+    std::vector<int> seq;
+    for (int i = 0; i < lo; ++i)
+      seq.push_back(i == 0 ? a : t_.clone(a));
+    if (hi < 0)
+      seq.push_back(t_.add(STAR, {lo == 0 ? a : t_.clone(a)}));
+    else
+    {
+      // X{lo,hi}: X^lo (X (X ...)?)? nested optionals
+      int tail = -1;
+      for (int i = hi - lo; i > 0; --i)
+      {
+        int x = (lo == 0 && i == 1) ? a : t_.clone(a);
+        tail = t_.add(OPT, {tail < 0 ? x : t_.add(CAT, {x, tail})});
+      }
+      if (tail >= 0)
+        seq.push_back(tail);
+    }
+    if (seq.empty())
+      return t_.add(EMPTY);
+    return seq.size() == 1 ? seq[0] : t_.add(CAT, seq);
+  }
+
+  int parse_repeat()
+  {
+    bool dot = p_ < s_.size() && s_[p_] == '.';
+    // convert.cpp:2118-2160: a Unicode '.' becomes one UTF-8 character unless
+    // it is followed by '*' or '+', where it stays the byte class [^\n]
+    bool dot_byte = dot && p_ + 1 < s_.size() && (s_[p_ + 1] == '*' || s_[p_ + 1] == '+');
+    int a = parse_atom(dot_byte);
+    while (p_ < s_.size())
+    {
+      char c = s_[p_];
+      int lo, hi;
+      if (c == '*')
+      {
+        ++p_;
+        a = t_.add(STAR, {a});
+      }
+      else if (c == '+')
+      {
+        ++p_;
+        a = t_.add(PLUS, {a});
+      }
+      else if (c == '?')
+      {
+        ++p_;
+        a = t_.add(OPT, {a});
+      }
+      else if (c == '{')
+      {
+        if (!parse_braces(lo, hi))
+          fail(UGPU_INVAL, "bad repeat");
+        a = repeat(a, lo, hi);
+      }
+      else
+        break;
+      if (p_ < s_.size() && s_[p_] == '?')
+        fail(UGPU_UNSUPPORTED, "lazy quantifier");
+      if (p_ < s_.size() && s_[p_] == '+' )
+        fail(UGPU_UNSUPPORTED, "possessive quantifier");
+    }
+    return a;
+  }
+
+  uint32_t utf8_char()
+  {
+    // decode one (valid) UTF-8 character of the pattern at p_
+    uint8_t c = static_cast<uint8_t>(s_[p_++]);
+    if (c < 0x80)
+      return c;
+    int n = c >= 0xF0 ? 3 : c >= 0xE0 ? 2 : c >= 0xC0 ? 1 : -1;
+    if (n < 0)
+      fail(UGPU_UNSUPPORTED, "invalid UTF-8 in pattern");
+    uint32_t v = c & (0x3F >> n);
+    for (int i = 0; i < n; ++i)
+    {
+      if (p_ >= s_.size() || (static_cast<uint8_t>(s_[p_]) & 0xC0) != 0x80)
+        fail(UGPU_UNSUPPORTED, "invalid UTF-8 in pattern");
+      v = (v << 6) | (static_cast<uint8_t>(s_[p_++]) & 0x3F);
+    }
+    return v;
+  }
+
+  int hexval(char c)
+  {
+    if (c >= '0' && c <= '9')
+      return c - '0';
+    if (c >= 'a' && c <= 'f')
+      return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F')
+      return c - 'A' + 10;
+    return -1;
+  }
+
+  // escape at p_ (just past '\'): returns true and a class set in `set`, or a
+  // single code point in `cp`
+  bool parse_escape(CpSet &set, uint32_t &cp, bool in_bracket)
+  {
+    if (p_ >= s_.size())
+      fail(UGPU_INVAL, "trailing backslash");
+    char c = s_[p_++];
+    switch (c)
+    {
+      case 'w': set = word_set(); return true;
+      case 'd': set = digit_set(); return true;
+      case 's': set = space_set(); return true;
+      case 'h': set = hspace_set(); return true;
+      // negated classes, as the reference's DFAs have them (probed per code
+      // point, tests/test_compile.py): outside brackets \W \D \H complement
+      // over all scalar values (also '\n') and \S excludes '\n'; inside a
+      // bracket \W and \D complement only up to the table's last code point,
+      // while \S and \H keep the surrogate encodings
+      case 'W':
+        set = in_bracket ? no_surrogates(complement_upto(word_set(), word_set().back().second))
+                         : complement(word_set());
+        return true;
+      case 'D':
+        set = in_bracket ? no_surrogates(complement_upto(digit_set(), digit_set().back().second))
+                         : complement(digit_set());
+        return true;
+      case 'S':
+        set = minus(in_bracket ? complement_upto(space_set(), kMaxCp) : complement(space_set()),
+                    CpSet{{'\n', '\n'}});
+        return true;
+      case 'H':
+        set = in_bracket ? complement_upto(hspace_set(), kMaxCp) : complement(hspace_set());
+        return true;
+      case 't': cp = '\t'; return false;
+      case 'n': cp = '\n'; return false;
+      case 'r': cp = '\r'; return false;
+      case 'f': cp = '\f'; return false;
+      case 'v': cp = '\v'; return false;
+      case 'a': cp = '\a'; return false;
+      case 'e': cp = 0x1B; return false;
+      case 'x':
+      {
+        uint32_t v = 0;
+        if (p_ < s_.size() && s_[p_] == '{')
+        {
+          size_t q = p_ + 1;
+          int digits = 0;
+          while (q < s_.size() && hexval(s_[q]) >= 0)
+          {
+            v = v * 16 + hexval(s_[q++]);
+            if (++digits > 6)
+              fail(UGPU_INVAL, "bad \\x{}");
+          }
+          if (q >= s_.size() || s_[q] != '}' || digits == 0 || v > kMaxCp)
+            fail(UGPU_INVAL, "bad \\x{}");
+          p_ = q + 1;
+        }
+        else
+        {
+          int digits = 0;
+          while (digits < 2 && p_ < s_.size() && hexval(s_[p_]) >= 0)
+          {
+            v = v * 16 + hexval(s_[p_++]);
+            ++digits;
+          }
+          if (digits == 0)
+            fail(UGPU_INVAL, "bad \\x");
+        }
+        cp = v;
+        return false;
+      }
+      case '0':
+      {
+        uint32_t v = 0;
+        for (int i = 0; i < 3 && p_ < s_.size() && s_[p_] >= '0' && s_[p_] <= '7'; ++i)
+          v = v * 8 + (s_[p_++] - '0');
+        cp = v;
+        return false;
+      }
+      default:
+        break;
+    }
+    if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '1' && c <= '9'))
+      fail(UGPU_UNSUPPORTED, std::string("escape \\") + c + (in_bracket ? " in bracket" : ""));
+    --p_;
+    cp = utf8_char();
+    return false;
+  }
+
+  CpSet parse_bracket()
+  {
+    // p_ just past '['
+    bool neg = false;
+    if (p_ < s_.size() && s_[p_] == '^')
+    {
+      neg = true;
+      ++p_;
+    }
+    CpSet set;
+    bool first = true;
+    for (;;)
+    {
+      if (p_ >= s_.size())
+        fail(UGPU_INVAL, "unterminated bracket");
+      char c = s_[p_];
+      if (c == ']' && !first)
+      {
+        ++p_;
+        break;
+      }
+      first = false;
+      if (c == '[' && p_ + 1 < s_.size() && (s_[p_ + 1] == ':' || s_[p_ + 1] == '.' || s_[p_ + 1] == '='))
+        fail(UGPU_UNSUPPORTED, "POSIX bracket class");
+      uint32_t lo;
+      CpSet cls;
+      if (c == '\\')
+      {
+        ++p_;
+        if (parse_escape(cls, lo, true))
+        {
+          set.insert(set.end(), cls.begin(), cls.end());
+          continue;
+        }
+      }
+      else
+        lo = utf8_char();
+      uint32_t hi = lo;
+      if (p_ + 1 < s_.size() && s_[p_] == '-' && s_[p_ + 1] != ']')
+      {
+        ++p_;
+        if (s_[p_] == '\\')
+        {
+          ++p_;
+          if (parse_escape(cls, hi, true))
+            fail(UGPU_INVAL, "class in range");
+        }
+        else
+          hi = utf8_char();
+        if (hi < lo)
+          fail(UGPU_INVAL, "bad range");
+      }
+      set.push_back({lo, hi});
+    }
+    set = normalize(set);
+    if (icase())
+    {
+      for (auto &r : set)
+        if (r.second >= 0x80 && !(r.first == 0 && r.second == kMaxCp))
+          fail(UGPU_UNSUPPORTED, "Unicode case folding");
+      add_ascii_case(set);
+    }
+    if (neg)
+      set = minus(complement(set), CpSet{{'\n', '\n'}});  // notnewline
+    return set;
+  }
+
+  int parse_atom(bool dot_byte)
+  {
+    char c = s_[p_];
+    switch (c)
+    {
+      case '(':
+      {
+        ++p_;
+        if (p_ < s_.size() && s_[p_] == '?')
+        {
+          if (p_ + 1 < s_.size() && s_[p_ + 1] == ':')
+            p_ += 2;
+          else
+            fail(UGPU_UNSUPPORTED, "(? group");
+        }
+        int a = parse_alt();
+        if (p_ >= s_.size() || s_[p_] != ')')
+          fail(UGPU_INVAL, "missing ')'");
+        ++p_;
+        return a;
+      }
+      case '[':
+        ++p_;
+        return t_.cpset(parse_bracket());
+      case '.':
+        ++p_;
+        if (dot_byte)
+        {
+          ByteSet b;
+          b.set();
+          b.reset('\n');
+          return t_.leaf(b);
+        }
+        else
+        {
+          // [^\n\x80-\xbf][\x80-\xbf]*  (convert.cpp:2118-2150)
+          ByteSet lead, cont;
+          for (unsigned x = 0; x < 256; ++x)
+            (x >= 0x80 && x <= 0xBF ? cont : lead).set(x);
+          lead.reset('\n');
+          int l = t_.leaf(lead);
+          return t_.add(CAT, {l, t_.add(STAR, {t_.leaf(cont)})});
+        }
+      case '^':
+      case '$':
+        fail(UGPU_UNSUPPORTED, "anchor");
+      case '*':
+      case '+':
+      case '?':
+      case '{':
+        fail(UGPU_INVAL, "nothing to repeat");
+      case '\\':
+      {
+        ++p_;
+        if (p_ < s_.size() && strchr("bBAzZ<>`'GkKQEpPXRNuUcCl", s_[p_]) != NULL)
+          fail(UGPU_UNSUPPORTED, std::string("escape \\") + s_[p_]);
+        CpSet set;
+        uint32_t cp;
+        if (parse_escape(set, cp, false))
+        {
+          if (icase())
+            add_ascii_case(set);
+          return t_.cpset(set);
+        }
+        return code_point(cp);
+      }
+      default:
+        return code_point(utf8_char());
+    }
+  }
+
+  int code_point(uint32_t cp)
+  {
+    if (icase() && cp >= 0x80)
+      fail(UGPU_UNSUPPORTED, "Unicode case folding");
+    if (cp < 0x80)
+      return literal_byte(static_cast<uint8_t>(cp));
+    return t_.cpset(CpSet{{cp, cp}});
+  }
+};
+
+// ---------------------------------------------------------------- Glushkov + subsets
+
+struct Glushkov
+{
+  const Tree &t;
+  std::vector<int> pos_of;               // node -> position (leaves)
+  std::vector<ByteSet> bytes;            // position -> bytes
+  std::vector<std::vector<int>> follow;  // position -> follow positions
+  std::vector<int> accept;               // position -> accept index (end markers), 0 otherwise
+
+  struct Info
+  {
+    bool nullable;
+    std::vector<int> first, last;
+  };
+
+  explicit Glushkov(const Tree &tree) : t(tree), pos_of(tree.nodes.size(), -1) {}
+
+  static void merge(std::vector<int> &a, const std::vector<int> &b)
+  {
+    std::vector<int> out;
+    std::set_union(a.begin(), a.end(), b.begin(), b.end(), std::back_inserter(out));
+    a.swap(out);
+  }
+
+  void link(const std::vector<int> &from, const std::vector<int> &to)
+  {
+    for (int p : from)
+      merge(follow[p], to);
+  }
+
+  int new_pos(const ByteSet &b, int acc)
+  {
+    bytes.push_back(b);
+    follow.emplace_back();
+    accept.push_back(acc);
+    return static_cast<int>(bytes.size() - 1);
+  }
+
+  Info walk(int n)
+  {
+    const Node &nd = t.nodes[n];
+    Info r;
+    switch (nd.kind)
+    {
+      case LEAF:
+      {
+        int p = new_pos(nd.bytes, 0);
+        return Info{false, {p}, {p}};
+      }
+      case EMPTY:
+        return Info{true, {}, {}};
+      case CAT:
+      {
+        r = walk(nd.kids[0]);
+        for (size_t i = 1; i < nd.kids.size(); ++i)
+        {
+          Info b = walk(nd.kids[i]);
+          link(r.last, b.first);
+          if (r.nullable)
+            merge(r.first, b.first);
+          if (b.nullable)
+            merge(b.last, r.last);
+          r.last.swap(b.last);
+          r.nullable = r.nullable && b.nullable;
+        }
+        return r;
+      }
+      case ALT:
+      {
+        r.nullable = false;
+        for (int k : nd.kids)
+        {
+          Info b = walk(k);
+          r.nullable = r.nullable || b.nullable;
+          merge(r.first, b.first);
+          merge(r.last, b.last);
+        }
+        return r;
+      }
+      case STAR:
+      case PLUS:
+      case OPT:
+      {
+        r = walk(nd.kids[0]);
+        if (nd.kind != OPT)
+          link(r.last, r.first);
+        if (nd.kind != PLUS)
+          r.nullable = true;
+        return r;
+      }
+    }
+    return r;
+  }
+};
+
+struct Dfa
+{
+  std::vector<std::vector<uint32_t>> next;  // state -> 256 targets (0 = dead state)
+  std::vector<uint32_t> acc;                // accept index, 0 = none
+};
+
+Dfa subsets(Glushkov &g, const std::vector<int> &start)
+{
+  Dfa d;
+  std::map<std::vector<int>, uint32_t> id;
+  std::vector<std::vector<int>> sets;
+  auto intern = [&](const std::vector<int> &s) -> uint32_t {
+    auto it = id.find(s);
+    if (it != id.end())
+      return it->second;
+    if (sets.size() >= kMaxStates)
+      fail(UGPU_UNSUPPORTED, "DFA too large");
+    uint32_t k = static_cast<uint32_t>(sets.size());
+    id.emplace(s, k);
+    sets.push_back(s);
+    return k;
+  };
+  intern({});  // state 0: dead
+  intern(start);
+  // byte classes over all positions, to do one union per class
+  std::vector<int> cls(256, 0);
+  {
+    std::map<std::vector<bool>, int> sig;
+    for (int b = 0; b < 256; ++b)
+    {
+      std::vector<bool> v(g.bytes.size());
+      for (size_t p = 0; p < g.bytes.size(); ++p)
+        v[p] = g.bytes[p].test(b);
+      auto it = sig.emplace(v, static_cast<int>(sig.size())).first;
+      cls[b] = it->second;
+    }
+  }
+  int ncls = *std::max_element(cls.begin(), cls.end()) + 1;
+  std::vector<int> rep(ncls, -1);
+  for (int b = 0; b < 256; ++b)
+    if (rep[cls[b]] < 0)
+      rep[cls[b]] = b;
+  for (size_t k = 0; k < sets.size(); ++k)
+  {
+    std::vector<int> cur = sets[k];  // copy: sets grows
+    uint32_t a = 0;
+    for (int p : cur)
+      if (g.accept[p] && (a == 0 || static_cast<uint32_t>(g.accept[p]) < a))
+        a = g.accept[p];
+    d.acc.push_back(a);
+    std::vector<uint32_t> row(256, 0);
+    std::vector<uint32_t> by_cls(ncls, 0);
+    for (int c = 0; c < ncls; ++c)
+    {
+      std::vector<int> nx;
+      for (int p : cur)
+        if (!g.accept[p] && g.bytes[p].test(rep[c]))
+          Glushkov::merge(nx, g.follow[p]);
+      by_cls[c] = nx.empty() ? 0 : intern(nx);
+    }
+    for (int b = 0; b < 256; ++b)
+      row[b] = by_cls[cls[b]];
+    d.next.push_back(row);
+  }
+  return d;
+}
+
+// Moore minimisation; states that cannot reach an accept collapse into the
+// dead state 0.  Returns the minimal DFA with the start state at index 1.
+Dfa minimize(const Dfa &d, uint32_t start)
+{
+  size_t n = d.acc.size();
+  std::vector<uint32_t> part(n);
+  {
+    std::map<uint32_t, uint32_t> m;
+    for (size_t s = 0; s < n; ++s)
+      part[s] = m.emplace(d.acc[s], static_cast<uint32_t>(m.size())).first->second;
+  }
+  size_t nparts = 0;
+  for (;;)
+  {
+    std::map<std::vector<uint32_t>, uint32_t> m;
+    std::vector<uint32_t> np(n);
+    for (size_t s = 0; s < n; ++s)
+    {
+      std::vector<uint32_t> sig;
+      sig.reserve(257);
+      sig.push_back(part[s]);
+      for (int b = 0; b < 256; ++b)
+        sig.push_back(part[d.next[s][b]]);
+      np[s] = m.emplace(sig, static_cast<uint32_t>(m.size())).first->second;
+    }
+    part.swap(np);
+    if (m.size() == nparts)
+      break;
+    nparts = m.size();
+  }
+  // renumber by BFS from the start; the dead state's block becomes 0
+  uint32_t dead = part[0];
+  std::vector<int64_t> newid(nparts, -1);
+  std::vector<uint32_t> rep(nparts);
+  for (size_t s = n; s-- > 0;)
+    rep[part[s]] = static_cast<uint32_t>(s);
+  Dfa out;
+  newid[dead] = 0;
+  out.acc.push_back(0);
+  out.next.push_back(std::vector<uint32_t>(256, 0));
+  std::vector<uint32_t> order{part[start]};
+  if (part[start] != dead)
+    newid[part[start]] = 1;
+  for (size_t i = 0; i < order.size(); ++i)
+  {
+    uint32_t blk = order[i];
+    if (blk == dead)
+      continue;
+    uint32_t s = rep[blk];
+    std::vector<uint32_t> row(256);
+    for (int b = 0; b < 256; ++b)
+    {
+      uint32_t tb = part[d.next[s][b]];
+      if (newid[tb] < 0)
+      {
+        newid[tb] = static_cast<int64_t>(order.size()) + 1;
+        order.push_back(tb);
+      }
+      row[b] = static_cast<uint32_t>(newid[tb]);
+    }
+    out.acc.push_back(d.acc[s]);
+    out.next.push_back(row);
+  }
+  return out;
+}
+
+// Split states by their walk gap (bytes since the walk's last accept, 0 on
+// accepting states and at the start) so that every state has one gap, the
+// property xg_kernel's tables need (tables.cpp, "gap transducer").  Minimising
+// can merge states the reference's construction keeps apart (e.g. UTF-8
+// continuation states reached from the start and after an accept); unfolding
+// restores a layout the gap kernel takes.  Gives up (returns d) when a gap
+// exceeds the kernel's bound or the table would grow past 4x.
+Dfa unfold_gaps(const Dfa &d)
+{
+  const int kMaxGap = 6;
+  size_t n = d.acc.size();
+  if (n < 2)
+    return d;
+  std::map<std::pair<uint32_t, int>, uint32_t> id;
+  std::vector<std::pair<uint32_t, int>> order{{0, -1}, {1, 0}};
+  id[order[0]] = 0;
+  id[order[1]] = 1;
+  Dfa out;
+  for (size_t i = 0; i < order.size(); ++i)
+  {
+    uint32_t s = order[i].first;
+    int g = order[i].second;
+    std::vector<uint32_t> row(256, 0);
+    if (s != 0)
+      for (int b = 0; b < 256; ++b)
+      {
+        uint32_t t = d.next[s][b];
+        if (t == 0)
+          continue;
+        int ng = d.acc[t] ? 0 : g + 1;
+        if (ng > kMaxGap)
+          return d;
+        auto key = std::make_pair(t, ng);
+        auto it = id.find(key);
+        if (it == id.end())
+        {
+          if (order.size() >= 4 * n)
+            return d;
+          it = id.emplace(key, static_cast<uint32_t>(order.size())).first;
+          order.push_back(key);
+        }
+        row[b] = it->second;
+      }
+    out.next.push_back(row);
+    out.acc.push_back(d.acc[s]);
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------- opcode encoding
+
+std::vector<uint32_t> encode(const Dfa &d)
+{
+  // states 1..n-1 are emitted in order; state 1 (start) at word 0
+  size_t n = d.acc.size();
+  if (n < 2)
+  {
+    // no live start: a start state that halts on every byte
+    return std::vector<uint32_t>{0x00FFFFFFu};
+  }
+  struct Run
+  {
+    unsigned lo, hi;
+    uint32_t target;
+  };
+  std::vector<std::vector<Run>> runs(n);
+  for (size_t s = 1; s < n; ++s)
+  {
+    int b = 255;
+    while (b >= 0)
+    {
+      uint32_t t = d.next[s][b];
+      int e = b;
+      while (e > 0 && d.next[s][e - 1] == t)
+        --e;
+      // dead runs become HALT words: every byte of a state block is covered
+      // and its last word has lo == 0, as encode_dfa emits them
+      runs[s].push_back(Run{static_cast<unsigned>(e), static_cast<unsigned>(b), t});
+      b = e - 1;
+    }
+  }
+  for (int pass = 0; pass < 2; ++pass)
+  {
+    bool lng = pass == 1;
+    std::vector<uint32_t> at(n, 0);
+    uint32_t w = 0;
+    for (size_t s = 1; s < n; ++s)
+    {
+      at[s] = w;
+      w += d.acc[s] ? 1 : 0;
+      for (auto &r : runs[s])
+        w += (lng && r.target != 0) ? 2 : 1;
+    }
+    if (!lng && w >= 0xFFFE)
+      continue;
+    if (w > 0xFFFFFF)
+      fail(UGPU_UNSUPPORTED, "opcode table too large");
+    std::vector<uint32_t> out;
+    out.reserve(w);
+    for (size_t s = 1; s < n; ++s)
+    {
+      if (d.acc[s])
+        out.push_back(0xFE000000u | d.acc[s]);
+      for (auto &r : runs[s])
+      {
+        if (r.target == 0)
+          out.push_back(r.lo << 24 | r.hi << 16 | 0xFFFFu);
+        else if (lng)
+        {
+          out.push_back(r.lo << 24 | r.hi << 16 | 0xFFFEu);
+          out.push_back(0xFF000000u | at[r.target]);
+        }
+        else
+          out.push_back(r.lo << 24 | r.hi << 16 | at[r.target]);
+      }
+    }
+    return out;
+  }
+  fail(UGPU_UNSUPPORTED, "opcode table too large");
+}
+
+thread_local std::string g_compile_error;
+
+}  // namespace
+
+extern "C" {
+
+int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, uint32_t *nop)
+{
+  if (!opc || !nop || (!regex && len))
+    return UGPU_INVAL;
+  *opc = NULL;
+  *nop = 0;
+  try
+  {
+    std::string rx(regex ? regex : "", len);
+    Tree tree;
+    Parser parser(rx, flags, tree);
+    std::vector<int> alts = parser.parse_top();
+    Glushkov g(tree);
+    std::vector<int> start;
+    std::vector<std::pair<std::vector<int>, int>> ends;
+    for (size_t k = 0; k < alts.size(); ++k)
+    {
+      Glushkov::Info info = g.walk(alts[k]);
+      int end = g.new_pos(ByteSet(), static_cast<int>(k + 1));
+      g.link(info.last, std::vector<int>{end});
+      Glushkov::merge(start, info.first);
+      if (info.nullable)
+        Glushkov::merge(start, std::vector<int>{end});
+    }
+    Dfa d = subsets(g, start);
+    Dfa m = unfold_gaps(minimize(d, 1));
+    std::vector<uint32_t> words = encode(m);
+    uint32_t *buf = static_cast<uint32_t *>(malloc(words.size() * sizeof(uint32_t)));
+    if (!buf)
+      return UGPU_NOMEM;
+    memcpy(buf, words.data(), words.size() * sizeof(uint32_t));
+    *opc = buf;
+    *nop = static_cast<uint32_t>(words.size());
+    g_compile_error.clear();
+    return UGPU_OK;
+  }
+  catch (const CompileError &e)
+  {
+    g_compile_error = e.msg;
+    return e.code;
+  }
+  catch (const std::bad_alloc &)
+  {
+    g_compile_error = "out of memory";
+    return UGPU_NOMEM;
+  }
+}
+
+void ugpu_opc_free(uint32_t *opc)
+{
+  free(opc);
+}
+
+const char *ugpu_compile_error(void)
+{
+  return g_compile_error.c_str();
+}
+
+}  // extern "C"

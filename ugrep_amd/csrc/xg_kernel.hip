@@ -89,6 +89,13 @@ struct GSum {
   uint32_t cnt = 0, sq = 0, sfl = 0, sl = 0;
 };
 
+__device__ __forceinline__ void gfold(const GSum& a, uint64_t base, uint64_t& cnt, uint64_t& sst, uint64_t& len)
+{
+  cnt += a.cnt;
+  sst += (uint64_t)a.cnt * base + (uint32_t)(a.sq - a.sfl);  // sum of starts r + 1 - L
+  len += a.sl;
+}
+
 // One byte of the main loop.  MASK: events of the lane's head (up to and
 // including its first sync byte) are dropped.  off1 = the byte's offset in its
 // block + 1 (a constant once unrolled): sq gets f (off1) here and f bb per block.
@@ -149,8 +156,12 @@ __device__ __forceinline__ uint32_t gdist(uint64_t lim, uint64_t base)  // lim -
 // byte has been read.  Returns the coverage end (as xi_kernel's xtail).
 template <int FMT>
 __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, uint64_t ts, uint32_t o,
-                                          uint32_t seg, uint32_t& m, uint32_t& acc, GSum& s, uint64_t hi, uint64_t rend, uint32_t at_eof, uint32_t& ovf, bool act)
+                                          uint32_t& m, uint32_t& acc, uint64_t& cnt, uint64_t& sst,
+                                          uint64_t& len, uint64_t hi, uint64_t rend, uint32_t at_eof, uint32_t& ovf,
+                                          bool act)
 {
+  // (sums per 16-byte chunk, folded into 64-bit totals at the chunk's base:
+  // a tail may run far when sync bytes are rare, e.g. \D over text)
   uint64_t xit = ~0ull, last = 0;
   const uint64_t rend16 = (rend + 15) & ~uint64_t(15);
   uint4 vn = gload16(grsrc(g + ts, rend16 > ts ? rend16 - ts : 0), o);
@@ -160,7 +171,7 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
     vn = gload16(grsrc(g + cb, rend16 > cb ? rend16 - cb : 0), o);
     const uint64_t base = ts + o + c;
     const uint32_t dh = gdist(hi, base), dr = gdist(rend, base);
-    const uint32_t r0 = (uint32_t)(o + c - seg);  // lane-relative position of byte 0
+    GSum s;
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
       bool go = act;
@@ -185,7 +196,7 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
           act = false;
         } else {
           s.cnt += f;
-          s.sq += __umul24(f, r0 + k + 1);
+          s.sq += __umul24(f, k + 1);
           s.sfl += __umul24(f, L);
           s.sl += L;
           if (t & 1u) last = base + k + 1;
@@ -198,6 +209,7 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
         m = e;
       }
     }
+    gfold(s, base, cnt, sst, len);
   }
   return xit;
 }
@@ -209,7 +221,8 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
 template <int FMT>
 __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t* g, uint64_t ts, uint32_t seg,
                                                uint32_t slen, uint64_t wlo, uint64_t hi, uint64_t fresh,
-                                               uint64_t rend, uint32_t at_eof, GSum& s, uint64_t& fs, uint32_t& ovf)
+                                               uint64_t rend, uint32_t at_eof, uint64_t& cnt, uint64_t& sst,
+                                               uint64_t& len, uint64_t& fs, uint32_t& ovf)
 {
   bool act = ts + seg + slen > wlo && ts + seg < hi;
   bool synced = false;
@@ -225,6 +238,7 @@ __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t
     const uint32_t dh = gdist(hi, base), dr = gdist(rend, base), dl = gdist(wlo, base);
     const uint32_t df = fresh >= base && fresh - base < 16 ? (uint32_t)(fresh - base) : 0xffffffffu;
     const uint32_t dseg = c >= (uint64_t)slen ? 0u : (uint32_t)(slen - c);
+    GSum s;  // this chunk's sums, relative to base
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
       bool go = act && k >= dl;
@@ -257,7 +271,7 @@ __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t
           act = false;
         } else if (synced) {
           s.cnt += f;
-          s.sq += __umul24(f, (uint32_t)(c + k + 1));
+          s.sq += __umul24(f, k + 1);
           s.sfl += __umul24(f, L);
           s.sl += L;
           if (t & 1u) last = base + k + 1;
@@ -273,6 +287,7 @@ __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t
         m = e;
       }
     }
+    gfold(s, base, cnt, sst, len);
   }
   return xit;
 }
@@ -298,12 +313,6 @@ __device__ __forceinline__ uint64_t gwave_max_set(uint64_t v)
   return m;
 }
 
-__device__ __forceinline__ void gfold(const GSum& a, uint64_t base, uint64_t& cnt, uint64_t& sst, uint64_t& len)
-{
-  cnt += a.cnt;
-  sst += (uint64_t)a.cnt * base + (uint32_t)(a.sq - a.sfl);  // sum of starts r + 1 - L
-  len += a.sl;
-}
 
 // stage the tables of P into LDS (all threads of the block)
 template <int FMT>
@@ -387,7 +396,9 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
     s.sl = s4.sl;
     if (!synced) s = GSum();  // covered by an earlier tail
     acc = (acc >> 2) & 1u;    // the tail keeps the accepted bit in bit 0
-    const uint64_t xit = gtail<FMT>(T, P.g, ts, seg + kGS, seg, m, acc, s, P.hi, P.rend, P.at_eof, ovf, synced);
+    gfold(s, ts + seg, cnt, sst, len);
+    const uint64_t xit =
+        gtail<FMT>(T, P.g, ts, seg + kGS, m, acc, cnt, sst, len, P.hi, P.rend, P.at_eof, ovf, synced);
     const uint64_t f = synced && fs != ~0u ? ts + seg + fs : ~0ull;
     if (entry == ~0ull) {
       const uint64_t mn = gwave_min64(f);
@@ -395,7 +406,6 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
     }
     const uint64_t mx = gwave_max_set(xit);
     if (mx) exit = mx;
-    gfold(s, ts + seg, cnt, sst, len);
   }
   if (entry == ~0ull && !has_edge) entry = exit;
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
@@ -444,12 +454,9 @@ __global__ __launch_bounds__(kGEdgeThreads) void xg_edge_kernel(ScanParams P, GE
     const uint64_t wlo = clampu(tb * kGTile, P.lo, P.hi);
     const uint64_t t = E.tile[k], ts = t * (uint64_t)kGTile;
     const uint64_t fresh = wlo == P.lo && t == tb ? wlo : ~0ull;
-    GSum s;
-    uint64_t fs = ~0ull;
+    uint64_t fs = ~0ull, cnt = 0, sst = 0, len = 0;
     const uint64_t xit =
-        gslow_lane<FMT>(T, P.g, ts, seg, kGEdgeSeg, wlo, P.hi, fresh, P.rend, P.at_eof, s, fs, ovf);
-    uint64_t cnt = 0, sst = 0, len = 0;
-    gfold(s, ts + seg, cnt, sst, len);
+        gslow_lane<FMT>(T, P.g, ts, seg, kGEdgeSeg, wlo, P.hi, fresh, P.rend, P.at_eof, cnt, sst, len, fs, ovf);
     const uint64_t c = wave_sum(cnt), sm = wave_sum(sst), l = wave_sum(len);
     const uint64_t mx = gwave_max_set(xit), mf = gwave_min64(fs);
     if (lane == 0) {

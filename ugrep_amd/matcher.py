@@ -25,6 +25,32 @@ def _as_u32(opc):
     return a, a.ctypes.data_as(_lib.c_u32p)
 
 
+RX_FIXED = 1
+RX_ICASE = 2
+
+
+def compile_regex(regex, fixed=False, icase=False):
+    """Opcode words (numpy u32) for `regex` from the native compiler
+    (ugpu_compile, regex_compile.cpp): ugrep's default ERE in Unicode mode, as
+    Matcher::convert(rx, notnewline|unicode) + Pattern(conv, "r") produce them
+    (src/ugrep.cpp:8574-8578, lib/pattern.cpp:171-3063).  Syntax errors raise
+    UgpuError(UGPU_INVAL) where the reference throws regex_error; constructs the
+    GPU tables do not cover raise Unsupported."""
+    if isinstance(regex, str):
+        regex = regex.encode("utf-8")
+    words = _lib.c_u32p()
+    n = ctypes.c_uint32()
+    flags = (RX_FIXED if fixed else 0) | (RX_ICASE if icase else 0)
+    rc = lib.ugpu_compile(regex, len(regex), flags, ctypes.byref(words), ctypes.byref(n))
+    if rc != _lib.UGPU_OK:
+        msg = lib.ugpu_compile_error().decode(errors="replace")
+        raise (_lib.Unsupported if rc == _lib.UGPU_UNSUPPORTED else _lib.UgpuError)(rc, msg)
+    try:
+        return np.ctypeslib.as_array(words, shape=(n.value,)).copy()
+    finally:
+        lib.ugpu_opc_free(words)
+
+
 def host_tables(opc):
     """Dense tables built on the host (no device needed): dict of numpy arrays."""
     a, p = _as_u32(opc)
@@ -91,6 +117,8 @@ class Pattern:
     """Compiled pattern (opcode words) with its device tables."""
 
     def __init__(self, opc):
+        if isinstance(opc, (str, bytes)):
+            opc = compile_regex(opc)
         self.opc, p = _as_u32(opc)
         h = ctypes.c_void_p()
         check(lib.ugpu_dfa_create(p, len(self.opc), 0, ctypes.byref(h)))
