@@ -377,7 +377,10 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       sync[c] = y;
       if (y && first_sync < 0) first_sync = c;
     }
-    if (ok && order.size() <= 32 && first_sync >= 0) {
+    // sync bytes must be common in text (a space or a newline among them):
+    // with only rare ones (\D: digits) lane tails serialise over long runs,
+    // and dense_kernel's speculative walk is the better choice
+    if (ok && order.size() <= 32 && first_sync >= 0 && (sync[' '] || sync['\n'])) {
       t.immediate = true;
       t.sync_byte = (uint8_t)first_sync;
       t.xid_rows = (uint32_t)order.size() * 8;
@@ -433,7 +436,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       sync[c] = y ? 1 : 0;
       any_sync |= y;
     }
-    if (ok && any_sync) {
+    if (ok && any_sync && (sync[' '] || sync['\n'])) {  // common sync bytes (see above)
       t.gap = true;
       t.xg_sync = sync;
       t.xg.assign((size_t)S * R, 0);

@@ -92,7 +92,8 @@ struct GSum {
 __device__ __forceinline__ void gfold(const GSum& a, uint64_t base, uint64_t& cnt, uint64_t& sst, uint64_t& len)
 {
   cnt += a.cnt;
-  sst += (uint64_t)a.cnt * base + (uint32_t)(a.sq - a.sfl);  // sum of starts r + 1 - L
+  // sum of starts r + 1 - L; signed: in a tail chunk a match may start before the chunk base
+  sst += (uint64_t)a.cnt * base + (uint64_t)(int64_t)(int32_t)(a.sq - a.sfl);
   len += a.sl;
 }
 
