@@ -94,7 +94,13 @@ typedef struct ugpu_result
 /* --- pattern tables (replaces the Pattern -> Matcher table consumer) --- */
 
 /* Build the dense device tables from opcode words and upload them once to the
-   current device.  pattern_flags: reserved (pass 0). */
+   current device.  pattern_flags: 0, or UGPU_PAT_WORD for Matcher option W
+   (ugrep -w: matches bounded by word boundaries, src/ugrep.cpp:8616-8618,
+   lib/matcher.cpp:107, :142, :208, include/reflex/matcher.h:1194-1237); W scans
+   run wfind_kernel on whole buffers (ugpu_find_all, ugpu_scan with the buffer
+   start at dbuf[0]); ugpu_chain_fix and the stream API return UGPU_UNSUPPORTED
+   for W patterns. */
+#define UGPU_PAT_WORD 1u
 int ugpu_dfa_create(const uint32_t *opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa **out);
 int ugpu_dfa_destroy(ugpu_dfa *dfa);
 int ugpu_dfa_info_get(const ugpu_dfa *dfa, ugpu_dfa_info *info);

@@ -125,10 +125,13 @@ struct Tally
   uint64_t count = 0, digest = 0, dcap = 0;
 };
 
+// matcher options (mode suffix "W" = ugrep -w: Matcher option W, src/ugrep.cpp:8616-8618)
+static std::string g_matcher_opt;
+
 static Tally scan(const reflex::Pattern& pat, char *base, size_t n, size_t bias, std::vector<uint64_t> *list)
 {
   Tally t;
-  reflex::Matcher m(pat);
+  reflex::Matcher m(pat, reflex::Input(), g_matcher_opt.empty() ? NULL : g_matcher_opt.c_str());
   m.buffer(base, n + 1);
   while (size_t cap = m.find())
   {
@@ -171,6 +174,11 @@ int main(int argc, char **argv)
     return 0;
   }
   std::string cmd = argv[1], mode = argv[2], rx = argv[3];
+  if (mode.size() > 1 && mode[mode.size() - 1] == 'W')
+  {
+    g_matcher_opt = "W";
+    mode.erase(mode.size() - 1);
+  }
   std::string conv = build_regex(mode, rx);
   reflex::Pattern pat(conv, "r");
   if (cmd == "dump")

@@ -239,6 +239,155 @@ uint64_t orc_find(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t sta
   return cnt;
 }
 
+/* ---- option W (ugrep -w, src/ugrep.cpp:8616-8618) ----
+ * Matcher::match with opt_.W (lib/matcher.cpp:76, :107, :142, :208, :664): a
+ * walk starts at p only if at_wb() holds there, and a TAKE counts only if
+ * at_we() holds at the match end (include/reflex/matcher.h:1194-1237, WITH_SPAN
+ * forms); otherwise the search moves to p+1 as for no match.  iswword is the
+ * Unicode 15.1 Word table (matcher.h:457-1192), the same ranges as \w: the
+ * data file is shared with the product's compiler (it is pinned to the
+ * reference by tools/gen_unicode_ranges.py, and this restatement by the W
+ * goldens of tests/test_oracle.py).  Bytes at and past n read as 0 (the
+ * reference buffer's NUL terminator). */
+#include "../ugrep_amd/csrc/unicode_ranges.inc"
+
+static int orc_iswword(uint32_t c)
+{
+  int lo = 0, hi = (int)(sizeof(k_word_ranges) / sizeof(k_word_ranges[0])) - 1;
+  while (lo <= hi)
+  {
+    int mid = (lo + hi) / 2;
+    if (c < k_word_ranges[mid][0])
+      hi = mid - 1;
+    else if (c > k_word_ranges[mid][1])
+      lo = mid + 1;
+    else
+      return 1;
+  }
+  return 0;
+}
+
+static inline uint32_t orc_rd(const uint8_t *buf, uint64_t n, uint64_t k) { return k < n ? buf[k] : 0; }
+
+/* reflex::utf8(const char*) (include/reflex/utf8.h:138-215), restricted form */
+static uint32_t orc_utf8(const uint8_t *buf, uint64_t n, uint64_t k)
+{
+  uint32_t c = orc_rd(buf, n, k), c1, c2, c3;
+  if (c < 0x80)
+    return c;
+  c1 = orc_rd(buf, n, k + 1);
+  if (c < 0xC0 || (c == 0xC0 && c1 != 0x80) || c == 0xC1 || (c1 & 0xC0) != 0x80)
+    return 0xFFFD;
+  c1 &= 0x3F;
+  if (c < 0xE0)
+    return ((c & 0x1F) << 6) | c1;
+  c2 = orc_rd(buf, n, k + 2);
+  if ((c == 0xE0 && c1 < 0x20) || (c2 & 0xC0) != 0x80)
+    return 0xFFFD;
+  c2 &= 0x3F;
+  if (c < 0xF0)
+    return ((c & 0x0F) << 12) | (c1 << 6) | c2;
+  c3 = orc_rd(buf, n, k + 3);
+  if ((c == 0xF0 && c1 < 0x10) || (c == 0xF4 && c1 >= 0x10) || c >= 0xF5 || (c3 & 0xC0) != 0x80)
+    return 0xFFFD;
+  return ((c & 0x07) << 18) | (c1 << 12) | (c2 << 6) | (c3 & 0x3F);
+}
+
+static int orc_isalnum(uint32_t c) { return (c >= '0' && c <= '9') || ((c | 0x20) >= 'a' && (c | 0x20) <= 'z'); }
+
+/* at_wb() before position p (matcher.h:1194-1216) */
+static int orc_at_wb(const uint8_t *buf, uint64_t n, uint64_t p)
+{
+  uint32_t c;
+  if (p == 0)
+    return 1; /* BOB */
+  c = buf[p - 1];
+  if (c == '\n')
+    return 1;
+  if (c == '_')
+    return 0;
+  if ((c & 0xC0) == 0x80)
+  {
+    uint64_t k = p - 1;
+    if (k > 0 && (buf[--k] & 0xC0) == 0x80)
+      if (k > 0 && (buf[--k] & 0xC0) == 0x80)
+        if (k > 0)
+          --k;
+    return !orc_iswword(orc_utf8(buf, n, k));
+  }
+  return !orc_isalnum(c);
+}
+
+/* at_we() at match end q (matcher.h:1217-1237); q == n is EOF */
+static int orc_at_we(const uint8_t *buf, uint64_t n, uint64_t q)
+{
+  uint32_t c;
+  if (q >= n)
+    return 1;
+  c = buf[q];
+  if (c == '_')
+    return 0;
+  if ((c & 0xC0) == 0xC0)
+    return !orc_iswword(orc_utf8(buf, n, q));
+  return !orc_isalnum(c);
+}
+
+static inline uint64_t orc_step_w(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t p, uint32_t *acc)
+{
+  uint32_t s = d->start, a = 0;
+  uint64_t q = p, last = p;
+  *acc = 0;
+  if (!orc_at_wb(buf, n, p))
+    return 0;
+  while (q < n)
+  {
+    uint32_t t = d->next[(size_t)s * 256 + buf[q]];
+    if (t == 0)
+      break;
+    s = t;
+    ++q;
+    if (d->accept[s] && orc_at_we(buf, n, q))
+    {
+      last = q;
+      a = d->accept[s];
+    }
+  }
+  *acc = a;
+  return last - p;
+}
+
+/* orc_find with option W (whole buffer buf[0..n), search from start) */
+uint64_t orc_find_w(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t start, uint64_t *digest,
+                    uint64_t *dcap, uint64_t *list, uint64_t list_cap)
+{
+  uint64_t p = start, cnt = 0, dg = 0, dc = 0;
+  while (p < n)
+  {
+    uint32_t a;
+    uint64_t len = orc_step_w(d, buf, n, p, &a);
+    if (len > 0)
+    {
+      if (list && cnt < list_cap)
+      {
+        list[3 * cnt] = p;
+        list[3 * cnt + 1] = len;
+        list[3 * cnt + 2] = a;
+      }
+      ++cnt;
+      dg += p * 31 + len;
+      dc += (p + 1) * a;
+      p += len;
+    }
+    else
+      ++p;
+  }
+  if (digest)
+    *digest = dg;
+  if (dcap)
+    *dcap = dc;
+  return cnt;
+}
+
 /* Chain exit of a segment: the first chain position >= e starting from entry x. */
 uint64_t orc_chain_exit(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t x, uint64_t e)
 {

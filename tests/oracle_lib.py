@@ -30,6 +30,8 @@ def _load():
     L.orc_find.restype = U64
     L.orc_find_mt.argtypes = [V, V, U64, ctypes.c_int, P64, P64]
     L.orc_find_mt.restype = U64
+    L.orc_find_w.argtypes = [V, V, U64, U64, P64, P64, V, U64]
+    L.orc_find_w.restype = U64
     L.orc_chain_exit.argtypes = [V, V, U64, U64, U64]
     L.orc_chain_exit.restype = U64
     L.orc_gen.argtypes = [ctypes.c_int, U64, U64, V, U64]
@@ -67,6 +69,18 @@ class OracleDfa:
         if want_list:
             arr = np.zeros(3 * max(cnt, 1), np.uint64)
             L.orc_find(self.h, buf.ctypes.data, buf.size, start, bias, None, None, arr.ctypes.data, cnt)
+            lst = arr[:3 * cnt].reshape(-1, 3).tolist()
+        return cnt, dg.value, dc.value, lst
+
+    def find_w(self, data, start=0, want_list=False):
+        """FIND with option W (ugrep -w, orc_find_w): (count, digest, dcap, list|None)."""
+        buf = _u8(data)
+        dg, dc = ctypes.c_uint64(), ctypes.c_uint64()
+        cnt = L.orc_find_w(self.h, buf.ctypes.data, buf.size, start, ctypes.byref(dg), ctypes.byref(dc), None, 0)
+        lst = None
+        if want_list:
+            arr = np.zeros(3 * max(cnt, 1), np.uint64)
+            L.orc_find_w(self.h, buf.ctypes.data, buf.size, start, None, None, arr.ctypes.data, cnt)
             lst = arr[:3 * cnt].reshape(-1, 3).tolist()
         return cnt, dg.value, dc.value, lst
 

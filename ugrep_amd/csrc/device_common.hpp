@@ -28,18 +28,111 @@ struct Win {
   const uint8_t* g;
   uint64_t rend;
   uint32_t eof;
+  // option W only (walk<FMT, true>): Word ranges and the buffer's first byte
+  const uint32_t* wtab = nullptr;
+  uint32_t nwtab = 0;
+  uint64_t bob = 0;
 };
+
+// ---------------------------------------------------------------- option W
+// Matcher option W (ugrep -w): a walk starts only where at_wb() holds and a
+// TAKE counts only where at_we() holds (lib/matcher.cpp:107, :142, :208;
+// include/reflex/matcher.h:1194-1237, WITH_SPAN forms).  Bytes are read from
+// global memory; at and past the readable end they read as 0 (the reference
+// buffer's NUL terminator).  iswword = binary search over the Unicode 15.1
+// Word ranges (matcher.h:457-1192).
+__device__ __forceinline__ uint32_t wrd(const Win& w, uint64_t k) { return k < w.rend ? w.g[k] : 0u; }
+
+__device__ __forceinline__ bool wisword(const Win& w, uint32_t c)
+{
+  int lo = 0, hi = (int)w.nwtab - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    if (c < w.wtab[2 * mid])
+      hi = mid - 1;
+    else if (c > w.wtab[2 * mid + 1])
+      lo = mid + 1;
+    else
+      return true;
+  }
+  return false;
+}
+
+// reflex::utf8(const char*) (include/reflex/utf8.h:138-215, restricted form)
+__device__ __forceinline__ uint32_t wutf8(const Win& w, uint64_t k)
+{
+  const uint32_t c = wrd(w, k);
+  if (c < 0x80) return c;
+  uint32_t c1 = wrd(w, k + 1);
+  if (c < 0xC0 || (c == 0xC0 && c1 != 0x80) || c == 0xC1 || (c1 & 0xC0) != 0x80) return 0xFFFD;
+  c1 &= 0x3F;
+  if (c < 0xE0) return ((c & 0x1F) << 6) | c1;
+  uint32_t c2 = wrd(w, k + 2);
+  if ((c == 0xE0 && c1 < 0x20) || (c2 & 0xC0) != 0x80) return 0xFFFD;
+  c2 &= 0x3F;
+  if (c < 0xF0) return ((c & 0x0F) << 12) | (c1 << 6) | c2;
+  const uint32_t c3 = wrd(w, k + 3);
+  if ((c == 0xF0 && c1 < 0x10) || (c == 0xF4 && c1 >= 0x10) || c >= 0xF5 || (c3 & 0xC0) != 0x80) return 0xFFFD;
+  return ((c & 0x07) << 18) | (c1 << 12) | (c2 << 6) | (c3 & 0x3F);
+}
+
+__device__ __forceinline__ bool walnum(uint32_t c) { return (c - '0' < 10u) || ((c | 0x20u) - 'a' < 26u); }
+
+// at_wb() for a walk starting at p
+__device__ __forceinline__ bool at_wb(const Win& w, uint64_t p)
+{
+  if (p <= w.bob) return true;  // BOB
+  const uint32_t c = w.g[p - 1];
+  if (c == '\n') return true;
+  if (c == '_') return false;
+  if ((c & 0xC0) == 0x80) {
+    uint64_t k = p - 1;
+    if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
+      if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
+        if (k > w.bob) --k;
+    return !wisword(w, wutf8(w, k));
+  }
+  return !walnum(c);
+}
+
+// at_we() for a match ending at q (q at the end of the stream: EOF)
+__device__ __forceinline__ bool at_we(const Win& w, uint64_t q, uint32_t& ovf)
+{
+  if (q >= w.rend) {
+    if (!w.eof) ovf = 1;
+    return true;
+  }
+  const uint32_t c = w.g[q];
+  if (c == '_') return false;
+  if ((c & 0xC0) == 0xC0) return !wisword(w, wutf8(w, q));
+  return !walnum(c);
+}
 
 // Longest match starting at p (0 = none).  `le` = entry of the last accepting
 // state (its row identifies the accept index).  Mirrors the reference walk:
 // TAKE on entering an accepting state (lib/matcher.cpp:207-217), stop on HALT
 // (:528-541) or EOF (:460-465).
-template <int FMT>
+template <int FMT, bool W = false>
 __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64_t p, uint32_t& le, uint32_t& ovf)
 {
   uint32_t s = T.start;
   uint64_t q = p, last = p;
   le = 0;
+  if constexpr (W) {
+    if (!at_wb(w, p)) return 0;
+    while (q < w.rend) {
+      const uint32_t e = T.step(s, w.g[q]);
+      if (e == 0) return last - p;
+      s = e;
+      ++q;
+      if (e >= T.accb && at_we(w, q, ovf)) {
+        last = q;
+        le = e;
+      }
+    }
+    if (!w.eof) ovf = 1;
+    return last - p;
+  }
   const uint64_t l1 = w.lend < w.rend ? w.lend : w.rend;
   while (q < l1) {
     uint32_t e = T.step(s, w.lds[q - w.base]);
@@ -112,12 +205,12 @@ struct WriteEm {
 
 // One step of the FIND chain from p: the longest match at p (emitted with
 // `sign`, then the chain continues at its end) or p+1.
-template <int FMT, class Em>
+template <int FMT, class Em, bool W = false>
 __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t p, Em& em,
                                                int sign, uint32_t& ovf)
 {
   uint32_t le;
-  const uint64_t len = walk<FMT>(T, w, p, le, ovf);
+  const uint64_t len = walk<FMT, W>(T, w, p, le, ovf);
   if (len) {
     em.put(c, p, len, le, sign);
     return p + len;
@@ -127,7 +220,7 @@ __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, 
 
 // Re-enter [.., e) at xn instead of xo.  Adds (true - speculative) matches to em.
 // Returns true if the chains met (exit unchanged), else sets nexit.
-template <int FMT>
+template <int FMT, bool W = false>
 __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t xo, uint64_t xn,
                                       uint64_t e, CountEm& em, uint64_t& nexit, uint32_t& ovf)
 {
@@ -139,9 +232,9 @@ __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx
       return false;
     }
     if (po < pn)
-      po = chain_step<FMT>(T, w, c, po, em, -1, ovf);
+      po = chain_step<FMT, CountEm, W>(T, w, c, po, em, -1, ovf);
     else
-      pn = chain_step<FMT>(T, w, c, pn, em, +1, ovf);
+      pn = chain_step<FMT, CountEm, W>(T, w, c, pn, em, +1, ovf);
   }
 }
 

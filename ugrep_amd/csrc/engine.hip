@@ -26,6 +26,9 @@
 #include "scan_kernels.hpp"
 #include "tables.hpp"
 
+// Unicode Word ranges as flat [lo, hi] pairs (regex_compile.cpp, the table of \w)
+void ugpu_word_ranges(std::vector<uint32_t>& out);
+
 using namespace ugpu;
 
 struct ugpu_dfa {
@@ -39,6 +42,8 @@ struct ugpu_dfa {
   uint8_t* d_xg_sync = nullptr;
   uint8_t* d_cls = nullptr;
   uint32_t* d_caps = nullptr;
+  uint32_t* d_wtab = nullptr;  // option W: Unicode Word ranges (UGPU_PAT_WORD)
+  uint32_t nwtab = 0;
 };
 
 struct ugpu_scanner {
@@ -48,6 +53,7 @@ struct ugpu_scanner {
   bool sparse = false;   // prefiltered wave-persistent kernel (sparse_kernel.hip)
   bool xi = false;       // COUNT scans run xi_kernel (immediate tables); OFFSETS use the dense kernel
   bool xg = false;       // COUNT scans run xg_kernel (gap tables); OFFSETS use the dense kernel
+  bool word = false;     // option W: every pass runs wfind_kernel (wfind.hip)
   size_t smem = 0;       // sparse / dense kernel
   size_t xi_smem = 0;
   int xi_rec = 0;        // chain records of an xi scan
@@ -106,6 +112,8 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.log_row = d->t.log_row;
   P.nstates = d->t.states;
   P.cap1 = d->t.cap1;
+  P.wtab = d->d_wtab;
+  P.nwtab = d->nwtab;
   for (int i = 0; i < 5; ++i)
     P.ft[i] = (uint32_t)d->t.ft[4 * i] | ((uint32_t)d->t.ft[4 * i + 1] << 8) | ((uint32_t)d->t.ft[4 * i + 2] << 16) |
               ((uint32_t)d->t.ft[4 * i + 3] << 24);
@@ -134,6 +142,7 @@ void geometry(ScanParams& P, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint
   const uint64_t tpr = (nt + nrec - 1) / nrec;
   nrec = (nt + tpr - 1) / tpr;
   const uint64_t grid = (nrec + per - 1) / per;
+  P.bob = off;  // dbuf[0]: the buffer's first byte (option W: at_wb there)
   P.t0 = t0;
   P.t1 = t1;
   P.tpb = tpr;
@@ -145,7 +154,9 @@ void geometry(ScanParams& P, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint
 void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi,
                   uint64_t read_end, uint64_t& off, bool xi = false)
 {
-  if (xi && s->xg)
+  if (s->word)
+    geometry(P, dbuf, lo, hi, read_end, s->max_rec, wfind_unit(), kWfindLanes, off);
+  else if (xi && s->xg)
     geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xg_unit(), xg_waves(), off);
   else if (xi)
     geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xi_unit(), xi_waves(), off);
@@ -157,6 +168,7 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
 
 hipError_t launch_main(const ugpu_scanner* s, const ScanParams& P, bool write, hipStream_t st, bool xi = false)
 {
+  if (s->word) return launch_wfind(P, s->dfa->t.format, write, st);
   if (xi && s->xg) return launch_xg(P, st);
   if (xi) return launch_xi(P, s->xi_smem, st);
   if (s->sparse) return launch_sparse(P, write, s->smem, st);
@@ -183,8 +195,8 @@ const char* ugpu_version(void) { return "ugrep_amd 0.1 (gfx950)"; }
 
 int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa** out)
 {
-  (void)pattern_flags;
   if (!out) return fail(UGPU_INVAL, "out is NULL");
+  if (pattern_flags & ~UGPU_PAT_WORD) return fail(UGPU_INVAL, "unknown pattern flags");
   *out = nullptr;
   ugpu_dfa* d = new (std::nothrow) ugpu_dfa();
   if (!d) return fail(UGPU_NOMEM, "host allocation");
@@ -211,6 +223,18 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       (e = hipMemcpy(d->d_caps, d->t.caps.data(), d->t.caps.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
     ugpu_dfa_destroy(d);
     return hip_fail(e, "table upload");
+  }
+  if (pattern_flags & UGPU_PAT_WORD) {
+    std::vector<uint32_t> wt;
+    ugpu_word_ranges(wt);
+    d->nwtab = (uint32_t)(wt.size() / 2);
+    if ((e = hipMalloc(&d->d_wtab, wt.size() * 4)) != hipSuccess ||
+        (e = hipMemcpy(d->d_wtab, wt.data(), wt.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+      ugpu_dfa_destroy(d);
+      return hip_fail(e, "word table upload");
+    }
+    *out = d;  // option W runs wfind_kernel only: no transducer tables
+    return UGPU_OK;
   }
   if (d->t.restart_local && !d->t.filter && d->t.cap1 != 0) {
     std::vector<uint16_t> xt(d->ntrans_pad, 0);
@@ -248,6 +272,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   if (!d) return UGPU_OK;
   if (d->d_trans) (void)hipFree(d->d_trans);
   if (d->d_xtrans) (void)hipFree(d->d_xtrans);
+  if (d->d_wtab) (void)hipFree(d->d_wtab);
   if (d->d_xid) (void)hipFree(d->d_xid);
   if (d->d_xg) (void)hipFree(d->d_xg);
   if (d->d_xg_sync) (void)hipFree(d->d_xg_sync);
@@ -378,6 +403,25 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   if (!s) return fail(UGPU_NOMEM, "host allocation");
   s->dfa = dfa;
   HIP_TRY(hipGetDevice(&s->device));
+  if (dfa->d_wtab) {  // option W: wfind_kernel (tables read through the caches, no LDS)
+    s->word = true;
+    s->max_rec = kMaxRec;
+    if (const char* env = std::getenv("UGPU_MAX_GRID")) {
+      int v = std::atoi(env);
+      if (v >= 1 && v <= kMaxRec) s->max_rec = v;
+    }
+    HIP_TRY(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
+    HIP_TRY(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
+    HIP_TRY(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
+    HIP_TRY(hipMalloc(&s->d_tot, sizeof(DevTotals)));
+    HIP_TRY(hipMalloc(&s->d_flags, sizeof(uint32_t)));
+    HIP_TRY(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
+    HIP_TRY(hipHostMalloc(&s->h_flags, sizeof(uint32_t)));
+    HIP_TRY(hipEventCreate(&s->ev0));
+    HIP_TRY(hipEventCreate(&s->ev1));
+    *out = s;
+    return UGPU_OK;
+  }
   s->sparse = dfa->t.filter && dfa->t.format == FMT_BYTE;
   s->smem = s->sparse ? sparse_smem_bytes(dfa->ntrans_pad, dfa->t.states)
                       : dense_smem_bytes(dfa->t.format, dfa->ntrans_pad, dfa->t.states);
@@ -566,6 +610,7 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
                    uint64_t bias, uint64_t old_entry, uint64_t new_entry, ugpu_totals* delta, void* stream)
 {
   if (!s || !dbuf || !delta) return fail(UGPU_INVAL, "NULL argument");
+  if (s->word) return fail(UGPU_UNSUPPORTED, "option W across shards (at_wb needs the previous shard's bytes)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P{};
   fill_tables(P, s->dfa);
@@ -1015,6 +1060,10 @@ int ugpu_stream_create(const ugpu_dfa* dfa, uint64_t keep, ugpu_stream** out)
   *out = nullptr;
   ugpu_stream* st = new (std::nothrow) ugpu_stream();
   if (!st) return fail(UGPU_NOMEM, "host allocation");
+  if (dfa->d_wtab) {
+    delete st;
+    return fail(UGPU_UNSUPPORTED, "option W on streamed input");
+  }
   st->dfa = dfa;
   st->keep = keep ? keep : (64ull << 10);
   int rc = ugpu_scanner_create(dfa, &st->sc);

@@ -1127,6 +1127,18 @@ thread_local std::string g_compile_error;
 
 }  // namespace
 
+// Word ranges for option W (engine.hip: at_wb/at_we's iswword table,
+// include/reflex/matcher.h:457-1192, the same Unicode 15.1 ranges as \w)
+void ugpu_word_ranges(std::vector<uint32_t> &out)
+{
+  out.clear();
+  for (auto &r : k_word_ranges)
+  {
+    out.push_back(r[0]);
+    out.push_back(r[1]);
+  }
+}
+
 extern "C" {
 
 int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, uint32_t *nop)

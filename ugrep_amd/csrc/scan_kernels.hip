@@ -29,6 +29,9 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
   w.g = P.g;
   w.rend = P.rend;
   w.eof = P.at_eof;
+  w.wtab = P.wtab;
+  w.nwtab = P.nwtab;
+  w.bob = P.bob;
   uint32_t ovf = 0;
 
   uint64_t cnt[PER], dg[PER], dc[PER];
@@ -72,7 +75,9 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
       const uint64_t bhi = clampu(te * P.unit, P.lo, P.hi);
       CountEm d;
       uint64_t ne;
-      if (!merge<FMT>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf)) exi[b] = ne;
+      const bool met = P.wtab ? merge<FMT, true>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf)
+                              : merge<FMT>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf);
+      if (!met) exi[b] = ne;
       ent[b] = nx[j];
       cnt[j] += d.cnt;
       dg[j] += d.dg;

@@ -103,6 +103,11 @@ struct ScanParams {
   DevTotals* totals;
   uint64_t* entries_out;     // fix_kernel: exact block entries
   uint64_t* out_base_out;    // fix_kernel: exclusive scan of block counts
+  // option W (ugrep -w): Unicode Word ranges ([lo, hi] pairs) or NULL, and the
+  // base coordinate of the buffer's first byte (at_wb is true there: BOB)
+  const uint32_t* wtab;
+  uint32_t nwtab;
+  uint64_t bob;
 };
 
 // launchers (scan_kernels.hip, gen.hip)
@@ -153,6 +158,11 @@ struct Utf8Params {
 };
 hipError_t launch_utf8(const Utf8Params& U, bool nul, hipStream_t stream);
 uint32_t utf8_tile();
+// option W (-w) FIND, wfind.hip: one chain record per lane, exact W walks
+// (device_common.hpp), stitched by fix_kernel; COUNT and OFFSETS passes
+constexpr uint32_t kWfindLanes = 64;  // records (lanes) per workgroup
+hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream);
+uint32_t wfind_unit();
 // immediate-transducer kernel, xi_kernel.hip (COUNT mode only)
 hipError_t launch_xi(const ScanParams& P, size_t smem, hipStream_t stream);
 hipError_t xi_occupancy(size_t smem, int* blocks_per_cu);

@@ -27,6 +27,7 @@ def _as_u32(opc):
 
 RX_FIXED = 1
 RX_ICASE = 2
+PAT_WORD = 1  # ugpu_dfa_create pattern_flags: option W
 
 
 def compile_regex(regex, fixed=False, icase=False):
@@ -116,12 +117,16 @@ def host_gap(opc):
 class Pattern:
     """Compiled pattern (opcode words) with its device tables."""
 
-    def __init__(self, opc):
+    def __init__(self, opc, word=False):
+        """opc: opcode words (or a regex for compile_regex).  word=True is
+        Matcher option W (ugrep -w, reflex::Matcher(pat, input, "W"),
+        src/ugrep.cpp:8616-8618): whole-buffer scans on wfind_kernel."""
         if isinstance(opc, (str, bytes)):
             opc = compile_regex(opc)
         self.opc, p = _as_u32(opc)
+        self.word = bool(word)
         h = ctypes.c_void_p()
-        check(lib.ugpu_dfa_create(p, len(self.opc), 0, ctypes.byref(h)))
+        check(lib.ugpu_dfa_create(p, len(self.opc), PAT_WORD if word else 0, ctypes.byref(h)))
         self._h = h
 
     @property
