@@ -87,7 +87,7 @@ def cpu_baseline(cfg, sample, threads):
                 sample="%d MiB, oracle restatement (dense-table walker), %d threads" % (sample >> 20, threads))
 
 
-KERNELS = {0: "sparse_kernel", 1: "dense_kernel", 2: "xi_kernel", 3: "xg_kernel"}
+KERNELS = {0: "sparse_kernel", 1: "dense_kernel", 2: "xi_kernel", 3: "xg_kernel", 4: "wfind_kernel"}
 
 
 def measured_traffic(cfg, nbytes, kernel):
@@ -143,6 +143,8 @@ def main():
     ap.add_argument("--compile", action="store_true",
                     help="tables from the native regex compiler (ugpu_compile) instead of the reference's "
                          "dumped opcode words")
+    ap.add_argument("--word", action="store_true",
+                    help="Matcher option W (ugrep -w) on the same pattern: wfind_kernel (not a BASELINE config)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,7 +175,7 @@ def main():
         opc = json.load(f)[pkey]["opc"]
     if args.compile:
         opc = ugrep_amd.compile_regex(rx, fixed=(mode == "F"))
-    pat = ugrep_amd.Pattern(opc)
+    pat = ugrep_amd.Pattern(opc, word=args.word)
     info = pat.info()
 
     stream = torch.cuda.current_stream(dev)
@@ -275,7 +277,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc, "config": args.config, "pattern": rx, "bytes_per_gpu": per_gpu,
                    "total_bytes": total, "corpus_kind": kind, "parallelism": "shard%d" % world,
-                   "tables": "compiled" if args.compile else "reference", "dfa_states": info["states"], "dfa_row": info["row"], "prefilter_ppm": info["prefilter_ppm"]},
+                   "tables": "compiled" if args.compile else "reference", "word": args.word, "dfa_states": info["states"], "dfa_row": info["row"], "prefilter_ppm": info["prefilter_ppm"]},
         "matches": res["count"],
         "matches_per_s": round(matches_per_s, 1),
         "digest": res["digest"],

@@ -64,7 +64,8 @@ typedef struct ugpu_dfa_info
   uint32_t first_bytes; /* number of bytes that can start a match (|fst_|) */
   uint32_t accepting;   /* accepting states */
   uint32_t kernel;      /* kernel of a COUNT scan: 0 sparse (prefiltered), 1 dense, 2 xi (immediate
-                           transducer; UGPU_XI=0 selects dense), 3 xg (gap transducer; UGPU_XG=0) */
+                           transducer; UGPU_XI=0 selects dense), 3 xg (gap transducer; UGPU_XG=0),
+                           4 wfind (option W, UGPU_PAT_WORD) */
 } ugpu_dfa_info;
 
 /* Totals of one scan.  digest = sum(start*31 + len), dcap = sum((start+1)*cap),

@@ -155,7 +155,7 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
                   uint64_t read_end, uint64_t& off, bool xi = false)
 {
   if (s->word)
-    geometry(P, dbuf, lo, hi, read_end, s->max_rec, wfind_unit(), kWfindLanes, off);
+    geometry(P, dbuf, lo, hi, read_end, s->max_rec, wfind_unit(), wfind_waves(), off);
   else if (xi && s->xg)
     geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xg_unit(), xg_waves(), off);
   else if (xi)
@@ -295,7 +295,8 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->accepting = d->t.accepting;
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
-  info->kernel = (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
+  info->kernel = d->d_wtab                                    ? 4u
+                 : (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
                  : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u
                  : (d->d_xg && !(genv && genv[0] == '0'))  ? 3u
                                                            : 1u;

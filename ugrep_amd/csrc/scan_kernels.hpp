@@ -158,11 +158,12 @@ struct Utf8Params {
 };
 hipError_t launch_utf8(const Utf8Params& U, bool nul, hipStream_t stream);
 uint32_t utf8_tile();
-// option W (-w) FIND, wfind.hip: one chain record per lane, exact W walks
-// (device_common.hpp), stitched by fix_kernel; COUNT and OFFSETS passes
-constexpr uint32_t kWfindLanes = 64;  // records (lanes) per workgroup
+// option W (-w) FIND, wfind.hip: one chain record per wave (64 lane segments
+// stitched in the wave), exact W walks (device_common.hpp), records stitched
+// by fix_kernel; COUNT and OFFSETS passes
 hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream);
 uint32_t wfind_unit();
+uint32_t wfind_waves();
 // immediate-transducer kernel, xi_kernel.hip (COUNT mode only)
 hipError_t launch_xi(const ScanParams& P, size_t smem, hipStream_t stream);
 hipError_t xi_occupancy(size_t smem, int* blocks_per_cu);

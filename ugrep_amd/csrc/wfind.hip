@@ -6,33 +6,42 @@
 // (include/reflex/matcher.h:1194-1237).  Both predicates look at up to four
 // bytes around a position and at the Unicode Word table, so they do not fit the
 // transducer kernels' one-lookup-per-byte steps.  This kernel runs the exact W
-// chain (walk<FMT, true>, device_common.hpp) with one chain record per lane:
-// lane r walks the chain of its byte range from the range start
-// (speculatively), and fix_kernel stitches the records exactly as for the
-// dense kernel's wave records.  The OFFSETS pass re-walks each range from its
-// exact entry and writes the records at the range's output base.
+// chain (walk<FMT, true>, device_common.hpp):
 //
-// Bound: dependent global byte reads along one chain per lane (latency, not
-// HBM bandwidth); word text resyncs the chains within a word, so fix_kernel
-// needs one round.
+//   * one chain record per wave; its range is cut into 64 lane segments;
+//   * every lane walks its segment's chain speculatively from the segment
+//     start, then the lanes are stitched in rounds: a lane whose entry differs
+//     from its predecessor's exit re-walks with merge() (two chains in lock
+//     step until they meet) -- word text resyncs within a word, so one round;
+//   * fix_kernel stitches the wave records the same way;
+//   * the OFFSETS pass repeats the lane stitch from the record's exact entry,
+//     scans the lane counts into output bases and re-walks, writing records.
+//
+// Bound: one dependent byte read per step along one chain per lane (global
+// memory through the caches), plus the table lookup; see DESIGN.md §3.8.
 #include "device_common.hpp"
 
 namespace ugpu {
 
 namespace {
 
-constexpr uint32_t kWUnit = 4096;  // bytes per tile (records hold whole tiles)
+constexpr uint32_t kWUnit = 4096;   // bytes per tile (records hold whole tiles)
+constexpr int kWWaves = 4;          // waves (records) per workgroup
 
 template <int FMT, bool WRITE>
-__global__ __launch_bounds__(kWfindLanes) void wfind_kernel(ScanParams P)
+__global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
 {
-  const uint64_t r = (uint64_t)blockIdx.x * kWfindLanes + threadIdx.x;
-  if (r >= P.nrec) return;
+  const int lane = threadIdx.x & 63;
+  const uint64_t r = (uint64_t)blockIdx.x * kWWaves + (threadIdx.x >> 6);
+  if (r >= P.nrec) return;  // wave-uniform
   uint64_t tb = P.t0 + r * P.tpb;
   uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
   if (tb > te) tb = te;
-  const uint64_t blo = clampu(tb * P.unit, P.lo, P.hi);
-  const uint64_t bhi = clampu(te * P.unit, P.lo, P.hi);
+  const uint64_t wlo = clampu(tb * P.unit, P.lo, P.hi);
+  const uint64_t whi = clampu(te * P.unit, P.lo, P.hi);
+  const uint64_t seg = (whi - wlo + 63) / 64;
+  const uint64_t slo = wlo + seg * lane < whi ? wlo + seg * lane : whi;
+  const uint64_t shi = slo + seg < whi ? slo + seg : whi;
   const Tab<FMT> T{P.trans, P.cls, P.start, P.accb};
   const Ctx C{P.caps, P.log_row, P.delta};
   Win w;
@@ -46,22 +55,49 @@ __global__ __launch_bounds__(kWfindLanes) void wfind_kernel(ScanParams P)
   w.nwtab = P.nwtab;
   w.bob = P.bob;
   uint32_t ovf = 0;
-  uint64_t p = WRITE ? P.entries[r] : blo;
+
+  // speculative lane chains (lane 0 enters at the record's entry)
+  uint64_t ent = (WRITE && lane == 0) ? P.entries[r] : slo;
+  CountEm acc;
+  uint64_t p = ent;
+  while (p < shi) p = chain_step<FMT, CountEm, true>(T, w, C, p, acc, +1, ovf);
+  uint64_t exi = p;  // first chain position >= shi (the entry itself when it lies beyond)
+  // lane stitch rounds
+  for (int round = 0; round < 64; ++round) {
+    uint64_t nx = __shfl_up(exi, 1, 64);
+    const bool ch = lane > 0 && nx != ent;
+    if (!__ballot(ch)) break;
+    if (ch) {
+      uint64_t ne;
+      if (!merge<FMT, true>(T, w, C, ent, nx, shi, acc, ne, ovf)) exi = ne;
+      ent = nx;
+    }
+  }
   if constexpr (WRITE) {
-    WriteEm em{P.out_base[r], P.out_capacity, P.out_start, P.out_len, P.out_cap};
-    while (p < bhi) p = chain_step<FMT, WriteEm, true>(T, w, C, p, em, +1, ovf);
+    // exclusive scan of lane counts -> output index of the lane's first match
+    uint64_t incl = acc.cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    WriteEm em{P.out_base[r] + incl - acc.cnt, P.out_capacity, P.out_start, P.out_len, P.out_cap};
+    uint64_t q = ent;
+    while (q < shi) q = chain_step<FMT, WriteEm, true>(T, w, C, q, em, +1, ovf);
     if (em.overflow) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
   } else {
-    CountEm em;
-    while (p < bhi) p = chain_step<FMT, CountEm, true>(T, w, C, p, em, +1, ovf);
-    BlockRec rec;
-    rec.entry = blo;
-    rec.exit = bhi > blo ? p : blo;
-    rec.cnt = em.cnt;
-    rec.dg = em.dg;
-    rec.dc = em.dc;
-    rec.pad0 = rec.pad1 = rec.pad2 = 0;
-    P.recs[r] = rec;
+    const uint64_t c = wave_sum(acc.cnt), d = wave_sum(acc.dg), dc = wave_sum(acc.dc);
+    const uint64_t x = __shfl(exi, 63, 64);
+    if (lane == 0) {
+      BlockRec rec;
+      rec.entry = wlo;
+      rec.exit = whi > wlo ? (x > whi ? x : whi) : wlo;
+      rec.cnt = c;
+      rec.dg = d;
+      rec.dc = dc;
+      rec.pad0 = rec.pad1 = rec.pad2 = 0;
+      P.recs[r] = rec;
+    }
   }
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
 }
@@ -69,13 +105,14 @@ __global__ __launch_bounds__(kWfindLanes) void wfind_kernel(ScanParams P)
 template <int FMT, bool WRITE>
 hipError_t wfind_one(const ScanParams& P, hipStream_t stream)
 {
-  hipLaunchKernelGGL((wfind_kernel<FMT, WRITE>), dim3(P.grid), dim3(kWfindLanes), 0, stream, P);
+  hipLaunchKernelGGL((wfind_kernel<FMT, WRITE>), dim3(P.grid), dim3(kWWaves * 64), 0, stream, P);
   return hipGetLastError();
 }
 
 }  // namespace
 
 uint32_t wfind_unit() { return kWUnit; }
+uint32_t wfind_waves() { return kWWaves; }
 
 hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream)
 {
