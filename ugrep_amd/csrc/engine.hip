@@ -295,7 +295,7 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->accepting = d->t.accepting;
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
-  info->kernel = d->d_wtab                                    ? 4u
+  info->kernel = (d->d_wtab && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
                  : (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
                  : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u
                  : (d->d_xg && !(genv && genv[0] == '0'))  ? 3u
@@ -404,7 +404,9 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   if (!s) return fail(UGPU_NOMEM, "host allocation");
   s->dfa = dfa;
   HIP_TRY(hipGetDevice(&s->device));
-  if (dfa->d_wtab) {  // option W: wfind_kernel (tables read through the caches, no LDS)
+  // option W: prefiltered tables keep sparse_kernel (its candidate walks check
+  // the W rules); every other table runs wfind_kernel (tables through the caches)
+  if (dfa->d_wtab && !(dfa->t.filter && dfa->t.format == FMT_BYTE)) {
     s->word = true;
     s->max_rec = kMaxRec;
     if (const char* env = std::getenv("UGPU_MAX_GRID")) {

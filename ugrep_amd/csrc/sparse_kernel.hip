@@ -178,7 +178,7 @@ __device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, ui
 // Walk the deferred candidates (one per lane) and resolve them.  Each lane
 // copies the 32 bytes from c & ~15 into its LDS window (the tiles are gone
 // from registers); longer walks continue from global memory.
-template <bool WRITE, int ABL>
+template <bool WRITE, int ABL, bool W = false>
 __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr, uint32_t dn, int lane, const Tab<0>& T,
                                             const Ctx& C, const ScanParams& P, uint64_t& x, CountEm& acc,
                                             uint64_t& widx, uint32_t& wover, uint32_t& ovf)
@@ -203,7 +203,12 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
     w.g = P.g;
     w.rend = P.rend;
     w.eof = P.at_eof;
-    len = walk<0>(T, w, c, le, ovf);
+    w.wtab = P.wtab;
+    w.nwtab = P.nwtab;
+    w.bob = P.bob;
+    // option W: the walk checks at_wb/at_we (device_common.hpp); candidates
+    // stay a superset (W only removes matches), so the prefilter is unchanged
+    len = walk<0, W>(T, w, c, le, ovf);
   }
   resolve<WRITE>(valid, c, len, le, lane, C, P, x, acc, widx, wover);
   wave_lds_sync();  // the aux region is reused
@@ -226,7 +231,7 @@ struct WaveChain {
 // by the wave's range [wlo, whi).
 // ABL (benchmarking only; results are not matches): 1 loads alone, 2 loads +
 // prefilter, 3 everything but the walks.
-template <bool WRITE, int ABL>
+template <bool WRITE, int ABL, bool W = false>
 __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3,
                                           uint64_t ts, bool edge, uint64_t wlo, uint64_t whi, int lane,
                                           const FTab& F, const Tab<0>& T, const Ctx& C, const ScanParams& P,
@@ -305,7 +310,7 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
     const uint32_t rank = incl - cnt;
     for (uint32_t done = 0; done < tot;) {
       if (w.dn == (uint32_t)kDefer) {
-        flush_deferred<WRITE, ABL>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
+        flush_deferred<WRITE, ABL, W>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
         w.dn = 0;
       }
       const uint32_t take = tot - done < kDefer - w.dn ? tot - done : kDefer - w.dn;
@@ -336,7 +341,7 @@ __device__ __forceinline__ TileLoad wave_tile(const uint8_t* wbase, uint32_t i, 
 
 }  // namespace
 
-template <bool WRITE, int ABL>
+template <bool WRITE, int ABL, bool W = false>
 __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -403,7 +408,7 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
   uint32_t i = 0;
   if (n >= 2) {
     do {
-      tile_pass<WRITE, ABL>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, i == 0 && clip_lo, wlo, whi, lane, F, T, C,
+      tile_pass<WRITE, ABL, W>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, i == 0 && clip_lo, wlo, whi, lane, F, T, C,
                             P, dl, scr, w);
       {
         const TileLoad L = wave_tile(wbase, i + 2, rel);
@@ -412,7 +417,7 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
         a2 = stream16(L, lo16 + 2048);
         a3 = stream16(L, lo16 + 3072);
       }
-      tile_pass<WRITE, ABL>(b0, b1, b2, b3, wb + (uint64_t)(i + 1) * kWaveTile, i + 2 == n && clip_hi, wlo, whi,
+      tile_pass<WRITE, ABL, W>(b0, b1, b2, b3, wb + (uint64_t)(i + 1) * kWaveTile, i + 2 == n && clip_hi, wlo, whi,
                             lane, F, T, C, P, dl, scr, w);
       {
         const TileLoad L = wave_tile(wbase, i + 3, rel);
@@ -425,9 +430,9 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
     } while (i + 1 < n);
   }
   if (i < n)  // a* holds tile i = n - 1
-    tile_pass<WRITE, ABL>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, (i == 0 && clip_lo) || clip_hi, wlo, whi,
+    tile_pass<WRITE, ABL, W>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, (i == 0 && clip_lo) || clip_hi, wlo, whi,
                           lane, F, T, C, P, dl, scr, w);
-  if (w.dn) flush_deferred<WRITE, ABL>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
+  if (w.dn) flush_deferred<WRITE, ABL, W>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
   uint64_t x = w.x > whi ? w.x : whi;  // chain exit: the last kept match end or the range end
   if (tb == te) x = wlo;
 
@@ -457,17 +462,17 @@ size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates)
 
 namespace {
 
-template <bool WRITE, int ABL>
+template <bool WRITE, int ABL, bool W = false>
 hipError_t sparse_one(const ScanParams& P, size_t smem, hipStream_t stream)
 {
   static size_t attr_smem = 65536;
   if (smem > attr_smem) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE, ABL>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE, ABL, W>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_smem = smem;
   }
-  hipLaunchKernelGGL((sparse_kernel<WRITE, ABL>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream, P);
+  hipLaunchKernelGGL((sparse_kernel<WRITE, ABL, W>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream, P);
   return hipGetLastError();
 }
 
@@ -475,6 +480,7 @@ hipError_t sparse_one(const ScanParams& P, size_t smem, hipStream_t stream)
 
 hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream_t stream)
 {
+  if (P.wtab) return write ? sparse_one<true, 0, true>(P, smem, stream) : sparse_one<false, 0, true>(P, smem, stream);
   if (write) return sparse_one<true, 0>(P, smem, stream);
   switch (P.ablate) {  // benchmarking knob (UGPU_ABLATE): count pass only
     case 1: return sparse_one<false, 1>(P, smem, stream);
