@@ -407,6 +407,10 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   // option W: prefiltered tables keep sparse_kernel (its candidate walks check
   // the W rules); every other table runs wfind_kernel (tables through the caches)
   if (dfa->d_wtab && !(dfa->t.filter && dfa->t.format == FMT_BYTE)) {
+    if (wfind_smem_bytes(dfa->ntrans_pad, dfa->t.states, dfa->nwtab) > 160 * 1024) {
+      delete s;
+      return fail(UGPU_UNSUPPORTED, "tables do not fit in LDS");
+    }
     s->word = true;
     s->max_rec = kMaxRec;
     if (const char* env = std::getenv("UGPU_MAX_GRID")) {

@@ -164,6 +164,7 @@ uint32_t utf8_tile();
 hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream);
 uint32_t wfind_unit();
 uint32_t wfind_waves();
+size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab);
 // immediate-transducer kernel, xi_kernel.hip (COUNT mode only)
 hipError_t launch_xi(const ScanParams& P, size_t smem, hipStream_t stream);
 hipError_t xi_occupancy(size_t smem, int* blocks_per_cu);

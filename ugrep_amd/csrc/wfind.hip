@@ -17,8 +17,10 @@
 //   * the OFFSETS pass repeats the lane stitch from the record's exact entry,
 //     scans the lane counts into output bases and re-walks, writing records.
 //
-// Bound: one dependent byte read per step along one chain per lane (global
-// memory through the caches), plus the table lookup; see DESIGN.md §3.8.
+// The tables (transitions, accept indices, classes, Word ranges) are staged in
+// LDS once per workgroup of kWWaves records.  Bound: one dependent global byte
+// read plus one LDS table lookup per step along one chain per lane; see
+// DESIGN.md §3.8.
 #include "device_common.hpp"
 
 namespace ugpu {
@@ -26,11 +28,38 @@ namespace ugpu {
 namespace {
 
 constexpr uint32_t kWUnit = 4096;   // bytes per tile (records hold whole tiles)
-constexpr int kWWaves = 4;          // waves (records) per workgroup
+#ifndef UGPU_WF_WAVES
+#define UGPU_WF_WAVES 16
+#endif
+constexpr int kWWaves = UGPU_WF_WAVES;  // waves (records) per workgroup: one staged table copy
+
+// LDS image: transitions (u16, ntrans_pad), accept indices (u32 per state),
+// Word ranges (2 x u32 each), class bytes (256)
+__host__ __device__ inline size_t wfind_smem(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab)
+{
+  return 2 * (size_t)ntrans_pad + 4 * (size_t)nstates + 8 * (size_t)nwtab + 256;
+}
 
 template <int FMT, bool WRITE>
 __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
 {
+  extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
+  {
+    // stage the tables once per workgroup (the walks look them up per byte)
+    uint16_t* tr = reinterpret_cast<uint16_t*>(wsm);
+    uint32_t* cp = reinterpret_cast<uint32_t*>(wsm + 2 * (size_t)P.ntrans_pad);
+    uint32_t* wt = cp + P.nstates;
+    uint8_t* cl = reinterpret_cast<uint8_t*>(wt + 2 * P.nwtab);
+    for (uint32_t i = threadIdx.x; i < P.ntrans_pad; i += blockDim.x) tr[i] = P.trans[i];
+    for (uint32_t i = threadIdx.x; i < P.nstates; i += blockDim.x) cp[i] = P.caps[i];
+    for (uint32_t i = threadIdx.x; i < 2 * P.nwtab; i += blockDim.x) wt[i] = P.wtab[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) cl[i] = P.cls[i];
+    __syncthreads();
+  }
+  const uint16_t* s_trans = reinterpret_cast<const uint16_t*>(wsm);
+  const uint32_t* s_caps = reinterpret_cast<const uint32_t*>(wsm + 2 * (size_t)P.ntrans_pad);
+  const uint32_t* s_wtab = s_caps + P.nstates;
+  const uint8_t* s_cls = reinterpret_cast<const uint8_t*>(s_wtab + 2 * P.nwtab);
   const int lane = threadIdx.x & 63;
   const uint64_t r = (uint64_t)blockIdx.x * kWWaves + (threadIdx.x >> 6);
   if (r >= P.nrec) return;  // wave-uniform
@@ -42,8 +71,8 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
   const uint64_t seg = (whi - wlo + 63) / 64;
   const uint64_t slo = wlo + seg * lane < whi ? wlo + seg * lane : whi;
   const uint64_t shi = slo + seg < whi ? slo + seg : whi;
-  const Tab<FMT> T{P.trans, P.cls, P.start, P.accb};
-  const Ctx C{P.caps, P.log_row, P.delta};
+  const Tab<FMT> T{s_trans, s_cls, P.start, P.accb};
+  const Ctx C{s_caps, P.log_row, P.delta};
   Win w;
   w.lds = nullptr;
   w.base = 0;
@@ -51,7 +80,7 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
   w.g = P.g;
   w.rend = P.rend;
   w.eof = P.at_eof;
-  w.wtab = P.wtab;
+  w.wtab = s_wtab;
   w.nwtab = P.nwtab;
   w.bob = P.bob;
   uint32_t ovf = 0;
@@ -105,7 +134,15 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
 template <int FMT, bool WRITE>
 hipError_t wfind_one(const ScanParams& P, hipStream_t stream)
 {
-  hipLaunchKernelGGL((wfind_kernel<FMT, WRITE>), dim3(P.grid), dim3(kWWaves * 64), 0, stream, P);
+  const size_t smem = wfind_smem(P.ntrans_pad, P.nstates, P.nwtab);
+  static size_t attr_smem = 65536;
+  if (smem > attr_smem) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wfind_kernel<FMT, WRITE>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    attr_smem = smem;
+  }
+  hipLaunchKernelGGL((wfind_kernel<FMT, WRITE>), dim3(P.grid), dim3(kWWaves * 64), smem, stream, P);
   return hipGetLastError();
 }
 
@@ -113,6 +150,10 @@ hipError_t wfind_one(const ScanParams& P, hipStream_t stream)
 
 uint32_t wfind_unit() { return kWUnit; }
 uint32_t wfind_waves() { return kWWaves; }
+size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab)
+{
+  return wfind_smem(ntrans_pad, nstates, nwtab);
+}
 
 hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream)
 {
