@@ -44,6 +44,16 @@ HAND = [
     ("F", "a.b*c"), ("F", "(x|y)"), ("F", "[é]"), ("F", "\\E\\Q"), ("F", ""),
     # -i (ASCII letters)
     ("i", "lorem"), ("i", "k"), ("i", "s"), ("i", "[a-z]+"), ("i", "foo|BAR"), ("i", r"\w+x"),
+    # \p{..} classes and POSIX brackets (Unicode tables, lib/unicode.cpp)
+    ("re", r"\p{L}"), ("re", r"\p{Lu}+"), ("re", r"\P{L}"), ("re", r"[\p{L}]"), ("re", r"[\P{L}]"),
+    ("re", r"[^\p{L}]"), ("re", r"\p{Greek}+"), ("re", r"\p{Han}"), ("re", r"\pL"), ("re", r"\PL"),
+    ("re", r"\p{Letter}"), ("re", r"\p{Zs}"), ("re", r"\P{Cc}"), ("re", r"[\P{Cc}]"), ("re", r"\P{Space}"),
+    ("re", r"[\P{Zs}]"), ("re", r"[x\P{Lu}]"), ("re", r"\p{L}\p{M}*"), ("re", r"[\p{Han}\p{Hiragana}\p{Katakana}]+"),
+    ("re", r"\p{Lu}\p{Ll}+"), ("re", "[[:alpha:]_][[:alnum:]_]*"), ("re", "[[:upper:]]"),
+    ("re", "[[:digit:][:space:]]"), ("re", "[[:punct:]]+"), ("re", "[[:xdigit:]]"), ("re", "[[:ascii:]]"),
+    ("re", "[[:cntrl:]]"), ("re", "[[:print:]]"), ("re", "[[:graph:]]"), ("re", "[[:word:]]"), ("re", "[[:blank:]]"),
+    ("re", "[[:lower:]]"), ("re", r"\p{Common}"), ("re", r"\P{Greek}"), ("re", r"\p{Nd}+|\p{Sc}"),
+    ("re", r"\p{Cyrillic}+"), ("re", r"\p{Arabic}\p{Mn}*"),
     # syntax errors (reference throws regex_error)
     ("re", "(|a)"), ("re", "()"), ("re", "{"), ("re", "a{"), ("re", "a{,3}"), ("re", "(a|)"), ("re", "|a"),
     ("re", "[a-z"), ("re", "(a"), ("re", "a)"),
@@ -51,7 +61,8 @@ HAND = [
 
 ATOMS = ['a', 'b', 'c', 'é', 'ж', '€', '😀', '.', r'\w', r'\d', r'\s', r'\W', r'\S', r'\D', r'\h', r'\H', '[abc]',
          '[^a]', '[a-cé]', r'[^\w]', r'[\d\s]', '[α-ω]', r'\.', r'\x41', 'x', '\t', r'[\W]', '[^ж-я]', '[0-9]',
-         r'\x{10000}', r'[\x{80}-\x{7ff}]', r'[^\x{800}-\x{ffff}]']
+         r'\x{10000}', r'[\x{80}-\x{7ff}]', r'[^\x{800}-\x{ffff}]', r'\p{L}', r'\P{Lu}', r'[\p{Greek}x]',
+         '[[:alpha:]]', r'\p{Nd}']
 
 
 def random_pattern(rng, d=0):

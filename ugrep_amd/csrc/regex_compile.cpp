@@ -17,14 +17,17 @@
 //
 // Supported: literals (UTF-8), escapes \t\n\r\f\v\a\e \xHH \x{H..} \0ooo and
 // escaped punctuation, '.', bracket expressions (ranges, negation, escapes,
-// \w\d\s\h inside), \w \W \d \D \s \S \h \H, groups ( ) (?: ), alternation,
+// \w\d\s\h and \p{..} inside, POSIX [:name:]), \w \W \d \D \s \S \h \H,
+// \p{NAME} \P{NAME} \pL (general categories and their long names, common
+// scripts, POSIX-style names), groups ( ) (?: ), alternation,
 // * + ? {n} {n,} {n,m}, -F literal mode, and ASCII -i case folding.
 // Returns UGPU_UNSUPPORTED for what the GPU tables cannot express or this
 // compiler does not cover (anchors, word boundaries, lazy quantifiers,
-// lookaround, backreferences, \p{..}, POSIX [:class:]): the caller keeps the
-// CPU matcher for those, as for any unsupported opcode table.
+// lookaround, backreferences, other \p names, non-ASCII -i): the caller keeps
+// the CPU matcher for those, as for any unsupported opcode table.
 #include <stdint.h>
 #include <stdlib.h>
+#include <ctype.h>
 #include <string.h>
 
 #include <algorithm>
@@ -134,6 +137,22 @@ CpSet table_set(const uint32_t (&t)[N][2])
   for (size_t i = 0; i < N; ++i)
     s.push_back({t[i][0], t[i][1]});
   return s;
+}
+
+// \p{NAME} / [[:name:]] tables (unicode_ranges.inc registry); false if unknown
+bool named_set(const std::string &name, CpSet &out, bool *pnl = NULL)
+{
+  for (const UClass &c : k_pclasses)
+    if (name == c.name)
+    {
+      if (pnl)
+        *pnl = c.pnl != 0;
+      out.clear();
+      for (unsigned i = 0; i < c.n; ++i)
+        out.push_back({c.ranges[i][0], c.ranges[i][1]});
+      return true;
+    }
+  return false;
 }
 
 CpSet word_set() { return table_set(k_word_ranges); }
@@ -569,6 +588,37 @@ class Parser
       case 'H':
         set = in_bracket ? complement_upto(hspace_set(), kMaxCp) : complement(hspace_set());
         return true;
+      case 'p':
+      case 'P':
+      {
+        // \p{NAME}, \pL (lib/unicode.cpp, lib/language_scripts.cpp); \P
+        // complements like \W: over all scalar values outside brackets, up to
+        // the table's last code point inside
+        std::string name;
+        if (p_ < s_.size() && s_[p_] == '{')
+        {
+          size_t q = s_.find('}', p_);
+          if (q == std::string::npos)
+            fail(UGPU_INVAL, "missing '}'");
+          name = s_.substr(p_ + 1, q - p_ - 1);
+          p_ = q + 1;
+        }
+        else if (p_ < s_.size())
+          name = std::string(1, s_[p_++]);
+        CpSet t;
+        bool pnl = true;
+        if (!named_set(name, t, &pnl))
+          fail(UGPU_UNSUPPORTED, "class \\p{" + name + "}");
+        if (c == 'p')
+          set = t;
+        else
+        {
+          set = complement(t);  // '\n' stays out when the class itself holds it (pnl)
+          if (!pnl)
+            set = minus(set, CpSet{{'\n', '\n'}});
+        }
+        return true;
+      }
       case 't': cp = '\t'; return false;
       case 'n': cp = '\n'; return false;
       case 'r': cp = '\r'; return false;
@@ -647,8 +697,29 @@ class Parser
         break;
       }
       first = false;
-      if (c == '[' && p_ + 1 < s_.size() && (s_[p_ + 1] == ':' || s_[p_ + 1] == '.' || s_[p_ + 1] == '='))
-        fail(UGPU_UNSUPPORTED, "POSIX bracket class");
+      if (c == '[' && p_ + 1 < s_.size() && s_[p_ + 1] == ':')
+      {
+        // [:name:] (lib/posix.cpp names, the Unicode tables in Unicode mode)
+        size_t q = s_.find(":]", p_ + 2);
+        std::string name = q == std::string::npos ? "" : s_.substr(p_ + 2, q - p_ - 2);
+        if (name.empty() || name[0] == '^')
+          fail(UGPU_UNSUPPORTED, "POSIX bracket class");
+        std::string cap = name;
+        cap[0] = static_cast<char>(toupper(static_cast<unsigned char>(cap[0])));
+        if (name == "xdigit")
+          cap = "XDigit";
+        else if (name == "ascii")
+          cap = "ASCII";
+        CpSet t;
+        if (!named_set(cap, t))
+          fail(UGPU_UNSUPPORTED, "POSIX bracket class [:" + name + ":]");
+        set.insert(set.end(), t.begin(), t.end());
+        p_ = q + 2;
+        first = false;
+        continue;
+      }
+      if (c == '[' && p_ + 1 < s_.size() && (s_[p_ + 1] == '.' || s_[p_ + 1] == '='))
+        fail(UGPU_UNSUPPORTED, "POSIX collating element");
       uint32_t lo;
       CpSet cls;
       if (c == '\\')
@@ -746,7 +817,7 @@ class Parser
       case '\\':
       {
         ++p_;
-        if (p_ < s_.size() && strchr("bBAzZ<>`'GkKQEpPXRNuUcCl", s_[p_]) != NULL)
+        if (p_ < s_.size() && strchr("bBAzZ<>`'GkKQEXRNuUcCl", s_[p_]) != NULL)
           fail(UGPU_UNSUPPORTED, std::string("escape \\") + s_[p_]);
         CpSet set;
         uint32_t cp;
