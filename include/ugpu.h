@@ -257,10 +257,10 @@ int ugpu_gen(int kind, uint64_t seed, uint64_t off, uint8_t *dbuf, uint64_t len,
    malloc'd, free it with ugpu_opc_free().  Returns UGPU_INVAL on a syntax error
    (the reference throws regex_error, lib/pattern.cpp:162-169) and
    UGPU_UNSUPPORTED for constructs the GPU tables do not cover (anchors, word
-   boundaries, lazy quantifiers, lookaround, rare \p{..} scripts, non-ASCII -i); the
+   boundaries, lazy quantifiers, lookaround, rare \p{..} scripts, \p{Lu} under -i); the
    message is in ugpu_compile_error(). */
 #define UGPU_RX_FIXED 1u /* -F: the pattern is a literal string (src/cnf.hpp:147-165) */
-#define UGPU_RX_ICASE 2u /* -i, ASCII letters only */
+#define UGPU_RX_ICASE 2u /* -i: ASCII letters and the reference's Unicode case pairs */
 int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, uint32_t *nop);
 void ugpu_opc_free(uint32_t *opc);
 const char *ugpu_compile_error(void);

@@ -53,7 +53,12 @@ def test_compile_equivalent_to_reference(chunk):
                 _compile(U, mode, rx)
             assert not isinstance(e.value, U.Unsupported), (mode, rx)
             continue
-        mine = _compile(U, mode, rx)
+        try:
+            mine = _compile(U, mode, rx)
+        except U.Unsupported as e:
+            # documented limitation: \p{Lu}/\p{Ll}/\p{Lt} under -i
+            assert mode == "i" and "under -i" in str(e), (mode, rx, e)
+            continue
         ce = counterexample(mine, ref)
         if ce is not None:
             bad.append((mode, rx, ce))
@@ -73,11 +78,11 @@ def test_config_tables_are_loadable():
 
 
 @pytest.mark.parametrize("rx", ["^a", "a$", r"\bfoo", r"\<x", "a*?", "a+?", r"(a)\1", r"\p{Tangut}", "[[:^alpha:]]",
-                                "(?=x)", r"\Qa\E", "é"])
+                                "(?=x)", r"\Qa\E", r"\p{Lu}"])
 def test_unsupported_constructs(rx):
     import ugrep_amd as U
     with pytest.raises(U.Unsupported):
-        U.compile_regex(rx, icase=(rx == "é"))
+        U.compile_regex(rx, icase=(rx == r"\p{Lu}"))
 
 
 def test_long_gotos():

@@ -44,6 +44,12 @@ HAND = [
     ("F", "a.b*c"), ("F", "(x|y)"), ("F", "[é]"), ("F", "\\E\\Q"), ("F", ""),
     # -i (ASCII letters)
     ("i", "lorem"), ("i", "k"), ("i", "s"), ("i", "[a-z]+"), ("i", "foo|BAR"), ("i", r"\w+x"),
+    # -i over Unicode (case_fold.inc; (?i) leaves \x{..} escapes unfolded)
+    ("i", "é"), ("i", "ж"), ("i", "straße"), ("i", "ÉCOLE"), ("i", "[à-ÿ]+"), ("i", "[é]"), ("i", r"\x{e9}"),
+    ("i", r"[\x{e9}]"), ("i", r"\x41"), ("i", "Ωμέγα"), ("i", "ǅ"), ("i", "ſ"), ("i", "K"), ("i", "ß"), ("i", "İ"),
+    ("i", "ı"), ("i", "[α-ω]"), ("i", r"\p{Greek}"), ("i", "[^é]"), ("i", "Ⓐ"), ("i", "ⅰ"), ("i", r"\W"),
+    ("i", r"\p{L}"), ("i", r"\p{Latin}+"), ("i", r"\P{L}"), ("i", r"[\p{Greek}a]"), ("i", "[[:lower:]]"),
+    ("i", "[[:alpha:]]+"), ("i", "Straße|ΣΊΣΥΦΟΣ|Привет"),
     # \p{..} classes and POSIX brackets (Unicode tables, lib/unicode.cpp)
     ("re", r"\p{L}"), ("re", r"\p{Lu}+"), ("re", r"\P{L}"), ("re", r"[\p{L}]"), ("re", r"[\P{L}]"),
     ("re", r"[^\p{L}]"), ("re", r"\p{Greek}+"), ("re", r"\p{Han}"), ("re", r"\pL"), ("re", r"\PL"),
@@ -91,7 +97,7 @@ def main():
         rx = random_pattern(rng)
         if rng.random() < 0.3:
             rx += '|' + random_pattern(rng, 1)
-        cases.append(("re", rx))
+        cases.append(("i" if rng.random() < 0.25 else "re", rx))
     modes, pats, offs, words = [], [], [0], []
     for mode, rx in cases:
         opc = ref_opc(mode, rx)

@@ -20,10 +20,10 @@
 // \w\d\s\h and \p{..} inside, POSIX [:name:]), \w \W \d \D \s \S \h \H,
 // \p{NAME} \P{NAME} \pL (general categories and their long names, common
 // scripts, POSIX-style names), groups ( ) (?: ), alternation,
-// * + ? {n} {n,} {n,m}, -F literal mode, and ASCII -i case folding.
+// * + ? {n} {n,} {n,m}, -F literal mode, and -i (ASCII plus case_fold.inc pairs).
 // Returns UGPU_UNSUPPORTED for what the GPU tables cannot express or this
 // compiler does not cover (anchors, word boundaries, lazy quantifiers,
-// lookaround, backreferences, other \p names, non-ASCII -i): the caller keeps
+// lookaround, backreferences, other \p names, \p{Lu} under -i): the caller keeps
 // the CPU matcher for those, as for any unsupported opcode table.
 #include <stdint.h>
 #include <stdlib.h>
@@ -41,6 +41,7 @@
 namespace {
 
 #include "unicode_ranges.inc"
+#include "case_fold.inc"
 
 typedef std::vector<std::pair<uint32_t, uint32_t>> CpSet;  // sorted, disjoint, inclusive
 typedef std::bitset<256> ByteSet;
@@ -159,6 +160,36 @@ CpSet word_set() { return table_set(k_word_ranges); }
 CpSet digit_set() { return table_set(k_digit_ranges); }
 CpSet space_set() { return table_set(k_space_ranges); }
 CpSet hspace_set() { return CpSet{{'\t', '\t'}, {' ', ' '}}; }
+
+// the other case of c >= 0x80 under (?i), or 0 (case_fold.inc)
+uint32_t case_variant(uint32_t c)
+{
+  size_t lo = 0, hi = sizeof(k_case_sets) / sizeof(k_case_sets[0]);
+  while (lo < hi)
+  {
+    size_t mid = (lo + hi) / 2;
+    if (k_case_sets[mid][0] < c)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < sizeof(k_case_sets) / sizeof(k_case_sets[0]) && k_case_sets[lo][0] == c ? k_case_sets[lo][2] : 0;
+}
+
+// add the (?i) variants of every member >= 0x80 (rows of case_fold.inc)
+void add_unicode_case(CpSet &s)
+{
+  CpSet extra;
+  for (auto &row : k_case_sets)
+  {
+    uint32_t c = row[0];
+    auto it = std::upper_bound(s.begin(), s.end(), std::make_pair(c, 0xFFFFFFFFu));
+    if (it != s.begin() && (it - 1)->first <= c && c <= (it - 1)->second)
+      extra.push_back({row[2], row[2]});
+  }
+  s.insert(s.end(), extra.begin(), extra.end());
+  s = normalize(s);
+}
 
 void add_ascii_case(CpSet &s)
 {
@@ -609,6 +640,9 @@ class Parser
         bool pnl = true;
         if (!named_set(name, t, &pnl))
           fail(UGPU_UNSUPPORTED, "class \\p{" + name + "}");
+        if (icase() && (name == "Lu" || name == "Ll" || name == "Lt" || name == "Upper" || name == "Lower" ||
+                        name == "Uppercase_Letter" || name == "Lowercase_Letter" || name == "Titlecase_Letter"))
+          fail(UGPU_UNSUPPORTED, "case class under -i");  // the reference widens these differently
         if (c == 'p')
           set = t;
         else
@@ -753,10 +787,8 @@ class Parser
     set = normalize(set);
     if (icase())
     {
-      for (auto &r : set)
-        if (r.second >= 0x80 && !(r.first == 0 && r.second == kMaxCp))
-          fail(UGPU_UNSUPPORTED, "Unicode case folding");
       add_ascii_case(set);
+      add_unicode_case(set);
     }
     if (neg)
       set = minus(complement(set), CpSet{{'\n', '\n'}});  // notnewline
@@ -824,23 +856,30 @@ class Parser
         if (parse_escape(set, cp, false))
         {
           if (icase())
+          {
             add_ascii_case(set);
+            add_unicode_case(set);
+          }
           return t_.cpset(set);
         }
-        return code_point(cp);
+        return code_point(cp, true);
       }
       default:
         return code_point(utf8_char());
     }
   }
 
-  int code_point(uint32_t cp)
+  // escaped: from \x{..}/\0ooo, which (?i) leaves unfolded (measured on the
+  // reference's tables: (?i)\x{e9} matches only U+00E9, (?i)é also U+00C9)
+  int code_point(uint32_t cp, bool escaped = false)
   {
-    if (icase() && cp >= 0x80)
-      fail(UGPU_UNSUPPORTED, "Unicode case folding");
     if (cp < 0x80)
       return literal_byte(static_cast<uint8_t>(cp));
-    return t_.cpset(CpSet{{cp, cp}});
+    CpSet s{{cp, cp}};
+    uint32_t v = icase() && !escaped ? case_variant(cp) : 0;
+    if (v)
+      s.push_back({v, v});
+    return t_.cpset(s);
   }
 };
 
