@@ -22,9 +22,10 @@
 // exact whenever the new cur_ is not inside one; otherwise (and for a new
 // buffer) the scan is re-run from cur_.
 //
-// Everything else -- SCAN/SPLIT/MATCH, streaming input(), options A/N/W,
-// tables the engine rejects (anchors, \b, lookahead: UGPU_UNSUPPORTED) --
-// stays on the CPU matcher, unchanged.
+// Option W (ugrep -w, src/ugrep.cpp:8616-8618) is served from a second table
+// handle created with UGPU_PAT_WORD (wdfa).  Everything else -- SCAN/SPLIT/
+// MATCH, streaming input(), options A/N, tables the engine rejects (anchors,
+// \b, lookahead: UGPU_UNSUPPORTED) -- stays on the CPU matcher, unchanged.
 #ifndef REFLEX_GPU_MATCHER_H
 #define REFLEX_GPU_MATCHER_H
 
@@ -36,9 +37,10 @@ namespace reflex {
 
 class GpuMatcher : public Matcher {
  public:
-  /// dfa: ugpu_dfa_create(pattern's opc_ words) or NULL (CPU only); not owned.
-  GpuMatcher(const Pattern& pattern, const ugpu_dfa* dfa, const char* opt = NULL)
-      : Matcher(pattern, Input(), opt), dfa_(dfa)
+  /// dfa: ugpu_dfa_create(pattern's opc_ words, 0) or NULL (CPU only); wdfa:
+  /// the same words with UGPU_PAT_WORD, used when opt has W; not owned.
+  GpuMatcher(const Pattern& pattern, const ugpu_dfa* dfa, const char* opt = NULL, const ugpu_dfa* wdfa = NULL)
+      : Matcher(pattern, Input(), opt), dfa_(opt_.W ? wdfa : dfa)
   {
   }
   ~GpuMatcher() { ugpu_result_free(gres_); }
@@ -49,7 +51,7 @@ class GpuMatcher : public Matcher {
  protected:
   virtual size_t match(Method method)
   {
-    if (method != Const::FIND || dfa_ == NULL || own_ || !eof_ || opt_.A || opt_.N || opt_.W)
+    if (method != Const::FIND || dfa_ == NULL || own_ || !eof_ || opt_.A || opt_.N)
       return Matcher::match(method);
     if (gres_ == NULL || gbuf_ != buf_ || gend_ != end_ || cur_ < gfrom_ || inside_match())
       if (!rescan())

@@ -130,10 +130,16 @@ int main(int argc, char** argv)
     if (line.empty() || line[0] == '#')
       continue;
     size_t t1 = line.find('\t'), t2 = line.find('\t', t1 + 1);
-    const std::string mode = line.substr(0, t1), rx = line.substr(t1 + 1, t2 - t1 - 1), in = line.substr(t2 + 1);
+    std::string mode = line.substr(0, t1);
+    const std::string rx = line.substr(t1 + 1, t2 - t1 - 1), in = line.substr(t2 + 1);
+    // mode suffix W: Matcher option W (ugrep -w) on both sides, UGPU_PAT_WORD tables
+    const bool word = mode.size() > 1 && mode[mode.size() - 1] == 'W';
+    if (word)
+      mode.erase(mode.size() - 1);
+    const char* opt = word ? "W" : NULL;
     reflex::Pattern pat(build_regex(mode, rx), "r");
     ugpu_dfa* dfa = NULL;
-    const int rc = ugpu_dfa_create(pat.opc_, static_cast<uint32_t>(pat.nop_), 0, &dfa);
+    const int rc = ugpu_dfa_create(pat.opc_, static_cast<uint32_t>(pat.nop_), word ? UGPU_PAT_WORD : 0u, &dfa);
     if (rc != UGPU_OK && rc != UGPU_UNSUPPORTED)
     {
       printf("FAIL /%s/: ugpu_dfa_create: %d %s\n", rx.c_str(), rc, ugpu_last_error());
@@ -143,16 +149,17 @@ int main(int argc, char** argv)
     std::vector<char> a = load_input(in), b = a;
     for (int kind = 0; kind < 3; ++kind)
     {
-      reflex::Matcher cpu(pat);
-      reflex::GpuMatcher gpu(pat, rc == UGPU_OK ? dfa : NULL);
+      reflex::Matcher cpu(pat, reflex::Input(), opt);
+      reflex::GpuMatcher gpu(pat, word || rc != UGPU_OK ? NULL : dfa, opt, word && rc == UGPU_OK ? dfa : NULL);
       bool ea = false, eb = false;
       std::vector<Hit> ra = run(cpu, a, kind, ea), rb = run(gpu, b, kind, eb);
       size_t diff = 0;
       while (diff < ra.size() && diff < rb.size() && !(ra[diff] != rb[diff]))
         ++diff;
       const bool ok = ra.size() == rb.size() && diff == ra.size() && ea == eb;
-      printf("%s %s kind=%d /%s/ %s: cpu %zu gpu %zu matches, gpu scans %zu%s\n", ok ? "ok" : "FAIL",
-             rc == UGPU_OK ? "gpu" : "cpu-only", kind, rx.c_str(), in.substr(0, 40).c_str(), ra.size(), rb.size(),
+      printf("%s %s kind=%d /%s/%s %s: cpu %zu gpu %zu matches, gpu scans %zu%s\n", ok ? "ok" : "FAIL",
+             rc == UGPU_OK ? "gpu" : "cpu-only", kind, rx.c_str(), word ? "W" : "", in.substr(0, 40).c_str(),
+             ra.size(), rb.size(),
              gpu.gpu_scans(), rc == UGPU_OK ? "" : " (engine: unsupported table)");
       if (!ok)
       {
