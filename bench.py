@@ -125,6 +125,27 @@ def verify_whole(args, kind, total, pat, res, rank, dev, sptr):
     return ok
 
 
+def pcie_inclusive(pat, buf, nbytes, dev, reps=3):
+    """Host-buffer rate: ugpu_find_all on a pinned host copy of the first `nbytes`
+    (hipMalloc + H2D + scan + fix + free per call). Never `value`:
+    the boundary's device-resident entry point is what `value` measures."""
+    host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    host.copy_(buf[:nbytes])
+    torch.cuda.synchronize(dev)
+    want = ugrep_amd.find_all(pat, buf[:nbytes], offsets=False)  # same bytes, device-resident
+    best = float("inf")
+    got = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        got = ugrep_amd.find_all(pat, host, offsets=False)
+        best = min(best, time.perf_counter() - t0)
+    ok = (got.count, got.digest, got.dcap) == (want.count, want.digest, want.dcap)
+    del host
+    return {"value": round(nbytes / best / 1e9, 2), "unit": "GB/s", "sample_bytes": nbytes,
+            "path": "ugpu_find_all on a pinned host buffer (hipMalloc + H2D + scan + fix), best of %d" % reps,
+            "equals_device_resident": ok}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -135,6 +156,8 @@ def main():
     ap.add_argument("--halo", type=int, default=1 << 20, help="readable bytes past a shard end")
     ap.add_argument("--cpu-sample-mib", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pcie-sample-mib", type=int, default=2048,
+                    help="host-buffer sample for the PCIe-inclusive leg (0 = skip)")
     ap.add_argument("--offsets", action="store_true",
                     help="each step also materialises the match records (start, len, accept) in HBM and, "
                          "for N > 1, all-gathers them to every rank (SURVEY.md §8e step 4)")
@@ -247,6 +270,9 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    pcie = None
+    if rank == 0 and world == 1 and args.pcie_sample_mib > 0:
+        pcie = pcie_inclusive(pat, buf, min(args.pcie_sample_mib << 20, hi - lo), dev)
     verified = None
     if args.verify:
         del buf
@@ -286,6 +312,8 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel_ms": round(k_avg, 4), "algorithmic_bytes_per_launch": hi - lo},
     }
+    if pcie is not None:
+        out["pcie_inclusive"] = pcie
     if verified is not None:
         out["verified_whole_stream"] = verified
     if args.offsets:
