@@ -231,6 +231,26 @@ def test_nonsynchronising_chain(U, pats):
         os.environ.pop("UGPU_MAX_GRID", None)
 
 
+def test_nonsynchronising_unicode_phases(U):
+    """`\\D\\D` over the word corpus (no digits, multi-byte UTF-8): FIND phases that
+    never meet, on dense_kernel + fix_kernel.  Count and full match lists equal the
+    oracle's.  Sizes stay small: this is DESIGN.md section 7's known slow case
+    (fix_kernel walks whole records serially, about 2 s at 256 KiB)."""
+    from oracle_lib import OracleDfa, gen
+    opc = U.compile_regex(r"\D\D")
+    pat = U.Pattern(opc)
+    assert pat.info()["kernel"] == 1
+    o = OracleDfa(opc)
+    for kib in (64, 256):
+        host = gen(4, 11, 0, kib << 10)
+        dev = torch.from_numpy(host).to("cuda")
+        r = U.find_all(pat, dev, offsets=False)
+        assert (r.count, r.digest, r.dcap) == o.find(host)[:3], kib
+        if kib == 64:
+            r = U.find_all(pat, dev, offsets=True)
+            assert r.triples() == o.find(host, want_list=True)[3]
+
+
 def test_offsets_at_scale(U, pats):
     """Full match lists at 16 MiB (dense C3/C4 matches) equal the oracle's."""
     from oracle_lib import OracleDfa, gen
