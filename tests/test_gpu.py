@@ -235,7 +235,7 @@ def test_nonsynchronising_unicode_phases(U):
     """`\\D\\D` over the word corpus (no digits, multi-byte UTF-8): FIND phases that
     never meet, on dense_kernel + fix_kernel.  Count and full match lists equal the
     oracle's.  Sizes stay small: this is DESIGN.md section 7's known slow case
-    (fix_kernel walks whole records serially, about 2 s at 256 KiB)."""
+    (fix_kernel merges whole records, 0.3 s at 256 KiB)."""
     from oracle_lib import OracleDfa, gen
     opc = U.compile_regex(r"\D\D")
     pat = U.Pattern(opc)

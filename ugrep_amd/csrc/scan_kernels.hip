@@ -37,7 +37,7 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
   uint64_t cnt[PER], dg[PER], dc[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    const int b = tid * PER + j;
+    const int b = j * kFixThreads + tid;
     if (b < G) {
       BlockRec r = P.recs[b];
       ent[b] = r.entry;
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
     bool ch[PER], any = false;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const int b = tid * PER + j;
+      const int b = j * kFixThreads + tid;
       ch[j] = false;
       if (b > 0 && b < G) {
         nx[j] = exi[b - 1];
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       if (!ch[j]) continue;
-      const uint64_t b = tid * PER + j;
+      const uint64_t b = (uint64_t)j * kFixThreads + tid;
       uint64_t tb = P.t0 + b * P.tpb;
       uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
       if (tb > te) tb = te;
@@ -86,47 +86,52 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
     if (!__syncthreads_or(any)) break;
     ++rounds;
   }
-  // totals + exclusive scan of block counts
-  uint64_t mc = 0, md = 0, mdc = 0;
+  // totals + exclusive scan of block counts (block order b = j * kFixThreads + tid:
+  // one workgroup scan per j, carried across j)
+  uint64_t md = 0, mdc = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    mc += cnt[j];
     md += dg[j];
     mdc += dc[j];
   }
-  uint64_t incl = mc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint64_t y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
-  }
   const uint64_t sd = wave_sum(md), sdc = wave_sum(mdc);
-  if (lane == 63) wscan[wid] = incl;
   if (lane == 0) {
     wred[1][wid] = sd;
     wred[2][wid] = sdc;
   }
-  __syncthreads();
-  uint64_t off = 0;
-  for (int k = 0; k < wid; ++k) off += wscan[k];
-  uint64_t run = off + incl - mc;
+  uint64_t carry = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    const int b = tid * PER + j;
-    if (b < G) {
-      P.out_base_out[b] = run;
-      P.entries_out[b] = ent[b];
-      run += cnt[j];
+    uint64_t incl = cnt[j];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      uint64_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
     }
+    __syncthreads();
+    if (lane == 63) wscan[wid] = incl;
+    __syncthreads();
+    uint64_t off = carry, tot = 0;
+    for (int k = 0; k < kFixThreads / 64; ++k) {
+      if (k < wid) off += wscan[k];
+      tot += wscan[k];
+    }
+    const int b = j * kFixThreads + tid;
+    if (b < G) {
+      P.out_base_out[b] = off + incl - cnt[j];
+      P.entries_out[b] = ent[b];
+    }
+    carry += tot;
   }
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
+  __syncthreads();
   if (tid == 0) {
-    uint64_t c = 0, d = 0, e = 0;
+    uint64_t d = 0, e = 0;
     for (int k = 0; k < kFixThreads / 64; ++k) {
-      c += wscan[k];
       d += wred[1][k];
       e += wred[2][k];
     }
+    const uint64_t c = carry;
     DevTotals* t = P.totals;
     t->count = c;
     t->digest = d;
