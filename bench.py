@@ -48,33 +48,58 @@ def log(msg):
     print("[bench] " + msg, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg, sample, threads):
-    """Reference CPU matcher (oracle/_ref/ref_harness, libreflex compiled from the
-    reference sources) on a bounded sample of the same corpus; falls back to the
-    oracle restatement ("port") when the reference build is absent."""
-    pkey, mode, rx, kind, _, _ = CONFIGS[cfg]
-    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    seed = 1
+def _harness(exe, mode, rx, spec, threads, reps):
+    out = subprocess.run([exe, "bench", mode, rx, spec, str(threads), str(reps)], capture_output=True,
+                         timeout=900, check=True).stdout.decode()
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def _spec(kind, sample):
     if kind == 0:
-        spec = "file:%s:%d" % (os.path.join(REPO, "tests", "golden", "lorem.utf8.txt"), sample)
-    else:
-        spec = "gen:%d:%d:0:%d" % (kind, seed, sample)
-    if os.path.exists(harness):
+        return "file:%s:%d" % (os.path.join(REPO, "tests", "golden", "lorem.utf8.txt"), sample)
+    return "gen:%d:1:0:%d" % (kind, sample)
+
+
+def cpu_baseline(cfg, sample, threads):
+    """The reference CPU matcher on a bounded sample of the same corpus.
+
+    `value` is the reference AVX2 path (oracle/_ref/ref_harness_avx2: libreflex
+    compiled from the reference sources with -DHAVE_AVX2, BASELINE.json's
+    "reference AVX2 CPU path") on all `threads` host cores, newline-split shards
+    sharing one Pattern as ugrep's workers do (src/ugrep.cpp:4206).  Also
+    reported: the same build on 1 core (on a smaller sample), and the
+    AVX512BW-dispatching build on all cores.  Returns (baseline dict, the
+    reference's count/digest/dcap of the whole sample) -- the latter is compared
+    with the GPU scan of the same bytes.  Falls back to the oracle restatement
+    ("port") when the reference build is absent."""
+    pkey, mode, rx, kind, _, _ = CONFIGS[cfg]
+    avx2 = os.path.join(REPO, "oracle", "_ref", "ref_harness_avx2")
+    avx512 = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if os.path.exists(avx2):
         try:
-            out = subprocess.run([harness, "bench", mode, rx, spec, str(threads), "3"], capture_output=True,
-                                 timeout=600, check=True).stdout.decode()
-            j = json.loads(out.strip().splitlines()[-1])
-            return dict(value=round(j["bytes"] / j["seconds"] / 1e9, 3), unit="GB/s", cores=threads, kind="reference",
-                        sample="%d MiB of the same corpus (seed %d), reference libreflex Matcher::find() loop, "
-                               "newline-split across %d threads sharing one Pattern, best of 3; %d matches"
-                               % (sample >> 20, seed, threads, j["count"]))
+            j = _harness(avx2, mode, rx, _spec(kind, sample), threads, 3)
+            one_sample = min(sample, 1 << 30 if info_dense(cfg) else sample)
+            j1 = _harness(avx2, mode, rx, _spec(kind, one_sample), 1, 2)
+            out = dict(value=round(j["bytes"] / j["seconds"] / 1e9, 3), unit="GB/s", cores=threads, kind="reference",
+                       build="AVX2 (-DHAVE_AVX2)",
+                       sample="%d MiB of the same corpus (seed 1, bytes [0, %d)), reference libreflex Matcher::find() "
+                              "loop, newline-split across %d threads sharing one Pattern, best of 3; %d matches"
+                              % (sample >> 20, sample, threads, j["count"]),
+                       one_core={"value": round(j1["bytes"] / j1["seconds"] / 1e9, 3), "unit": "GB/s",
+                                 "sample_bytes": one_sample, "best_of": 2},
+                       host_cpus_visible=len(os.sched_getaffinity(0)))
+            if os.path.exists(avx512):
+                j5 = _harness(avx512, mode, rx, _spec(kind, sample), threads, 3)
+                out["avx512bw_build"] = {"value": round(j5["bytes"] / j5["seconds"] / 1e9, 3), "unit": "GB/s",
+                                         "cores": threads}
+            return out, (j["count"], j["digest"], j["dcap"])
         except Exception as e:  # pragma: no cover - diagnostic path
             log("reference harness failed (%s); using the oracle restatement" % e)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_lib import OracleDfa, gen as host_gen
     with open(os.path.join(REPO, "ugrep_amd", "data", "config_patterns.json")) as f:
         opc = json.load(f)[pkey]["opc"]
-    buf = host_gen(kind, seed, 0, sample) if kind else np.frombuffer(
+    buf = host_gen(kind, 1, 0, sample) if kind else np.frombuffer(
         (open(os.path.join(REPO, "tests", "golden", "lorem.utf8.txt"), "rb").read() * (sample // 9419 + 1))[:sample],
         np.uint8)
     d = OracleDfa(opc)
@@ -84,7 +109,24 @@ def cpu_baseline(cfg, sample, threads):
         d.find_mt(buf, threads)
         best = min(best, time.perf_counter() - t0)
     return dict(value=round(sample / best / 1e9, 3), unit="GB/s", cores=threads, kind="port",
-                sample="%d MiB, oracle restatement (dense-table walker), %d threads" % (sample >> 20, threads))
+                sample="%d MiB, oracle restatement (dense-table walker), %d threads" % (sample >> 20, threads)), None
+
+
+def info_dense(cfg):
+    """Configs the reference walks byte by byte (no SIMD prefilter): ~0.2 GB/s per core."""
+    return cfg in ("c3", "c4")
+
+
+def gpu_reference_check(pat, buf, sample, want, sptr):
+    """Scan the cpu_baseline sample [0, sample) of this GPU's buffer as one whole
+    buffer (EOF at its end, as the reference harness sees it) and compare
+    count/digest/dcap with the reference's."""
+    sc = ugrep_amd.Scanner(pat)
+    sc.scan(buf.data_ptr(), 0, sample, sample, True, 0, sptr)
+    t = sc.totals()
+    got = (t.count, t.digest, t.dcap)
+    return {"equal": got == tuple(want), "bytes": sample, "gpu": list(got), "reference": list(want),
+            "fields": ["count", "digest", "dcap"]}
 
 
 KERNELS = {0: "sparse_kernel", 1: "dense_kernel", 2: "xi_kernel", 3: "xg_kernel", 4: "wfind_kernel"}
@@ -248,7 +290,9 @@ def main():
         if args.offsets:
             count = t.count
             if world > 1 and rec["entries"][rank] != lo:  # chain re-entered this shard: re-scan from there
-                sc.scan(ptr, rec["entries"][rank] - lo, hi - lo, n_read, eof, lo, sptr)
+                # (an entry at or past hi: the previous shard's last match covers this whole shard)
+                ent = min(rec["entries"][rank], hi)
+                sc.scan(ptr, ent - lo, hi - lo, n_read, eof, lo, sptr)
                 count = sc.totals().count
             rec["records"] = records(count)
         return rec
@@ -273,6 +317,18 @@ def main():
     pcie = None
     if rank == 0 and world == 1 and args.pcie_sample_mib > 0:
         pcie = pcie_inclusive(pat, buf, min(args.pcie_sample_mib << 20, hi - lo), dev)
+    cpu_leg = (None, None)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the box's CPU share for one GPU is 16 cores (os.sched_getaffinity shows the whole machine)
+        threads = min(16, len(os.sched_getaffinity(0)))
+        sample = min(args.cpu_sample_mib << 20, per_gpu)
+        log("cpu baseline: %d MiB, %d threads" % (sample >> 20, threads))
+        base, ref = cpu_baseline(args.config, sample, threads)
+        chk = None
+        if ref is not None and not args.word:  # the same bytes on the GPU, compared with the reference
+            chk = gpu_reference_check(pat, buf, sample, ref, sptr)
+            log("reference parity on [0, %d): %s" % (sample, chk))
+        cpu_leg = (base, chk)
     verified = None
     if args.verify:
         del buf
@@ -327,11 +383,10 @@ def main():
     if tr:
         out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
         out["roofline"]["traffic_source"] = tr["source"]
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, len(os.sched_getaffinity(0)))
-        sample = min(args.cpu_sample_mib << 20, per_gpu)
-        log("cpu baseline: %d MiB, %d threads" % (sample >> 20, threads))
-        out["cpu_baseline"] = cpu_baseline(args.config, sample, threads)
+    if cpu_leg[0] is not None:
+        out["cpu_baseline"] = cpu_leg[0]
+        if cpu_leg[1] is not None:
+            out["parity_vs_reference"] = cpu_leg[1]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

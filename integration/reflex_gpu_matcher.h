@@ -53,7 +53,12 @@ class GpuMatcher : public Matcher {
   {
     if (method != Const::FIND || dfa_ == NULL || own_ || !eof_ || opt_.A || opt_.N)
       return Matcher::match(method);
-    if (gres_ == NULL || gbuf_ != buf_ || gend_ != end_ || cur_ < gfrom_ || inside_match())
+    // buffer() and reset() are non-virtual and rewind cur_ without telling this
+    // class (absmatcher.h:542-591), and the caller may hand over new bytes at
+    // the same address and size (ugrep re-buffers one std::string per line,
+    // src/ugrep.cpp:733-740): any cursor behind the one this class last left
+    // means the records may be stale, so scan again
+    if (gres_ == NULL || gbuf_ != buf_ || gend_ != end_ || cur_ < gcur_ || inside_match())
       if (!rescan())
         return Matcher::match(method);
     while (gi_ < gres_->count && gres_->start[gi_] < cur_)
@@ -63,6 +68,7 @@ class GpuMatcher : public Matcher {
       set_current(end_);
       txt_ = buf_ + end_;
       len_ = 0;
+      gcur_ = cur_;
       return cap_ = 0;
     }
     const size_t start = static_cast<size_t>(gres_->start[gi_]);
@@ -70,6 +76,7 @@ class GpuMatcher : public Matcher {
     len_ = gres_->len[gi_];
     cap_ = gres_->cap[gi_];
     set_current(start + len_);
+    gcur_ = cur_;
     ++gi_;
     return cap_;
   }
@@ -95,7 +102,7 @@ class GpuMatcher : public Matcher {
     ++scans_;
     gbuf_ = buf_;
     gend_ = end_;
-    gfrom_ = cur_;
+    gcur_ = cur_;
     gi_ = 0;
     return true;
   }
@@ -103,7 +110,8 @@ class GpuMatcher : public Matcher {
   const ugpu_dfa* dfa_;
   ugpu_result* gres_ = NULL;
   const char* gbuf_ = NULL;
-  size_t gend_ = 0, gfrom_ = 0, gi_ = 0, scans_ = 0;
+  // gcur_: the cursor this class left behind (after the scan or the last hit)
+  size_t gend_ = 0, gcur_ = 0, gi_ = 0, scans_ = 0;
 };
 
 }  // namespace reflex

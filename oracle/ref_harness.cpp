@@ -246,8 +246,10 @@ int main(int argc, char **argv)
         tot.dcap += p.dcap;
       }
     }
-    printf("{\"bytes\": %zu, \"seconds\": %.6f, \"threads\": %d, \"count\": %llu, \"digest\": %llu}\n",
-        n, best, threads, (unsigned long long)tot.count, (unsigned long long)tot.digest);
+    printf("{\"bytes\": %zu, \"seconds\": %.6f, \"threads\": %d, \"count\": %llu, \"digest\": %llu, "
+           "\"dcap\": %llu}\n",
+        n, best, threads, (unsigned long long)tot.count, (unsigned long long)tot.digest,
+        (unsigned long long)tot.dcap);
     return 0;
   }
   return 2;

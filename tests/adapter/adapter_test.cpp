@@ -16,6 +16,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <fstream>
 #include <string>
 #include <vector>
@@ -97,19 +98,27 @@ struct Hit {
   }
 };
 
-// loop kind: 0 plain, 1 skip('\n') after each hit, 2 skip(' ') after every other hit
+// loop kind: 0 plain, 1 skip('\n') after each hit, 2 skip(' ') after every other
+// hit, 3 plain loop, then new bytes at the same address and size handed over
+// with buffer() and a second plain loop (ugrep re-buffers one reused std::string
+// per line, src/ugrep.cpp:733-740; buffer() is non-virtual, absmatcher.h:542)
 template <class M>
 static std::vector<Hit> run(M& m, std::vector<char>& buf, int kind, bool& at_end)
 {
   std::vector<Hit> out;
-  m.buffer(buf.data(), buf.size());
-  while (m.find())
+  for (int pass = 0; pass < (kind == 3 ? 2 : 1); ++pass)
   {
-    out.push_back(Hit{m.first(), m.size(), m.accept(), m.lineno(), m.columno()});
-    if (kind == 1)
-      m.skip('\n');
-    else if (kind == 2 && (out.size() & 1))
-      m.skip(' ');
+    if (pass == 1 && buf.size() > 2)  // rotate the data bytes in place, keep the NUL
+      std::rotate(buf.begin(), buf.begin() + (buf.size() - 1) / 3, buf.end() - 1);
+    m.buffer(buf.data(), buf.size());
+    while (m.find())
+    {
+      out.push_back(Hit{m.first(), m.size(), m.accept(), m.lineno(), m.columno()});
+      if (kind == 1)
+        m.skip('\n');
+      else if (kind == 2 && (out.size() & 1))
+        m.skip(' ');
+    }
   }
   at_end = m.at_end();
   return out;
@@ -147,7 +156,7 @@ int main(int argc, char** argv)
       continue;
     }
     std::vector<char> a = load_input(in), b = a;
-    for (int kind = 0; kind < 3; ++kind)
+    for (int kind = 0; kind < 4; ++kind)
     {
       reflex::Matcher cpu(pat, reflex::Input(), opt);
       reflex::GpuMatcher gpu(pat, word || rc != UGPU_OK ? NULL : dfa, opt, word && rc == UGPU_OK ? dfa : NULL);

@@ -274,3 +274,46 @@ def test_start_offset(U, pats):
         o = OracleDfa(pats["c3_ident"].opc).find(host, start=start, want_list=True)
         assert (r.count, r.digest, r.dcap) == o[:3]
         assert r.triples() == o[3]
+
+
+def test_stitch_budget_falls_back(U):
+    """A chain that never resynchronises under a small stitch budget
+    (UGPU_FIX_BUDGET) is reported as UGPU_UNSUPPORTED, so the caller keeps the
+    CPU matcher, instead of walking whole records serially for hours
+    (fix_kernel's round budget).  With the default budget the same
+    input is bit-exact."""
+    from oracle_lib import OracleDfa, gen
+    opc = U.compile_regex(r"\D\D")
+    pat = U.Pattern(opc)
+    host = gen(4, 11, 0, 256 << 10)
+    dev = torch.from_numpy(host).to("cuda")
+    os.environ["UGPU_FIX_BUDGET"] = "4096"
+    try:
+        with pytest.raises(U.Unsupported):
+            U.find_all(pat, dev, offsets=False)
+    finally:
+        os.environ.pop("UGPU_FIX_BUDGET", None)
+    r = U.find_all(pat, dev, offsets=False)
+    assert (r.count, r.digest, r.dcap) == OracleDfa(opc).find(host)[:3]
+
+
+def test_matcher_skip_inside_match_rescans(U, pats):
+    """Matcher.skip_to() into the middle of a match: the next find() is the
+    reference's FIND from that cursor (a suffix match), as the C++ adapter does."""
+    from oracle_lib import OracleDfa, gen
+    host = gen(3, 9, 0, 1 << 16)
+    o = OracleDfa(pats["c3_ident"].opc)
+    m = U.Matcher(pats["c3_ident"], host.tobytes())
+    got, want, cur = [], [], 0
+    for i in range(200):
+        if not m.find():
+            break
+        got.append((m.first(), m.size(), m.accept()))
+        _, _, _, lst = o.find(host, start=cur, want_list=True)
+        want.append(tuple(lst[0]))
+        cur = m.last()
+        if m.size() > 2 and i % 3 == 0:  # land strictly inside the next match or this one's successor
+            cur = m.first() + 1 if i % 2 else cur + 1
+            m.skip_to(cur)
+            m._cur = cur  # skip_to only moves forward; rewind into the returned match on purpose
+    assert got == want

@@ -117,3 +117,19 @@ def test_init_window_trim():
     assert O.is_binary(b"a\x00b", nul_only=True) is True
     assert O.is_binary(b"a\xffb", nul_only=True) is False
     assert O.is_binary(b"a\x00b", null_data=True) is False
+
+
+def test_oracle_long_streams_vs_reference(patterns):
+    """The restatement over the 128-512 MiB corpus prefixes of
+    tests/golden/streams.json equals the reference matcher's count, digest and
+    dcap (pins the fixture the multi-shard GPU tests and bench.py rely on)."""
+    import json
+    import os
+    from oracle_lib import GOLDEN, OracleDfa, gen
+    with open(os.path.join(GOLDEN, "streams.json")) as f:
+        streams = json.load(f)
+    for name, s in streams.items():
+        buf = gen(s["kind"], s["seed"], 0, s["bytes"])
+        got = OracleDfa(patterns[s["pattern"]]["opc"]).find_mt(buf, 8)
+        assert got == (s["count"], s["digest"], s["dcap"]), name
+        del buf

@@ -1,7 +1,8 @@
 """GPU: streaming FIND (ugpu_stream).  Feeding any chunking
 of an input -- one byte at a time, ragged sizes, chunks that split matches,
-matches longer than the carry margin -- yields exactly the whole-buffer FIND
-result (ugpu_find_all), which the other GPU tests pin to the reference."""
+matches longer than the carry margin -- yields exactly the FIND result of the
+oracle restatement over the whole input (tests/oracle_lib.py, itself pinned to
+the reference matcher by tests/test_oracle.py), record by record."""
 import numpy as np
 import pytest
 
@@ -39,8 +40,10 @@ def _stream(U, pat, data, sizes, keep, offsets=True):
 
 
 def _whole(U, pat, data):
-    r = U.find_all(pat, data.tobytes(), offsets=True)
-    return r.triples(), r.count, r.digest, r.dcap
+    """The oracle's FIND over the whole input: (triples, count, digest, dcap)."""
+    from oracle_lib import OracleDfa
+    cnt, dg, dc, lst = OracleDfa(pat.opc).find(np.ascontiguousarray(data), want_list=True)
+    return lst, cnt, dg, dc
 
 
 @pytest.mark.parametrize("pname,kind", [("c2_foobarbaz", 1), ("c3_ident", 3), ("c4_word", 4)])

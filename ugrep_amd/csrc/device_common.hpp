@@ -219,14 +219,22 @@ __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, 
 }
 
 // Re-enter [.., e) at xn instead of xo.  Adds (true - speculative) matches to em.
-// Returns true if the chains met (exit unchanged), else sets nexit.
+// Returns true if the chains met (exit unchanged), else sets nexit.  A merge
+// whose chains cross more than `budget` bytes without meeting sets `over` and
+// stops (the result is then invalid: UGPU_FLAG_BUDGET).
 template <int FMT, bool W = false>
 __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t xo, uint64_t xn,
-                                      uint64_t e, CountEm& em, uint64_t& nexit, uint32_t& ovf)
+                                      uint64_t e, CountEm& em, uint64_t& nexit, uint32_t& ovf,
+                                      uint64_t budget = ~0ull, uint32_t* over = nullptr)
 {
   uint64_t po = xo, pn = xn;
+  const uint64_t lim = (xo < xn ? xo : xn) + budget < (xo < xn ? xo : xn) ? ~0ull : (xo < xn ? xo : xn) + budget;
   for (;;) {
     if (po == pn) return true;
+    if (over && (po > lim || pn > lim)) {
+      *over = 1;
+      return true;
+    }
     if (po >= e && pn >= e) {
       nexit = pn;
       return false;

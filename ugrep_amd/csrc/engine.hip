@@ -78,6 +78,9 @@ namespace {
 
 thread_local std::string g_err;
 
+const char* const kBudgetMsg =
+    "the FIND chains of this table do not resynchronise on this input (stitch budget exceeded): use the CPU matcher";
+
 int fail(int code, const std::string& msg)
 {
   g_err = msg;
@@ -95,6 +98,23 @@ int hip_fail(hipError_t e, const char* what)
     hipError_t _e = (expr);                        \
     if (_e != hipSuccess) return hip_fail(_e, #expr); \
   } while (0)
+
+uint64_t env_u64(const char* name, uint64_t dflt)
+{
+  const char* v = std::getenv(name);
+  return v && *v ? std::strtoull(v, nullptr, 0) : dflt;
+}
+
+// fix_kernel rounds allowed for a geometry: at most ~16 MiB of serial re-walks
+// in total (UGPU_FIX_BUDGET), at least 4 rounds (normal tables need 0-1)
+uint32_t fix_rounds_for(const ScanParams& P)
+{
+  const uint64_t rec = P.tpb * P.unit ? P.tpb * P.unit : 1;
+  uint64_t r = env_u64("UGPU_FIX_BUDGET", 16ull << 20) / rec;
+  if (r < 4) r = 4;
+  if (r > 1u << 20) r = 1u << 20;
+  return (uint32_t)r;
+}
 
 void fill_tables(ScanParams& P, const ugpu_dfa* d)
 {
@@ -114,6 +134,7 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.cap1 = d->t.cap1;
   P.wtab = d->d_wtab;
   P.nwtab = d->nwtab;
+  P.merge_budget = env_u64("UGPU_MERGE_BUDGET", 1ull << 20);
   for (int i = 0; i < 5; ++i)
     P.ft[i] = (uint32_t)d->t.ft[4 * i] | ((uint32_t)d->t.ft[4 * i + 1] << 8) | ((uint32_t)d->t.ft[4 * i + 2] << 16) |
               ((uint32_t)d->t.ft[4 * i + 3] << 24);
@@ -149,6 +170,7 @@ void geometry(ScanParams& P, const uint8_t* dbuf, uint64_t lo, uint64_t hi, uint
   P.unit = unit;
   P.grid = (uint32_t)grid;
   P.nrec = (uint32_t)(grid * per);
+  P.max_rounds = fix_rounds_for(P);
 }
 
 void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi,
@@ -403,7 +425,17 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   ugpu_scanner* s = new (std::nothrow) ugpu_scanner();
   if (!s) return fail(UGPU_NOMEM, "host allocation");
   s->dfa = dfa;
-  HIP_TRY(hipGetDevice(&s->device));
+  // every failure below releases what was allocated so far
+#define HIP_TRY_S(expr)                      \
+  do {                                       \
+    hipError_t _e = (expr);                  \
+    if (_e != hipSuccess) {                  \
+      const int _rc = hip_fail(_e, #expr);   \
+      ugpu_scanner_destroy(s);               \
+      return _rc;                            \
+    }                                        \
+  } while (0)
+  HIP_TRY_S(hipGetDevice(&s->device));
   // option W: prefiltered tables keep sparse_kernel (its candidate walks check
   // the W rules); every other table runs wfind_kernel (tables through the caches)
   if (dfa->d_wtab && !(dfa->t.filter && dfa->t.format == FMT_BYTE)) {
@@ -417,15 +449,15 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
       int v = std::atoi(env);
       if (v >= 1 && v <= kMaxRec) s->max_rec = v;
     }
-    HIP_TRY(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
-    HIP_TRY(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
-    HIP_TRY(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
-    HIP_TRY(hipMalloc(&s->d_tot, sizeof(DevTotals)));
-    HIP_TRY(hipMalloc(&s->d_flags, sizeof(uint32_t)));
-    HIP_TRY(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
-    HIP_TRY(hipHostMalloc(&s->h_flags, sizeof(uint32_t)));
-    HIP_TRY(hipEventCreate(&s->ev0));
-    HIP_TRY(hipEventCreate(&s->ev1));
+    HIP_TRY_S(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
+    HIP_TRY_S(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
+    HIP_TRY_S(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
+    HIP_TRY_S(hipMalloc(&s->d_tot, sizeof(DevTotals)));
+    HIP_TRY_S(hipMalloc(&s->d_flags, sizeof(uint32_t)));
+    HIP_TRY_S(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
+    HIP_TRY_S(hipHostMalloc(&s->h_flags, sizeof(uint32_t)));
+    HIP_TRY_S(hipEventCreate(&s->ev0));
+    HIP_TRY_S(hipEventCreate(&s->ev1));
     *out = s;
     return UGPU_OK;
   }
@@ -439,12 +471,12 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   int per_cu = 0;
   if (s->sparse) {
     ScanParams probe{};
-    HIP_TRY(sparse_occupancy(probe, s->smem, &per_cu));
+    HIP_TRY_S(sparse_occupancy(probe, s->smem, &per_cu));
   } else {
-    HIP_TRY(dense_occupancy(dfa->t.format, dfa->t.cap1 != 0, dfa->d_xtrans != nullptr, s->smem, &per_cu));
+    HIP_TRY_S(dense_occupancy(dfa->t.format, dfa->t.cap1 != 0, dfa->d_xtrans != nullptr, s->smem, &per_cu));
   }
   hipDeviceProp_t prop;
-  HIP_TRY(hipGetDeviceProperties(&prop, s->device));
+  HIP_TRY_S(hipGetDeviceProperties(&prop, s->device));
   if (per_cu < 1) per_cu = 1;
   int g = prop.multiProcessorCount * per_cu * (s->sparse ? kSpWaves : dense_waves(dfa->t.format));
   if (g > kMaxRec) g = kMaxRec;
@@ -459,7 +491,7 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   const char* genv = std::getenv("UGPU_XG");
   if (!s->sparse && !(dfa->d_xid && !(xenv && xenv[0] == '0')) && dfa->d_xg && !(genv && genv[0] == '0')) {
     int gpc = 0;
-    HIP_TRY(xg_occupancy(dfa->t.format, &gpc));
+    HIP_TRY_S(xg_occupancy(dfa->t.format, &gpc));
     if (gpc >= 1) {
       s->xg = true;
       int gg = prop.multiProcessorCount * gpc * (int)xg_waves();
@@ -473,7 +505,7 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   if (!s->sparse && dfa->d_xid && !(xenv && xenv[0] == '0')) {
     s->xi_smem = (size_t)dfa->t.xid_rows * 256;
     int xpc = 0;
-    HIP_TRY(xi_occupancy(s->xi_smem, &xpc));
+    HIP_TRY_S(xi_occupancy(s->xi_smem, &xpc));
     if (xpc >= 1) {
       s->xi = true;
       int xg = prop.multiProcessorCount * xpc * (int)xi_waves();
@@ -484,17 +516,18 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
       }
     }
   }
-  HIP_TRY(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
-  HIP_TRY(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
-  HIP_TRY(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
-  HIP_TRY(hipMalloc(&s->d_tot, sizeof(DevTotals)));
-  HIP_TRY(hipMalloc(&s->d_flags, sizeof(uint32_t)));
-  HIP_TRY(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
-  HIP_TRY(hipHostMalloc(&s->h_flags, sizeof(uint32_t)));
-  HIP_TRY(hipEventCreate(&s->ev0));
-  HIP_TRY(hipEventCreate(&s->ev1));
+  HIP_TRY_S(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
+  HIP_TRY_S(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
+  HIP_TRY_S(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
+  HIP_TRY_S(hipMalloc(&s->d_tot, sizeof(DevTotals)));
+  HIP_TRY_S(hipMalloc(&s->d_flags, sizeof(uint32_t)));
+  HIP_TRY_S(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
+  HIP_TRY_S(hipHostMalloc(&s->h_flags, sizeof(uint32_t)));
+  HIP_TRY_S(hipEventCreate(&s->ev0));
+  HIP_TRY_S(hipEventCreate(&s->ev1));
   *out = s;
   return UGPU_OK;
+#undef HIP_TRY_S
 }
 
 int ugpu_scanner_destroy(ugpu_scanner* s)
@@ -564,6 +597,7 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
   out->flags = *s->h_flags;
   out->fix_rounds = t.rounds;
   if (out->flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
+  if (out->flags & UGPU_FLAG_BUDGET) return fail(UGPU_UNSUPPORTED, kBudgetMsg);
   return UGPU_OK;
 }
 
@@ -638,6 +672,7 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
   delta->flags = t.flags;
   delta->fix_rounds = t.rounds;
   if (t.flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
+  if (t.flags & UGPU_FLAG_BUDGET) return fail(UGPU_UNSUPPORTED, kBudgetMsg);
   return UGPU_OK;
 }
 
@@ -1049,7 +1084,14 @@ int stream_grow(ugpu_stream* st, uint64_t need)
       return hip_fail(e, "stream buffer");
     }
   }
-  if (st->carry) HIP_TRY(hipMemcpy(nb[0], st->buf[st->cur], st->carry, hipMemcpyDeviceToDevice));
+  if (st->carry) {
+    const hipError_t e = hipMemcpy(nb[0], st->buf[st->cur], st->carry, hipMemcpyDeviceToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(nb[0]);
+      (void)hipFree(nb[1]);
+      return hip_fail(e, "stream carry copy");
+    }
+  }
   for (int i = 0; i < 2; ++i)
     if (st->buf[i]) (void)hipFree(st->buf[i]);
   st->buf[0] = nb[0];

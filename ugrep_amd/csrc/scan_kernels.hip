@@ -32,7 +32,7 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
   w.wtab = P.wtab;
   w.nwtab = P.nwtab;
   w.bob = P.bob;
-  uint32_t ovf = 0;
+  uint32_t ovf = 0, over = 0;
 
   uint64_t cnt[PER], dg[PER], dc[PER];
 #pragma unroll
@@ -75,8 +75,8 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
       const uint64_t bhi = clampu(te * P.unit, P.lo, P.hi);
       CountEm d;
       uint64_t ne;
-      const bool met = P.wtab ? merge<FMT, true>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf)
-                              : merge<FMT>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf);
+      const bool met = P.wtab ? merge<FMT, true>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over)
+                              : merge<FMT>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over);
       if (!met) exi[b] = ne;
       ent[b] = nx[j];
       cnt[j] += d.cnt;
@@ -84,7 +84,10 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
       dc[j] += d.dc;
     }
     if (!__syncthreads_or(any)) break;
-    ++rounds;
+    if (__syncthreads_or(over) || ++rounds >= P.max_rounds) {  // chains that do not resynchronise
+      over = 1;
+      break;
+    }
   }
   // totals + exclusive scan of block counts (block order b = j * kFixThreads + tid:
   // one workgroup scan per j, carried across j)
@@ -124,6 +127,7 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
     carry += tot;
   }
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
+  if (over && tid == 0) atomicOr(P.flags, UGPU_FLAG_BUDGET);
   __syncthreads();
   if (tid == 0) {
     uint64_t d = 0, e = 0;
@@ -156,17 +160,17 @@ __global__ void chain_fix_kernel(ScanParams P, uint64_t old_entry, uint64_t new_
   w.g = P.g;
   w.rend = P.rend;
   w.eof = P.at_eof;
-  uint32_t ovf = 0;
+  uint32_t ovf = 0, over = 0;
   CountEm d;
   uint64_t ne = 0;
-  bool met = merge<FMT>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf);
+  bool met = merge<FMT>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over);
   DevTotals* t = P.totals;
   t->count = d.cnt;
   t->digest = d.dg;
   t->dcap = d.dc;
   t->entry = new_entry;
   t->exit = met ? ~0ull : ne;  // ~0 = exit unchanged
-  t->flags = ovf ? UGPU_FLAG_HALO : 0;
+  t->flags = (ovf ? UGPU_FLAG_HALO : 0) | (over ? UGPU_FLAG_BUDGET : 0);
   t->rounds = met ? 1 : 0;
 }
 

@@ -65,6 +65,11 @@ struct DevTotals {
 
 #define UGPU_FLAG_HALO 1u
 #define UGPU_FLAG_CAPACITY 2u
+// a stitch (fix_kernel rounds or one merge walk) ran past its work budget: the
+// FIND chains of this table do not resynchronise on this input (e.g. \D\D over
+// text without digits); the totals are invalid and the host reports
+// UGPU_UNSUPPORTED, so the caller keeps the CPU matcher
+#define UGPU_FLAG_BUDGET 4u
 
 struct ScanParams {
   const uint8_t* g;   // 16-byte aligned base of the scanned bytes
@@ -108,6 +113,10 @@ struct ScanParams {
   const uint32_t* wtab;
   uint32_t nwtab;
   uint64_t bob;
+  // stitch budgets (UGPU_FLAG_BUDGET): fix_kernel rounds, and chain bytes one
+  // merge may cross before giving up (fix_kernel, chain_fix_kernel)
+  uint32_t max_rounds;
+  uint64_t merge_budget;
 };
 
 // launchers (scan_kernels.hip, gen.hip)

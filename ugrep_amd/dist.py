@@ -33,43 +33,37 @@ def _to_u64(v):
     return int(np.array([v], dtype=np.int64).view(np.uint64)[0])
 
 
-def stitch(rec, fix_fn, device="cpu", group=None):
-    """Resolve shard records into exact totals.
+KEYS = ("entry", "exit", "count", "digest", "dcap")
 
-    rec    : dict(entry, exit, count, digest, dcap) of this rank's shard, positions global.
-    fix_fn : fix_fn(old_entry, new_entry) -> dict(count, digest, dcap, exit) correction for
-             THIS rank's shard (exit None if unchanged); only called on the rank that owns it.
-    Returns dict(count, digest, dcap, exit, fixes, entries, counts) identical on every
-    rank; entries[r] / counts[r] are shard r's true chain entry and match count (a
-    rank whose entry moved re-scans from it to materialise its records).
+
+def resolve(recs, fix):
+    """Resolve per-shard chain records, left to right, into exact totals.
+
+    recs : list of dict(entry, exit, count, digest, dcap), one per shard in
+           stream order, positions global, each scanned speculatively from
+           its shard start (entry).
+    fix  : fix(r, old_entry, new_entry) -> dict(count, digest, dcap, exit) with
+           the correction for shard r re-entered at new_entry (exit None when
+           unchanged: the two chains met inside the shard).
+    Shard r's speculative entry is right iff exit(r-1) == entry(r); otherwise r
+    is re-entered at exit(r-1), and a changed exit carries the correction on
+    to r+1.  Returns dict(count, digest, dcap, exit, fixes, entries, counts).
+    This is the whole protocol; stitch() runs it over torch.distributed and the
+    tests drive it in-process as well.
     """
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    keys = ("entry", "exit", "count", "digest", "dcap")
-    mine = torch.tensor([_to_i64(rec[k]) for k in keys], dtype=torch.int64, device=device)
-    allrec = [torch.empty_like(mine) for _ in range(world)]
-    dist.all_gather(allrec, mine, group=group)
-    recs = [dict(zip(keys, (_to_u64(int(x)) for x in t.cpu().tolist()))) for t in allrec]
+    recs = [dict(r) for r in recs]
     fixes = 0
     prev_exit = recs[0]["exit"]
-    for r in range(1, world):
+    for r in range(1, len(recs)):
         if prev_exit != recs[r]["entry"]:
             fixes += 1
-            buf = torch.zeros(5, dtype=torch.int64, device=device)
-            if rank == r:
-                d = fix_fn(recs[r]["entry"], prev_exit)
-                ex = d.get("exit")
-                buf = torch.tensor([_to_i64(d["count"]), _to_i64(d["digest"]), _to_i64(d["dcap"]),
-                                    1 if ex is not None else 0, _to_i64(ex if ex is not None else 0)],
-                                   dtype=torch.int64, device=device)
-            dist.broadcast(buf, src=r, group=group)
-            v = [_to_u64(int(x)) for x in buf.cpu().tolist()]
-            recs[r]["count"] = (recs[r]["count"] + v[0]) & MASK64
-            recs[r]["digest"] = (recs[r]["digest"] + v[1]) & MASK64
-            recs[r]["dcap"] = (recs[r]["dcap"] + v[2]) & MASK64
+            d = fix(r, recs[r]["entry"], prev_exit)
+            recs[r]["count"] = (recs[r]["count"] + d["count"]) & MASK64
+            recs[r]["digest"] = (recs[r]["digest"] + d["digest"]) & MASK64
+            recs[r]["dcap"] = (recs[r]["dcap"] + d["dcap"]) & MASK64
             recs[r]["entry"] = prev_exit
-            if v[3]:
-                recs[r]["exit"] = v[4]
+            if d.get("exit") is not None:
+                recs[r]["exit"] = d["exit"]
         prev_exit = recs[r]["exit"]
     out = dict(count=0, digest=0, dcap=0, exit=prev_exit, fixes=fixes,
                entries=[r["entry"] for r in recs], counts=[r["count"] for r in recs])
@@ -78,6 +72,40 @@ def stitch(rec, fix_fn, device="cpu", group=None):
         out["digest"] = (out["digest"] + r["digest"]) & MASK64
         out["dcap"] = (out["dcap"] + r["dcap"]) & MASK64
     return out
+
+
+def stitch(rec, fix_fn, device="cpu", group=None):
+    """Resolve shard records into exact totals across ranks (one all_gather).
+
+    rec    : dict(entry, exit, count, digest, dcap) of this rank's shard, positions global.
+    fix_fn : fix_fn(old_entry, new_entry) -> dict(count, digest, dcap, exit) correction for
+             THIS rank's shard (exit None if unchanged); only called on the rank that owns it,
+             whose result is broadcast to the others.
+    Returns resolve()'s dict, identical on every rank; entries[r] / counts[r] are
+    shard r's true chain entry and match count (a rank whose entry moved re-scans
+    from it to materialise its records).
+    """
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    mine = torch.tensor([_to_i64(rec[k]) for k in KEYS], dtype=torch.int64, device=device)
+    allrec = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allrec, mine, group=group)
+    recs = [dict(zip(KEYS, (_to_u64(int(x)) for x in t.cpu().tolist()))) for t in allrec]
+
+    def fix(r, old, new):
+        buf = torch.zeros(5, dtype=torch.int64, device=device)
+        if rank == r:
+            d = fix_fn(old, new)
+            ex = d.get("exit")
+            buf = torch.tensor([_to_i64(d["count"]), _to_i64(d["digest"]), _to_i64(d["dcap"]),
+                                1 if ex is not None else 0, _to_i64(ex if ex is not None else 0)],
+                               dtype=torch.int64, device=device)
+        # owner ranks r are visited in the same order on every rank
+        dist.broadcast(buf, src=r, group=group)
+        v = [_to_u64(int(x)) for x in buf.cpu().tolist()]
+        return dict(count=v[0], digest=v[1], dcap=v[2], exit=v[4] if v[3] else None)
+
+    return resolve(recs, fix)
 
 
 def shard_bounds(total, world, rank, halo):

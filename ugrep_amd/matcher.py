@@ -247,6 +247,7 @@ class Matcher:
         """AbstractMatcher::buffer(base, size): whole input, cursor at 0 (absmatcher.h:542-591)."""
         self._data = data
         self._cur = 0
+        self._from = 0
         self._res = None
         self._i = 0
         self._first = 0
@@ -254,14 +255,26 @@ class Matcher:
         self._cap = 0
         return self
 
+    def _inside_match(self):
+        """The cursor lies strictly inside a record of the current scan."""
+        r, i = self._res, max(self._i - 1, 0)
+        while i < r.count and int(r.start[i]) + int(r.length[i]) <= self._cur:
+            i += 1
+        return i < r.count and int(r.start[i]) < self._cur
+
     def find(self):
-        """Next match at or after the cursor; returns its accept index, 0 when exhausted."""
-        if self._res is None:
+        """Next match at or after the cursor; returns its accept index, 0 when exhausted.
+
+        The FIND chain passes through every position that is not strictly
+        inside one of its matches, so after skip_to() the remaining records
+        stay exact unless the cursor landed inside a match; then (as the C++
+        adapter, integration/reflex_gpu_matcher.h) the scan is re-run from the
+        cursor."""
+        if self._res is None or self._cur < self._from or self._inside_match():
             self._res = find_all(self.pattern, self._data, self._cur, offsets=True)
+            self._from = self._cur
             self._i = 0
         r = self._res
-        # re-synchronise after skip(): drop records before the cursor (exact for
-        # patterns whose matches cannot contain '\n', SURVEY.md §8b)
         while self._i < r.count and int(r.start[self._i]) < self._cur:
             self._i += 1
         if self._i >= r.count:
