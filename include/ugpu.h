@@ -77,9 +77,14 @@ typedef struct ugpu_totals
   uint64_t dcap;
   uint64_t entry;  /* chain position entering the range (== lo for a fresh scan) */
   uint64_t exit;   /* first chain position >= hi: where the search resumes after the range */
-  uint32_t flags;  /* bit0: a walk hit the readable end of a non-final shard (UGPU_HALO) */
+  uint32_t flags;  /* bit0: a walk hit the readable end of a non-final shard (UGPU_HALO);
+                      bit3 (UGPU_TOT_FOREST): the speculative stitch did not converge (FIND chains
+                      that never resynchronise, e.g. \D\D over text without digits) and the range
+                      was resolved exactly by the forest FIND (ugrep_amd/csrc/forest.hip) */
   uint32_t fix_rounds;
 } ugpu_totals;
+
+#define UGPU_TOT_FOREST 8u
 
 /* Library-owned match list for ugpu_find_all. */
 typedef struct ugpu_result

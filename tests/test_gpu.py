@@ -231,24 +231,88 @@ def test_nonsynchronising_chain(U, pats):
         os.environ.pop("UGPU_MAX_GRID", None)
 
 
+def _forest_totals(U, pat, dev, lo=0, bias=0):
+    """Scanner totals of dev[lo:] (bias added to starts) and whether the forest FIND resolved them."""
+    n = dev.numel()
+    sc = U.Scanner(pat)
+    sc.scan(dev.data_ptr(), lo, n, n, True, bias, _stream())
+    t = sc.totals()
+    return (t.count, t.digest, t.dcap), t.exit, bool(t.flags & 8)
+
+
 def test_nonsynchronising_unicode_phases(U):
     """`\\D\\D` over the word corpus (no digits, multi-byte UTF-8): FIND phases that
-    never meet, on dense_kernel + fix_kernel.  Count and full match lists equal the
-    oracle's.  Sizes stay small: this is DESIGN.md section 7's known slow case
-    (fix_kernel merges whole records, 0.3 s at 256 KiB)."""
+    never meet.  The speculative stitch gives up and the forest FIND (forest.hip)
+    resolves the range; counts and full match lists equal the oracle's, from
+    nonzero starts and with a start bias too."""
     from oracle_lib import OracleDfa, gen
     opc = U.compile_regex(r"\D\D")
     pat = U.Pattern(opc)
     assert pat.info()["kernel"] == 1
     o = OracleDfa(opc)
-    for kib in (64, 256):
+    for kib in (64, 1024, 16384):
         host = gen(4, 11, 0, kib << 10)
         dev = torch.from_numpy(host).to("cuda")
-        r = U.find_all(pat, dev, offsets=False)
-        assert (r.count, r.digest, r.dcap) == o.find(host)[:3], kib
-        if kib == 64:
-            r = U.find_all(pat, dev, offsets=True)
-            assert r.triples() == o.find(host, want_list=True)[3]
+        r = U.find_all(pat, dev, offsets=kib <= 1024)
+        want = o.find(host, want_list=kib <= 1024)
+        assert (r.count, r.digest, r.dcap) == want[:3], kib
+        if kib <= 1024:
+            assert r.triples() == want[3]
+        tot, _, forest = _forest_totals(U, pat, dev)
+        assert forest and tot == want[:3], kib
+        if kib == 1024:
+            for lo, bias in ((1, 0), (4097, 1 << 40), (777777, 5)):
+                tot, _, _ = _forest_totals(U, pat, dev, lo, bias)
+                assert tot == o.find(host, start=lo, bias=bias)[:3], (lo, bias)
+
+
+def test_forest_on_resynchronising_tables(U, pats):
+    """With a tiny stitch budget (UGPU_FIX_BUDGET / UGPU_MERGE_BUDGET) every scan
+    falls to the forest FIND, also for tables whose chains do resynchronise:
+    counts and match lists equal the oracle's on C2/C3/C4 corpora, sparse and
+    dense tables, class tables, several accept indices."""
+    from oracle_lib import OracleDfa, gen
+    os.environ["UGPU_FIX_BUDGET"] = "1"
+    os.environ["UGPU_MERGE_BUDGET"] = "1"
+    try:
+        for pname, kind, n in (("c2_foobarbaz", 1, 3 << 20), ("c3_ident", 3, (1 << 20) + 3),
+                               ("c4_word", 4, 2 << 20), ("s_plus", 4, 1 << 20), ("aa", 1, 1 << 20)):
+            host = gen(kind, 21, 0, n)
+            dev = torch.from_numpy(host).to("cuda")
+            o = OracleDfa(pats[pname].opc)
+            cnt, dg, dc, lst = o.find(host, want_list=True)
+            tot, _, forest = _forest_totals(U, pats[pname], dev)
+            assert tot == (cnt, dg, dc), pname
+            if not forest:  # (sparse/xi/xg scans whose records needed no merge at all)
+                continue
+            r = U.find_all(pats[pname], dev, offsets=True)
+            assert r.triples() == lst, pname
+    finally:
+        os.environ.pop("UGPU_FIX_BUDGET", None)
+        os.environ.pop("UGPU_MERGE_BUDGET", None)
+
+
+def test_forest_shard_chain_fix(U, pats):
+    """ugpu_chain_fix on chains that never meet ('aa' over a long run of a, cut at
+    odd and even offsets): the forest FIND gives the exact shard delta."""
+    from oracle_lib import OracleDfa
+    n = (6 << 20) + 1
+    host = np.full(n, ord("a"), np.uint8)
+    host[0] = ord("b")
+    t = _dev(host)
+    o = OracleDfa(pats["aa"].opc)
+    want = o.find(host)[:3]
+    for cut in (n // 2, n // 2 + 1, n - 4097):
+        a, b = U.Scanner(pats["aa"]), U.Scanner(pats["aa"])
+        a.scan(t.data_ptr(), 0, cut, n, True, 0, _stream())
+        ta = a.totals()
+        b.scan(t.data_ptr(), cut, n, n, True, 0, _stream())
+        tb = b.totals()
+        cnt, dg, dc = ta.count + tb.count, ta.digest + tb.digest, ta.dcap + tb.dcap
+        if ta.exit != cut:
+            d = b.chain_fix(t.data_ptr(), cut, n, n, True, 0, cut, ta.exit, _stream())
+            cnt, dg, dc = cnt + d.count, dg + d.digest, dc + d.dcap
+        assert (cnt % (1 << 64), dg % (1 << 64), dc % (1 << 64)) == want, cut
 
 
 def test_offsets_at_scale(U, pats):
@@ -276,25 +340,27 @@ def test_start_offset(U, pats):
         assert r.triples() == o[3]
 
 
-def test_stitch_budget_falls_back(U):
-    """A chain that never resynchronises under a small stitch budget
-    (UGPU_FIX_BUDGET) is reported as UGPU_UNSUPPORTED, so the caller keeps the
-    CPU matcher, instead of walking whole records serially for hours
-    (fix_kernel's round budget).  With the default budget the same
-    input is bit-exact."""
-    from oracle_lib import OracleDfa, gen
-    opc = U.compile_regex(r"\D\D")
-    pat = U.Pattern(opc)
-    host = gen(4, 11, 0, 256 << 10)
-    dev = torch.from_numpy(host).to("cuda")
-    os.environ["UGPU_FIX_BUDGET"] = "4096"
+def test_forest_word_option(U):
+    """Option W (wfind_kernel) on chains that never meet: the lane stitch gives up
+    and the forest FIND runs the exact W walks; counts and lists equal the
+    oracle's orc_find_w."""
+    from oracle_lib import OracleDfa
+    opc = U.compile_regex("[a-z_0-9\u00e9\u65e5\u672c]{2}")
+    pat = U.Pattern(opc, word=True)
+    words = [b"ab", b"abc", b"de", b"x", b"\xc3\xa9t", b"\xe6\x97\xa5\xe6\x9c\xac", b"_q", b"12"]
+    rng = np.random.default_rng(3)
+    host = np.frombuffer(b" ".join(words[i] for i in rng.integers(0, len(words), 300000)), np.uint8)
+    dev = torch.from_numpy(host.copy()).to("cuda")
+    want = OracleDfa(opc).find_w(host, want_list=True)
+    os.environ["UGPU_FIX_BUDGET"] = "1"
+    os.environ["UGPU_MERGE_BUDGET"] = "1"
     try:
-        with pytest.raises(U.Unsupported):
-            U.find_all(pat, dev, offsets=False)
+        r = U.find_all(pat, dev, offsets=True)
     finally:
         os.environ.pop("UGPU_FIX_BUDGET", None)
-    r = U.find_all(pat, dev, offsets=False)
-    assert (r.count, r.digest, r.dcap) == OracleDfa(opc).find(host)[:3]
+        os.environ.pop("UGPU_MERGE_BUDGET", None)
+    assert (r.count, r.digest, r.dcap) == want[:3]
+    assert r.triples() == want[3]
 
 
 def test_matcher_skip_inside_match_rescans(U, pats):

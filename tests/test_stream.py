@@ -88,3 +88,23 @@ def test_stream_count_mode_and_settled(U, patterns):
     assert st.settled() == 200000
     with pytest.raises(U.UgpuError):
         st.feed(b"x")
+
+
+def test_stream_forest_fallback(U, patterns):
+    """Streams whose feeds fall to the forest FIND (a tiny stitch budget forces it;
+    ragged last blocks, non-final feeds with walks open at the readable end) keep
+    the oracle's whole-input result, record by record."""
+    import os
+    from oracle_lib import gen
+    os.environ["UGPU_FIX_BUDGET"] = "1"
+    os.environ["UGPU_MERGE_BUDGET"] = "1"
+    try:
+        for pname, kind in (("c3_ident", 3), ("c4_word", 4), ("aa", 1)):
+            data = gen(kind, 13, 0, (1 << 20) + 777)
+            pat = U.Pattern(patterns[pname]["opc"])
+            want = _whole(U, pat, data)
+            for sizes, keep in (([12345, 70001], 4096), ([300000], 64)):
+                assert _stream(U, pat, data, sizes, keep) == want, (pname, keep)
+    finally:
+        os.environ.pop("UGPU_FIX_BUDGET", None)
+        os.environ.pop("UGPU_MERGE_BUDGET", None)

@@ -34,6 +34,7 @@ namespace ugpu {
 namespace {
 
 constexpr int kDHalo = 64;  // bytes staged past the tile end (walks crossing the tile end)
+constexpr uint32_t kLaneRounds = 16;  // in-wave fix-up rounds before UGPU_FLAG_BUDGET
 
 template <int S>
 struct DGeo {
@@ -472,6 +473,9 @@ __global__ __launch_bounds__((FMT == 0 ? kDWavesByte : kDWavesClass) * 64) void 
     for (int k = 0; k < G::kLoads; ++k) c[k] = dload16(r0, 16u * lane + 1024u * k);
   }
   for (uint32_t i = 0; i < n; ++i) {
+    // a wave that met chains which do not resynchronise stopped the scan: the
+    // host redoes the range with the forest FIND, so the rest is wasted work
+    if (__hip_atomic_load(P.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & UGPU_FLAG_BUDGET) break;
     // stage tile i, then start loading tile i+1 (empty resource past the range)
     dwave_sync();  // every read of the previous tile is done
 #pragma unroll
@@ -533,13 +537,23 @@ __global__ __launch_bounds__((FMT == 0 ? kDWavesByte : kDWavesClass) * 64) void 
       ex = L.p;
     }
     if (hit_end && !w.eof) ovf = 1;  // a live walk ran into the end of the readable bytes
-    // fix-up rounds: lane l's true entry is lane l-1's exit
-    for (;;) {
+    // fix-up rounds: lane l's true entry is lane l-1's exit.  Chains that do
+    // not resynchronise move a wrong phase one lane per round: past
+    // kLaneRounds the scan gives up (UGPU_FLAG_BUDGET) and the host resolves
+    // the range with the forest FIND (forest.hip)
+    // (only rounds that re-walk a segment count: an entry past a lane's
+    // segment, e.g. the empty segments after hi, just passes through)
+    for (uint32_t round = 0;;) {
       if (P.ablate == 4) break;  // benchmarking only: no fix-up (results are not matches)
       const uint32_t pv = dprev_lane(ex);
       const uint32_t nx = lane == 0 ? x0 : pv;
       const bool ch = nx != ent;
       if (!__ballot(ch)) break;
+      if (__ballot(ch && ent < b) && ++round > kLaneRounds) {
+        wover |= 2u;
+        if (lane == 0) atomicOr(P.flags, UGPU_FLAG_BUDGET);
+        break;
+      }
       bool done = false;
       if constexpr (XT) {
         const bool skip = ch && nx >= b;  // the true chain skips the whole segment
@@ -564,6 +578,7 @@ __global__ __launch_bounds__((FMT == 0 ? kDWavesByte : kDWavesClass) * 64) void 
       }
       if (ch) ent = nx;
     }
+    if (wover & 2u) break;
     const uint32_t ex63 = (uint32_t)__builtin_amdgcn_readlane(ex, 63);
     x = (x >= tend) ? x : ts + ex63;
 
@@ -591,7 +606,8 @@ __global__ __launch_bounds__((FMT == 0 ? kDWavesByte : kDWavesClass) * 64) void 
   if (x < whi) x = whi;  // (exits are >= the range end)
 
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
-  if (wover) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+  if (wover & 1u) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+  if (wover & 2u) atomicOr(P.flags, UGPU_FLAG_BUDGET);
   if constexpr (!WRITE) {
     const uint64_t c0 = wave_sum(acc.cnt), d = wave_sum(acc.dg), dc = wave_sum(acc.dc);
     if (lane == 0) {

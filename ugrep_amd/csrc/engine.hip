@@ -72,6 +72,15 @@ struct ugpu_scanner {
   ScanParams last{};
   uint64_t off = 0;  // alignment shift of the last scan
   bool have_scan = false;
+  // forest FIND (forest.hip): scratch, allocated on first use, and whether the
+  // last scan was resolved by it (its OFFSETS pass then runs the forest too)
+  bool forest = false;
+  uint64_t f_cap = 0;  // chain positions the scratch covers
+  uint32_t* d_fex = nullptr;
+  uint64_t* d_fvar = nullptr;  // entry, run[3]
+  uint64_t* d_fent = nullptr;
+  uint64_t* d_fsum = nullptr;
+  uint64_t* d_fbase = nullptr;
 };
 
 namespace {
@@ -99,20 +108,36 @@ int hip_fail(hipError_t e, const char* what)
     if (_e != hipSuccess) return hip_fail(_e, #expr); \
   } while (0)
 
+// UGPU_TRACE=1: one stderr line per pipeline step (debugging)
+bool trace_on()
+{
+  static const bool on = std::getenv("UGPU_TRACE") && std::getenv("UGPU_TRACE")[0] == '1';
+  return on;
+}
+#define UGPU_TRACE(...)                  \
+  do {                                   \
+    if (trace_on()) {                    \
+      std::fprintf(stderr, "[ugpu] " __VA_ARGS__); \
+      std::fflush(stderr);               \
+    }                                    \
+  } while (0)
+
 uint64_t env_u64(const char* name, uint64_t dflt)
 {
   const char* v = std::getenv(name);
   return v && *v ? std::strtoull(v, nullptr, 0) : dflt;
 }
 
-// fix_kernel rounds allowed for a geometry: at most ~16 MiB of serial re-walks
-// in total (UGPU_FIX_BUDGET), at least 4 rounds (normal tables need 0-1)
+// fix_kernel rounds allowed for a geometry before it gives up and the forest
+// FIND (forest.hip) resolves the range: resynchronising tables need 0-1 rounds
+// (more only for matches spanning several records), each round walks serially,
+// so about 256 KiB of re-walks in total (UGPU_FIX_BUDGET), 4 to 16 rounds
 uint32_t fix_rounds_for(const ScanParams& P)
 {
   const uint64_t rec = P.tpb * P.unit ? P.tpb * P.unit : 1;
-  uint64_t r = env_u64("UGPU_FIX_BUDGET", 16ull << 20) / rec;
+  uint64_t r = env_u64("UGPU_FIX_BUDGET", 256ull << 10) / rec;
   if (r < 4) r = 4;
-  if (r > 1u << 20) r = 1u << 20;
+  if (r > 16) r = 16;
   return (uint32_t)r;
 }
 
@@ -134,7 +159,10 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.cap1 = d->t.cap1;
   P.wtab = d->d_wtab;
   P.nwtab = d->nwtab;
-  P.merge_budget = env_u64("UGPU_MERGE_BUDGET", 1ull << 20);
+  // chain bytes one stitch merge may cross before the chains count as not
+  // resynchronising (two chains of a resynchronising table meet within a match
+  // or two; longer merges go to the forest FIND)
+  P.merge_budget = env_u64("UGPU_MERGE_BUDGET", 4096);
   for (int i = 0; i < 5; ++i)
     P.ft[i] = (uint32_t)d->t.ft[4 * i] | ((uint32_t)d->t.ft[4 * i + 1] << 8) | ((uint32_t)d->t.ft[4 * i + 2] << 16) |
               ((uint32_t)d->t.ft[4 * i + 3] << 24);
@@ -205,6 +233,57 @@ bool is_device_ptr(const void* p)
     return false;
   }
   return a.type == hipMemoryTypeDevice;
+}
+
+void forest_free(ugpu_scanner* s)
+{
+  (void)hipFree(s->d_fex);
+  (void)hipFree(s->d_fvar);
+  (void)hipFree(s->d_fent);
+  (void)hipFree(s->d_fsum);
+  (void)hipFree(s->d_fbase);
+  s->d_fex = nullptr;
+  s->d_fvar = s->d_fent = s->d_fsum = s->d_fbase = nullptr;
+  s->f_cap = 0;
+}
+
+// Forest FIND over chain positions [entry, P.hi) of P's buffer (COUNT, or
+// WRITE into P.out_*), synchronously; totals and flags land in h_tot / h_flags.
+int forest_run(ugpu_scanner* s, ScanParams P, uint64_t entry, bool write, hipStream_t st)
+{
+  const uint64_t fb = forest_block();
+  const uint64_t range = P.hi > entry ? P.hi - entry : 0;
+  uint64_t pos = range < kFChunk ? range : kFChunk;
+  pos = (pos + fb - 1) / fb * fb;
+  if (pos == 0) pos = fb;
+  if (pos > s->f_cap) {
+    forest_free(s);
+    const uint64_t nb = pos / fb;
+    hipError_t e;
+    if ((e = hipMalloc(&s->d_fex, pos * 4)) != hipSuccess || (e = hipMalloc(&s->d_fvar, 4 * 8)) != hipSuccess ||
+        (e = hipMalloc(&s->d_fent, nb * 8)) != hipSuccess || (e = hipMalloc(&s->d_fsum, nb * 24)) != hipSuccess ||
+        (e = hipMalloc(&s->d_fbase, nb * 8)) != hipSuccess) {
+      forest_free(s);
+      return hip_fail(e, "forest scratch");
+    }
+    s->f_cap = pos;
+  }
+  UGPU_TRACE("forest entry %llu hi %llu rend %llu write %d\n", (unsigned long long)entry,
+             (unsigned long long)P.hi, (unsigned long long)P.rend, (int)write);
+  ForestArgs A{};
+  A.ex = s->d_fex;
+  A.entry = s->d_fvar;
+  A.run = s->d_fvar + 1;
+  A.bentry = s->d_fent;
+  A.bsum = s->d_fsum;
+  A.bbase = s->d_fbase;
+  P.flags = s->d_flags;
+  HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
+  HIP_TRY(launch_forest(P, s->dfa->t.format, A, entry, write, s->d_tot, st));
+  HIP_TRY(hipMemcpyAsync(s->h_tot, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return UGPU_OK;
 }
 
 }  // namespace
@@ -540,6 +619,7 @@ int ugpu_scanner_destroy(ugpu_scanner* s)
   (void)hipFree(s->d_flags);
   (void)hipHostFree(s->h_tot);
   (void)hipHostFree(s->h_flags);
+  forest_free(s);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   delete s;
@@ -563,6 +643,9 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   P.totals = s->d_tot;
   P.entries_out = s->d_entries;
   P.out_base_out = s->d_obase;
+  UGPU_TRACE("scan lo %llu hi %llu rend %llu eof %d grid %u xi %d xg %d sparse %d word %d\n", (unsigned long long)P.lo,
+             (unsigned long long)P.hi, (unsigned long long)P.rend, at_eof, P.grid, (int)s->xi, (int)s->xg,
+             (int)s->sparse, (int)s->word);
   HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
   HIP_TRY(hipEventRecord(s->ev0, st));
   HIP_TRY(launch_main(s, P, false, st, s->xi || s->xg));
@@ -580,6 +663,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   s->last_args[4] = bias;
   s->stream = st;
   s->have_scan = true;
+  s->forest = false;
   return UGPU_OK;
 }
 
@@ -588,13 +672,22 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
   if (!s || !out) return fail(UGPU_INVAL, "NULL argument");
   if (!s->have_scan) return fail(UGPU_INVAL, "no scan issued");
   HIP_TRY(hipStreamSynchronize(s->stream));
+  UGPU_TRACE("totals flags %u count %llu rounds %u\n", *s->h_flags, (unsigned long long)s->h_tot->count,
+             s->h_tot->rounds);
+  if ((*s->h_flags & UGPU_FLAG_BUDGET) && !s->forest) {
+    // the speculative stitch gave up (chains that do not resynchronise):
+    // resolve the same range exactly with the forest FIND
+    const int rc = forest_run(s, s->last, s->last.lo, false, s->stream);
+    if (rc) return rc;
+    s->forest = true;
+  }
   const DevTotals& t = *s->h_tot;
   out->count = t.count;
   out->digest = t.digest;
   out->dcap = t.dcap;
   out->entry = t.entry - s->off;
   out->exit = t.exit - s->off;
-  out->flags = *s->h_flags;
+  out->flags = *s->h_flags | (s->forest ? UGPU_TOT_FOREST : 0u);
   out->fix_rounds = t.rounds;
   if (out->flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
   if (out->flags & UGPU_FLAG_BUDGET) return fail(UGPU_UNSUPPORTED, kBudgetMsg);
@@ -614,8 +707,10 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
 {
   if (!s || !s->have_scan) return fail(UGPU_INVAL, "no scan issued");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipStreamSynchronize(s->stream));
   ScanParams P = s->last;
-  if (s->last_xi) {
+  bool forest = s->forest || (*s->h_flags & UGPU_FLAG_BUDGET);
+  if (s->last_xi && !forest) {
     // xi_kernel has no record-writing pass: redo the chain records with the
     // dense kernel's geometry (COUNT + fix), then its WRITE pass
     P = ScanParams{};
@@ -629,8 +724,12 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
     P.totals = s->d_tot;
     P.entries_out = s->d_entries;
     P.out_base_out = s->d_obase;
+    HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
     HIP_TRY(launch_main(s, P, false, st));
     HIP_TRY(launch_fix(P, s->dfa->t.format, st));
+    HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    forest = (*s->h_flags & UGPU_FLAG_BUDGET) != 0;
   }
   P.entries = s->d_entries;
   P.out_base = s->d_obase;
@@ -638,10 +737,18 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
   P.out_len = d_len;
   P.out_cap = d_cap;
   P.out_capacity = capacity;
-  HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
-  HIP_TRY(launch_main(s, P, true, st));
-  HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  UGPU_TRACE("offsets forest %d capacity %llu\n", (int)forest, (unsigned long long)capacity);
+  if (!forest) {
+    HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
+    HIP_TRY(launch_main(s, P, true, st));
+    HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    forest = (*s->h_flags & UGPU_FLAG_BUDGET) != 0;  // a lane stitch ran past its round budget
+  }
+  if (forest) {
+    const int rc = forest_run(s, P, P.lo, true, st);
+    if (rc) return rc;
+  }
   if (*s->h_flags & UGPU_FLAG_CAPACITY) return fail(UGPU_CAPACITY, "output capacity exceeded");
   if (*s->h_flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
   return UGPU_OK;
@@ -664,6 +771,23 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
   DevTotals t;
   HIP_TRY(hipMemcpyAsync(&t, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  if (t.flags & UGPU_FLAG_BUDGET) {
+    // the two chains do not meet within the merge budget: the exact chains from
+    // both entries by the forest FIND, and their difference
+    int rc = forest_run(s, P, new_entry + off, false, st);
+    if (rc) return rc;
+    const DevTotals tn = *s->h_tot;
+    const uint32_t fn = *s->h_flags;
+    rc = forest_run(s, P, old_entry + off, false, st);
+    if (rc) return rc;
+    const DevTotals to = *s->h_tot;
+    t.count = tn.count - to.count;
+    t.digest = tn.digest - to.digest;
+    t.dcap = tn.dcap - to.dcap;
+    t.exit = tn.exit == to.exit ? ~0ull : tn.exit;
+    t.flags = (fn | *s->h_flags) & UGPU_FLAG_HALO;
+    t.rounds = 0;
+  }
   delta->count = t.count;
   delta->digest = t.digest;
   delta->dcap = t.dcap;
@@ -672,7 +796,6 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
   delta->flags = t.flags;
   delta->fix_rounds = t.rounds;
   if (t.flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
-  if (t.flags & UGPU_FLAG_BUDGET) return fail(UGPU_UNSUPPORTED, kBudgetMsg);
   return UGPU_OK;
 }
 

@@ -33,6 +33,9 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
   w.nwtab = P.nwtab;
   w.bob = P.bob;
   uint32_t ovf = 0, over = 0;
+  // the scan kernel already gave up on these chains (UGPU_FLAG_BUDGET): the host
+  // resolves the range with the forest FIND, nothing to stitch
+  if (__hip_atomic_load(P.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & UGPU_FLAG_BUDGET) return;
 
   uint64_t cnt[PER], dg[PER], dc[PER];
 #pragma unroll

@@ -119,6 +119,23 @@ struct ScanParams {
   uint64_t merge_budget;
 };
 
+// Forest FIND (forest.hip): exact for every table, no resynchronisation
+// assumed; runs when a speculative stitch exceeds its budget.
+struct ForestArgs {
+  uint64_t c_lo, c_hi;  // chunk of chain positions (base coordinates)
+  uint32_t nblk;        // blocks of forest_block() positions in the chunk
+  uint32_t* ex;         // per chunk position: its block exit - block end
+  uint64_t* entry;      // device: chain entry of the chunk (in) / its exit (out)
+  uint64_t* run;        // device: count, digest, dcap of the chunks so far
+  uint64_t* bentry;     // per block: exact chain entry
+  uint64_t* bsum;       // per block: count, digest, dcap
+  uint64_t* bbase;      // per block: first output index
+};
+constexpr uint64_t kFChunk = 64ull << 20;  // positions per forest chunk (4 B of exits each)
+hipError_t launch_forest(const ScanParams& P, uint32_t format, const ForestArgs& A, uint64_t entry, bool write,
+                         DevTotals* tot, hipStream_t stream);
+uint64_t forest_block();
+
 // launchers (scan_kernels.hip, gen.hip)
 hipError_t launch_fix(const ScanParams& P, uint32_t format, hipStream_t stream);
 hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_entry, uint64_t new_entry,

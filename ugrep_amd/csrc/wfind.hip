@@ -91,11 +91,17 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
   uint64_t p = ent;
   while (p < shi) p = chain_step<FMT, CountEm, true>(T, w, C, p, acc, +1, ovf);
   uint64_t exi = p;  // first chain position >= shi (the entry itself when it lies beyond)
-  // lane stitch rounds
-  for (int round = 0; round < 64; ++round) {
+  // lane stitch rounds (a wrong entry moves one lane per round; chains that do
+  // not resynchronise give up after 24 rounds: UGPU_FLAG_BUDGET, and the host
+  // resolves the range with the forest FIND, forest.hip)
+  for (int round = 0;;) {
     uint64_t nx = __shfl_up(exi, 1, 64);
     const bool ch = lane > 0 && nx != ent;
     if (!__ballot(ch)) break;
+    if (__ballot(ch && ent < shi) && ++round > 24) {
+      if (lane == 0) atomicOr(P.flags, UGPU_FLAG_BUDGET);
+      break;
+    }
     if (ch) {
       uint64_t ne;
       if (!merge<FMT, true>(T, w, C, ent, nx, shi, acc, ne, ovf)) exi = ne;
