@@ -266,6 +266,13 @@ int ugpu_gen(int kind, uint64_t seed, uint64_t off, uint8_t *dbuf, uint64_t len,
    message is in ugpu_compile_error(). */
 #define UGPU_RX_FIXED 1u /* -F: the pattern is a literal string (src/cnf.hpp:147-165) */
 #define UGPU_RX_ICASE 2u /* -i: ASCII letters and the reference's Unicode case pairs */
+/* The regex a reflex::Pattern holds (its public Pattern::operator[](0),
+   include/reflex/pattern.h:302): RE/flex syntax over bytes as produced by
+   Matcher::convert (lib/convert.cpp) -- Unicode classes, '.' and -i over
+   non-ASCII letters already expanded into byte sequences; inline (?i) (?s) (?m)
+   modifiers and (?i:...) scopes; \Q...\E.  The drop-in adapter builds its tables
+   from this, so it needs no access to Pattern's private opcode words. */
+#define UGPU_RX_REFLEX 4u
 int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, uint32_t *nop);
 void ugpu_opc_free(uint32_t *opc);
 const char *ugpu_compile_error(void);

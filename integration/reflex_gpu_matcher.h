@@ -1,33 +1,58 @@
 // reflex_gpu_matcher.h -- drop-in FIND matcher for ugrep: a reflex::Matcher
-// whose FIND over a fully buffered input is served by the MI355X engine
-// (include/ugpu.h).  This is the reference-side binding of INTEGRATION.md;
-// it includes the reference's <reflex/matcher.h>.
+// whose FIND is served by the MI355X engine (include/ugpu.h).  This is the
+// reference-side binding of INTEGRATION.md; it includes the reference's
+// <reflex/matcher.h> and uses only its public and protected interface.
+//
+// Drop-in: GpuMatcher(pattern, input, opt) has reflex::Matcher's constructor
+// (include/reflex/matcher.h, Matcher(const Pattern&, const Input&, const char*)),
+// so ugrep's construction site src/ugrep.cpp:8902
+//     new reflex::Matcher(Static::reflex_pattern, reflex::Input(), matcher_options.c_str())
+// becomes new reflex::GpuMatcher(...) and nothing else changes.  The device
+// tables are compiled from the regex the Pattern holds, read through its public
+// Pattern::operator[](0) (include/reflex/pattern.h:302) with
+// ugpu_compile(..., UGPU_RX_REFLEX): no private Pattern member is touched.
 //
 // Override point: virtual size_t Matcher::match(Method)
 // (include/reflex/matcher.h:1321, called by AbstractMatcher::find
 // include/reflex/absmatcher.h:276-280, :1401; ugrep's loop
 // `while (matcher->find())` src/ugrep.cpp:10544).
 //
-// FIND on a buffer() input (include/reflex/absmatcher.h:542-591: eof_ set,
-// own_ clear) runs one whole-buffer GPU scan from cur_ at the first call and
-// then pops one (start, len, accept) record per call, leaving the matcher in
-// the state lib/matcher.cpp:682-746 leaves after a hit:
+// Whole buffers (buffer(), absmatcher.h:542-591: eof_ set, own_ clear): one
+// GPU scan from cur_ at the first call, then one (start, len, accept) record
+// per call, leaving the matcher in the state lib/matcher.cpp:682-746 leaves
+// after a hit:
 //   txt_ = buf_ + start, len_ = len, cap_ = accept, cur_ = pos_ = start + len,
 //   got_ = buf_[cur_-1] (set_current, absmatcher.h:1571-1580)
 // and after exhaustion cap_ = len_ = 0, cur_ = pos_ = end_.
 //
+// Streamed input (input(): stdin, pipes, decompressed data, files ugrep does
+// not mmap, src/ugrep.cpp:3936-3944): the matcher keeps reading into its own
+// buffer with the reference's protocol (grow() + get(), absmatcher.h:1417-1593,
+// so buffer shifts, line counting and ugrep's flush handler behave as on the
+// CPU) and feeds the new bytes to a ugpu_stream in chunks of at least
+// UGPU_ADAPTER_CHUNK bytes; settled records come back with absolute offsets
+// (num_ + buffer position).
+//
 // Between finds the caller may move cur_ (skip('\n') for -c, --range, context
 // modes: src/ugrep.cpp:10583, :3989).  The FIND chain passes through every
 // position that is not strictly inside a match, so the remaining records are
-// exact whenever the new cur_ is not inside one; otherwise (and for a new
-// buffer) the scan is re-run from cur_.
+// exact whenever the new cur_ is not inside one; otherwise (and for new bytes
+// or a rewind) the scan restarts at cur_.
 //
-// Option W (ugrep -w, src/ugrep.cpp:8616-8618) is served from a second table
-// handle created with UGPU_PAT_WORD (wdfa).  Everything else -- SCAN/SPLIT/
-// MATCH, streaming input(), options A/N, tables the engine rejects (anchors,
-// \b, lookahead: UGPU_UNSUPPORTED) -- stays on the CPU matcher, unchanged.
+// Dispatch: inputs shorter than UGPU_ADAPTER_MIN_BYTES (default 1 MiB; a
+// stream counts when it ends before its first feed) stay on the CPU matcher: a
+// device round trip costs more than the reference's SIMD scan of a small
+// buffer (tools/bench_adapter.py).  UGPU_ADAPTER_STATS=1 prints each
+// matcher's GPU scan count to stderr when it is destroyed.  Everything else --
+// SCAN/SPLIT/MATCH, options A/N, option W on streams, tables the engine rejects
+// (anchors, \b, lookahead: UGPU_UNSUPPORTED) -- stays on the CPU matcher.
 #ifndef REFLEX_GPU_MATCHER_H
 #define REFLEX_GPU_MATCHER_H
+
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <string>
 
 #include <reflex/matcher.h>
 
@@ -37,25 +62,59 @@ namespace reflex {
 
 class GpuMatcher : public Matcher {
  public:
-  /// dfa: ugpu_dfa_create(pattern's opc_ words, 0) or NULL (CPU only); wdfa:
-  /// the same words with UGPU_PAT_WORD, used when opt has W; not owned.
-  GpuMatcher(const Pattern& pattern, const ugpu_dfa* dfa, const char* opt = NULL, const ugpu_dfa* wdfa = NULL)
-      : Matcher(pattern, Input(), opt), dfa_(opt_.W ? wdfa : dfa)
+  /// Drop-in constructor (reflex::Matcher's).  The device tables are compiled
+  /// from pattern[0] at the first FIND (and again after pattern() or a reset()
+  /// that changes option W).
+  GpuMatcher(const Pattern& pattern, const Input& input = Input(), const char* opt = NULL)
+      : Matcher(pattern, input, opt)
+  {
+    init_policy();
+  }
+  /// Clones (ugrep's worker threads, src/ugrep.cpp:4146, :9006) share the
+  /// device tables; per-input state starts empty.
+  GpuMatcher(const GpuMatcher& m)
+      : Matcher(m), tab_(m.tab_), tab_pat_(m.tab_pat_), tab_w_(m.tab_w_), min_bytes_(m.min_bytes_), chunk_(m.chunk_)
   {
   }
-  ~GpuMatcher() { ugpu_result_free(gres_); }
+  virtual GpuMatcher* clone() { return new GpuMatcher(*this); }
+  virtual ~GpuMatcher()
+  {
+    const char* st = std::getenv("UGPU_ADAPTER_STATS");
+    if (st != NULL && *st == '1')
+      std::fprintf(stderr, "[ugpu-adapter] scans=%zu\n", scans_);
+    ugpu_result_free(gres_);
+    ugpu_stream_destroy(gst_);
+  }
+  /// New input (input() calls this, absmatcher.h:533-540) or options.
+  virtual void reset(const char* opt = NULL)
+  {
+    Matcher::reset(opt);
+    drop_records();
+    ugpu_stream_destroy(gst_);
+    gst_ = NULL;
+    cpu_stream_ = false;
+  }
 
-  /// Number of whole-buffer GPU scans issued so far (for tests).
+  /// GPU scans (whole-buffer scans and stream feeds) issued so far (tests).
   size_t gpu_scans() const { return scans_; }
+  /// Whether the engine supports this pattern (builds the tables if needed).
+  bool gpu_ready() { return tables() != NULL; }
+  /// Smallest input sent to the GPU (0: every input).
+  void gpu_min_bytes(size_t n) { min_bytes_ = n; }
 
  protected:
   virtual size_t match(Method method)
   {
-    if (method != Const::FIND || dfa_ == NULL || own_ || !eof_ || opt_.A || opt_.N)
+    if (method != Const::FIND || opt_.A || opt_.N || tables() == NULL)
       return Matcher::match(method);
-    // buffer() and reset() are non-virtual and rewind cur_ without telling this
-    // class (absmatcher.h:542-591), and the caller may hand over new bytes at
-    // the same address and size (ugrep re-buffers one std::string per line,
+    if (own_)
+      return stream_match();
+    if (!eof_ || end_ < min_bytes_)
+      return Matcher::match(method);
+    reset_text();
+    // buffer() is non-virtual and rewinds cur_ without telling this class
+    // (absmatcher.h:542-591), and the caller may hand over new bytes at the
+    // same address and size (ugrep re-buffers one std::string per line,
     // src/ugrep.cpp:733-740): any cursor behind the one this class last left
     // means the records may be stale, so scan again
     if (gres_ == NULL || gbuf_ != buf_ || gend_ != end_ || cur_ < gcur_ || inside_match())
@@ -64,24 +123,74 @@ class GpuMatcher : public Matcher {
     while (gi_ < gres_->count && gres_->start[gi_] < cur_)
       ++gi_;
     if (gi_ >= gres_->count)
-    {
-      set_current(end_);
-      txt_ = buf_ + end_;
-      len_ = 0;
-      gcur_ = cur_;
-      return cap_ = 0;
-    }
+      return exhausted();
     const size_t start = static_cast<size_t>(gres_->start[gi_]);
-    txt_ = buf_ + start;
-    len_ = gres_->len[gi_];
-    cap_ = gres_->cap[gi_];
-    set_current(start + len_);
-    gcur_ = cur_;
+    const size_t len = gres_->len[gi_];
+    const size_t cap = gres_->cap[gi_];
     ++gi_;
-    return cap_;
+    return hit(start, len, cap);
   }
 
  private:
+  // device tables of (pattern, option W), shared with clones; NULL when the
+  // engine does not support the pattern
+  const ugpu_dfa* tables()
+  {
+    if (!tab_pat_ || tab_pat_ != pat_ || tab_w_ != opt_.W)
+    {
+      tab_.reset();
+      tab_pat_ = pat_;
+      tab_w_ = opt_.W;
+      if (pat_ != NULL)
+      {
+        const std::string rx = (*pat_)[0];
+        uint32_t* opc = NULL;
+        uint32_t nop = 0;
+        ugpu_dfa* d = NULL;
+        if (ugpu_compile(rx.data(), rx.size(), UGPU_RX_REFLEX, &opc, &nop) == UGPU_OK)
+        {
+          if (ugpu_dfa_create(opc, nop, opt_.W ? UGPU_PAT_WORD : 0u, &d) != UGPU_OK)
+            d = NULL;
+          ugpu_opc_free(opc);
+        }
+        if (d != NULL)
+          tab_.reset(d, ugpu_dfa_destroy);
+      }
+    }
+    return tab_.get();
+  }
+  void drop_records()
+  {
+    ugpu_result_free(gres_);
+    gres_ = NULL;
+    gi_ = 0;
+  }
+  size_t hit(size_t start, size_t len, size_t cap)
+  {
+    txt_ = buf_ + start;
+    len_ = len;
+    cap_ = cap;
+    set_current(start + len);
+    gcur_ = cur_;
+    return cap_;
+  }
+  size_t exhausted()
+  {
+    set_current(end_);
+    txt_ = buf_ + end_;
+    len_ = 0;
+    gcur_ = cur_;
+    return cap_ = 0;
+  }
+  void init_policy()
+  {
+    const char* e = std::getenv("UGPU_ADAPTER_MIN_BYTES");
+    min_bytes_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (1u << 20);
+    e = std::getenv("UGPU_ADAPTER_CHUNK");
+    chunk_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (8u << 20);
+    if (chunk_ == 0)
+      chunk_ = 1;
+  }
   // cur_ lies strictly inside a match of the current record set
   bool inside_match()
   {
@@ -92,26 +201,128 @@ class GpuMatcher : public Matcher {
   }
   bool rescan()
   {
-    ugpu_result_free(gres_);
-    gres_ = NULL;
-    if (ugpu_find_all(dfa_, reinterpret_cast<const uint8_t*>(buf_), end_, cur_, UGPU_MODE_OFFSETS, &gres_) != UGPU_OK)
-    {
-      dfa_ = NULL;  // engine unavailable for this input: stay on the CPU matcher
-      return false;
-    }
+    drop_records();
+    if (ugpu_find_all(tables(), reinterpret_cast<const uint8_t*>(buf_), end_, cur_, UGPU_MODE_OFFSETS, &gres_) !=
+        UGPU_OK)
+      return false;  // (this input stays on the CPU matcher)
     ++scans_;
     gbuf_ = buf_;
     gend_ = end_;
     gcur_ = cur_;
-    gi_ = 0;
     return true;
   }
 
-  const ugpu_dfa* dfa_;
+  // ---- streamed input
+  // Records of the current feed are absolute (sbase_ + record start); the
+  // stream was started at absolute offset sbase_ and has been fed up to sfed_.
+  size_t stream_match()
+  {
+    if (opt_.W || cpu_stream_)
+      return Matcher::match(Const::FIND);  // (W: at_wb at a window start needs the bytes before it)
+    reset_text();
+    txt_ = buf_ + cur_;  // bytes before the cursor may be shifted out (as lib/matcher.cpp:51)
+    const uint64_t at = static_cast<uint64_t>(num_ + cur_);
+    if (gst_ == NULL || at < gcur_abs_ || at > sfed_ || stream_inside(at))
+      if (!stream_restart(at))
+        return Matcher::match(Const::FIND);
+    for (;;)
+    {
+      while (gres_ != NULL && gi_ < gres_->count && sbase_ + gres_->start[gi_] < at)
+        ++gi_;
+      if (gres_ != NULL && gi_ < gres_->count)
+      {
+        const size_t start = static_cast<size_t>(sbase_ + gres_->start[gi_] - num_);
+        const size_t len = gres_->len[gi_], cap = gres_->cap[gi_];
+        ++gi_;
+        const size_t r = hit(start, len, cap);
+        gcur_abs_ = num_ + cur_;
+        return r;
+      }
+      if (sdone_)
+      {
+        const size_t r = exhausted();
+        gcur_abs_ = num_ + cur_;
+        return r;
+      }
+      // read until chunk_ unfed bytes are buffered or the input ends, then feed
+      while (!eof_ && num_ + end_ - sfed_ < chunk_)
+      {
+        if (end_ + blk_ + 1 >= max_)
+          (void)grow(chunk_ > Const::BLOCK ? chunk_ : Const::BLOCK);
+        const size_t n = get(buf_ + end_, blk_ > 0 ? blk_ : max_ - end_ - 1);
+        if (n == 0)
+          eof_ = !wrap();
+        else
+          end_ += n;
+      }
+      if (eof_ && scans_at_restart_ == scans_ && num_ + end_ - sbase_ < min_bytes_)
+      {
+        // a small input, all of it read before any feed: the CPU matcher is faster
+        cpu_stream_ = true;
+        ugpu_stream_destroy(gst_);
+        gst_ = NULL;
+        return Matcher::match(Const::FIND);
+      }
+      const size_t from = static_cast<size_t>(sfed_ - num_);
+      drop_records();
+      if (ugpu_stream_feed(gst_, reinterpret_cast<const uint8_t*>(buf_ + from), end_ - from, eof_ ? 1 : 0,
+                           UGPU_MODE_OFFSETS, &gres_) != UGPU_OK)
+      {
+        // engine unavailable for this input: the CPU matcher takes over at the cursor
+        cpu_stream_ = true;
+        ugpu_stream_destroy(gst_);
+        gst_ = NULL;
+        return Matcher::match(Const::FIND);
+      }
+      ++scans_;
+      sfed_ = num_ + end_;
+      sdone_ = eof_;
+    }
+  }
+  bool stream_inside(uint64_t at)
+  {
+    // the cursor moved strictly inside a pending match
+    if (gres_ == NULL)
+      return false;
+    for (size_t i = gi_ > 0 ? gi_ - 1 : 0; i < gres_->count; ++i)
+    {
+      const uint64_t s = sbase_ + gres_->start[i];
+      if (s >= at)
+        return false;
+      if (s + gres_->len[i] > at)
+        return true;
+    }
+    return false;
+  }
+  bool stream_restart(uint64_t at)
+  {
+    drop_records();
+    ugpu_stream_destroy(gst_);
+    gst_ = NULL;
+    if (ugpu_stream_create(tables(), 0, &gst_) != UGPU_OK)
+    {
+      cpu_stream_ = true;
+      return false;
+    }
+    sbase_ = at;
+    sfed_ = at;
+    sdone_ = false;
+    gcur_abs_ = at;
+    scans_at_restart_ = scans_;
+    return true;
+  }
+
+  std::shared_ptr<ugpu_dfa> tab_;
+  const Pattern* tab_pat_ = NULL;
+  bool tab_w_ = false;
   ugpu_result* gres_ = NULL;
   const char* gbuf_ = NULL;
   // gcur_: the cursor this class left behind (after the scan or the last hit)
-  size_t gend_ = 0, gcur_ = 0, gi_ = 0, scans_ = 0;
+  size_t gend_ = 0, gcur_ = 0, gi_ = 0, scans_ = 0, scans_at_restart_ = 0;
+  size_t min_bytes_ = 0, chunk_ = 0;
+  ugpu_stream* gst_ = NULL;
+  uint64_t sbase_ = 0, sfed_ = 0, gcur_abs_ = 0;
+  bool sdone_ = false, cpu_stream_ = false;
 };
 
 }  // namespace reflex

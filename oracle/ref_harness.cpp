@@ -188,7 +188,13 @@ int main(int argc, char **argv)
         (unsigned)pat.pin_, (unsigned)pat.npy_);
     for (size_t i = 0; i < pat.nop_; ++i)
       printf("%s%u", i ? ", " : "", (unsigned)pat.opc_[i]);
-    printf("]}\n");
+    // the regex the Pattern holds, through its public accessor (Pattern::operator[](0),
+    // include/reflex/pattern.h:302): what the drop-in adapter compiles (UGPU_RX_REFLEX)
+    const std::string whole = pat[0];
+    printf("], \"conv_hex\": \"");
+    for (size_t i = 0; i < whole.size(); ++i)
+      printf("%02x", (unsigned)(unsigned char)whole[i]);
+    printf("\"}\n");
     return 0;
   }
   if (argc < 5)

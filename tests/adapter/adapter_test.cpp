@@ -1,14 +1,20 @@
 // adapter_test.cpp -- TEST INFRASTRUCTURE (GPU box): the drop-in adapter
 // reflex::GpuMatcher (integration/reflex_gpu_matcher.h) against the reference
 // reflex::Matcher, both linked in one binary (the reference libreflex compiled
-// from its sources by oracle/Makefile into oracle/_ref/).
+// from its sources by oracle/Makefile into oracle/_ref/).  The adapter is built
+// exactly as ugrep would build it -- GpuMatcher(pattern, Input(), options) --
+// and compiles its tables from the Pattern's public operator[](0): this file
+// reads no private member.
 //
 // For every case line "MODE<TAB>REGEX<TAB>INPUT" of the spec file:
-//   1. plain loop   : while (m.find()) -> (first, size, accept) sequences equal
-//   2. -c loop      : while (m.find()) { ++n; m.skip('\n'); }  (src/ugrep.cpp:10583)
-//   3. skip(' ')    : cur_ moved to arbitrary positions between finds
-//   4. state        : after each hit lineno(), columno(), and after exhaustion
-//                     at_end() agree
+//   0. plain loop   : while (m.find()) -> (first, size, accept) sequences equal
+//   1. -c loop      : while (m.find()) { ++n; m.skip('\n'); }  (src/ugrep.cpp:10583)
+//   2. skip(' ')    : cur_ moved to arbitrary positions between finds
+//   3. re-buffer    : new bytes at the same address and size, second loop
+//   4. stream       : input() from a std::istream (GPU stream feeds of
+//                     UGPU_ADAPTER_CHUNK bytes, set small here), plain loop
+//   5. stream -c    : the same with skip('\n') after each hit
+//   in every loop lineno(), columno() after each hit and at_end() at the end agree
 // INPUT as in oracle/ref_harness.cpp (file:, gen:, hex:).  Prints one line
 // per case; exit status 1 if any case differs.
 #include <stdint.h>
@@ -18,14 +24,10 @@
 
 #include <algorithm>
 #include <fstream>
+#include <sstream>
 #include <string>
 #include <vector>
 
-// The opcode words are Pattern's private opc_ (reflex::Matcher is its friend);
-// INTEGRATION.md proposes a public accessor.  This test reads them directly.
-#define private public
-#include <reflex/pattern.h>
-#undef private
 #include <reflex/matcher.h>
 
 #include "gen.h"
@@ -108,13 +110,16 @@ static std::vector<Hit> run(M& m, std::vector<char>& buf, int kind, bool& at_end
   std::vector<Hit> out;
   for (int pass = 0; pass < (kind == 3 ? 2 : 1); ++pass)
   {
-    if (pass == 1 && buf.size() > 2)  // rotate the data bytes in place, keep the NUL
-      std::rotate(buf.begin(), buf.begin() + (buf.size() - 1) / 3, buf.end() - 1);
-    m.buffer(buf.data(), buf.size());
+    if (kind < 4)
+    {
+      if (pass == 1 && buf.size() > 2)  // rotate the data bytes in place, keep the NUL
+        std::rotate(buf.begin(), buf.begin() + (buf.size() - 1) / 3, buf.end() - 1);
+      m.buffer(buf.data(), buf.size());
+    }
     while (m.find())
     {
       out.push_back(Hit{m.first(), m.size(), m.accept(), m.lineno(), m.columno()});
-      if (kind == 1)
+      if (kind == 1 || kind == 5)
         m.skip('\n');
       else if (kind == 2 && (out.size() & 1))
         m.skip(' ');
@@ -131,6 +136,7 @@ int main(int argc, char** argv)
     fprintf(stderr, "usage: adapter_test SPECFILE\n");
     return 2;
   }
+  setenv("UGPU_ADAPTER_CHUNK", "100000", 0);  // many stream feeds per input
   std::ifstream spec(argv[1]);
   std::string line;
   int bad = 0, n = 0;
@@ -141,25 +147,21 @@ int main(int argc, char** argv)
     size_t t1 = line.find('\t'), t2 = line.find('\t', t1 + 1);
     std::string mode = line.substr(0, t1);
     const std::string rx = line.substr(t1 + 1, t2 - t1 - 1), in = line.substr(t2 + 1);
-    // mode suffix W: Matcher option W (ugrep -w) on both sides, UGPU_PAT_WORD tables
+    // mode suffix W: Matcher option W (ugrep -w) on both sides
     const bool word = mode.size() > 1 && mode[mode.size() - 1] == 'W';
     if (word)
       mode.erase(mode.size() - 1);
     const char* opt = word ? "W" : NULL;
     reflex::Pattern pat(build_regex(mode, rx), "r");
-    ugpu_dfa* dfa = NULL;
-    const int rc = ugpu_dfa_create(pat.opc_, static_cast<uint32_t>(pat.nop_), word ? UGPU_PAT_WORD : 0u, &dfa);
-    if (rc != UGPU_OK && rc != UGPU_UNSUPPORTED)
-    {
-      printf("FAIL /%s/: ugpu_dfa_create: %d %s\n", rx.c_str(), rc, ugpu_last_error());
-      ++bad;
-      continue;
-    }
     std::vector<char> a = load_input(in), b = a;
-    for (int kind = 0; kind < 4; ++kind)
+    const std::string text(a.data(), a.size() - 1);  // (stream input: no NUL)
+    for (int kind = 0; kind < 6; ++kind)
     {
-      reflex::Matcher cpu(pat, reflex::Input(), opt);
-      reflex::GpuMatcher gpu(pat, word || rc != UGPU_OK ? NULL : dfa, opt, word && rc == UGPU_OK ? dfa : NULL);
+      std::istringstream sa(text), sb(text);
+      reflex::Matcher cpu(pat, kind < 4 ? reflex::Input() : reflex::Input(sa), opt);
+      reflex::GpuMatcher gpu(pat, kind < 4 ? reflex::Input() : reflex::Input(sb), opt);
+      gpu.gpu_min_bytes(0);  // parity on every size (the size policy is measured separately)
+      const bool ready = gpu.gpu_ready();
       bool ea = false, eb = false;
       std::vector<Hit> ra = run(cpu, a, kind, ea), rb = run(gpu, b, kind, eb);
       size_t diff = 0;
@@ -167,26 +169,25 @@ int main(int argc, char** argv)
         ++diff;
       const bool ok = ra.size() == rb.size() && diff == ra.size() && ea == eb;
       printf("%s %s kind=%d /%s/%s %s: cpu %zu gpu %zu matches, gpu scans %zu%s\n", ok ? "ok" : "FAIL",
-             rc == UGPU_OK ? "gpu" : "cpu-only", kind, rx.c_str(), word ? "W" : "", in.substr(0, 40).c_str(),
-             ra.size(), rb.size(),
-             gpu.gpu_scans(), rc == UGPU_OK ? "" : " (engine: unsupported table)");
+             ready ? "gpu" : "cpu-only", kind, rx.c_str(), word ? "W" : "", in.substr(0, 40).c_str(), ra.size(),
+             rb.size(), gpu.gpu_scans(), ready ? "" : " (engine: unsupported table)");
       if (!ok)
       {
         ++bad;
         if (diff < ra.size() && diff < rb.size())
-          printf("  first difference at #%zu: cpu (%zu,%zu,%zu,%zu) gpu (%zu,%zu,%zu,%zu)\n", diff, ra[diff].first,
-                 ra[diff].size, ra[diff].accept, ra[diff].lineno, rb[diff].first, rb[diff].size, rb[diff].accept,
-                 rb[diff].lineno);
+          printf("  first difference at #%zu: cpu (%zu,%zu,%zu,%zu,%zu) gpu (%zu,%zu,%zu,%zu,%zu)\n", diff,
+                 ra[diff].first, ra[diff].size, ra[diff].accept, ra[diff].lineno, ra[diff].columno, rb[diff].first,
+                 rb[diff].size, rb[diff].accept, rb[diff].lineno, rb[diff].columno);
       }
-      // the GPU path must actually have served supported tables
-      if (rc == UGPU_OK && gpu.gpu_scans() == 0 && !ra.empty())
+      // the GPU path must actually have served supported tables (option W on
+      // streams stays on the CPU by design)
+      if (ready && gpu.gpu_scans() == 0 && !ra.empty() && !(word && kind >= 4))
       {
-        printf("FAIL gpu matcher fell back to the CPU for /%s/\n", rx.c_str());
+        printf("FAIL gpu matcher fell back to the CPU for /%s/ kind=%d\n", rx.c_str(), kind);
         ++bad;
       }
       ++n;
     }
-    ugpu_dfa_destroy(dfa);
   }
   printf("%d cases, %d failed\n", n, bad);
   return bad ? 1 : 0;

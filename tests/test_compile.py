@@ -65,6 +65,44 @@ def test_compile_equivalent_to_reference(chunk):
     assert not bad, bad[:5]
 
 
+def _reflex_cases():
+    z = np.load(os.path.join(HERE, "golden", "reflex_cases.npz"))
+    offs, words, ro, rx = z["offsets"], z["words"], z["roffsets"], z["regex"]
+    return [(str(m), bytes(rx[ro[i]:ro[i + 1]]), words[offs[i]:offs[i + 1]]) for i, m in enumerate(z["modes"])]
+
+
+REFLEX_CASES = _reflex_cases()
+
+
+@pytest.mark.parametrize("chunk", range(4))
+def test_reflex_mode_equivalent_to_reference(chunk):
+    """UGPU_RX_REFLEX: the converted regex the reference Pattern holds (its public
+    Pattern::operator[](0); tests/golden/reflex_cases.npz, tools/gen_reflex_golden.py)
+    compiles to a table language-equivalent to the reference's own, for every
+    case of compile_cases.npz the reference accepts (Unicode classes, -i, -F
+    quoting, inline modifiers).  This is how the drop-in adapter builds its tables."""
+    import ugrep_amd as U
+    bad, unsup = [], []
+    for mode, conv, ref in REFLEX_CASES[chunk::4]:
+        try:
+            mine = U.compile_regex(conv, reflex=True)
+        except U.Unsupported as e:
+            unsup.append((mode, conv[:60], str(e)))
+            continue
+        ce = counterexample(mine, ref)
+        if ce is not None:
+            bad.append((mode, conv[:80], ce))
+    assert not bad, bad[:5]
+    assert not unsup, unsup[:5]
+
+
+def test_reflex_mode_rejects_meta():
+    import ugrep_amd as U
+    for rx in (b"(?m)^a", b"(?m)a$", b"(?m)\\bfoo", b"(?m)x*?y", b"(?m)(?=x)y", b"(?mx)a b", b"(?m)\\x{100}"):
+        with pytest.raises(U.Unsupported):
+            U.compile_regex(rx, reflex=True)
+
+
 def test_config_tables_are_loadable():
     """Compiled tables pass the device-table builder (host side) and pick the
     same kernel class as the reference's tables for the BASELINE configs."""

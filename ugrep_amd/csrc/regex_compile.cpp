@@ -385,7 +385,10 @@ struct Tree
 class Parser
 {
  public:
-  Parser(const std::string &rx, uint32_t flags, Tree &t) : s_(rx), flags_(flags), t_(t) {}
+  Parser(const std::string &rx, uint32_t flags, Tree &t)
+      : s_(rx), flags_(flags), t_(t), ic_((flags & UGPU_RX_ICASE) != 0)
+  {
+  }
 
   // top-level alternatives (each gets its own accept index, as the reference's
   // Pattern numbers top-level choices: SURVEY Appendix D, foo|bar|baz -> TAKE 1/2/3)
@@ -418,8 +421,11 @@ class Parser
   uint32_t flags_;
   Tree &t_;
   size_t p_ = 0;
+  bool ic_;             // case-insensitive (flag, or RE/flex (?i) in REFLEX mode)
+  bool dotall_ = false;  // REFLEX mode (?s): '.' matches '\n'
 
-  bool icase() const { return flags_ & UGPU_RX_ICASE; }
+  bool icase() const { return ic_; }
+  bool reflex() const { return (flags_ & UGPU_RX_REFLEX) != 0; }
 
   int literal_byte(uint8_t c)
   {
@@ -451,8 +457,23 @@ class Parser
   int parse_concat()
   {
     std::vector<int> seq;
+    bool atoms = false;
     while (p_ < s_.size() && s_[p_] != '|' && s_[p_] != ')')
+    {
+      // REFLEX mode: a (?imsx) modifier after atoms of its branch opens a group
+      // that runs to the end of the enclosing group, later alternatives
+      // included ("x(?i)ab|cd" is x(?i:ab|cd)); a leading one just sets the
+      // flags for the rest of the enclosing group (measured on the reference's
+      // tables: "(?i)foo|BAR" keeps two case-insensitive alternatives)
+      if (reflex() && atoms && modifier_at(p_))
+      {
+        seq.push_back(parse_atom_reflex());  // sets the flags
+        seq.push_back(p_ >= s_.size() || s_[p_] == ')' ? t_.add(EMPTY) : parse_alt());
+        break;
+      }
+      atoms = atoms || !(reflex() && modifier_at(p_));
       seq.push_back(parse_repeat());
+    }
     if (seq.empty())
       return t_.add(EMPTY);
     return seq.size() == 1 ? seq[0] : t_.add(CAT, seq);
@@ -795,8 +816,235 @@ class Parser
     return set;
   }
 
+  // ---- REFLEX mode: the RE/flex regex a Pattern holds (Pattern::operator[](0),
+  // include/reflex/pattern.h:302), i.e. Matcher::convert's output
+  // (lib/convert.cpp): bytes, not code points -- Unicode classes, '.' and -i
+  // over non-ASCII letters are already expanded into byte sequences; inline
+  // modifiers (?i) (?s) (?m) and (?i:...) scopes; \Q...\E quoting.
+
+  // one byte escape at p_ (just past '\')
+  uint8_t reflex_escape_byte()
+  {
+    if (p_ >= s_.size())
+      fail(UGPU_INVAL, "trailing backslash");
+    const char c = s_[p_++];
+    switch (c)
+    {
+      case 't': return '\t';
+      case 'n': return '\n';
+      case 'r': return '\r';
+      case 'f': return '\f';
+      case 'v': return '\v';
+      case 'a': return '\a';
+      case 'e': return 0x1B;
+      case '0':
+      {
+        uint32_t v = 0;
+        for (int i = 0; i < 3 && p_ < s_.size() && s_[p_] >= '0' && s_[p_] <= '7'; ++i)
+          v = v * 8 + (s_[p_++] - '0');
+        if (v > 0xFF)
+          fail(UGPU_UNSUPPORTED, "octal escape above 0xFF in byte mode");
+        return static_cast<uint8_t>(v);
+      }
+      case 'x':
+      {
+        uint32_t v = 0;
+        int digits = 0;
+        const bool brace = p_ < s_.size() && s_[p_] == '{';
+        if (brace)
+          ++p_;
+        while ((brace || digits < 2) && p_ < s_.size() && hexval(s_[p_]) >= 0)
+        {
+          v = v * 16 + hexval(s_[p_++]);
+          if (++digits > 6)
+            fail(UGPU_INVAL, "bad \\x");
+        }
+        if (brace)
+        {
+          if (p_ >= s_.size() || s_[p_] != '}')
+            fail(UGPU_INVAL, "bad \\x{}");
+          ++p_;
+        }
+        if (digits == 0)
+          fail(UGPU_INVAL, "bad \\x");
+        if (v > 0xFF)
+          fail(UGPU_UNSUPPORTED, "\\x above 0xFF in byte mode");
+        return static_cast<uint8_t>(v);
+      }
+      default:
+        break;
+    }
+    if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '1' && c <= '9'))
+      fail(UGPU_UNSUPPORTED, std::string("escape \\") + c + " in byte mode");
+    return static_cast<uint8_t>(c);
+  }
+
+  // "(?imsx-imsx)" starts at q
+  bool modifier_at(size_t q) const
+  {
+    if (q + 1 >= s_.size() || s_[q] != '(' || s_[q + 1] != '?')
+      return false;
+    q += 2;
+    while (q < s_.size() && strchr("imsx-", s_[q]) != NULL)
+      ++q;
+    return q < s_.size() && s_[q] == ')';
+  }
+
+  void fold_ascii(ByteSet &b)
+  {
+    for (unsigned x = 'a'; x <= 'z'; ++x)
+      if (b.test(x) || b.test(x ^ 0x20))
+      {
+        b.set(x);
+        b.set(x ^ 0x20);
+      }
+  }
+
+  ByteSet parse_byte_bracket()
+  {
+    // p_ just past '['
+    bool neg = false;
+    if (p_ < s_.size() && s_[p_] == '^')
+    {
+      neg = true;
+      ++p_;
+    }
+    ByteSet b;
+    bool first = true;
+    for (;;)
+    {
+      if (p_ >= s_.size())
+        fail(UGPU_INVAL, "unterminated bracket");
+      const char c = s_[p_];
+      if (c == ']' && !first)
+      {
+        ++p_;
+        break;
+      }
+      first = false;
+      if (c == '[' && p_ + 1 < s_.size() && (s_[p_ + 1] == ':' || s_[p_ + 1] == '.' || s_[p_ + 1] == '='))
+        fail(UGPU_UNSUPPORTED, "POSIX bracket in byte mode");
+      uint8_t lo, hi;
+      ++p_;
+      lo = c == '\\' ? reflex_escape_byte() : static_cast<uint8_t>(c);
+      hi = lo;
+      if (p_ + 1 < s_.size() && s_[p_] == '-' && s_[p_ + 1] != ']')
+      {
+        ++p_;
+        const char d = s_[p_++];
+        hi = d == '\\' ? reflex_escape_byte() : static_cast<uint8_t>(d);
+        if (hi < lo)
+          fail(UGPU_INVAL, "bad range");
+      }
+      for (unsigned x = lo; x <= hi; ++x)
+        b.set(x);
+    }
+    if (icase())
+      fold_ascii(b);
+    if (neg)
+      b.flip();
+    return b;
+  }
+
+  int parse_atom_reflex()
+  {
+    const char c = s_[p_];
+    switch (c)
+    {
+      case '(':
+      {
+        ++p_;
+        const bool ic = ic_, dot = dotall_;
+        if (p_ < s_.size() && s_[p_] == '?')
+        {
+          // (?imsx-imsx) modifies the rest of the enclosing group,
+          // (?imsx-imsx:...) just the group; anything else ((?=, (?^ ...) is not a DFA
+          size_t q = p_ + 1;
+          bool on = true, i = ic_, d = dotall_;
+          while (q < s_.size() && strchr("imsx-", s_[q]) != NULL)
+          {
+            switch (s_[q])
+            {
+              case '-': on = false; break;
+              case 'i': i = on; break;
+              case 's': d = on; break;
+              case 'x': if (on) fail(UGPU_UNSUPPORTED, "free-space mode"); break;
+              default: break;  // m: multiline anchors (anchors are not supported anyway)
+            }
+            ++q;
+          }
+          if (q < s_.size() && s_[q] == ')')
+          {
+            p_ = q + 1;
+            ic_ = i;
+            dotall_ = d;
+            return t_.add(EMPTY);
+          }
+          if (q >= s_.size() || s_[q] != ':')
+            fail(UGPU_UNSUPPORTED, "(? group");
+          p_ = q + 1;
+          ic_ = i;
+          dotall_ = d;
+        }
+        int a = parse_alt();
+        if (p_ >= s_.size() || s_[p_] != ')')
+          fail(UGPU_INVAL, "missing ')'");
+        ++p_;
+        ic_ = ic;
+        dotall_ = dot;
+        return a;
+      }
+      case '[':
+        ++p_;
+        return t_.leaf(parse_byte_bracket());
+      case '.':
+      {
+        ++p_;
+        ByteSet b;
+        b.set();
+        if (!dotall_)
+          b.reset('\n');
+        return t_.leaf(b);
+      }
+      case '^':
+      case '$':
+        fail(UGPU_UNSUPPORTED, "anchor");
+      case '*':
+      case '+':
+      case '?':
+      case '{':
+        fail(UGPU_INVAL, "nothing to repeat");
+      case '\\':
+      {
+        ++p_;
+        if (p_ < s_.size() && s_[p_] == 'Q')
+        {
+          // \Q...\E: literal bytes
+          ++p_;
+          size_t q = s_.find("\\E", p_);
+          const size_t e = q == std::string::npos ? s_.size() : q;
+          std::vector<int> seq;
+          for (; p_ < e; ++p_)
+            seq.push_back(literal_byte(static_cast<uint8_t>(s_[p_])));
+          p_ = q == std::string::npos ? s_.size() : q + 2;
+          if (seq.empty())
+            return t_.add(EMPTY);
+          return seq.size() == 1 ? seq[0] : t_.add(CAT, seq);
+        }
+        if (p_ < s_.size() && strchr("bBAzZ<>`'GkKEXRNuUcCldDwWsShHpPiIjJ", s_[p_]) != NULL)
+          fail(UGPU_UNSUPPORTED, std::string("escape \\") + s_[p_] + " in byte mode");
+        return literal_byte(reflex_escape_byte());
+      }
+      default:
+        ++p_;
+        return literal_byte(static_cast<uint8_t>(c));
+    }
+  }
+
   int parse_atom(bool dot_byte)
   {
+    if (reflex())
+      return parse_atom_reflex();
     char c = s_[p_];
     switch (c)
     {

@@ -27,21 +27,24 @@ def _as_u32(opc):
 
 RX_FIXED = 1
 RX_ICASE = 2
+RX_REFLEX = 4
 PAT_WORD = 1  # ugpu_dfa_create pattern_flags: option W
 
 
-def compile_regex(regex, fixed=False, icase=False):
+def compile_regex(regex, fixed=False, icase=False, reflex=False):
     """Opcode words (numpy u32) for `regex` from the native compiler
     (ugpu_compile, regex_compile.cpp): ugrep's default ERE in Unicode mode, as
     Matcher::convert(rx, notnewline|unicode) + Pattern(conv, "r") produce them
     (src/ugrep.cpp:8574-8578, lib/pattern.cpp:171-3063).  Syntax errors raise
     UgpuError(UGPU_INVAL) where the reference throws regex_error; constructs the
-    GPU tables do not cover raise Unsupported."""
+    GPU tables do not cover raise Unsupported.  reflex=True: `regex` is the
+    RE/flex byte regex a Pattern holds after ugrep's conversion
+    (Pattern::operator[](0), UGPU_RX_REFLEX), as the drop-in adapter passes it."""
     if isinstance(regex, str):
         regex = regex.encode("utf-8")
     words = _lib.c_u32p()
     n = ctypes.c_uint32()
-    flags = (RX_FIXED if fixed else 0) | (RX_ICASE if icase else 0)
+    flags = (RX_FIXED if fixed else 0) | (RX_ICASE if icase else 0) | (RX_REFLEX if reflex else 0)
     rc = lib.ugpu_compile(regex, len(regex), flags, ctypes.byref(words), ctypes.byref(n))
     if rc != _lib.UGPU_OK:
         msg = lib.ugpu_compile_error().decode(errors="replace")
