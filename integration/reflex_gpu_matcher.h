@@ -39,16 +39,23 @@
 // exact whenever the new cur_ is not inside one; otherwise (and for new bytes
 // or a rewind) the scan restarts at cur_.
 //
-// Dispatch: inputs shorter than UGPU_ADAPTER_MIN_BYTES (default 1 MiB; a
-// stream counts when it ends before its first feed) stay on the CPU matcher: a
-// device round trip costs more than the reference's SIMD scan of a small
-// buffer (tools/bench_adapter.py).  UGPU_ADAPTER_STATS=1 prints each
+// Dispatch (tools/bench_adapter.py):
+//   * inputs shorter than UGPU_ADAPTER_MIN_BYTES (default 4 MiB for sparse
+//     tables, 256 KiB for dense ones; a stream counts when it ends before its
+//     first feed) stay on the CPU matcher: a device round trip costs more than
+//     the reference's scan of a small buffer;
+//   * patterns with a selective prefilter (sparse_kernel, e.g. foo|bar|baz) use
+//     the GPU only while at most UGPU_ADAPTER_SPARSE_MAX (default 4) GpuMatchers
+//     exist: host buffers cross PCIe at ~55 GB/s, which a few reference AVX2
+//     cores match on such patterns (11 GB/s each), while dense patterns (C3/C4
+//     class, ~0.2-2 GB/s per core) always gain.  UGPU_ADAPTER_STATS=1 prints each
 // matcher's GPU scan count to stderr when it is destroyed.  Everything else --
 // SCAN/SPLIT/MATCH, options A/N, option W on streams, tables the engine rejects
 // (anchors, \b, lookahead: UGPU_UNSUPPORTED) -- stays on the CPU matcher.
 #ifndef REFLEX_GPU_MATCHER_H
 #define REFLEX_GPU_MATCHER_H
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -69,12 +76,15 @@ class GpuMatcher : public Matcher {
       : Matcher(pattern, input, opt)
   {
     init_policy();
+    ++live();
   }
   /// Clones (ugrep's worker threads, src/ugrep.cpp:4146, :9006) share the
   /// device tables; per-input state starts empty.
   GpuMatcher(const GpuMatcher& m)
-      : Matcher(m), tab_(m.tab_), tab_pat_(m.tab_pat_), tab_w_(m.tab_w_), min_bytes_(m.min_bytes_), chunk_(m.chunk_)
+      : Matcher(m), tab_(m.tab_), tab_pat_(m.tab_pat_), tab_w_(m.tab_w_), sparse_(m.sparse_),
+        min_bytes_(m.min_bytes_), chunk_(m.chunk_), sparse_max_(m.sparse_max_)
   {
+    ++live();
   }
   virtual GpuMatcher* clone() { return new GpuMatcher(*this); }
   virtual ~GpuMatcher()
@@ -84,6 +94,7 @@ class GpuMatcher : public Matcher {
       std::fprintf(stderr, "[ugpu-adapter] scans=%zu\n", scans_);
     ugpu_result_free(gres_);
     ugpu_stream_destroy(gst_);
+    --live();
   }
   /// New input (input() calls this, absmatcher.h:533-540) or options.
   virtual void reset(const char* opt = NULL)
@@ -101,11 +112,13 @@ class GpuMatcher : public Matcher {
   bool gpu_ready() { return tables() != NULL; }
   /// Smallest input sent to the GPU (0: every input).
   void gpu_min_bytes(size_t n) { min_bytes_ = n; }
+  /// Prefiltered (sparse) patterns use the GPU while at most n GpuMatchers exist.
+  void gpu_sparse_max(int n) { sparse_max_ = n; }
 
  protected:
   virtual size_t match(Method method)
   {
-    if (method != Const::FIND || opt_.A || opt_.N || tables() == NULL)
+    if (method != Const::FIND || opt_.A || opt_.N || tables() == NULL || (sparse_ && live() > sparse_max_))
       return Matcher::match(method);
     if (own_)
       return stream_match();
@@ -154,10 +167,25 @@ class GpuMatcher : public Matcher {
           ugpu_opc_free(opc);
         }
         if (d != NULL)
+        {
           tab_.reset(d, ugpu_dfa_destroy);
+          ugpu_dfa_info info;
+          sparse_ = ugpu_dfa_info_get(d, &info) == UGPU_OK && info.kernel == 0;
+          // measured crossover against one reference matcher on a host buffer
+          // (profiles/r02_adapter_latency.jsonl): 4 MiB for C2-like sparse
+          // tables, 64-256 KiB for dense ones
+          if (min_bytes_ == ~static_cast<size_t>(0))
+            min_bytes_ = sparse_ ? (4u << 20) : (256u << 10);
+        }
       }
     }
     return tab_.get();
+  }
+  // live GpuMatchers of the process (ugrep: one per worker thread)
+  static std::atomic<int>& live()
+  {
+    static std::atomic<int> n(0);
+    return n;
   }
   void drop_records()
   {
@@ -185,7 +213,9 @@ class GpuMatcher : public Matcher {
   void init_policy()
   {
     const char* e = std::getenv("UGPU_ADAPTER_MIN_BYTES");
-    min_bytes_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (1u << 20);
+    min_bytes_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : ~static_cast<size_t>(0);  // ~0: per table
+    e = std::getenv("UGPU_ADAPTER_SPARSE_MAX");
+    sparse_max_ = e && *e ? std::atoi(e) : 4;
     e = std::getenv("UGPU_ADAPTER_CHUNK");
     chunk_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (8u << 20);
     if (chunk_ == 0)
@@ -315,11 +345,13 @@ class GpuMatcher : public Matcher {
   std::shared_ptr<ugpu_dfa> tab_;
   const Pattern* tab_pat_ = NULL;
   bool tab_w_ = false;
+  bool sparse_ = false;  // the table has a selective prefilter (sparse_kernel)
   ugpu_result* gres_ = NULL;
   const char* gbuf_ = NULL;
   // gcur_: the cursor this class left behind (after the scan or the last hit)
   size_t gend_ = 0, gcur_ = 0, gi_ = 0, scans_ = 0, scans_at_restart_ = 0;
   size_t min_bytes_ = 0, chunk_ = 0;
+  int sparse_max_ = 4;
   ugpu_stream* gst_ = NULL;
   uint64_t sbase_ = 0, sfed_ = 0, gcur_abs_ = 0;
   bool sdone_ = false, cpu_stream_ = false;

@@ -160,7 +160,8 @@ int main(int argc, char** argv)
       std::istringstream sa(text), sb(text);
       reflex::Matcher cpu(pat, kind < 4 ? reflex::Input() : reflex::Input(sa), opt);
       reflex::GpuMatcher gpu(pat, kind < 4 ? reflex::Input() : reflex::Input(sb), opt);
-      gpu.gpu_min_bytes(0);  // parity on every size (the size policy is measured separately)
+      gpu.gpu_min_bytes(0);  // parity on every size and pattern (the dispatch policy is measured separately)
+      gpu.gpu_sparse_max(1 << 30);
       const bool ready = gpu.gpu_ready();
       bool ea = false, eb = false;
       std::vector<Hit> ra = run(cpu, a, kind, ea), rb = run(gpu, b, kind, eb);

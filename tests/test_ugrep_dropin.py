@@ -10,8 +10,8 @@ reference's own golden file tests/out/*.out (tests/golden/verify_cases.json,
 tools/gen_verify_golden.py; inputs copied to tests/golden/verify/).
 
 CPU test: the reference build oracle/_ref/ugrep reproduces every golden (pins
-the harness).  GPU test: ugrep_gpu with UGPU_ADAPTER_MIN_BYTES=0 (every input
-on the GPU, the suite's files are tiny) reproduces them too, and the engine
+the harness).  GPU test: ugrep_gpu with UGPU_ADAPTER_MIN_BYTES=0 and no sparse
+limit (every input on the GPU, the suite's files are tiny) reproduces them too, and the engine
 really served the FIND calls (adapter statistics on stderr)."""
 import hashlib
 import json
@@ -58,7 +58,7 @@ def test_dropin_ugrep_reproduces_goldens():
     exe = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")
     if not os.path.exists(exe):
         pytest.skip("ugrep_gpu not built (make -C oracle ref, build container)")
-    env = dict(os.environ, UGPU_ADAPTER_MIN_BYTES="0", UGPU_ADAPTER_STATS="1")
+    env = dict(os.environ, UGPU_ADAPTER_MIN_BYTES="0", UGPU_ADAPTER_SPARSE_MAX="1000000", UGPU_ADAPTER_STATS="1")
     bad, scans = _run_all(exe, env)
     assert not bad, bad[:5]
     assert scans > 100, scans

@@ -44,6 +44,10 @@ struct ugpu_dfa {
   uint32_t* d_caps = nullptr;
   uint32_t* d_wtab = nullptr;  // option W: Unicode Word ranges (UGPU_PAT_WORD)
   uint32_t nwtab = 0;
+  // idle scanners of ugpu_find_all calls on this table (reused: creating one
+  // costs device allocations and property queries)
+  std::mutex pool_mu;
+  std::vector<ugpu_scanner*> pool;
 };
 
 struct ugpu_scanner {
@@ -371,6 +375,7 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
 int ugpu_dfa_destroy(ugpu_dfa* d)
 {
   if (!d) return UGPU_OK;
+  for (ugpu_scanner* s : d->pool) ugpu_scanner_destroy(s);
   if (d->d_trans) (void)hipFree(d->d_trans);
   if (d->d_xtrans) (void)hipFree(d->d_xtrans);
   if (d->d_wtab) (void)hipFree(d->d_wtab);
@@ -799,6 +804,105 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
   return UGPU_OK;
 }
 
+namespace {
+
+// Per-device workspace of ugpu_find_all, pooled (no hipMalloc/hipFree per
+// call: hipFree synchronises the device): a private non-blocking stream (calls
+// from several host threads do not serialise on the null stream), the device
+// copy of a host input and the device match arrays, grown on demand.
+struct FindWs {
+  int dev = -1;
+  hipStream_t st = nullptr;
+  uint8_t* d_in = nullptr;
+  uint64_t in_cap = 0;
+  uint64_t* d_start = nullptr;
+  uint32_t* d_len = nullptr;
+  uint32_t* d_cap = nullptr;
+  uint64_t out_cap = 0;
+
+  hipError_t reserve_in(uint64_t n)
+  {
+    if (n <= in_cap) return hipSuccess;
+    (void)hipFree(d_in);
+    d_in = nullptr;
+    in_cap = 0;
+    const uint64_t c = n + n / 4;
+    hipError_t e = hipMalloc(&d_in, c + 16);
+    if (e == hipSuccess) in_cap = c;
+    return e;
+  }
+  hipError_t reserve_out(uint64_t n)
+  {
+    if (n <= out_cap) return hipSuccess;
+    (void)hipFree(d_start);
+    (void)hipFree(d_len);
+    (void)hipFree(d_cap);
+    d_start = nullptr;
+    d_len = d_cap = nullptr;
+    out_cap = 0;
+    const uint64_t c = n + n / 4;
+    hipError_t e;
+    if ((e = hipMalloc(&d_start, c * 8)) != hipSuccess || (e = hipMalloc(&d_len, c * 4)) != hipSuccess ||
+        (e = hipMalloc(&d_cap, c * 4)) != hipSuccess)
+      return e;
+    out_cap = c;
+    return hipSuccess;
+  }
+};
+
+std::mutex g_find_mu;
+std::vector<FindWs*> g_find_pool;
+
+FindWs* find_ws_acquire(int dev)
+{
+  {
+    std::lock_guard<std::mutex> lk(g_find_mu);
+    for (size_t i = 0; i < g_find_pool.size(); ++i)
+      if (g_find_pool[i]->dev == dev) {
+        FindWs* w = g_find_pool[i];
+        g_find_pool.erase(g_find_pool.begin() + (long)i);
+        return w;
+      }
+  }
+  FindWs* w = new (std::nothrow) FindWs;
+  if (!w) return nullptr;
+  w->dev = dev;
+  if (hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking) != hipSuccess) {
+    delete w;
+    return nullptr;
+  }
+  return w;
+}
+
+void find_ws_release(FindWs* w)
+{
+  std::lock_guard<std::mutex> lk(g_find_mu);
+  g_find_pool.push_back(w);
+}
+
+int scanner_acquire(const ugpu_dfa* dfa, ugpu_scanner** out)
+{
+  ugpu_dfa* d = const_cast<ugpu_dfa*>(dfa);
+  {
+    std::lock_guard<std::mutex> lk(d->pool_mu);
+    if (!d->pool.empty()) {
+      *out = d->pool.back();
+      d->pool.pop_back();
+      return UGPU_OK;
+    }
+  }
+  return ugpu_scanner_create(dfa, out);
+}
+
+void scanner_release(const ugpu_dfa* dfa, ugpu_scanner* s)
+{
+  ugpu_dfa* d = const_cast<ugpu_dfa*>(dfa);
+  std::lock_guard<std::mutex> lk(d->pool_mu);
+  d->pool.push_back(s);
+}
+
+}  // namespace
+
 int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_t start, uint32_t mode,
                   ugpu_result** out)
 {
@@ -807,82 +911,66 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
   if (start > len) start = len;
   ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
   if (!r) return fail(UGPU_NOMEM, "host allocation");
-  ugpu_scanner* s = nullptr;
-  int rc = ugpu_scanner_create(dfa, &s);
-  if (rc) {
-    std::free(r);
-    return rc;
-  }
-  const bool dev = len > 0 && is_device_ptr(buf);
-  uint8_t* dcopy = nullptr;
-  const uint8_t* dbuf = buf;
-  uint64_t* d_start = nullptr;
-  uint32_t* d_len = nullptr;
-  uint32_t* d_cap = nullptr;
-  ugpu_totals tot{};
-  auto cleanup = [&]() {
-    if (dcopy) (void)hipFree(dcopy);
-    if (d_start) (void)hipFree(d_start);
-    if (d_len) (void)hipFree(d_len);
-    if (d_cap) (void)hipFree(d_cap);
-    ugpu_scanner_destroy(s);
-  };
-  hipError_t e;
-  if (!dev) {
-    if ((e = hipMalloc(&dcopy, len + 16)) != hipSuccess) {
-      cleanup();
-      std::free(r);
-      return hip_fail(e, "hipMalloc input");
-    }
-    if (len && (e = hipMemcpy(dcopy, buf, len, hipMemcpyHostToDevice)) != hipSuccess) {
-      cleanup();
-      std::free(r);
-      return hip_fail(e, "hipMemcpy input");
-    }
-    dbuf = dcopy;
-  }
-  static const uint8_t zero16[16] = {0};
-  if (len == 0 && !dcopy) dbuf = zero16;  // never read
   if (len == 0) {
-    cleanup();
     *out = r;
     return UGPU_OK;
   }
-  rc = ugpu_scan(s, dbuf, start, len, len, 1, 0, nullptr);
-  if (!rc) rc = ugpu_scan_totals(s, &tot);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) {
+    std::free(r);
+    return hip_fail(e, "hipGetDevice");
+  }
+  ugpu_scanner* s = nullptr;
+  int rc = scanner_acquire(dfa, &s);
   if (rc) {
-    cleanup();
     std::free(r);
     return rc;
   }
-  r->count = tot.count;
-  r->digest = tot.digest;
-  r->dcap = tot.dcap;
-  if (mode == UGPU_MODE_OFFSETS && tot.count > 0) {
+  FindWs* ws = find_ws_acquire(dev);
+  if (!ws) {
+    scanner_release(dfa, s);
+    std::free(r);
+    return fail(UGPU_NOMEM, "find workspace");
+  }
+  const uint8_t* dbuf = buf;
+  ugpu_totals tot{};
+  if (!is_device_ptr(buf)) {
+    if ((e = ws->reserve_in(len)) != hipSuccess || (e = hipMemcpyAsync(ws->d_in, buf, len, hipMemcpyHostToDevice,
+                                                                        ws->st)) != hipSuccess)
+      rc = hip_fail(e, "input copy");
+    dbuf = ws->d_in;
+  }
+  if (!rc) rc = ugpu_scan(s, dbuf, start, len, len, 1, 0, ws->st);
+  if (!rc) rc = ugpu_scan_totals(s, &tot);
+  if (!rc) {
+    r->count = tot.count;
+    r->digest = tot.digest;
+    r->dcap = tot.dcap;
+  }
+  if (!rc && mode == UGPU_MODE_OFFSETS && tot.count > 0) {
     const uint64_t n = tot.count;
     r->start = static_cast<uint64_t*>(std::malloc(n * 8));
     r->len = static_cast<uint32_t*>(std::malloc(n * 4));
     r->cap = static_cast<uint32_t*>(std::malloc(n * 4));
-    if (!r->start || !r->len || !r->cap || hipMalloc(&d_start, n * 8) != hipSuccess ||
-        hipMalloc(&d_len, n * 4) != hipSuccess || hipMalloc(&d_cap, n * 4) != hipSuccess) {
-      cleanup();
-      ugpu_result_free(r);
-      return fail(UGPU_NOMEM, "match list allocation");
-    }
-    rc = ugpu_scan_offsets(s, d_start, d_len, d_cap, n, nullptr);
-    if (!rc) {
-      if ((e = hipMemcpy(r->start, d_start, n * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
-          (e = hipMemcpy(r->len, d_len, n * 4, hipMemcpyDeviceToHost)) != hipSuccess ||
-          (e = hipMemcpy(r->cap, d_cap, n * 4, hipMemcpyDeviceToHost)) != hipSuccess)
-        rc = hip_fail(e, "hipMemcpy matches");
-    }
-    if (rc) {
-      cleanup();
-      ugpu_result_free(r);
-      return rc;
-    }
+    if (!r->start || !r->len || !r->cap)
+      rc = fail(UGPU_NOMEM, "match list allocation");
+    else if ((e = ws->reserve_out(n)) != hipSuccess)
+      rc = hip_fail(e, "match list");
+    if (!rc) rc = ugpu_scan_offsets(s, ws->d_start, ws->d_len, ws->d_cap, n, ws->st);
+    if (!rc && ((e = hipMemcpyAsync(r->start, ws->d_start, n * 8, hipMemcpyDeviceToHost, ws->st)) != hipSuccess ||
+                (e = hipMemcpyAsync(r->len, ws->d_len, n * 4, hipMemcpyDeviceToHost, ws->st)) != hipSuccess ||
+                (e = hipMemcpyAsync(r->cap, ws->d_cap, n * 4, hipMemcpyDeviceToHost, ws->st)) != hipSuccess ||
+                (e = hipStreamSynchronize(ws->st)) != hipSuccess))
+      rc = hip_fail(e, "hipMemcpy matches");
   }
-  cleanup();
+  (void)hipStreamSynchronize(ws->st);
+  find_ws_release(ws);
+  scanner_release(dfa, s);
+  if (rc) {
+    ugpu_result_free(r);
+    return rc;
+  }
   *out = r;
   return UGPU_OK;
 }
