@@ -122,7 +122,7 @@ class GpuMatcher : public Matcher {
       return Matcher::match(method);
     if (own_)
       return stream_match();
-    if (!eof_ || end_ < min_bytes_)
+    if (!eof_ || end_ < min_bytes())
       return Matcher::match(method);
     reset_text();
     // buffer() is non-virtual and rewinds cur_ without telling this class
@@ -171,15 +171,18 @@ class GpuMatcher : public Matcher {
           tab_.reset(d, ugpu_dfa_destroy);
           ugpu_dfa_info info;
           sparse_ = ugpu_dfa_info_get(d, &info) == UGPU_OK && info.kernel == 0;
-          // measured crossover against one reference matcher on a host buffer
-          // (profiles/r02_adapter_latency.jsonl): 4 MiB for C2-like sparse
-          // tables, 64-256 KiB for dense ones
-          if (min_bytes_ == ~static_cast<size_t>(0))
-            min_bytes_ = sparse_ ? (4u << 20) : (256u << 10);
+
         }
       }
     }
     return tab_.get();
+  }
+  // smallest input for the GPU: measured crossover against one reference
+  // matcher on a host buffer (profiles/r02_adapter_latency.jsonl): 4 MiB for
+  // C2-like sparse tables, 64-256 KiB for dense ones
+  size_t min_bytes() const
+  {
+    return min_bytes_ != ~static_cast<size_t>(0) ? min_bytes_ : (sparse_ ? (4u << 20) : (256u << 10));
   }
   // live GpuMatchers of the process (ugrep: one per worker thread)
   static std::atomic<int>& live()
@@ -285,7 +288,7 @@ class GpuMatcher : public Matcher {
         else
           end_ += n;
       }
-      if (eof_ && scans_at_restart_ == scans_ && num_ + end_ - sbase_ < min_bytes_)
+      if (eof_ && scans_at_restart_ == scans_ && num_ + end_ - sbase_ < min_bytes())
       {
         // a small input, all of it read before any feed: the CPU matcher is faster
         cpu_stream_ = true;
