@@ -153,6 +153,9 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.xid_rows = d->t.xid_rows;
   P.xg = d->d_xg;
   P.xg_sync = d->d_xg_sync;
+  P.xg_cls = d->d_xg_sync ? d->d_xg_sync + 256 : nullptr;
+  P.xg_stride = 2 * d->t.xg2_pad;
+  P.xg_entries = (uint32_t)((d->t.xg2.size() + 7) & ~size_t(7));
   P.cls = d->d_cls;
   P.caps = d->d_caps;
   P.ntrans_pad = d->ntrans_pad;
@@ -358,12 +361,14 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     }
   }
   if (d->t.gap && !d->t.filter && d->t.cap1 != 0) {
-    std::vector<uint16_t> xg(d->ntrans_pad, 0);
-    std::copy(d->t.xg.begin(), d->t.xg.end(), xg.begin());
+    // device form: the class-major product table (tables.hpp xg2), padded to 8 entries
+    std::vector<uint16_t> xg((d->t.xg2.size() + 7) & ~size_t(7), 0);
+    std::copy(d->t.xg2.begin(), d->t.xg2.end(), xg.begin());
     if ((e = hipMalloc(&d->d_xg, xg.size() * 2)) != hipSuccess ||
         (e = hipMemcpy(d->d_xg, xg.data(), xg.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMalloc(&d->d_xg_sync, 256)) != hipSuccess ||
-        (e = hipMemcpy(d->d_xg_sync, d->t.xg_sync.data(), 256, hipMemcpyHostToDevice)) != hipSuccess) {
+        (e = hipMalloc(&d->d_xg_sync, 512)) != hipSuccess ||
+        (e = hipMemcpy(d->d_xg_sync, d->t.xg_sync.data(), 256, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(d->d_xg_sync + 256, d->t.xg2_cls.data(), 256, hipMemcpyHostToDevice)) != hipSuccess) {
       ugpu_dfa_destroy(d);
       return hip_fail(e, "gap transducer upload");
     }
@@ -575,7 +580,7 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   const char* genv = std::getenv("UGPU_XG");
   if (!s->sparse && !(dfa->d_xid && !(xenv && xenv[0] == '0')) && dfa->d_xg && !(genv && genv[0] == '0')) {
     int gpc = 0;
-    HIP_TRY_S(xg_occupancy(dfa->t.format, &gpc));
+    HIP_TRY_S(xg_occupancy((uint32_t)((dfa->t.xg2.size() + 7) & ~size_t(7)), &gpc));
     if (gpc >= 1) {
       s->xg = true;
       int gg = prop.multiProcessorCount * gpc * (int)xg_waves();

@@ -88,8 +88,11 @@ struct ScanParams {
   const uint16_t* xtrans;  // FIND transducer table or NULL (dense kernel, tables.hpp)
   const uint8_t* xid;      // immediate transducer byte ids (xi_kernel, tables.hpp) or NULL
   uint32_t xid_rows;
-  const uint16_t* xg;      // gap transducer (xg_kernel, tables.hpp) or NULL
+  const uint16_t* xg;      // gap transducer, device form (xg_kernel, tables.hpp xg2) or NULL
   const uint8_t* xg_sync;  // its sync-byte flags
+  const uint8_t* xg_cls;   // its byte columns
+  uint32_t xg_stride;      // bytes per column
+  uint32_t xg_entries;     // u16 entries (multiple of 8)
   const uint8_t* cls;
   const uint32_t* caps;
   uint32_t ntrans_pad;   // u16 entries, multiple of 8
@@ -198,7 +201,8 @@ uint32_t xi_unit();
 uint32_t xi_waves();
 // gap-transducer kernel, xg_kernel.hip (COUNT mode only)
 hipError_t launch_xg(const ScanParams& P, hipStream_t stream);
-hipError_t xg_occupancy(uint32_t format, int* blocks_per_cu);
+hipError_t xg_occupancy(uint32_t entries, int* blocks_per_cu);  // 0 blocks: the table does not fit
+size_t xg_smem_bytes(uint32_t entries);
 uint32_t xg_unit();
 uint32_t xg_waves();
 // dense wave-persistent kernel, dense_kernel.hip

@@ -454,6 +454,66 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
           }
           t.xg[(size_t)s2 * R + col] = (uint16_t)x;
         }
+      // device form: product states (s, accepted) by BFS from (start, 0)
+      std::map<std::pair<uint32_t, int>, uint32_t> pid;
+      std::vector<std::pair<uint32_t, int> > pst;
+      auto prod = [&](uint32_t s2, int a) {
+        auto it = pid.find(std::make_pair(s2, a));
+        if (it != pid.end()) return it->second;
+        const uint32_t id = (uint32_t)pst.size();
+        pid.emplace(std::make_pair(s2, a), id);
+        pst.push_back(std::make_pair(s2, a));
+        return id;
+      };
+      std::vector<int> rep(C, -1);
+      for (int c = 0; c < 256; ++c)
+        if (rep[cls[c]] < 0) rep[cls[c]] = c;
+      prod(start_sid, 0);
+      std::vector<std::vector<uint16_t> > rows;  // per product state: entry per column
+      for (size_t i = 0; i < pst.size() && pst.size() <= kXg2MaxStates; ++i) {
+        const uint32_t s2 = pst[i].first;
+        const int a = pst[i].second;
+        std::vector<uint16_t> row(C, 0);
+        for (uint32_t col = 0; col < C; ++col) {
+          const int c = rep[col];
+          const uint32_t nx = nxt[(size_t)s2 * 256 + c], r = nxt[(size_t)start_sid * 256 + c];
+          uint32_t to, L = 0, F = 0, D = 0;
+          if (nx) {
+            int a2 = a;
+            if (nx >= first_acc) {
+              L = (uint32_t)(gap[s2] < 0 ? 0 : gap[s2]) + 1;
+              F = a ? 0u : 1u;
+              a2 = 1;
+            }
+            to = prod(nx, a2);
+          } else {
+            D = 1;
+            if (r && r >= first_acc) {
+              L = 1;
+              F = 1;
+              to = prod(r, 1);
+            } else {
+              to = prod(r ? r : start_sid, 0);
+            }
+          }
+          row[col] = (uint16_t)((2 * to) << XG2_ROWSHIFT | D * XG2_D | F * XG2_F | L);
+        }
+        rows.push_back(row);
+      }
+      uint32_t pad = (uint32_t)pst.size();
+      while (pad % 4 != 2) ++pad;
+      // (the kernel stages the table plus 512 B of byte tables in 160 KB of LDS)
+      if (pst.size() <= kXg2MaxStates && ((uint64_t)C * pad + 7) / 8 * 16 <= 160u * 1024 - 1536) {
+        t.xg2_states = (uint32_t)pst.size();
+        t.xg2_cols = C;
+        t.xg2_pad = pad;
+        t.xg2.assign((size_t)C * pad, 0);
+        for (uint32_t p2 = 0; p2 < t.xg2_states; ++p2)
+          for (uint32_t col = 0; col < C; ++col) t.xg2[(size_t)col * pad + p2] = rows[p2][col];
+        t.xg2_cls = cls;
+      } else {
+        t.gap = false;  // (product table too large: dense_kernel serves it)
+      }
     }
   }
   t.start = start_sid * R;

@@ -78,6 +78,15 @@ struct DfaTables {
   bool gap = false;             // xg table valid
   std::vector<uint16_t> xg;     // states * row
   std::vector<uint8_t> xg_sync; // 256
+  // Device form of the gap transducer (xg_kernel.hip): product states
+  // p = (DFA state, "the walk has accepted"), so an entry carries the events
+  // of its byte outright (see XG2_* below); stored class-major, column c at
+  // entry c * xg2_pad, xg2_pad = 2 (mod 4) so that lanes reading one column in
+  // different states, or one state in different columns, hit different LDS
+  // banks.  Product state 0 = (start, not accepted).
+  std::vector<uint16_t> xg2;    // xg2_cols * xg2_pad
+  std::vector<uint8_t> xg2_cls; // 256: column of each byte
+  uint32_t xg2_pad = 0, xg2_cols = 0, xg2_states = 0;
 };
 
 constexpr uint8_t XI_ST = 1, XI_IN = 2, XI_Y = 4;
@@ -96,6 +105,13 @@ constexpr uint8_t XI_ST = 1, XI_IN = 2, XI_Y = 4;
 // start none).
 constexpr uint16_t XG_A = 4;
 constexpr uint32_t XG_LSHIFT = 3;
+
+// xg2 entries (u16): bits 0-2 L (gap + 1 of an accept on this byte, 0 = no
+// accept), bit 3 F (the first accept of a walk: a match starts at
+// q + 1 - L), bit 4 D (the walk died on this byte; the entry is the restart),
+// bits 5-15 = 2 * the target product state (its byte offset within a column).
+constexpr uint32_t XG2_L = 7, XG2_F = 8, XG2_D = 16, XG2_ROWSHIFT = 5;
+constexpr uint32_t kXg2MaxStates = 1024;
 
 constexpr uint16_t XT_DEAD = 1;  // the walk died on this byte; the row is the restart state
 constexpr uint16_t XT_LIVE = 2;  // the restart at this byte is alive (a walk begins here)

@@ -9,13 +9,18 @@
 //
 // Same lane/tile/wave scheme as xi_kernel.hip (1 KiB lane segments read
 // directly from HBM, sync-byte exact lanes, tails to the next sync byte, edge
-// tiles in a one-wave kernel), with a different per-byte step: a byte costs a
-// class lookup (class tables) and one u16 transition lookup in LDS, and the
-// match bookkeeping is incremental -- every accept adds its gap + 1 bytes to
-// the current match, the first accept of a walk (tracked by one bit per lane)
-// counts the match and its start q + 1 - (gap + 1).  So no walk start or last
-// accept registers, and no work at the death of a walk:
+// tiles in a one-wave kernel).  Per byte: a column lookup (u8) and one u16
+// transition lookup in LDS, on the product transducer of tables.hpp (xg2):
+// states (DFA state, "the walk has accepted"), so each entry carries its byte's
+// events outright -- L = gap + 1 of an accept (every accept adds L bytes to the
+// current match), F = the first accept of a walk (the match starts at
+// q + 1 - L):
 //   count = #F, sum start = sum_F (q + 1) - sum_F L, sum len = sum L.
+// The table is class-major with an odd dword stride per column, so lanes in
+// different states reading one column (or one state reading different
+// columns) hit different LDS banks.  Events are packed four bytes to a dword
+// and summed with v_dot4_u32_u8; the main loop keeps no per-byte
+// bookkeeping beyond the three VALU of the lookup itself.
 #include "device_common.hpp"
 #include "tables.hpp"
 
@@ -23,16 +28,28 @@ namespace ugpu {
 
 namespace {
 
-constexpr int kGS = 1024;          // lane segment bytes
-constexpr int kGTile = 64 * kGS;   // wave tile
-constexpr int kGBlk = 64;          // bytes per block (4 x 16 B per lane, double buffered)
+// Each lane walks UGPU_XG_NCH chains, over the segments of virtual lanes
+// v = lane + 64 j.  Measured on C4 (8 GiB): 1 chain x 16 waves 3.07 ms, 2 x 8
+// 4.44, 2 x 16 9.3, 4 x 4 10.9 (register spills): one chain per lane it is
+#ifndef UGPU_XG_NCH
+#define UGPU_XG_NCH 1
+#endif
+constexpr int kGCh = UGPU_XG_NCH;
+constexpr int kGTile = 65536;            // wave tile
+constexpr int kGS = kGTile / 64 / kGCh;  // segment bytes per chain
+#ifndef UGPU_XG_BLK
+#define UGPU_XG_BLK 64
+#endif
+constexpr int kGBlk = UGPU_XG_BLK;  // bytes per block (16 B loads per chain, double buffered)
 constexpr int kGLd = kGBlk / 16;
 constexpr int kGBlocks = kGS / kGBlk;
 #ifndef UGPU_XG_WAVES
 #define UGPU_XG_WAVES 16
 #endif
 constexpr int kGWaves = UGPU_XG_WAVES;  // waves per workgroup: one staged table per CU
-constexpr int kGMaxEntries = 65536;  // u16 table entries (128 KB)
+// LDS: the table (up to ~158 KB: C4's \w+ has 99 columns x 794 product states)
+// plus 512 B of byte columns and sync flags, dynamic
+constexpr uint32_t kGMaxTableBytes = 160u * 1024 - 512 - 1024;
 
 __device__ __forceinline__ uint4 gload16(__amdgpu_buffer_rsrc_t rs, uint32_t off)
 {
@@ -53,34 +70,19 @@ __device__ __forceinline__ uint32_t gsel4(const uint4& v, uint32_t j)
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
 
-// Tables in LDS: transitions (u16), class x 2 (FMT 1), sync flags.
-template <int FMT>
+// Tables in LDS: transitions (u16, class-major), columns and sync flags per byte.
 struct GTab {
-  const uint16_t* xg;
-  const uint8_t* c2;
-  const uint8_t* sy;
-  uint32_t rowmask;
-  uint32_t start_row;
-  // entry after byte k of dword w from entry m
-  template <int K>
-  __device__ __forceinline__ uint32_t step(uint32_t m, uint32_t w) const
+  const uint8_t* xg;   // byte address of the table
+  const uint8_t* col;  // column of each byte
+  const uint8_t* sy;   // sync-byte flags
+  uint32_t stride;     // bytes per column
+  // entry after byte b from entry m (the row offset of m is m >> XG2_ROWSHIFT)
+  __device__ __forceinline__ uint32_t step(uint32_t m, uint32_t b) const
   {
-    if constexpr (FMT == 1) {
-      const uint32_t c = c2[(w >> (8 * K)) & 0xffu];
-      return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(xg) + (((m & rowmask) << 1) | c));
-    } else {
-      return xg[__builtin_amdgcn_perm(m, w, 0x0c0c0500u | (uint32_t)K)];  // (m & 0xff00) | byte
-    }
+    const uint32_t c = col[b];
+    return *reinterpret_cast<const uint16_t*>(xg + __umul24(c, stride) + (m >> XG2_ROWSHIFT));
   }
-  __device__ __forceinline__ uint32_t stepb(uint32_t m, uint32_t b) const
-  {
-    if constexpr (FMT == 1)
-      return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(xg) +
-                                                (((m & rowmask) << 1) | c2[b]));
-    else
-      return xg[(m & 0xff00u) | b];
-  }
-  __device__ __forceinline__ bool in_walk(uint32_t m) const { return (m & rowmask) != start_row; }
+  __device__ __forceinline__ static bool in_walk(uint32_t m) { return (m >> XG2_ROWSHIFT) != 0; }
 };
 
 // Lane sums (lane-relative positions r): cnt = #F, sq = sum_F (r + 1),
@@ -97,55 +99,72 @@ __device__ __forceinline__ void gfold(const GSum& a, uint64_t base, uint64_t& cn
   len += a.sl;
 }
 
-// One byte of the main loop.  MASK: events of the lane's head (up to and
-// including its first sync byte) are dropped.  off1 = the byte's offset in its
-// block + 1 (a constant once unrolled): sq gets f (off1) here and f bb per block.
-template <int FMT, int K, bool MASK>
-__device__ __forceinline__ void gbyte(const GTab<FMT>& T, uint32_t w, uint32_t& m, uint32_t& acc, GSum& s,
-                                      uint32_t bb, uint32_t off1, bool& synced, uint32_t& fs)
+// Events of four entries packed into one dword (bits 0-2 L, bit 3 F per byte),
+// summed into s with the dword's position weights wq = (q + 1) of each byte.
+__device__ __forceinline__ void gevents(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t keep,
+                                        uint32_t wq, GSum& s)
 {
-  const uint32_t e = T.template step<K>(m, w);
-  // bit 2 (XG_A): the new state accepts; d2 bit 2: the walk died here
-  const uint32_t d2 = e << 2;
-  uint32_t f = e & (d2 | ~acc) & XG_A;  // first accept of the walk (XG_A or 0; a death restarts it)
-  acc = e | (acc & ~d2);                // bit 2: the walk has accepted
-  uint32_t L = (e >> XG_LSHIFT) & 7u;
-  if constexpr (MASK) {
-    const uint32_t y = T.sy[(w >> (8 * K)) & 0xffu];
-    if (!synced) {
-      f = 0;
-      L = 0;
-      if (y) fs = bb + off1 - 1;
-    }
-    synced = synced || y != 0;
-  }
-  s.cnt += f;  // (sums of f are 4x: XG_A == 4)
-  s.sq += __umul24(f, off1);
-  s.sfl += __umul24(f, L);
-  s.sl += L;
-  m = e;
+  const uint32_t ev = (__builtin_amdgcn_perm(e1, e0, 0x0c0c0400u) | __builtin_amdgcn_perm(e3, e2, 0x04000c0cu)) & keep;
+  const uint32_t Lb = ev & 0x07070707u;
+  const uint32_t Fb = (ev >> 3) & 0x01010101u;
+  s.cnt = __builtin_amdgcn_udot4(Fb, 0x01010101u, s.cnt, false);
+  s.sq = __builtin_amdgcn_udot4(Fb, wq, s.sq, false);
+  s.sfl = __builtin_amdgcn_udot4(Fb, Lb, s.sfl, false);
+  s.sl = __builtin_amdgcn_udot4(Lb, 0x01010101u, s.sl, false);
 }
 
-// acc: bit 2 = the walk has accepted (main-loop form; the tail's form is bit 0)
-template <int FMT, bool MASK>
-__device__ __forceinline__ void gblock(const GTab<FMT>& T, const uint4 (&v)[kGLd], uint32_t& m, uint32_t& acc,
-                                       GSum& s4, bool& synced, uint32_t& fs, uint32_t bb)
+// One dword of the main loop (block offset of its byte 0: bo; block offset in
+// the segment: bb).  MASK: events up to and including the lane's first sync
+// byte are dropped (the previous lane's tail counts them); fs gets that byte's
+// segment offset.
+template <bool MASK>
+__device__ __forceinline__ void gdword(const GTab& T, uint32_t w, uint32_t& m, GSum& s, uint32_t bo, uint32_t bb,
+                                       bool& synced, uint32_t& fs)
 {
-  GSum& s = s4;  // cnt, sq and sfl are scaled by 4 (f = XG_A or 0); sl is exact
-  const uint32_t c0 = s.cnt;
+  const uint32_t e0 = T.step(m, w & 0xffu);
+  const uint32_t e1 = T.step(e0, (w >> 8) & 0xffu);
+  const uint32_t e2 = T.step(e1, (w >> 16) & 0xffu);
+  const uint32_t e3 = T.step(e2, w >> 24);
+  m = e3;
+  uint32_t keep = 0xffffffffu;
+  if constexpr (MASK) {
+    const uint32_t y = (uint32_t)T.sy[w & 0xffu] | (uint32_t)T.sy[(w >> 8) & 0xffu] << 8 |
+                       (uint32_t)T.sy[(w >> 16) & 0xffu] << 16 | (uint32_t)T.sy[w >> 24] << 24;
+    const uint32_t t = y & (0u - y);  // bit 0 of the first sync byte k
+    if (!synced) {
+      keep = ~((t << 8) - 1u);  // bytes after k (none when there is no sync byte)
+      if (y) fs = bb + bo + ((uint32_t)__builtin_ctz(y) >> 3);
+    }
+    synced = synced || y != 0u;
+  }
+  const uint32_t wq = (bo + 1) | ((bo + 2) << 8) | ((bo + 3) << 16) | ((bo + 4) << 24);
+  gevents(e0, e1, e2, e3, keep, wq, s);
+}
+
+// One block of kGBlk bytes of every chain, from registers, block offset bb
+// within the chains' segments; the chains advance a dword each in turn, so
+// their lookups overlap.  Position weights are block-relative (< 256),
+// bb * #F is added after.
+template <bool MASK>
+__device__ __forceinline__ void gblock(const GTab& T, const uint4 (&v)[kGCh][kGLd], uint32_t (&m)[kGCh],
+                                       GSum (&s)[kGCh], bool (&synced)[kGCh], uint32_t (&fs)[kGCh], uint32_t bb)
+{
+  uint32_t c0[kGCh];
+#pragma unroll
+  for (int j = 0; j < kGCh; ++j) c0[j] = s[j].cnt;
 #pragma unroll
   for (int k = 0; k < kGLd; ++k) {
-    const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t o1 = 16u * k + 4u * j + 1u;
-      gbyte<FMT, 0, MASK>(T, w[j], m, acc, s, bb, o1, synced, fs);
-      gbyte<FMT, 1, MASK>(T, w[j], m, acc, s, bb, o1 + 1, synced, fs);
-      gbyte<FMT, 2, MASK>(T, w[j], m, acc, s, bb, o1 + 2, synced, fs);
-      gbyte<FMT, 3, MASK>(T, w[j], m, acc, s, bb, o1 + 3, synced, fs);
+    for (int d = 0; d < 4; ++d) {
+#pragma unroll
+      for (int j = 0; j < kGCh; ++j) {
+        const uint32_t w = d == 0 ? v[j][k].x : d == 1 ? v[j][k].y : d == 2 ? v[j][k].z : v[j][k].w;
+        gdword<MASK>(T, w, m[j], s[j], 16u * k + 4u * d, bb, synced[j], fs[j]);
+      }
     }
   }
-  s.sq += __umul24(s.cnt - c0, bb);  // the block's starts at offset bb
+#pragma unroll
+  for (int j = 0; j < kGCh; ++j) s[j].sq += __umul24(s[j].cnt - c0[j], bb);  // the block's starts at offset bb
 }
 
 __device__ __forceinline__ uint32_t gdist(uint64_t lim, uint64_t base)  // lim - base clamped to [0, 64]
@@ -155,11 +174,9 @@ __device__ __forceinline__ uint32_t gdist(uint64_t lim, uint64_t base)  // lim -
 
 // Tail of a lane from tile offset o (its segment end): walk until a sync
 // byte has been read.  Returns the coverage end (as xi_kernel's xtail).
-template <int FMT>
-__device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, uint64_t ts, uint32_t o,
-                                          uint32_t& m, uint32_t& acc, uint64_t& cnt, uint64_t& sst,
-                                          uint64_t& len, uint64_t hi, uint64_t rend, uint32_t at_eof, uint32_t& ovf,
-                                          bool act)
+__device__ __forceinline__ uint64_t gtail(const GTab& T, const uint8_t* g, uint64_t ts, uint32_t o, uint32_t& m,
+                                          uint64_t& cnt, uint64_t& sst, uint64_t& len, uint64_t hi, uint64_t rend,
+                                          uint32_t at_eof, uint32_t& ovf, bool act)
 {
   // (sums per 16-byte chunk, folded into 64-bit totals at the chunk's base:
   // a tail may run far when sync bytes are rare, e.g. \D over text)
@@ -176,7 +193,7 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
       bool go = act;
-      const bool walk = T.in_walk(m);
+      const bool walk = GTab::in_walk(m);
       if (go && k >= dh && !walk) {  // nothing crosses into this byte: the chain is here
         xit = base + k;
         act = go = false;
@@ -187,12 +204,10 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
         act = go = false;
       }
       const uint32_t b = (gsel4(v, k >> 2) >> (8 * (k & 3))) & 0xffu;
-      const uint32_t e = T.stepb(m, b);
+      const uint32_t e = T.step(m, b);
       if (go) {
-        const uint32_t t = e >> 2;
-        const uint32_t f = t & (e | ~acc) & 1u;
-        const uint32_t L = (e >> XG_LSHIFT) & 7u;
-        if (k >= dh && (e & XT_DEAD)) {  // the walk crossing hi died here
+        const uint32_t L = e & XG2_L, f = (e >> 3) & 1u;
+        if (k >= dh && (e & XG2_D)) {  // the walk crossing hi died here
           xit = last > hi ? last : hi;
           act = false;
         } else {
@@ -200,8 +215,7 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
           s.sq += __umul24(f, k + 1);
           s.sfl += __umul24(f, L);
           s.sl += L;
-          if (t & 1u) last = base + k + 1;
-          acc = t | (acc & ~e);
+          if (L) last = base + k + 1;
           if (k < dh && T.sy[b]) {
             xit = base + k + 1;
             act = false;
@@ -219,15 +233,14 @@ __device__ __forceinline__ uint64_t gtail(const GTab<FMT>& T, const uint8_t* g, 
 // xslow_lane rules: bytes before wlo are outside; fresh entry at `fresh`;
 // other lanes count after their first sync byte; tails to the next sync
 // byte; past hi only the crossing walk).
-template <int FMT>
-__device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t* g, uint64_t ts, uint32_t seg,
-                                               uint32_t slen, uint64_t wlo, uint64_t hi, uint64_t fresh,
-                                               uint64_t rend, uint32_t at_eof, uint64_t& cnt, uint64_t& sst,
-                                               uint64_t& len, uint64_t& fs, uint32_t& ovf)
+__device__ __forceinline__ uint64_t gslow_lane(const GTab& T, const uint8_t* g, uint64_t ts, uint32_t seg,
+                                               uint32_t slen, uint64_t wlo, uint64_t hi, uint64_t fresh, uint64_t rend,
+                                               uint32_t at_eof, uint64_t& cnt, uint64_t& sst, uint64_t& len,
+                                               uint64_t& fs, uint32_t& ovf)
 {
   bool act = ts + seg + slen > wlo && ts + seg < hi;
   bool synced = false;
-  uint32_t m = T.start_row, acc = 0;
+  uint32_t m = 0;
   uint64_t xit = ~0ull, last = 0;
   const uint64_t rend16 = (rend + 15) & ~uint64_t(15);
   uint4 vn = gload16(grsrc(g + ts, rend16 > ts ? rend16 - ts : 0), seg);
@@ -244,12 +257,11 @@ __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t
     for (uint32_t k = 0; k < 16; ++k) {
       bool go = act && k >= dl;
       if (go && k == df) {
-        m = T.start_row;
-        acc = 0;
+        m = 0;
         synced = true;
       }
       if (go && !synced && k >= dseg) act = go = false;  // no sync in the segment: covered by a tail
-      const bool walk = T.in_walk(m);
+      const bool walk = GTab::in_walk(m);
       if (go && k >= dh && !(synced && walk)) {
         if (synced) xit = base + k;
         act = go = false;
@@ -262,12 +274,10 @@ __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t
         act = go = false;
       }
       const uint32_t b = (gsel4(v, k >> 2) >> (8 * (k & 3))) & 0xffu;
-      const uint32_t e = T.stepb(m, b);
+      const uint32_t e = T.step(m, b);
       if (go) {
-        const uint32_t t = e >> 2;
-        const uint32_t f = t & (e | ~acc) & 1u;
-        const uint32_t L = (e >> XG_LSHIFT) & 7u;
-        if (k >= dh && (e & XT_DEAD)) {
+        const uint32_t L = e & XG2_L, f = (e >> 3) & 1u;
+        if (k >= dh && (e & XG2_D)) {
           xit = last > hi ? last : hi;
           act = false;
         } else if (synced) {
@@ -275,7 +285,7 @@ __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t
           s.sq += __umul24(f, k + 1);
           s.sfl += __umul24(f, L);
           s.sl += L;
-          if (t & 1u) last = base + k + 1;
+          if (L) last = base + k + 1;
           if (k < dh && T.sy[b] && k >= dseg) {  // the tail ends at a sync byte
             xit = base + k + 1;
             act = false;
@@ -284,7 +294,6 @@ __device__ __forceinline__ uint64_t gslow_lane(const GTab<FMT>& T, const uint8_t
           synced = true;
           fs = base + k;
         }
-        acc = t | (acc & ~e);
         m = e;
       }
     }
@@ -314,39 +323,37 @@ __device__ __forceinline__ uint64_t gwave_max_set(uint64_t v)
   return m;
 }
 
-
-// stage the tables of P into LDS (all threads of the block)
-template <int FMT>
-__device__ __forceinline__ GTab<FMT> gstage(const ScanParams& P, uint16_t* xg, uint8_t* c2, uint8_t* sy, int tid,
-                                            int nthreads)
+// stage the tables of P into LDS (all threads of the block): table, then the
+// byte columns and sync flags
+__device__ __forceinline__ GTab gstage(const ScanParams& P, uint8_t* smem, int tid, int nthreads)
 {
+  uint16_t* xg = reinterpret_cast<uint16_t*>(smem);
+  uint8_t* sy = smem + 2 * (size_t)P.xg_entries;
+  uint8_t* col = sy + 256;
   const uint4* src = reinterpret_cast<const uint4*>(P.xg);
   uint4* dst = reinterpret_cast<uint4*>(xg);
-  for (uint32_t i = tid; i < P.ntrans_pad / 8; i += nthreads) dst[i] = src[i];
+  for (uint32_t i = tid; i < P.xg_entries / 8; i += nthreads) dst[i] = src[i];
   for (int i = tid; i < 256; i += nthreads) {
-    c2[i] = (uint8_t)(2 * P.cls[i]);
+    col[i] = P.xg_cls[i];
     sy[i] = P.xg_sync[i];
   }
   __syncthreads();
-  GTab<FMT> T;
-  T.xg = xg;
-  T.c2 = c2;
+  GTab T;
+  T.xg = reinterpret_cast<const uint8_t*>(xg);
+  T.col = col;
   T.sy = sy;
-  T.rowmask = ~((1u << P.log_row) - 1u);
-  T.start_row = P.start;
+  T.stride = P.xg_stride;
   return T;
 }
 
 }  // namespace
 
-template <int FMT>
 __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
 {
-  __shared__ __attribute__((aligned(16))) uint16_t gxg[kGMaxEntries];
-  __shared__ uint8_t gc2[256], gsy[256];
+  extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const GTab<FMT> T = gstage<FMT>(P, gxg, gc2, gsy, tid, kGWaves * 64);
+  const GTab T = gstage(P, gsm, tid, kGWaves * 64);
 
   const uint64_t gw = (uint64_t)blockIdx.x * kGWaves + wid;
   uint64_t tb = P.t0 + gw * P.tpb;
@@ -356,7 +363,6 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
   const uint64_t whi = clampu(te * kGTile, P.lo, P.hi);
   const uint32_t n = (uint32_t)(te - tb);
   const bool first_wave = wlo == P.lo;
-  const uint32_t seg = (uint32_t)lane * kGS;
 
   uint64_t cnt = 0, sst = 0, len = 0;
   uint64_t entry = first_wave ? wlo : ~0ull, exit = whi;
@@ -373,39 +379,52 @@ __global__ __launch_bounds__(kGWaves * 64) void xg_kernel(ScanParams P)
       has_edge = true;
       continue;
     }
-    bool synced = first_wave && i == 0 && lane == 0 && ts == wlo;  // fresh entry at the tile start
-    uint32_t fs = ~0u, m = T.start_row, acc = 0;
-    GSum s4;  // main loop: cnt, sq and sfl x4
-    uint4 cur[kGLd], nxt[kGLd];
+    bool synced[kGCh];
+    uint32_t fs[kGCh], m[kGCh], seg[kGCh];
+    GSum s[kGCh];
+    uint4 cur[kGCh][kGLd], nxt[kGCh][kGLd];
 #pragma unroll
-    for (int k = 0; k < kGLd; ++k) cur[k] = gload16(rs, seg + 16u * k);
+    for (int j = 0; j < kGCh; ++j) {
+      seg[j] = (uint32_t)(lane + 64 * j) * kGS;
+      synced[j] = first_wave && i == 0 && lane == 0 && j == 0 && ts == wlo;  // fresh entry at the tile start
+      fs[j] = ~0u;
+      m[j] = 0;
+#pragma unroll
+      for (int k = 0; k < kGLd; ++k) cur[j][k] = gload16(rs, seg[j] + 16u * k);
+    }
     for (uint32_t b = 0; b < (uint32_t)kGBlocks; ++b) {
       const uint32_t nb = b + 1 < (uint32_t)kGBlocks ? b + 1 : b;
 #pragma unroll
-      for (int k = 0; k < kGLd; ++k) nxt[k] = gload16(rs, seg + nb * kGBlk + 16u * k);
-      if (__ballot(!synced))
-        gblock<FMT, true>(T, cur, m, acc, s4, synced, fs, b * kGBlk);
-      else
-        gblock<FMT, false>(T, cur, m, acc, s4, synced, fs, b * kGBlk);
+      for (int j = 0; j < kGCh; ++j)
 #pragma unroll
-      for (int k = 0; k < kGLd; ++k) cur[k] = nxt[k];
+        for (int k = 0; k < kGLd; ++k) nxt[j][k] = gload16(rs, seg[j] + nb * kGBlk + 16u * k);
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < kGCh; ++j) any = any || !synced[j];
+      if (__ballot(any))
+        gblock<true>(T, cur, m, s, synced, fs, b * kGBlk);
+      else
+        gblock<false>(T, cur, m, s, synced, fs, b * kGBlk);
+#pragma unroll
+      for (int j = 0; j < kGCh; ++j)
+#pragma unroll
+        for (int k = 0; k < kGLd; ++k) cur[j][k] = nxt[j][k];
     }
-    GSum s;
-    s.cnt = s4.cnt >> 2;
-    s.sq = s4.sq >> 2;
-    s.sfl = s4.sfl >> 2;
-    s.sl = s4.sl;
-    if (!synced) s = GSum();  // covered by an earlier tail
-    acc = (acc >> 2) & 1u;    // the tail keeps the accepted bit in bit 0
-    gfold(s, ts + seg, cnt, sst, len);
-    const uint64_t xit =
-        gtail<FMT>(T, P.g, ts, seg + kGS, m, acc, cnt, sst, len, P.hi, P.rend, P.at_eof, ovf, synced);
-    const uint64_t f = synced && fs != ~0u ? ts + seg + fs : ~0ull;
+    uint64_t f = ~0ull, xmax = 0;
+#pragma unroll
+    for (int j = 0; j < kGCh; ++j) {
+      if (!synced[j]) s[j] = GSum();  // covered by an earlier tail
+      gfold(s[j], ts + seg[j], cnt, sst, len);
+      const uint64_t xit =
+          gtail(T, P.g, ts, seg[j] + kGS, m[j], cnt, sst, len, P.hi, P.rend, P.at_eof, ovf, synced[j]);
+      if (synced[j] && fs[j] != ~0u && ts + seg[j] + fs[j] < f) f = ts + seg[j] + fs[j];
+      if (xit != ~0ull && xit > xmax) xmax = xit;
+    }
     if (entry == ~0ull) {
       const uint64_t mn = gwave_min64(f);
       if (mn != ~0ull) entry = mn + 1;
     }
-    const uint64_t mx = gwave_max_set(xit);
+    const uint64_t mx = gwave_max_set(xmax ? xmax : ~0ull);
     if (mx) exit = mx;
   }
   if (entry == ~0ull && !has_edge) entry = exit;
@@ -437,14 +456,12 @@ struct GBlockRed {
   uint64_t v[kGEdgeThreads / 64][5];
 };
 
-template <int FMT>
 __global__ __launch_bounds__(kGEdgeThreads) void xg_edge_kernel(ScanParams P, GEdges E)
 {
-  __shared__ __attribute__((aligned(16))) uint16_t gxg[kGMaxEntries];
-  __shared__ uint8_t gc2[256], gsy[256];
+  extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
   __shared__ GBlockRed R;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const GTab<FMT> T = gstage<FMT>(P, gxg, gc2, gsy, tid, kGEdgeThreads);
+  const GTab T = gstage(P, gsm, tid, kGEdgeThreads);
   const uint32_t seg = (uint32_t)tid * kGEdgeSeg;
   uint32_t ovf = 0;
   for (uint32_t k = 0; k < E.n; ++k) {
@@ -457,7 +474,7 @@ __global__ __launch_bounds__(kGEdgeThreads) void xg_edge_kernel(ScanParams P, GE
     const uint64_t fresh = wlo == P.lo && t == tb ? wlo : ~0ull;
     uint64_t fs = ~0ull, cnt = 0, sst = 0, len = 0;
     const uint64_t xit =
-        gslow_lane<FMT>(T, P.g, ts, seg, kGEdgeSeg, wlo, P.hi, fresh, P.rend, P.at_eof, cnt, sst, len, fs, ovf);
+        gslow_lane(T, P.g, ts, seg, kGEdgeSeg, wlo, P.hi, fresh, P.rend, P.at_eof, cnt, sst, len, fs, ovf);
     const uint64_t c = wave_sum(cnt), sm = wave_sum(sst), l = wave_sum(len);
     const uint64_t mx = gwave_max_set(xit), mf = gwave_min64(fs);
     if (lane == 0) {
@@ -505,24 +522,34 @@ hipError_t launch_xg(const ScanParams& P, hipStream_t stream)
     E.wave[E.n] = (P.t1 - 1 - P.t0) / P.tpb;
     ++E.n;
   }
-  if (P.log_row == 8) {
-    hipLaunchKernelGGL(xg_kernel<0>, dim3(P.grid), dim3(kGWaves * 64), 0, stream, P);
-    hipLaunchKernelGGL(xg_edge_kernel<0>, dim3(1), dim3(kGEdgeThreads), 0, stream, P, E);
-  } else {
-    hipLaunchKernelGGL(xg_kernel<1>, dim3(P.grid), dim3(kGWaves * 64), 0, stream, P);
-    hipLaunchKernelGGL(xg_edge_kernel<1>, dim3(1), dim3(kGEdgeThreads), 0, stream, P, E);
-  }
+  const size_t smem = xg_smem_bytes(P.xg_entries);
+  hipError_t e;
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(xg_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)smem)) != hipSuccess ||
+      (e = hipFuncSetAttribute(reinterpret_cast<const void*>(xg_edge_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(xg_kernel, dim3(P.grid), dim3(kGWaves * 64), smem, stream, P);
+  hipLaunchKernelGGL(xg_edge_kernel, dim3(1), dim3(kGEdgeThreads), smem, stream, P, E);
   return hipGetLastError();
 }
 
-hipError_t xg_occupancy(uint32_t format, int* n)
+size_t xg_smem_bytes(uint32_t entries) { return 2 * (size_t)entries + 512; }
+
+hipError_t xg_occupancy(uint32_t entries, int* n)
 {
-  if (format == 0) return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xg_kernel<0>, kGWaves * 64, 0);
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xg_kernel<1>, kGWaves * 64, 0);
+  const size_t smem = xg_smem_bytes(entries);
+  if (2 * (size_t)entries > kGMaxTableBytes) {
+    *n = 0;
+    return hipSuccess;
+  }
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(xg_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  if (e != hipSuccess) return e;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xg_kernel, kGWaves * 64, smem);
 }
 
 uint32_t xg_unit() { return kGTile; }
 uint32_t xg_waves() { return kGWaves; }
-uint32_t xg_max_entries() { return kGMaxEntries; }
 
 }  // namespace ugpu
