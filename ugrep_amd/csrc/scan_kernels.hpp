@@ -67,8 +67,8 @@ struct DevTotals {
 #define UGPU_FLAG_CAPACITY 2u
 // a stitch (fix_kernel rounds or one merge walk) ran past its work budget: the
 // FIND chains of this table do not resynchronise on this input (e.g. \D\D over
-// text without digits); the totals are invalid and the host reports
-// UGPU_UNSUPPORTED, so the caller keeps the CPU matcher
+// text without digits); the totals are invalid and the host resolves the
+// range with the forest FIND (forest.hip)
 #define UGPU_FLAG_BUDGET 4u
 
 struct ScanParams {
