@@ -129,7 +129,7 @@ def gpu_reference_check(pat, buf, sample, want, sptr):
             "fields": ["count", "digest", "dcap"]}
 
 
-KERNELS = {0: "sparse_kernel", 1: "dense_kernel", 2: "xi_kernel", 3: "xg_kernel", 4: "wfind_kernel"}
+KERNELS = {0: "sparse_kernel", 1: "dense_kernel", 2: "xi_kernel", 3: "xg_kernel", 4: "wfind_kernel", 5: "xc_kernel"}
 
 
 def measured_traffic(cfg, nbytes, kernel):

@@ -57,6 +57,7 @@ struct ugpu_scanner {
   bool sparse = false;   // prefiltered wave-persistent kernel (sparse_kernel.hip)
   bool xi = false;       // COUNT scans run xi_kernel (immediate tables); OFFSETS use the dense kernel
   bool xg = false;       // COUNT scans run xg_kernel (gap tables); OFFSETS use the dense kernel
+  bool xc = false;       // COUNT scans run xc_kernel (two-state tables); OFFSETS use the dense kernel
   bool word = false;     // option W: every pass runs wfind_kernel (wfind.hip)
   size_t smem = 0;       // sparse / dense kernel
   size_t xi_smem = 0;
@@ -145,6 +146,13 @@ uint32_t fix_rounds_for(const ScanParams& P)
   return (uint32_t)r;
 }
 
+// two-state tables run xc_kernel for COUNT scans (UGPU_XC=0: xi/xg/dense)
+bool dfa_xc(const ugpu_dfa* d)
+{
+  const char* env = std::getenv("UGPU_XC");
+  return d->t.xc && !d->t.filter && d->t.cap1 != 0 && !d->d_wtab && !(env && env[0] == '0');
+}
+
 void fill_tables(ScanParams& P, const ugpu_dfa* d)
 {
   P.trans = d->d_trans;
@@ -166,6 +174,8 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.cap1 = d->t.cap1;
   P.wtab = d->d_wtab;
   P.nwtab = d->nwtab;
+  for (int i = 0; i < 14; ++i) P.xc[i] = d->t.xc_k[i];
+  P.xc_shape = d->t.xc_shape;
   // chain bytes one stitch merge may cross before the chains count as not
   // resynchronising (two chains of a resynchronising table meet within a match
   // or two; longer merges go to the forest FIND)
@@ -213,6 +223,8 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
 {
   if (s->word)
     geometry(P, dbuf, lo, hi, read_end, s->max_rec, wfind_unit(), wfind_waves(), off);
+  else if (xi && s->xc)
+    geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xc_unit(), xc_waves(), off);
   else if (xi && s->xg)
     geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xg_unit(), xg_waves(), off);
   else if (xi)
@@ -226,6 +238,7 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
 hipError_t launch_main(const ugpu_scanner* s, const ScanParams& P, bool write, hipStream_t st, bool xi = false)
 {
   if (s->word) return launch_wfind(P, s->dfa->t.format, write, st);
+  if (xi && s->xc) return launch_xc(P, st);
   if (xi && s->xg) return launch_xg(P, st);
   if (xi) return launch_xi(P, s->xi_smem, st);
   if (s->sparse) return launch_sparse(P, write, s->smem, st);
@@ -408,6 +421,7 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   const char* genv = std::getenv("UGPU_XG");
   info->kernel = (d->d_wtab && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
                  : (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
+                 : dfa_xc(d)                                   ? 5u
                  : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u
                  : (d->d_xg && !(genv && genv[0] == '0'))  ? 3u
                                                            : 1u;
@@ -432,6 +446,7 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
   info->kernel = (t.filter && t.format == FMT_BYTE) ? 0u
+                 : (t.xc && t.cap1 != 0)             ? 5u
                  : (t.immediate && t.cap1 != 0)      ? 2u
                  : (t.gap && t.cap1 != 0)            ? 3u
                                                      : 1u;
@@ -507,6 +522,19 @@ int ugpu_tables_gap_host(const uint32_t* opc, uint32_t nop, uint16_t* xg, uint32
   return UGPU_OK;
 }
 
+int ugpu_tables_xc_host(const uint32_t* opc, uint32_t nop, uint32_t* shape, uint32_t* k, int* ok)
+{
+  if (!ok || !shape || !k) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *ok = t.xc ? 1 : 0;
+  *shape = t.xc_shape;
+  std::copy(t.xc_k, t.xc_k + 14, k);
+  return UGPU_OK;
+}
+
 int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
 {
   if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
@@ -550,7 +578,9 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
     *out = s;
     return UGPU_OK;
   }
-  s->sparse = dfa->t.filter && dfa->t.format == FMT_BYTE;
+  // (UGPU_SPARSE=0: prefiltered tables take the dense-pattern kernels; testing)
+  const char* senv = std::getenv("UGPU_SPARSE");
+  s->sparse = dfa->t.filter && dfa->t.format == FMT_BYTE && !(senv && senv[0] == '0');
   s->smem = s->sparse ? sparse_smem_bytes(dfa->ntrans_pad, dfa->t.states)
                       : dense_smem_bytes(dfa->t.format, dfa->ntrans_pad, dfa->t.states);
   if (s->smem > 160 * 1024) {
@@ -605,6 +635,22 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
       }
     }
   }
+  // two-state tables: COUNT scans on xc_kernel, ahead of xi/xg (UGPU_XC=0
+  // keeps those)
+  if (!s->sparse && dfa_xc(dfa)) {
+    int cpc = 0;
+    HIP_TRY_S(xc_occupancy(&cpc));
+    if (cpc >= 1) {
+      s->xc = true;
+      s->xi = s->xg = false;
+      const int cg = prop.multiProcessorCount * cpc * (int)xc_waves();
+      s->xi_rec = cg > kMaxRec ? kMaxRec : cg;
+      if (const char* env = std::getenv("UGPU_MAX_GRID")) {
+        int v = std::atoi(env);
+        if (v >= 1 && v <= kMaxRec) s->xi_rec = v;
+      }
+    }
+  }
   HIP_TRY_S(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
   HIP_TRY_S(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
   HIP_TRY_S(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
@@ -644,7 +690,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P{};
   fill_tables(P, s->dfa);
-  geometry_for(P, s, dbuf, lo, hi, read_end, s->off, s->xi || s->xg);
+  geometry_for(P, s, dbuf, lo, hi, read_end, s->off, s->xi || s->xg || s->xc);
   P.delta = (int64_t)bias - (int64_t)s->off;
   P.at_eof = at_eof ? 1u : 0u;
   if (const char* ab = std::getenv("UGPU_ABLATE")) P.ablate = (uint32_t)std::atoi(ab);
@@ -658,13 +704,13 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
              (int)s->sparse, (int)s->word);
   HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
   HIP_TRY(hipEventRecord(s->ev0, st));
-  HIP_TRY(launch_main(s, P, false, st, s->xi || s->xg));
+  HIP_TRY(launch_main(s, P, false, st, s->xi || s->xg || s->xc));
   HIP_TRY(hipEventRecord(s->ev1, st));
   HIP_TRY(launch_fix(P, s->dfa->t.format, st));
   HIP_TRY(hipMemcpyAsync(s->h_tot, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   s->last = P;
-  s->last_xi = s->xi || s->xg;
+  s->last_xi = s->xi || s->xg || s->xc;
   s->last_buf = dbuf;
   s->last_args[0] = lo;
   s->last_args[1] = hi;

@@ -120,6 +120,9 @@ struct ScanParams {
   // merge may cross before giving up (fix_kernel, chain_fix_kernel)
   uint32_t max_rounds;
   uint64_t merge_budget;
+  // two-state tables (xc_kernel.hip): the byte-class range program (tables.hpp)
+  uint32_t xc[14];
+  uint32_t xc_shape;
 };
 
 // Forest FIND (forest.hip): exact for every table, no resynchronisation
@@ -205,6 +208,11 @@ hipError_t xg_occupancy(uint32_t entries, int* blocks_per_cu);  // 0 blocks: the
 size_t xg_smem_bytes(uint32_t entries);
 uint32_t xg_unit();
 uint32_t xg_waves();
+// two-state carry-chain kernel, xc_kernel.hip (COUNT mode only)
+hipError_t launch_xc(const ScanParams& P, hipStream_t stream);
+hipError_t xc_occupancy(int* blocks_per_cu);
+uint32_t xc_unit();
+uint32_t xc_waves();
 // dense wave-persistent kernel, dense_kernel.hip
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);
 hipError_t dense_occupancy(uint32_t format, bool cap1, bool xt, size_t smem, int* blocks_per_cu);

@@ -117,6 +117,17 @@ def host_gap(opc):
     return (x, sy) if ok.value else None
 
 
+def host_xc(opc):
+    """Range program of xc_kernel (two-state tables): (shape, k uint32[14]) or None."""
+    a = np.ascontiguousarray(opc, dtype=np.uint32)
+    p = a.ctypes.data_as(_lib.c_u32p)
+    shape = ctypes.c_uint32(0)
+    ok = ctypes.c_int(0)
+    k = np.zeros(14, np.uint32)
+    check(lib.ugpu_tables_xc_host(p, len(a), ctypes.byref(shape), k.ctypes.data_as(_lib.c_u32p), ctypes.byref(ok)))
+    return (shape.value, k) if ok.value else None
+
+
 class Pattern:
     """Compiled pattern (opcode words) with its device tables."""
 
