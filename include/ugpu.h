@@ -146,12 +146,14 @@ int ugpu_tables_immediate_host(const uint32_t *opc, uint32_t nop, uint8_t *xid, 
    *gap = 0 (nothing written) when the table does not qualify. */
 int ugpu_tables_gap_host(const uint32_t *opc, uint32_t nop, uint16_t *xg, uint32_t xg_cap, uint8_t *sync, int *gap);
 
-/* Host-only: the byte-class range program of xc_kernel (two-state tables:
-   start --G--> A --X--> A, ugrep_amd/csrc/tables.hpp): *shape = NF | NG << 4
-   | NP << 8 range tests, k[14] their per-byte add constants.  *ok = 0 when the
-   table does not qualify.  (Replaces, for these tables, the per-byte opcode
-   scan of lib/matcher.cpp:460-545.) */
-int ugpu_tables_xc_host(const uint32_t *opc, uint32_t nop, uint32_t *shape, uint32_t *k, int *ok);
+/* Host-only: the byte classes of xc_kernel (two-state tables: start --G--> A
+   --X--> A, ugrep_amd/csrc/tables.hpp): cls[256] = G << 7 | X << 6 (may be
+   NULL), and the SWAR range program of the same sets, *shape = NF | NG << 4 |
+   NP << 8 range tests with k[14] their per-byte add constants (*shape = 0 when
+   the sets do not fit one).  *ok = 0 when the table does not qualify.
+   (Replaces, for these tables, the per-byte opcode scan of
+   lib/matcher.cpp:460-545.) */
+int ugpu_tables_xc_host(const uint32_t *opc, uint32_t nop, uint8_t *cls, uint32_t *shape, uint32_t *k, int *ok);
 
 /* --- whole-buffer FIND (Matcher::buffer(); while (find()) ...) --- */
 

@@ -1,8 +1,9 @@
 """CPU: the two-state carry-chain FIND of xc_kernel (ugrep_amd/csrc/xc_kernel.hip).
 
-1. The range program that tables.cpp derives from a table (ugpu_tables_xc_host)
-   reproduces the table's G (start -> A) and X (A -> A) byte sets exactly, when
-   evaluated with the kernel's SWAR arithmetic on all 256 bytes.
+1. The byte classes tables.cpp derives from a table (ugpu_tables_xc_host: the
+   LDS class table, and the SWAR range program of the UGPU_XC_SWAR build)
+   reproduce the table's G (start -> A) and X (A -> A) byte sets exactly, the
+   range program evaluated with the kernel's SWAR arithmetic on all 256 bytes.
 2. The kernel's arithmetic -- one big addition S = X' + G' over the byte
    encoding X' = 0x7f | X << 7, G' = G << 7, carry-in bytes S ^ X' ^ G', starts
    G & !carry, the exit rule past hi -- restated here with Python integers over
@@ -88,9 +89,13 @@ def test_range_program_reproduces_byte_sets(patterns):
             continue
         seen += 1
         G, X, _ = _sets(p["opc"])
-        g, x = _classify(xc[0], xc[1], np.arange(256, dtype=np.uint8))
-        assert np.array_equal(g, G), name
-        assert np.array_equal(x, X), name
+        cls, shape, k = xc
+        assert np.array_equal((cls & 0x80) != 0, G), name  # the LDS class table
+        assert np.array_equal((cls & 0x40) != 0, X), name
+        if shape:
+            g, x = _classify(shape, k, np.arange(256, dtype=np.uint8))
+            assert np.array_equal(g, G), name
+            assert np.array_equal(x, X), name
     assert seen >= 2
 
 
@@ -112,7 +117,10 @@ def test_range_program_on_synthetic_sets():
         if xc is None:
             continue
         G, X, _ = _sets(opc)
-        g, x = _classify(xc[0], xc[1], np.arange(256, dtype=np.uint8))
+        assert np.array_equal((xc[0] & 0x80) != 0, G) and np.array_equal((xc[0] & 0x40) != 0, X), rx
+        if not xc[1]:
+            continue  # more ranges than the SWAR shapes hold: the LDS classes only
+        g, x = _classify(xc[1], xc[2], np.arange(256, dtype=np.uint8))
         assert np.array_equal(g, G), rx
         assert np.array_equal(x, X), rx
         done += 1
@@ -176,7 +184,7 @@ def _inputs():
 @pytest.mark.parametrize("pname", TWO_STATE)
 def test_restated_arithmetic_equals_oracle(patterns, pname):
     opc = patterns[pname]["opc"]
-    shape, k = _xc(opc)
+    _, shape, k = _xc(opc)
     rng = np.random.default_rng(11)
     for name, host in _inputs().items():
         n = host.size
@@ -194,7 +202,7 @@ def test_restated_arithmetic_equals_oracle(patterns, pname):
 
 def test_restated_halo_at_readable_end(patterns):
     opc = patterns["c3_ident"]["opc"]
-    shape, k = _xc(opc)
+    _, shape, k = _xc(opc)
     data = np.frombuffer(b"abc def ghij", np.uint8)
     # readable end inside "ghij", not EOF: the match may go on
     assert xc_restated(shape, k, 1, data, 0, 9, 10, False)[4]

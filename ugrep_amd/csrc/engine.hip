@@ -175,7 +175,8 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.wtab = d->d_wtab;
   P.nwtab = d->nwtab;
   for (int i = 0; i < 14; ++i) P.xc[i] = d->t.xc_k[i];
-  P.xc_shape = d->t.xc_shape;
+  P.xc_shape = d->t.xc_swar ? d->t.xc_shape : 0;
+  P.xc_cls = d->d_cls + 256;
   // chain bytes one stitch merge may cross before the chains count as not
   // resynchronising (two chains of a resynchronising table meet within a match
   // or two; longer merges go to the forest FIND)
@@ -337,10 +338,12 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
   std::vector<uint16_t> tr(d->ntrans_pad, 0);
   std::copy(d->t.trans.begin(), d->t.trans.end(), tr.begin());
   if ((e = hipMalloc(&d->d_trans, tr.size() * 2)) != hipSuccess ||
-      (e = hipMalloc(&d->d_cls, 256)) != hipSuccess ||
+      (e = hipMalloc(&d->d_cls, 512)) != hipSuccess ||  // cls, then the xc byte classes
       (e = hipMalloc(&d->d_caps, d->t.caps.size() * 4)) != hipSuccess ||
       (e = hipMemcpy(d->d_trans, tr.data(), tr.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(d->d_cls, d->t.cls.data(), 256, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(d->d_cls + 256, d->t.xc ? d->t.xc_tab.data() : d->t.cls.data(), 256, hipMemcpyHostToDevice)) !=
+          hipSuccess ||
       (e = hipMemcpy(d->d_caps, d->t.caps.data(), d->t.caps.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
     ugpu_dfa_destroy(d);
     return hip_fail(e, "table upload");
@@ -522,7 +525,7 @@ int ugpu_tables_gap_host(const uint32_t* opc, uint32_t nop, uint16_t* xg, uint32
   return UGPU_OK;
 }
 
-int ugpu_tables_xc_host(const uint32_t* opc, uint32_t nop, uint32_t* shape, uint32_t* k, int* ok)
+int ugpu_tables_xc_host(const uint32_t* opc, uint32_t nop, uint8_t* cls, uint32_t* shape, uint32_t* k, int* ok)
 {
   if (!ok || !shape || !k) return fail(UGPU_INVAL, "NULL argument");
   DfaTables t;
@@ -530,8 +533,9 @@ int ugpu_tables_xc_host(const uint32_t* opc, uint32_t nop, uint32_t* shape, uint
   int rc = build_tables(opc, nop, t, err);
   if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
   *ok = t.xc ? 1 : 0;
-  *shape = t.xc_shape;
+  *shape = t.xc_swar ? t.xc_shape : 0;
   std::copy(t.xc_k, t.xc_k + 14, k);
+  if (cls && t.xc) std::copy(t.xc_tab.begin(), t.xc_tab.end(), cls);
   return UGPU_OK;
 }
 

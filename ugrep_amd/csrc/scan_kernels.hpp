@@ -123,6 +123,7 @@ struct ScanParams {
   // two-state tables (xc_kernel.hip): the byte-class range program (tables.hpp)
   uint32_t xc[14];
   uint32_t xc_shape;
+  const uint8_t* xc_cls;  // byte classes G << 7 | X << 6 (256 B)
 };
 
 // Forest FIND (forest.hip): exact for every table, no resynchronisation

@@ -577,10 +577,16 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       if (nx && nx != A) ok = false;
       G[c] = nxt[(size_t)start_sid * 256 + c] == A;
       X[c] = nx == A;
-      if ((G[c] && !X[c]) || (c >= 0x80 && X[c])) ok = false;
+      if (G[c] && !X[c]) ok = false;
     }
-    if (ok) ok = xc_program(G, X, t.xc_shape, t.xc_k);
-    t.xc = ok;
+    if (ok) {
+      t.xc = true;
+      t.xc_tab.assign(256, 0);
+      for (int c = 0; c < 256; ++c) t.xc_tab[c] = (uint8_t)((G[c] ? 0x80 : 0) | (X[c] ? 0x40 : 0));
+      bool ascii = true;
+      for (int c = 0x80; c < 256; ++c) ascii = ascii && !X[c];
+      t.xc_swar = ascii && xc_program(G, X, t.xc_shape, t.xc_k);
+    }
   }
   t.start = start_sid * R;
   t.accepting = S - first_acc;

@@ -49,7 +49,13 @@ namespace {
 
 constexpr int kCWaves = 4;             // waves per workgroup
 constexpr uint32_t kCChunk = 1024;     // one wave-load: 16 bytes per lane
-constexpr int kCIter = 4;              // chunks per iteration (loads in flight per wave)
+#ifndef UGPU_XC_ITER
+#define UGPU_XC_ITER 4
+#endif
+#ifndef UGPU_XC_MINW
+#define UGPU_XC_MINW 1  // waves per SIMD the register budget must allow
+#endif
+constexpr int kCIter = UGPU_XC_ITER;   // chunks per iteration (loads in flight per wave)
 constexpr uint32_t kCTile = kCChunk * kCIter;
 constexpr int kCLook = 8;              // look-back chunks before giving up
 
@@ -93,6 +99,30 @@ struct CProg {
     for (int i = 0; i < NP; ++i) p |= (x7 + k[10 + 2 * i]) & ~(x7 + k[11 + 2 * i]);
     X = (p & ~x) | G | 0x7f7f7f7fu;
   }
+};
+
+// The byte classes by lookup (the default): xc_cls[byte] = G << 7 | X << 6 in
+// LDS, four independent ds_read_u8 per dword (any byte sets, ASCII or not).
+// Text bytes < 0x80 sit in 32 dwords, one per bank: lanes never conflict.
+struct CLds {
+  const uint8_t* t;
+  __device__ __forceinline__ void operator()(uint32_t x, uint32_t& G, uint32_t& X) const
+  {
+    const uint32_t r0 = t[x & 0xffu] | ((uint32_t)t[(x >> 16) & 0xffu] << 16);
+    const uint32_t r1 = t[(x >> 8) & 0xffu] | ((uint32_t)t[x >> 24] << 16);
+    const uint32_t e = r0 | (r1 << 8);
+    G = e & 0x80808080u;
+    X = (e << 1) | 0x7f7f7f7fu;  // (bit 7 of a byte shifts into the next byte's bit 0, which is set anyway)
+  }
+};
+
+template <int NF, int NG, int NP>
+struct CSel {
+  typedef CProg<NF, NG, NP> type;
+};
+template <>
+struct CSel<-1, 0, 0> {
+  typedef CLds type;
 };
 
 // bytes of the dword at q that lie below lim (0xff per byte)
@@ -185,10 +215,38 @@ template <bool MASK, class PROG>
 __device__ __forceinline__ void cchunk(const PROG& pr, const uint4& v, uint64_t q, const CLim& lim, uint32_t& cw,
                                        uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4])
 {
+#if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 1  // loads only (benchmarking; wrong counts)
+  if (!MASK) {
+    cs += v.x ^ v.y ^ v.z ^ v.w;
+    return;
+  }
+#endif
   CLane L;
+#if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 4  // trivial classes (benchmarking; wrong counts)
+  if (!MASK) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      L.G[d] = w[d] & 0x80808080u;
+      L.X[d] = w[d] | 0x7f7f7f7fu;
+    }
+  } else
+#endif
   cclass<MASK>(pr, v, L, q, lim);
   bool prop;
   const bool gen = cadd(L, prop);
+#if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 3  // no events (benchmarking; wrong counts)
+  if (!MASK) {
+    cs += L.S[0] ^ L.S[1] ^ L.S[2] ^ L.S[3] ^ (gen ? 1u : 0u) ^ (prop ? 2u : 0u);
+    return;
+  }
+#endif
+#if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 2  // no lane carry-lookahead (benchmarking; wrong counts)
+  if (!MASK) {
+    cfinish(L, gen ^ prop ? 1u : 0u, cs, ws, ls, cb);
+    return;
+  }
+#endif
   const uint64_t cin = clook(__ballot(gen), __ballot(prop), cw, cw);
   cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb);
 }
@@ -220,11 +278,18 @@ __device__ __forceinline__ uint64_t cexit(const uint32_t cb[4], uint64_t q, uint
 }  // namespace
 
 template <int NF, int NG, int NP>
-__global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
+__global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanParams P)
 {
-  CProg<NF, NG, NP> pr;
+  typename CSel<NF, NG, NP>::type pr;
+  __shared__ uint32_t ctab[NF < 0 ? 64 : 1];
+  if constexpr (NF < 0) {
+    if (threadIdx.x < 64) ctab[threadIdx.x] = reinterpret_cast<const uint32_t*>(P.xc_cls)[threadIdx.x];
+    __syncthreads();
+    pr.t = reinterpret_cast<const uint8_t*>(ctab);
+  } else {
 #pragma unroll
-  for (int i = 0; i < 14; ++i) pr.k[i] = P.xc[i];
+    for (int i = 0; i < 14; ++i) pr.k[i] = P.xc[i];
+  }
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kCWaves + wid;
@@ -297,8 +362,10 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
     }
   };
   uint64_t q0 = wlo & ~uint64_t(kCChunk - 1);
+#ifndef UGPU_XC_NOEDGE
   if (fte > ftb)
     for (; q0 < ftb * kCTile; q0 += kCChunk) masked(q0);
+#endif
 
   uint4 cur[kCIter], nxt[kCIter];
   if (fte > ftb) {
@@ -319,9 +386,14 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
     uint32_t cb[4];
 #pragma unroll
     for (int j = 0; j < kCIter; ++j) cchunk<false>(pr, cur[j], 0, lim, cw, a.cs[j], a.ws, a.ls, cb);
-    const uint32_t c = a.cs[0] + a.cs[1] + a.cs[2] + a.cs[3];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kCIter; ++j) c += a.cs[j];
     cnt += c;
-    pos += (uint64_t)c * (ts + lo16) + (a.ws >> 7) + kCChunk * (a.cs[1] + 2 * a.cs[2] + 3 * a.cs[3]);
+    uint32_t cj = 0;
+#pragma unroll
+    for (int j = 1; j < kCIter; ++j) cj += j * a.cs[j];
+    pos += (uint64_t)c * (ts + lo16) + (a.ws >> 7) + kCChunk * cj;
     lbits += a.ls;
 #pragma unroll
     for (int j = 0; j < kCIter; ++j) cur[j] = nxt[j];
@@ -331,8 +403,10 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   // (the match crossing hi runs on through X bytes, no starts past hi).  Bytes
   // past the readable end are K, so the search ends at the latest in the chunk
   // after the one holding rend (its loads read nothing: the resource is empty).
+#ifndef UGPU_XC_NOEDGE
   if (n)
     for (; q0 < whi || (last_wave && !found); q0 += kCChunk) masked(q0);
+#endif
   if (found) cw = 0;  // past the exit every carry is clear
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
   const uint64_t c = wave_sum(cnt), s = wave_sum(pos), lb = wave_sum(lbits);
@@ -359,6 +433,7 @@ hipError_t launch_shape(const ScanParams& P, hipStream_t stream)
   hipLaunchKernelGGL((xc_kernel<NF, NG, NP>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   return hipGetLastError();
 }
+#ifdef UGPU_XC_SWAR
 template <int NF, int NG>
 hipError_t launch_np(const ScanParams& P, uint32_t np, hipStream_t stream)
 {
@@ -378,16 +453,22 @@ hipError_t launch_ng(const ScanParams& P, uint32_t ng, uint32_t np, hipStream_t 
     default: return launch_np<NF, 3>(P, np, stream);
   }
 }
+#endif
 }  // namespace
 
+// The SWAR classifier (range tests instead of the LDS lookup) is a build
+// option, UGPU_XC_SWAR (measured slower on C3: docs in DESIGN.md).
 hipError_t launch_xc(const ScanParams& P, hipStream_t stream)
 {
+#ifdef UGPU_XC_SWAR
   const uint32_t nf = P.xc_shape & 15, ng = (P.xc_shape >> 4) & 15, np = (P.xc_shape >> 8) & 15;
-  if (nf > 1 || ng > 3 || np > 2 || nf + ng == 0) return hipErrorInvalidValue;
-  return nf ? launch_ng<1>(P, ng, np, stream) : launch_ng<0>(P, ng, np, stream);
+  if (nf <= 1 && ng <= 3 && np <= 2 && nf + ng > 0)
+    return nf ? launch_ng<1>(P, ng, np, stream) : launch_ng<0>(P, ng, np, stream);
+#endif
+  return launch_shape<-1, 0, 0>(P, stream);
 }
 
-hipError_t xc_occupancy(int* n) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<1, 1, 1>, kCWaves * 64, 0); }
+hipError_t xc_occupancy(int* n) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<-1, 0, 0>, kCWaves * 64, 0); }
 uint32_t xc_unit() { return kCTile; }
 uint32_t xc_waves() { return kCWaves; }
 

@@ -118,14 +118,17 @@ def host_gap(opc):
 
 
 def host_xc(opc):
-    """Range program of xc_kernel (two-state tables): (shape, k uint32[14]) or None."""
+    """Byte classes of xc_kernel (two-state tables): (cls uint8[256] = G << 7 | X << 6,
+    SWAR range program shape (0: none), k uint32[14]) or None."""
     a = np.ascontiguousarray(opc, dtype=np.uint32)
     p = a.ctypes.data_as(_lib.c_u32p)
     shape = ctypes.c_uint32(0)
     ok = ctypes.c_int(0)
     k = np.zeros(14, np.uint32)
-    check(lib.ugpu_tables_xc_host(p, len(a), ctypes.byref(shape), k.ctypes.data_as(_lib.c_u32p), ctypes.byref(ok)))
-    return (shape.value, k) if ok.value else None
+    cls = np.zeros(256, np.uint8)
+    check(lib.ugpu_tables_xc_host(p, len(a), cls.ctypes.data_as(_lib.c_u8p), ctypes.byref(shape),
+                                  k.ctypes.data_as(_lib.c_u32p), ctypes.byref(ok)))
+    return (cls, shape.value, k) if ok.value else None
 
 
 class Pattern:
