@@ -80,11 +80,14 @@ typedef struct ugpu_totals
   uint32_t flags;  /* bit0: a walk hit the readable end of a non-final shard (UGPU_HALO);
                       bit3 (UGPU_TOT_FOREST): the speculative stitch did not converge (FIND chains
                       that never resynchronise, e.g. \D\D over text without digits) and the range
-                      was resolved exactly by the forest FIND (ugrep_amd/csrc/forest.hip) */
+                      was resolved exactly by the forest FIND (ugrep_amd/csrc/forest.hip);
+                      bit4 (UGPU_TOT_WFAST): option W on a \w+ table ran the non-W kernels
+                      (the scanned bytes are valid UTF-8, so W removes nothing) */
   uint32_t fix_rounds;
 } ugpu_totals;
 
 #define UGPU_TOT_FOREST 8u
+#define UGPU_TOT_WFAST 16u
 
 /* Library-owned match list for ugpu_find_all. */
 typedef struct ugpu_result
@@ -154,6 +157,11 @@ int ugpu_tables_gap_host(const uint32_t *opc, uint32_t nop, uint16_t *xg, uint32
    (Replaces, for these tables, the per-byte opcode scan of
    lib/matcher.cpp:460-545.) */
 int ugpu_tables_xc_host(const uint32_t *opc, uint32_t nop, uint8_t *cls, uint32_t *shape, uint32_t *k, int *ok);
+
+/* Host-only: *eq = 1 when two opcode tables accept the same strings with the
+   same accept indices (so their FIND chains agree on every input).  The
+   engine uses it to recognise \w+ under option W. */
+int ugpu_tables_equivalent_host(const uint32_t *opc_a, uint32_t nop_a, const uint32_t *opc_b, uint32_t nop_b, int *eq);
 
 /* --- whole-buffer FIND (Matcher::buffer(); while (find()) ...) --- */
 

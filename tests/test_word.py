@@ -78,3 +78,54 @@ def test_gpu_w_large_vs_oracle():
         assert (res.count, res.digest, res.dcap) == OracleDfa(opc).find_w(host)[:3], rx
         res = U.find_all(pat, dev, start=12345)
         assert (res.count, res.digest, res.dcap) == OracleDfa(opc).find_w(host, start=12345)[:3], rx
+
+
+def test_word_plus_is_recognised():
+    """The engine serves W on \\w+ tables by the non-W kernels when the bytes
+    are valid UTF-8; it recognises them by table equivalence with its own \\w+."""
+    import ugrep_amd as U
+    from ugrep_amd.matcher import host_equivalent
+    w = U.compile_regex(r"\w+")
+    ref = next(c["opc"] for c in CASES if c["pattern"] == r"\w+")
+    assert host_equivalent(ref, w)
+    for rx in (r"\w*x", r"[A-Za-z_][A-Za-z0-9_]*", r"\S+", r"\w+\d"):
+        assert not host_equivalent(U.compile_regex(rx), w), rx
+
+
+@pytest.mark.gpu
+def test_gpu_w_word_plus_fast_path():
+    """\\w+ with W: on valid UTF-8 the scan runs xg_kernel (UGPU_TOT_WFAST) and
+    equals the oracle's W restatement; invalid UTF-8 (a stray continuation byte
+    after a word character changes at_wb) and entries after a word character
+    fall back to wfind_kernel, also exact."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd as U
+    ref = next(c["opc"] for c in CASES if c["pattern"] == r"\w+")
+    host = gen(4, 17, 0, 24 << 20)
+    bad = host.copy()
+    bad[5 << 20] = ord("x")
+    bad[(5 << 20) + 1] = 0x80  # "x\x80a": at_wb(a) looks back past the stray byte
+    bad[(5 << 20) + 2] = ord("a")
+    for opc in (ref, U.compile_regex(r"\w+")):
+        pat = U.Pattern(opc, word=True)
+        assert pat.info()["kernel"] == 3
+        for data, fast in ((host, True), (bad, False)):
+            dev = torch.from_numpy(data).to("cuda")
+            torch.cuda.synchronize()
+            want = OracleDfa(opc).find_w(data)[:3]
+            sc = U.Scanner(pat)
+            sc.scan(dev.data_ptr(), 0, data.size, data.size, True, 0, torch.cuda.current_stream().cuda_stream)
+            t = sc.totals()
+            assert (t.count, t.digest, t.dcap) == want
+            assert bool(t.flags & 16) == fast
+            res = U.find_all(pat, dev, offsets=True)
+            assert (res.count, res.digest, res.dcap) == want
+        # entries: after a space (fast), inside a word (fallback)
+        dev = torch.from_numpy(host).to("cuda")
+        torch.cuda.synchronize()
+        sp = int(np.nonzero(host[1000:] == ord(" "))[0][0]) + 1001
+        for start in (sp, sp + 1, 777):
+            res = U.find_all(pat, dev, start=start)
+            assert (res.count, res.digest, res.dcap) == OracleDfa(opc).find_w(host, start=start)[:3], start

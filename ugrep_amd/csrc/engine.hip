@@ -28,6 +28,30 @@
 
 // Unicode Word ranges as flat [lo, hi] pairs (regex_compile.cpp, the table of \w)
 void ugpu_word_ranges(std::vector<uint32_t>& out);
+// Geometry of a UTF-8 / NUL scan of the device bytes dbuf[0, len) (U.out unset).
+ugpu::Utf8Params utf8_params(const uint8_t* dbuf, uint64_t len)
+{
+  static int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n;
+  }();
+  ugpu::Utf8Params U{};
+  U.head = reinterpret_cast<uintptr_t>(dbuf) & 15u;
+  U.g = dbuf - U.head;
+  U.len = len;
+  U.span = (U.head + len + 15u) & ~15ull;
+  const uint64_t tile = ugpu::utf8_tile();
+  const uint64_t tiles = (U.span + tile - 1) / tile;
+  const uint64_t want = (uint64_t)cus * 16;  // about 16 waves per CU
+  const uint64_t tpw = (tiles + want - 1) / want;
+  U.per = tpw * tile;
+  U.nwaves = (tiles + tpw - 1) / tpw;
+  return U;
+}
+
 
 using namespace ugpu;
 
@@ -44,6 +68,9 @@ struct ugpu_dfa {
   uint32_t* d_caps = nullptr;
   uint32_t* d_wtab = nullptr;  // option W: Unicode Word ranges (UGPU_PAT_WORD)
   uint32_t nwtab = 0;
+  // option W on a table equivalent to \w+: on valid UTF-8 the W
+  // rules remove nothing, so such scans run the non-W kernels (xg_kernel)
+  bool wplus = false;
   // idle scanners of ugpu_find_all calls on this table (reused: creating one
   // costs device allocations and property queries)
   std::mutex pool_mu;
@@ -58,7 +85,9 @@ struct ugpu_scanner {
   bool xi = false;       // COUNT scans run xi_kernel (immediate tables); OFFSETS use the dense kernel
   bool xg = false;       // COUNT scans run xg_kernel (gap tables); OFFSETS use the dense kernel
   bool xc = false;       // COUNT scans run xc_kernel (two-state tables); OFFSETS use the dense kernel
-  bool word = false;     // option W: every pass runs wfind_kernel (wfind.hip)
+  bool word = false;     // option W: every pass runs wfind_kernel (wfind.hip) (per scan when wfast)
+  bool wfast = false;    // option W on a \w+ table: non-W kernels when the scanned bytes are valid UTF-8
+  int word_rec = 0;      // chain records of a wfind scan
   size_t smem = 0;       // sparse / dense kernel
   size_t xi_smem = 0;
   int xi_rec = 0;        // chain records of an xi scan
@@ -146,6 +175,25 @@ uint32_t fix_rounds_for(const ScanParams& P)
   return (uint32_t)r;
 }
 
+// \w+ as ugpu_compile builds it (language-equivalent to the reference's table,
+// tests/test_compile.py), compiled once
+bool is_word_plus(const DfaTables& t)
+{
+  static DfaTables wp;
+  static bool ok = [] {
+    uint32_t* opc = nullptr;
+    uint32_t nop = 0;
+    if (ugpu_compile("\\w+", 3, 0, &opc, &nop) != UGPU_OK) return false;
+    std::string err;
+    const bool built = build_tables(opc, nop, wp, err) == 0;
+    ugpu_opc_free(opc);
+    return built;
+  }();
+  return ok && tables_equivalent(t, wp);
+}
+
+int utf8_scan(const uint8_t* dbuf, uint64_t len, bool nul, uint64_t* pos, void* stream);
+
 // two-state tables run xc_kernel for COUNT scans (UGPU_XC=0: xi/xg/dense)
 bool dfa_xc(const ugpu_dfa* d)
 {
@@ -223,7 +271,7 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
                   uint64_t read_end, uint64_t& off, bool xi = false)
 {
   if (s->word)
-    geometry(P, dbuf, lo, hi, read_end, s->max_rec, wfind_unit(), wfind_waves(), off);
+    geometry(P, dbuf, lo, hi, read_end, s->word_rec, wfind_unit(), wfind_waves(), off);
   else if (xi && s->xc)
     geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xc_unit(), xc_waves(), off);
   else if (xi && s->xg)
@@ -357,8 +405,13 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       ugpu_dfa_destroy(d);
       return hip_fail(e, "word table upload");
     }
-    *out = d;  // option W runs wfind_kernel only: no transducer tables
-    return UGPU_OK;
+    d->wplus = d->t.gap && !d->t.filter && d->t.cap1 != 0 && !(std::getenv("UGPU_WFAST") &&
+                                                                 std::getenv("UGPU_WFAST")[0] == '0') &&
+               is_word_plus(d->t);
+    if (!d->wplus) {
+      *out = d;  // option W runs wfind_kernel only: no transducer tables
+      return UGPU_OK;
+    }
   }
   if (d->t.restart_local && !d->t.filter && d->t.cap1 != 0) {
     std::vector<uint16_t> xt(d->ntrans_pad, 0);
@@ -422,7 +475,7 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->accepting = d->t.accepting;
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
-  info->kernel = (d->d_wtab && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
+  info->kernel = (d->d_wtab && !d->wplus && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
                  : (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
                  : dfa_xc(d)                                   ? 5u
                  : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u
@@ -539,6 +592,18 @@ int ugpu_tables_xc_host(const uint32_t* opc, uint32_t nop, uint8_t* cls, uint32_
   return UGPU_OK;
 }
 
+int ugpu_tables_equivalent_host(const uint32_t* opc_a, uint32_t nop_a, const uint32_t* opc_b, uint32_t nop_b, int* eq)
+{
+  if (!eq) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables a, b;
+  std::string err;
+  int rc = build_tables(opc_a, nop_a, a, err);
+  if (rc == 0) rc = build_tables(opc_b, nop_b, b, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *eq = tables_equivalent(a, b) ? 1 : 0;
+  return UGPU_OK;
+}
+
 int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
 {
   if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
@@ -565,11 +630,19 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
       return fail(UGPU_UNSUPPORTED, "tables do not fit in LDS");
     }
     s->word = true;
-    s->max_rec = kMaxRec;
+    s->word_rec = kMaxRec;
     if (const char* env = std::getenv("UGPU_MAX_GRID")) {
       int v = std::atoi(env);
-      if (v >= 1 && v <= kMaxRec) s->max_rec = v;
+      if (v >= 1 && v <= kMaxRec) s->word_rec = v;
     }
+    s->max_rec = s->word_rec;
+  }
+  if (s->word && dfa->wplus) {
+    // \w+ under option W: set up the non-W kernels too; ugpu_scan picks per scan
+    s->word = false;
+    s->wfast = true;
+  }
+  if (s->word) {
     HIP_TRY_S(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
     HIP_TRY_S(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
     HIP_TRY_S(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
@@ -692,8 +765,30 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   if (!s || !dbuf) return fail(UGPU_INVAL, "NULL argument");
   if (lo > hi || hi > read_end) return fail(UGPU_INVAL, "need lo <= hi <= read_end");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (s->wfast) {
+    // option W on \w+: matches are maximal runs of Word code points, so on valid
+    // UTF-8 at_wb/at_we hold at every match edge -- provided the
+    // chain enters at the buffer start or after an ASCII non-word byte
+    bool fast = true;
+    if (lo > 0) {
+      uint8_t b = 0;
+      HIP_TRY(hipMemcpyAsync(&b, dbuf + lo - 1, 1, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      fast = b == '\n' || (b < 0x80 && b != '_' && !((b | 0x20u) - 'a' < 26u) && !(b - '0' < 10u));
+    }
+    // isutf8 over [lo, read_end) first (run beside the scan on a second stream
+    // it gained nothing: the two kernels slowed each other down)
+    if (fast && read_end > lo) {
+      uint64_t bad = ~0ull;
+      const int rc = utf8_scan(dbuf + lo, read_end - lo, false, &bad, stream);
+      if (rc) return rc;
+      fast = bad == ~0ull;
+    }
+    s->word = !fast;
+  }
   ScanParams P{};
   fill_tables(P, s->dfa);
+  if (s->wfast && !s->word) P.wtab = nullptr, P.nwtab = 0;  // the non-W kernels, stitches and forest
   geometry_for(P, s, dbuf, lo, hi, read_end, s->off, s->xi || s->xg || s->xc);
   P.delta = (int64_t)bias - (int64_t)s->off;
   P.at_eof = at_eof ? 1u : 0u;
@@ -714,7 +809,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   HIP_TRY(hipMemcpyAsync(s->h_tot, s->d_tot, sizeof(DevTotals), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   s->last = P;
-  s->last_xi = s->xi || s->xg || s->xc;
+  s->last_xi = !s->word && (s->xi || s->xg || s->xc);
   s->last_buf = dbuf;
   s->last_args[0] = lo;
   s->last_args[1] = hi;
@@ -732,6 +827,7 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
   if (!s || !out) return fail(UGPU_INVAL, "NULL argument");
   if (!s->have_scan) return fail(UGPU_INVAL, "no scan issued");
   HIP_TRY(hipStreamSynchronize(s->stream));
+
   UGPU_TRACE("totals flags %u count %llu rounds %u\n", *s->h_flags, (unsigned long long)s->h_tot->count,
              s->h_tot->rounds);
   if ((*s->h_flags & UGPU_FLAG_BUDGET) && !s->forest) {
@@ -747,7 +843,7 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
   out->dcap = t.dcap;
   out->entry = t.entry - s->off;
   out->exit = t.exit - s->off;
-  out->flags = *s->h_flags | (s->forest ? UGPU_TOT_FOREST : 0u);
+  out->flags = *s->h_flags | (s->forest ? UGPU_TOT_FOREST : 0u) | (s->wfast && !s->word ? UGPU_TOT_WFAST : 0u);
   out->fix_rounds = t.rounds;
   if (out->flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
   if (out->flags & UGPU_FLAG_BUDGET) return fail(UGPU_UNSUPPORTED, kBudgetMsg);
@@ -775,6 +871,7 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
     // dense kernel's geometry (COUNT + fix), then its WRITE pass
     P = ScanParams{};
     fill_tables(P, s->dfa);
+    if (s->wfast) P.wtab = nullptr, P.nwtab = 0;  // (only a non-W scan gets here)
     uint64_t off = 0;
     geometry_for(P, s, s->last_buf, s->last_args[0], s->last_args[1], s->last_args[2], off, false);
     P.delta = (int64_t)s->last_args[4] - (int64_t)off;
@@ -818,7 +915,7 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
                    uint64_t bias, uint64_t old_entry, uint64_t new_entry, ugpu_totals* delta, void* stream)
 {
   if (!s || !dbuf || !delta) return fail(UGPU_INVAL, "NULL argument");
-  if (s->word) return fail(UGPU_UNSUPPORTED, "option W across shards (at_wb needs the previous shard's bytes)");
+  if (s->word || s->wfast) return fail(UGPU_UNSUPPORTED, "option W across shards (at_wb needs the previous shard's bytes)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P{};
   fill_tables(P, s->dfa);
@@ -1246,20 +1343,9 @@ int utf8_scan(const uint8_t* dbuf, uint64_t len, bool nul, uint64_t* pos, void* 
   if (len == 0) return UGPU_OK;
   if (!is_device_ptr(dbuf)) return fail(UGPU_INVAL, "buffer must be device memory");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  int dev = 0, cus = 256;
+  int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
-  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  Utf8Params U{};
-  U.head = reinterpret_cast<uintptr_t>(dbuf) & 15u;
-  U.g = dbuf - U.head;
-  U.len = len;
-  U.span = (U.head + len + 15u) & ~15ull;
-  const uint64_t tile = utf8_tile();
-  const uint64_t tiles = (U.span + tile - 1) / tile;
-  const uint64_t want = (uint64_t)cus * 16;  // about 16 waves per CU
-  const uint64_t tpw = (tiles + want - 1) / want;
-  U.per = tpw * tile;
-  U.nwaves = (tiles + tpw - 1) / tpw;
+  Utf8Params U = utf8_params(dbuf, len);
   SlotWs* w = slot_acquire(dev);
   if (!w) return fail(UGPU_NOMEM, "result slot");
   U.out = w->d;

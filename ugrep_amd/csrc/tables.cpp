@@ -216,6 +216,61 @@ bool xc_program(const bool G[256], const bool X[256], uint32_t& shape, uint32_t 
   return true;
 }
 
+// Language equivalence with accept indices (tables.hpp): breadth-first over
+// state pairs from the two start states; states that cannot reach an
+// accepting state count as dead.
+bool tables_equivalent(const DfaTables& a, const DfaTables& b)
+{
+  auto step = [](const DfaTables& t, uint32_t s, int c) {
+    return (uint32_t)t.trans[(size_t)s * t.row + (t.format == FMT_BYTE ? (uint32_t)c : t.cls[c])] / t.row;
+  };
+  auto live = [&](const DfaTables& t) {  // co-reachable states
+    std::vector<std::vector<uint32_t> > rev(t.states);
+    for (uint32_t s = 1; s < t.states; ++s)
+      for (int c = 0; c < 256; ++c) {
+        const uint32_t n = step(t, s, c);
+        if (n) rev[n].push_back(s);
+      }
+    std::vector<bool> ok(t.states, false);
+    std::vector<uint32_t> work;
+    for (uint32_t s = 1; s < t.states; ++s)
+      if (t.caps[s]) {
+        ok[s] = true;
+        work.push_back(s);
+      }
+    while (!work.empty()) {
+      const uint32_t s = work.back();
+      work.pop_back();
+      for (uint32_t r : rev[s])
+        if (!ok[r]) {
+          ok[r] = true;
+          work.push_back(r);
+        }
+    }
+    return ok;
+  };
+  const std::vector<bool> la = live(a), lb = live(b);
+  const uint32_t sa = a.start / a.row, sb = b.start / b.row;
+  std::set<std::pair<uint32_t, uint32_t> > seen;
+  std::vector<std::pair<uint32_t, uint32_t> > work;
+  auto norm = [](const std::vector<bool>& l, uint32_t s) { return s && l[s] ? s : 0u; };
+  const std::pair<uint32_t, uint32_t> p0(norm(la, sa), norm(lb, sb));
+  work.push_back(p0);
+  seen.insert(p0);
+  while (!work.empty()) {
+    const std::pair<uint32_t, uint32_t> p = work.back();
+    work.pop_back();
+    if ((p.first == 0) != (p.second == 0)) return false;
+    if (p.first == 0) continue;
+    if (a.caps[p.first] != b.caps[p.second]) return false;
+    for (int c = 0; c < 256; ++c) {
+      const std::pair<uint32_t, uint32_t> q(norm(la, step(a, p.first, c)), norm(lb, step(b, p.second, c)));
+      if (seen.insert(q).second) work.push_back(q);
+    }
+  }
+  return true;
+}
+
 int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string& err)
 {
   if (opc == nullptr || nop == 0) {

@@ -105,6 +105,10 @@ struct DfaTables {
 
 bool xc_program(const bool G[256], const bool X[256], uint32_t& shape, uint32_t k[14]);
 
+// True when the two tables accept the same strings with the same accept
+// indices (so the FIND chains agree on every input).
+bool tables_equivalent(const DfaTables& a, const DfaTables& b);
+
 constexpr uint8_t XI_ST = 1, XI_IN = 2, XI_Y = 4;
 
 // Gap transducer (xg_kernel.hip), for restart-local tables in which the

@@ -117,6 +117,15 @@ def host_gap(opc):
     return (x, sy) if ok.value else None
 
 
+def host_equivalent(opc_a, opc_b):
+    """True when two opcode tables accept the same strings with the same accept indices."""
+    a, pa = _as_u32(opc_a)
+    b, pb = _as_u32(opc_b)
+    eq = ctypes.c_int(0)
+    check(lib.ugpu_tables_equivalent_host(pa, len(a), pb, len(b), ctypes.byref(eq)))
+    return bool(eq.value)
+
+
 def host_xc(opc):
     """Byte classes of xc_kernel (two-state tables): (cls uint8[256] = G << 7 | X << 6,
     SWAR range program shape (0: none), k uint32[14]) or None."""
