@@ -129,3 +129,45 @@ def test_gpu_w_word_plus_fast_path():
         for start in (sp, sp + 1, 777):
             res = U.find_all(pat, dev, start=start)
             assert (res.count, res.digest, res.dcap) == OracleDfa(opc).find_w(host, start=start)[:3], start
+
+
+@pytest.mark.gpu
+def test_gpu_w_identifiers_on_xc():
+    """Option W on the identifier table runs xc_kernel with the W rules
+    (UGPU_TOT_WFAST) on ASCII input -- runs that begin with a digit, entries
+    inside words and after digits, several grids -- and falls back to
+    wfind_kernel when bytes >= 0x80 appear; all equal to the oracle."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd as U
+    ref = next(c["opc"] for c in CASES if c["pattern"] == "[A-Za-z_][A-Za-z0-9_]*")
+    pat = U.Pattern(ref, word=True)
+    assert pat.info()["kernel"] == 5
+    code = gen(3, 19, 0, 6 << 20)
+    code[4096:4096 + 3000] = ord("7")  # a digit run across chunks, then letters
+    code[4096 + 3000:4096 + 3010] = ord("q")
+    utf = gen(4, 19, 0, 2 << 20)
+    st = torch.cuda.current_stream().cuda_stream
+    for data, fast in ((code, True), (utf, False)):
+        dev = torch.from_numpy(data).to("cuda")
+        torch.cuda.synchronize()
+        want_all = OracleDfa(ref).find_w(data)[:3]
+        for g in ("", "3", "77"):
+            if g:
+                os.environ["UGPU_MAX_GRID"] = g
+            try:
+                sc = U.Scanner(pat)
+                sc.scan(dev.data_ptr(), 0, data.size, data.size, True, 0, st)
+                t = sc.totals()
+            finally:
+                os.environ.pop("UGPU_MAX_GRID", None)
+            assert (t.count, t.digest, t.dcap) == want_all, g
+            assert bool(t.flags & 16) == fast
+        for start in (1, 4096 + 2999, 4096 + 3001, 12345, 1 << 20):
+            res = U.find_all(pat, dev, start=start)
+            assert (res.count, res.digest, res.dcap) == OracleDfa(ref).find_w(data, start=start)[:3], start
+        res = U.find_all(pat, dev, offsets=True)
+        cnt, dg, dc, lst = OracleDfa(ref).find_w(data, want_list=True)
+        assert (res.count, res.digest, res.dcap) == (cnt, dg, dc)
+        assert res.triples() == lst

@@ -71,6 +71,9 @@ struct ugpu_dfa {
   // option W on a table equivalent to \w+: on valid UTF-8 the W
   // rules remove nothing, so such scans run the non-W kernels (xg_kernel)
   bool wplus = false;
+  // option W on a two-state table whose X is the ASCII word bytes: xc_kernel
+  // applies the W rules itself (non-ASCII input falls back to wfind_kernel)
+  bool xcw = false;
   // idle scanners of ugpu_find_all calls on this table (reused: creating one
   // costs device allocations and property queries)
   std::mutex pool_mu;
@@ -88,6 +91,7 @@ struct ugpu_scanner {
   bool word = false;     // option W: every pass runs wfind_kernel (wfind.hip) (per scan when wfast)
   bool wfast = false;    // option W on a \w+ table: non-W kernels when the scanned bytes are valid UTF-8
   int word_rec = 0;      // chain records of a wfind scan
+  bool wxc = false;      // option W on xc_kernel (dfa->xcw), wfind_kernel when it flags UGPU_FLAG_WSLOW
   size_t smem = 0;       // sparse / dense kernel
   size_t xi_smem = 0;
   int xi_rec = 0;        // chain records of an xi scan
@@ -198,7 +202,7 @@ int utf8_scan(const uint8_t* dbuf, uint64_t len, bool nul, uint64_t* pos, void* 
 bool dfa_xc(const ugpu_dfa* d)
 {
   const char* env = std::getenv("UGPU_XC");
-  return d->t.xc && !d->t.filter && d->t.cap1 != 0 && !d->d_wtab && !(env && env[0] == '0');
+  return d->t.xc && !d->t.filter && d->t.cap1 != 0 && (!d->d_wtab || d->xcw) && !(env && env[0] == '0');
 }
 
 void fill_tables(ScanParams& P, const ugpu_dfa* d)
@@ -225,6 +229,7 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   for (int i = 0; i < 14; ++i) P.xc[i] = d->t.xc_k[i];
   P.xc_shape = d->t.xc_swar ? d->t.xc_shape : 0;
   P.xc_cls = d->d_cls + 256;
+  P.xc_w = d->xcw ? 1u : 0u;
   // chain bytes one stitch merge may cross before the chains count as not
   // resynchronising (two chains of a resynchronising table meet within a match
   // or two; longer merges go to the forest FIND)
@@ -405,10 +410,10 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       ugpu_dfa_destroy(d);
       return hip_fail(e, "word table upload");
     }
-    d->wplus = d->t.gap && !d->t.filter && d->t.cap1 != 0 && !(std::getenv("UGPU_WFAST") &&
-                                                                 std::getenv("UGPU_WFAST")[0] == '0') &&
-               is_word_plus(d->t);
-    if (!d->wplus) {
+    const bool wf = !(std::getenv("UGPU_WFAST") && std::getenv("UGPU_WFAST")[0] == '0');
+    d->wplus = wf && d->t.gap && !d->t.filter && d->t.cap1 != 0 && is_word_plus(d->t);
+    d->xcw = wf && d->t.xc && d->t.xc_w && !d->t.filter && d->t.cap1 != 0;
+    if (!d->wplus && !d->xcw) {
       *out = d;  // option W runs wfind_kernel only: no transducer tables
       return UGPU_OK;
     }
@@ -475,7 +480,7 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->accepting = d->t.accepting;
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
-  info->kernel = (d->d_wtab && !d->wplus && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
+  info->kernel = (d->d_wtab && !d->wplus && !d->xcw && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
                  : (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
                  : dfa_xc(d)                                   ? 5u
                  : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u
@@ -641,6 +646,9 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
     // \w+ under option W: set up the non-W kernels too; ugpu_scan picks per scan
     s->word = false;
     s->wfast = true;
+  } else if (s->word && dfa->xcw) {
+    s->word = false;  // xc_kernel with the W rules; wfind_kernel when it flags non-ASCII bytes
+    s->wxc = true;
   }
   if (s->word) {
     HIP_TRY_S(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
@@ -765,6 +773,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   if (!s || !dbuf) return fail(UGPU_INVAL, "NULL argument");
   if (lo > hi || hi > read_end) return fail(UGPU_INVAL, "need lo <= hi <= read_end");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (s->wxc) s->word = false;
   if (s->wfast) {
     // option W on \w+: matches are maximal runs of Word code points, so on valid
     // UTF-8 at_wb/at_we hold at every match edge -- provided the
@@ -827,6 +836,17 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
   if (!s || !out) return fail(UGPU_INVAL, "NULL argument");
   if (!s->have_scan) return fail(UGPU_INVAL, "no scan issued");
   HIP_TRY(hipStreamSynchronize(s->stream));
+  if (s->wxc && !s->word && (*s->h_flags & UGPU_FLAG_WSLOW)) {
+    // option W met bytes >= 0x80 (their at_wb/at_we need the UTF-8 decode):
+    // redo the range with wfind_kernel
+    s->wxc = false;
+    s->word = true;
+    const int rc = ugpu_scan(s, s->last_buf, s->last_args[0], s->last_args[1], s->last_args[2],
+                             (int)s->last_args[3], s->last_args[4], s->stream);
+    s->wxc = true;
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+  }
 
   UGPU_TRACE("totals flags %u count %llu rounds %u\n", *s->h_flags, (unsigned long long)s->h_tot->count,
              s->h_tot->rounds);
@@ -843,7 +863,8 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
   out->dcap = t.dcap;
   out->entry = t.entry - s->off;
   out->exit = t.exit - s->off;
-  out->flags = *s->h_flags | (s->forest ? UGPU_TOT_FOREST : 0u) | (s->wfast && !s->word ? UGPU_TOT_WFAST : 0u);
+  out->flags = (*s->h_flags & ~UGPU_FLAG_WSLOW) | (s->forest ? UGPU_TOT_FOREST : 0u) |
+               ((s->wfast || s->wxc) && !s->word ? UGPU_TOT_WFAST : 0u);
   out->fix_rounds = t.rounds;
   if (out->flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
   if (out->flags & UGPU_FLAG_BUDGET) return fail(UGPU_UNSUPPORTED, kBudgetMsg);
@@ -866,6 +887,7 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
   HIP_TRY(hipStreamSynchronize(s->stream));
   ScanParams P = s->last;
   bool forest = s->forest || (*s->h_flags & UGPU_FLAG_BUDGET);
+  if (s->last_xi && s->wxc) s->word = true;  // the records of an xc W scan: wfind_kernel's passes
   if (s->last_xi && !forest) {
     // xi_kernel has no record-writing pass: redo the chain records with the
     // dense kernel's geometry (COUNT + fix), then its WRITE pass
@@ -915,7 +937,7 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
                    uint64_t bias, uint64_t old_entry, uint64_t new_entry, ugpu_totals* delta, void* stream)
 {
   if (!s || !dbuf || !delta) return fail(UGPU_INVAL, "NULL argument");
-  if (s->word || s->wfast) return fail(UGPU_UNSUPPORTED, "option W across shards (at_wb needs the previous shard's bytes)");
+  if (s->word || s->wfast || s->wxc) return fail(UGPU_UNSUPPORTED, "option W across shards (at_wb needs the previous shard's bytes)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P{};
   fill_tables(P, s->dfa);

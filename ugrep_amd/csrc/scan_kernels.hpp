@@ -70,6 +70,9 @@ struct DevTotals {
 // text without digits); the totals are invalid and the host resolves the
 // range with the forest FIND (forest.hip)
 #define UGPU_FLAG_BUDGET 4u
+// option W on xc_kernel met a byte >= 0x80 (the W rules then need the UTF-8
+// decode): the host redoes the range with wfind_kernel
+#define UGPU_FLAG_WSLOW 32u
 
 struct ScanParams {
   const uint8_t* g;   // 16-byte aligned base of the scanned bytes
@@ -124,6 +127,7 @@ struct ScanParams {
   uint32_t xc[14];
   uint32_t xc_shape;
   const uint8_t* xc_cls;  // byte classes G << 7 | X << 6 (256 B)
+  uint32_t xc_w;          // option W on xc_kernel (X = the ASCII word bytes)
 };
 
 // Forest FIND (forest.hip): exact for every table, no resynchronisation

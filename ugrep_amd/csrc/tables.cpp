@@ -12,6 +12,7 @@
 #include "tables.hpp"
 
 #include <algorithm>
+#include <cctype>
 #include <map>
 #include <set>
 #include <unordered_map>
@@ -641,6 +642,12 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       bool ascii = true;
       for (int c = 0x80; c < 256; ++c) ascii = ascii && !X[c];
       t.xc_swar = ascii && xc_program(G, X, t.xc_shape, t.xc_k);
+      bool wordset = true;  // X = the ASCII word bytes [0-9A-Za-z_] (option W on xc_kernel)
+      for (int c = 0; c < 256; ++c) {
+        const bool w = c < 0x80 && (std::isalnum(c) || c == '_');
+        wordset = wordset && X[c] == w;
+      }
+      t.xc_w = wordset;
     }
   }
   t.start = start_sid * R;

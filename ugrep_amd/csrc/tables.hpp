@@ -97,7 +97,8 @@ struct DfaTables {
   // (G), k[10 + 2i] (P).
   // xc_tab[byte] = G << 7 | X << 6: the kernel's byte classes (an LDS lookup);
   // xc_swar: the sets are ASCII and fit the range program (SWAR classifier)
-  bool xc = false, xc_swar = false;
+  // xc_w: X is exactly the ASCII word bytes [0-9A-Za-z_] (option W on xc_kernel)
+  bool xc = false, xc_swar = false, xc_w = false;
   std::vector<uint8_t> xc_tab;
   uint32_t xc_shape = 0;
   uint32_t xc_k[14] = {};

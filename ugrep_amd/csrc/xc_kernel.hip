@@ -143,13 +143,50 @@ struct CLane {
   uint32_t G[4], X[4], S[4];
 };
 
-template <bool MASK, class PROG>
-__device__ __forceinline__ void cclass(const PROG& pr, const uint4& v, CLane& L, uint64_t q, const CLim& lim)
+// Option W (ugrep -w) for tables whose X is exactly the ASCII word bytes
+// [0-9A-Za-z_] (tables.cpp xc_w): a match must start where at_wb holds, i.e.
+// after a non-word byte, so a G byte starts a match only where the byte before
+// it is not in X (an X-run beginning with a P byte, "9abc", yields nothing),
+// and every match ends before a non-X byte, which is a non-word byte when it
+// is ASCII (at_we holds).  Runs next to bytes >= 0x80 need the reference's
+// UTF-8 decode (include/reflex/matcher.h:1194-1237): the wave flags any such
+// byte and the host redoes the range with wfind_kernel.
+struct CW {
+  uint32_t cx = 0;   // bit 31: the byte before the chunk is in X (uniform)
+  uint32_t hi = 0;   // lane: OR of the bytes seen (bit 7s: a byte >= 0x80)
+  uint64_t bob = 0;  // buffer start (base coordinates): at_wb holds there
+};
+
+template <bool MASK, bool W, class PROG>
+__device__ __forceinline__ void cclass(const PROG& pr, const uint4& v, CLane& L, uint64_t q, const CLim& lim, CW& wc)
 {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
+  for (int d = 0; d < 4; ++d) pr(w[d], L.G[d], L.X[d]);
+  if constexpr (W) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t m = 0xffffffffu;
+      if constexpr (MASK) {  // bytes before the buffer are neither word bytes nor seen
+        m = ~below(q + 4 * d, wc.bob);
+        L.X[d] &= m | 0x7f7f7f7fu;
+      }
+      wc.hi |= w[d] & m;
+    }
+    // X of the byte before each byte: the previous dword, lane, or chunk
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t prev = __shfl_up(L.X[3], 1, 64);
+    if (lane == 0) prev = wc.cx;
+    wc.cx = __shfl(L.X[3], 63, 64);
+    uint32_t xp[4];
+    xp[0] = __builtin_amdgcn_alignbyte(L.X[0], prev, 3);
+#pragma unroll
+    for (int d = 1; d < 4; ++d) xp[d] = __builtin_amdgcn_alignbyte(L.X[d], L.X[d - 1], 3);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) L.G[d] &= ~xp[d];
+  }
+#pragma unroll
   for (int d = 0; d < 4; ++d) {
-    pr(w[d], L.G[d], L.X[d]);
     if constexpr (MASK) {
       const uint64_t qd = q + 4 * d;
       const uint32_t live = ~below(qd, lim.qlo) & below(qd, lim.qr);
@@ -211,9 +248,9 @@ __device__ __forceinline__ void cfinish(CLane& L, uint32_t ci, uint32_t& cs, uin
 
 // One chunk (16 bytes per lane at q = chunk base + 16 lane); cw = the wave's
 // carry, updated.  Returns the lane's carry-in bytes.
-template <bool MASK, class PROG>
+template <bool MASK, bool W, class PROG>
 __device__ __forceinline__ void cchunk(const PROG& pr, const uint4& v, uint64_t q, const CLim& lim, uint32_t& cw,
-                                       uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4])
+                                       uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4], CW& wc)
 {
 #if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 1  // loads only (benchmarking; wrong counts)
   if (!MASK) {
@@ -232,7 +269,7 @@ __device__ __forceinline__ void cchunk(const PROG& pr, const uint4& v, uint64_t 
     }
   } else
 #endif
-  cclass<MASK>(pr, v, L, q, lim);
+  cclass<MASK, W>(pr, v, L, q, lim, wc);
   bool prop;
   const bool gen = cadd(L, prop);
 #if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 3  // no events (benchmarking; wrong counts)
@@ -277,7 +314,7 @@ __device__ __forceinline__ uint64_t cexit(const uint32_t cb[4], uint64_t q, uint
 
 }  // namespace
 
-template <int NF, int NG, int NP>
+template <int NF, int NG, int NP, bool W>
 __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanParams P)
 {
   typename CSel<NF, NG, NP>::type pr;
@@ -302,6 +339,16 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
   const bool last_wave = n && whi == P.hi;
   const uint64_t rend16 = (P.rend + 15) & ~uint64_t(15);
   const uint32_t lo16 = 16u * (uint32_t)lane;
+  CW wc;
+  wc.bob = P.bob;
+  // option W: bit 31 = the byte before position p is in X (at_wb fails there)
+  auto xprev = [&](uint64_t p) -> uint32_t {
+    if constexpr (W) {
+      if (p <= P.bob) return 0u;
+      return (uint32_t)(pr.t[P.g[p - 1]] & 0x40u) << 25;
+    }
+    return 0u;
+  };
 
   // ---- the wave's carry-in: the chain enters P.lo fresh; other waves look back
   uint32_t cw = 0;
@@ -312,7 +359,8 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
       const CLim lim{P.lo, wlo, wlo};
       CLane L;
       const uint4 v = cload(crsrc(P.g + cb0, rend16 > cb0 ? rend16 - cb0 : 0), lo16);
-      cclass<true>(pr, v, L, cb0 + lo16, lim);
+      wc.cx = xprev(cb0);
+      cclass<true, W>(pr, v, L, cb0 + lo16, lim, wc);
       bool prop;
       const bool gen = cadd(L, prop);
       const uint64_t g = __ballot(gen), p = __ballot(prop);
@@ -349,7 +397,7 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
   auto masked = [&](uint64_t q0) {
     const uint4 v = cload(crsrc(P.g + q0, rend16 > q0 ? rend16 - q0 : 0), lo16);
     uint32_t cs = 0, ws = 0, ls = 0, cb[4];
-    cchunk<true>(pr, v, q0 + lo16, lim, cw, cs, ws, ls, cb);
+    cchunk<true, W>(pr, v, q0 + lo16, lim, cw, cs, ws, ls, cb, wc);
     cnt += cs;
     pos += (uint64_t)cs * (q0 + lo16) + (ws >> 7);
     lbits += ls;
@@ -362,6 +410,8 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
     }
   };
   uint64_t q0 = wlo & ~uint64_t(kCChunk - 1);
+  wc.cx = xprev(fte > ftb && q0 >= ftb * kCTile ? ftb * kCTile : q0);
+  wc.hi = 0;
 #ifndef UGPU_XC_NOEDGE
   if (fte > ftb)
     for (; q0 < ftb * kCTile; q0 += kCChunk) masked(q0);
@@ -385,7 +435,7 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
     CIt a;
     uint32_t cb[4];
 #pragma unroll
-    for (int j = 0; j < kCIter; ++j) cchunk<false>(pr, cur[j], 0, lim, cw, a.cs[j], a.ws, a.ls, cb);
+    for (int j = 0; j < kCIter; ++j) cchunk<false, W>(pr, cur[j], 0, lim, cw, a.cs[j], a.ws, a.ls, cb, wc);
     uint32_t c = 0;
 #pragma unroll
     for (int j = 0; j < kCIter; ++j) c += a.cs[j];
@@ -409,6 +459,9 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
 #endif
   if (found) cw = 0;  // past the exit every carry is clear
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
+  if constexpr (W) {
+    if (__ballot((wc.hi & 0x80808080u) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_WSLOW);
+  }
   const uint64_t c = wave_sum(cnt), s = wave_sum(pos), lb = wave_sum(lbits);
   if (lane == 0) {
     // In bytes = carry-in bits / 8, minus the carry into the first byte, plus
@@ -430,7 +483,10 @@ namespace {
 template <int NF, int NG, int NP>
 hipError_t launch_shape(const ScanParams& P, hipStream_t stream)
 {
-  hipLaunchKernelGGL((xc_kernel<NF, NG, NP>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  if (P.xc_w)
+    hipLaunchKernelGGL((xc_kernel<-1, 0, 0, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  else
+    hipLaunchKernelGGL((xc_kernel<NF, NG, NP, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   return hipGetLastError();
 }
 #ifdef UGPU_XC_SWAR
@@ -468,7 +524,10 @@ hipError_t launch_xc(const ScanParams& P, hipStream_t stream)
   return launch_shape<-1, 0, 0>(P, stream);
 }
 
-hipError_t xc_occupancy(int* n) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<-1, 0, 0>, kCWaves * 64, 0); }
+hipError_t xc_occupancy(int* n)
+{
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<-1, 0, 0, true>, kCWaves * 64, 0);
+}
 uint32_t xc_unit() { return kCTile; }
 uint32_t xc_waves() { return kCWaves; }
 
