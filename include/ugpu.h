@@ -151,12 +151,9 @@ int ugpu_tables_gap_host(const uint32_t *opc, uint32_t nop, uint16_t *xg, uint32
 
 /* Host-only: the byte classes of xc_kernel (two-state tables: start --G--> A
    --X--> A, ugrep_amd/csrc/tables.hpp): cls[256] = G << 7 | X << 6 (may be
-   NULL), and the SWAR range program of the same sets, *shape = NF | NG << 4 |
-   NP << 8 range tests with k[14] their per-byte add constants (*shape = 0 when
-   the sets do not fit one).  *ok = 0 when the table does not qualify.
-   (Replaces, for these tables, the per-byte opcode scan of
-   lib/matcher.cpp:460-545.) */
-int ugpu_tables_xc_host(const uint32_t *opc, uint32_t nop, uint8_t *cls, uint32_t *shape, uint32_t *k, int *ok);
+   NULL).  *ok = 0 when the table does not qualify.  (Replaces, for these
+   tables, the per-byte opcode scan of lib/matcher.cpp:460-545.) */
+int ugpu_tables_xc_host(const uint32_t *opc, uint32_t nop, uint8_t *cls, int *ok);
 
 /* Host-only: *eq = 1 when two opcode tables accept the same strings with the
    same accept indices (so their FIND chains agree on every input).  The

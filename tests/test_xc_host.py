@@ -1,14 +1,12 @@
 """CPU: the two-state carry-chain FIND of xc_kernel (ugrep_amd/csrc/xc_kernel.hip).
 
-1. The byte classes tables.cpp derives from a table (ugpu_tables_xc_host: the
-   LDS class table, and the SWAR range program of the UGPU_XC_SWAR build)
-   reproduce the table's G (start -> A) and X (A -> A) byte sets exactly, the
-   range program evaluated with the kernel's SWAR arithmetic on all 256 bytes.
-2. The kernel's arithmetic -- one big addition S = X' + G' over the byte
-   encoding X' = 0x7f | X << 7, G' = G << 7, carry-in bytes S ^ X' ^ G', starts
-   G & !carry, the exit rule past hi -- restated here with Python integers over
-   whole buffers, equals the oracle's FIND chain (counts, digests, exit) on
-   seeded corpora and edge cases, from arbitrary [lo, hi).
+1. The byte classes tables.cpp derives from a table (ugpu_tables_xc_host)
+   reproduce the table's G (start -> A) and X (A -> A) byte sets exactly.
+2. The kernel's arithmetic -- one big addition S = e + 0x0101..01 over the
+   byte codes e = 0xFF (G), 0xFE (P), 0x00 (K), carry-in bits bit 0 of
+   S ^ e ^ 0x01, starts G & !carry, the exit rule past hi -- restated here with
+   Python integers over whole buffers, equals the oracle's FIND chain (counts,
+   digests, exit) on seeded corpora and edge cases, from arbitrary [lo, hi).
 """
 import numpy as np
 import pytest
@@ -40,35 +38,10 @@ def _sets(opc):
     return G, X, row
 
 
-def _swar(shape, k, x):
-    """The kernel's class program (CProg) on uint32 words x: (G80, X')."""
-    nf, ng, np_ = shape & 15, (shape >> 4) & 15, (shape >> 8) & 15
-    x = x.astype(np.uint64)
-    m32 = np.uint64(0xFFFFFFFF)
-    x7 = x & np.uint64(0x7F7F7F7F)
-    g = np.zeros_like(x)
-    h = x7 | np.uint64(0x20202020)
-    for i in range(nf):
-        g |= ((h + np.uint64(k[2 * i])) & m32) & ~((h + np.uint64(k[2 * i + 1])) & m32)
-    for i in range(ng):
-        g |= ((x7 + np.uint64(k[4 + 2 * i])) & m32) & ~((x7 + np.uint64(k[5 + 2 * i])) & m32)
-    G = g & ~x & np.uint64(0x80808080)
-    p = np.zeros_like(x)
-    for i in range(np_):
-        p |= ((x7 + np.uint64(k[10 + 2 * i])) & m32) & ~((x7 + np.uint64(k[11 + 2 * i])) & m32)
-    X = ((p & ~x) | G | np.uint64(0x7F7F7F7F)) & m32
-    return G & m32, X
-
-
-def _classify(shape, k, data):
-    """Per byte (G, X) booleans through the SWAR program."""
-    n = data.size
-    pad = np.zeros((n + 3) // 4 * 4, np.uint8)
-    pad[:n] = data
-    G, X = _swar(shape, k, pad.view("<u4"))
-    gb = np.frombuffer(G.astype("<u4").tobytes(), np.uint8)[:n] & 0x80
-    xb = np.frombuffer(X.astype("<u4").tobytes(), np.uint8)[:n] & 0x80
-    return gb != 0, xb != 0
+def _codes(cls, data):
+    """The kernel's byte codes: 0xFF (G), 0xFE (P), 0x00 (K)."""
+    c = cls[data]
+    return np.where(c & 0x80, 0xFF, np.where(c & 0x40, 0xFE, 0)).astype(np.uint8)
 
 
 @pytest.mark.parametrize("pname", TWO_STATE)
@@ -76,74 +49,62 @@ def test_two_state_tables_qualify(patterns, pname):
     assert _xc(patterns[pname]["opc"]) is not None
 
 
-def test_range_program_reproduces_byte_sets(patterns):
+def test_byte_classes_reproduce_byte_sets(patterns):
     seen = 0
     for name, p in patterns.items():
-        if p.get("unsupported"):
-            continue
         try:
-            xc = _xc(p["opc"])
+            cls = _xc(p["opc"])
         except Exception:
-            continue
-        if xc is None:
+            continue  # (unsupported tables)
+        if cls is None:
             continue
         seen += 1
         G, X, _ = _sets(p["opc"])
-        cls, shape, k = xc
-        assert np.array_equal((cls & 0x80) != 0, G), name  # the LDS class table
+        assert np.array_equal((cls & 0x80) != 0, G), name
         assert np.array_equal((cls & 0x40) != 0, X), name
-        if shape:
-            g, x = _classify(shape, k, np.arange(256, dtype=np.uint8))
-            assert np.array_equal(g, G), name
-            assert np.array_equal(x, X), name
     assert seen >= 2
 
 
-def test_range_program_on_synthetic_sets():
-    """Random ASCII sets through tables.cpp's program builder via the compiler:
-    every compiled two-state bracket pattern must classify exactly."""
+def test_byte_classes_of_compiled_brackets():
+    """Random byte-class patterns through the native compiler: every two-state
+    table's classes equal its G/X sets."""
     import ugrep_amd
     rng = np.random.default_rng(7)
     done = 0
     for _ in range(60):
         lo1, lo2 = sorted(rng.integers(0x21, 0x7F, 2))
-        hi_extra = int(rng.integers(0x21, 0x7F))
-        rx = "[\\x%02x-\\x%02x\\x%02x][\\x%02x-\\x%02x\\x%02x0-9]*" % (lo1, lo2, hi_extra, lo1, lo2, hi_extra)
+        extra = int(rng.integers(0x21, 0x7F))
+        rx = "[\\x%02x-\\x%02x\\x%02x][\\x%02x-\\x%02x\\x%02x0-9]*" % (lo1, lo2, extra, lo1, lo2, extra)
         try:
             opc = ugrep_amd.compile_regex(rx)
         except Exception:
             continue
-        xc = _xc(opc)
-        if xc is None:
+        cls = _xc(opc)
+        if cls is None:
             continue
         G, X, _ = _sets(opc)
-        assert np.array_equal((xc[0] & 0x80) != 0, G) and np.array_equal((xc[0] & 0x40) != 0, X), rx
-        if not xc[1]:
-            continue  # more ranges than the SWAR shapes hold: the LDS classes only
-        g, x = _classify(xc[1], xc[2], np.arange(256, dtype=np.uint8))
-        assert np.array_equal(g, G), rx
-        assert np.array_equal(x, X), rx
+        assert np.array_equal((cls & 0x80) != 0, G) and np.array_equal((cls & 0x40) != 0, X), rx
         done += 1
     assert done >= 20
 
 
-def xc_restated(shape, k, cap, data, lo, hi, rend, at_eof):
-    """The kernel's chain arithmetic over the whole buffer as one integer.
+def xc_restated(cls, cap, data, lo, hi, rend, at_eof):
+    """The kernel's chain arithmetic over the whole buffer as one integer:
+    codes e (0xFF G, 0xFE P, 0x00 K; K outside [lo, rend), G -> P past hi),
+    S = e + 0x0101..01, carry into byte i = bit 0 of (S ^ e ^ 0x01).
     Returns (count, digest, dcap, exit, halo)."""
-    g, x = _classify(shape, k, data[:rend])
+    e = _codes(cls, data[:rend]).copy()
     pos = np.arange(rend)
-    g &= (pos >= lo) & (pos < hi)
-    x &= pos >= lo
-    xb = np.where(x, 0xFF, 0x7F).astype(np.uint8)
-    gb = np.where(g, 0x80, 0x00).astype(np.uint8)
-    Xi = int.from_bytes(xb.tobytes(), "little")
-    Gi = int.from_bytes(gb.tobytes(), "little")
-    S = Xi + Gi
-    cbytes = np.frombuffer(((S ^ Xi ^ Gi) & ((1 << (8 * rend)) - 1)).to_bytes(rend, "little"), np.uint8)
+    e[pos < lo] = 0
+    e[(pos >= hi) & (e == 0xFF)] = 0xFE
+    Ei = int.from_bytes(e.tobytes(), "little")
+    Oi = int.from_bytes(b"\x01" * rend, "little")
+    S = Ei + Oi
+    x = np.frombuffer(((S ^ Ei ^ Oi) & ((1 << (8 * rend)) - 1)).to_bytes(rend, "little"), np.uint8)
     carry = np.zeros(rend + 1, bool)  # carry INTO position q (In_{q-1})
-    carry[:rend] = cbytes != 0
+    carry[:rend] = (x & 1) != 0
     carry[rend] = (S >> (8 * rend)) & 1 == 1
-    starts = np.nonzero(g & ~carry[:rend])[0]
+    starts = np.nonzero((e & 1).astype(bool) & ~carry[:rend])[0]
     inb = carry[1:]  # In_q
     after = np.nonzero(~carry[hi + 1:rend + 1])[0]  # exit: the first q >= hi with In_q clear
     ex = min(hi + int(after[0]), rend) if after.size else rend
@@ -184,7 +145,7 @@ def _inputs():
 @pytest.mark.parametrize("pname", TWO_STATE)
 def test_restated_arithmetic_equals_oracle(patterns, pname):
     opc = patterns[pname]["opc"]
-    _, shape, k = _xc(opc)
+    cls = _xc(opc)
     rng = np.random.default_rng(11)
     for name, host in _inputs().items():
         n = host.size
@@ -194,18 +155,17 @@ def test_restated_arithmetic_equals_oracle(patterns, pname):
             ranges.append((lo, int(rng.integers(lo, n + 1))))
         for lo, hi in ranges:
             want = _oracle_range(opc, host, lo, hi)
-            got = xc_restated(shape, k, 1, host, lo, hi, n, True)
+            got = xc_restated(cls, 1, host, lo, hi, n, True)
             # the table's accept index: every two-state pattern here has cap 1
             assert got[:4] == want, (pname, name, lo, hi, got, want)
             assert not got[4]
 
 
 def test_restated_halo_at_readable_end(patterns):
-    opc = patterns["c3_ident"]["opc"]
-    _, shape, k = _xc(opc)
+    cls = _xc(patterns["c3_ident"]["opc"])
     data = np.frombuffer(b"abc def ghij", np.uint8)
     # readable end inside "ghij", not EOF: the match may go on
-    assert xc_restated(shape, k, 1, data, 0, 9, 10, False)[4]
-    assert not xc_restated(shape, k, 1, data, 0, 9, 10, True)[4]
+    assert xc_restated(cls, 1, data, 0, 9, 10, False)[4]
+    assert not xc_restated(cls, 1, data, 0, 9, 10, True)[4]
     # the match ending before the readable end's byte: no halo
-    assert not xc_restated(shape, k, 1, data, 0, 5, 8, False)[4]
+    assert not xc_restated(cls, 1, data, 0, 5, 8, False)[4]

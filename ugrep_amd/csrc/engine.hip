@@ -226,8 +226,6 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.cap1 = d->t.cap1;
   P.wtab = d->d_wtab;
   P.nwtab = d->nwtab;
-  for (int i = 0; i < 14; ++i) P.xc[i] = d->t.xc_k[i];
-  P.xc_shape = d->t.xc_swar ? d->t.xc_shape : 0;
   P.xc_cls = d->d_cls + 256;
   P.xc_w = d->xcw ? 1u : 0u;
   // chain bytes one stitch merge may cross before the chains count as not
@@ -583,16 +581,14 @@ int ugpu_tables_gap_host(const uint32_t* opc, uint32_t nop, uint16_t* xg, uint32
   return UGPU_OK;
 }
 
-int ugpu_tables_xc_host(const uint32_t* opc, uint32_t nop, uint8_t* cls, uint32_t* shape, uint32_t* k, int* ok)
+int ugpu_tables_xc_host(const uint32_t* opc, uint32_t nop, uint8_t* cls, int* ok)
 {
-  if (!ok || !shape || !k) return fail(UGPU_INVAL, "NULL argument");
+  if (!ok) return fail(UGPU_INVAL, "NULL argument");
   DfaTables t;
   std::string err;
   int rc = build_tables(opc, nop, t, err);
   if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
   *ok = t.xc ? 1 : 0;
-  *shape = t.xc_swar ? t.xc_shape : 0;
-  std::copy(t.xc_k, t.xc_k + 14, k);
   if (cls && t.xc) std::copy(t.xc_tab.begin(), t.xc_tab.end(), cls);
   return UGPU_OK;
 }

@@ -123,9 +123,7 @@ struct ScanParams {
   // merge may cross before giving up (fix_kernel, chain_fix_kernel)
   uint32_t max_rounds;
   uint64_t merge_budget;
-  // two-state tables (xc_kernel.hip): the byte-class range program (tables.hpp)
-  uint32_t xc[14];
-  uint32_t xc_shape;
+  // two-state tables (xc_kernel.hip)
   const uint8_t* xc_cls;  // byte classes G << 7 | X << 6 (256 B)
   uint32_t xc_w;          // option W on xc_kernel (X = the ASCII word bytes)
 };

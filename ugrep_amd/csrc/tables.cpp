@@ -173,50 +173,6 @@ bool restart_local(const std::vector<uint32_t>& nxt, uint32_t start, uint32_t fi
 
 }  // namespace
 
-// Range program of a two-state table (tables.hpp XcProg): case-folded ranges
-// of G first (pairs v, v - 0x20 with v in 0x60..0x7f, both in G), then the
-// rest of G and X \ G as byte ranges.  False when more ranges are needed than
-// xc_kernel's shapes hold (1 folded, 3 raw G, 2 P).
-bool xc_program(const bool G[256], const bool X[256], uint32_t& shape, uint32_t k[14])
-{
-  bool fold[128] = {}, g[128] = {}, p[128] = {};
-  for (int v = 0; v < 128; ++v) {
-    g[v] = G[v];
-    p[v] = X[v] && !G[v];
-  }
-  for (int v = 0x60; v < 0x80; ++v)
-    if (G[v] && G[v - 0x20]) {
-      fold[v] = true;
-      g[v] = g[v - 0x20] = false;
-    }
-  auto runs = [](const bool* s, std::vector<std::pair<int, int> >& out) {
-    for (int v = 0; v < 128; ++v)
-      if (s[v] && (v == 0 || !s[v - 1])) {
-        int e = v;
-        while (e + 1 < 128 && s[e + 1]) ++e;
-        out.push_back(std::make_pair(v, e));
-      }
-  };
-  std::vector<std::pair<int, int> > rf, rg, rp;
-  runs(fold, rf);
-  runs(g, rg);
-  runs(p, rp);
-  if (rf.size() > 1 || rg.size() > 3 || rp.size() > 2 || rf.size() + rg.size() == 0) return false;
-  auto rep = [](int b) { return (uint32_t)b * 0x01010101u; };
-  std::fill(k, k + 14, 0u);
-  auto put = [&](const std::vector<std::pair<int, int> >& r, int base) {
-    for (size_t i = 0; i < r.size(); ++i) {
-      k[base + 2 * i] = rep(0x80 - r[i].first);
-      k[base + 2 * i + 1] = rep(0x7f - r[i].second);
-    }
-  };
-  put(rf, 0);
-  put(rg, 4);
-  put(rp, 10);
-  shape = (uint32_t)rf.size() | (uint32_t)rg.size() << 4 | (uint32_t)rp.size() << 8;
-  return true;
-}
-
 // Language equivalence with accept indices (tables.hpp): breadth-first over
 // state pairs from the two start states; states that cannot reach an
 // accepting state count as dead.
@@ -639,9 +595,6 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       t.xc = true;
       t.xc_tab.assign(256, 0);
       for (int c = 0; c < 256; ++c) t.xc_tab[c] = (uint8_t)((G[c] ? 0x80 : 0) | (X[c] ? 0x40 : 0));
-      bool ascii = true;
-      for (int c = 0x80; c < 256; ++c) ascii = ascii && !X[c];
-      t.xc_swar = ascii && xc_program(G, X, t.xc_shape, t.xc_k);
       bool wordset = true;  // X = the ASCII word bytes [0-9A-Za-z_] (option W on xc_kernel)
       for (int c = 0; c < 256; ++c) {
         const bool w = c < 0x80 && (std::isalnum(c) || c == '_');

@@ -88,23 +88,13 @@ struct DfaTables {
   std::vector<uint8_t> xg2_cls; // 256: column of each byte
   uint32_t xg2_pad = 0, xg2_cols = 0, xg2_states = 0;
   // Two-state tables (xc_kernel.hip): start --G--> A, A --X--> A with A
-  // accepting, G a subset of X, every other edge dead.
-  // The FIND chain is then a carry chain (In_i = G_i | X_i & In_{i-1}) and the
-  // byte classes are a SWAR range program ("XcProg"): xc_shape = NF | NG << 4 |
-  // NP << 8 range tests, NF on the case-folded byte (b | 0x20) and NG on the
-  // byte giving G, NP giving X \ G; xc_k holds per test the two per-byte add
-  // constants (0x80 - lo, 0x7f - hi) x 0x01010101 at k[2i] (folded), k[4 + 2i]
-  // (G), k[10 + 2i] (P).
-  // xc_tab[byte] = G << 7 | X << 6: the kernel's byte classes (an LDS lookup);
-  // xc_swar: the sets are ASCII and fit the range program (SWAR classifier)
-  // xc_w: X is exactly the ASCII word bytes [0-9A-Za-z_] (option W on xc_kernel)
-  bool xc = false, xc_swar = false, xc_w = false;
+  // accepting, G a subset of X, every other edge dead.  The FIND chain is then
+  // a carry chain (In_i = G_i | X_i & In_{i-1}); xc_tab[byte] = G << 7 | X << 6
+  // are the kernel's byte classes.  xc_w: X is exactly the ASCII word bytes
+  // [0-9A-Za-z_] (option W on xc_kernel).
+  bool xc = false, xc_w = false;
   std::vector<uint8_t> xc_tab;
-  uint32_t xc_shape = 0;
-  uint32_t xc_k[14] = {};
 };
-
-bool xc_program(const bool G[256], const bool X[256], uint32_t& shape, uint32_t k[14]);
 
 // True when the two tables accept the same strings with the same accept
 // indices (so the FIND chains agree on every input).

@@ -1,7 +1,7 @@
 // xc_kernel.hip -- FIND over two-state tables by carry propagation: token
 // patterns whose DFA is  start --G--> A,  A --X--> A  (A accepting, G a subset
-// of X, every other edge dead), over ASCII byte sets: identifiers
-// [A-Za-z_][A-Za-z0-9_]*, digit runs [0-9]+, ASCII words.  No table walk at all.
+// of X, every other edge dead): identifiers [A-Za-z_][A-Za-z0-9_]*, digit runs
+// [0-9]+, byte-class words.  No table walk at all.
 //
 // What it replaces: the reference's per-match FIND loop (lib/matcher.cpp:
 // 42-750) with its DFA opcode walk (:125-546) for such patterns; results are
@@ -11,15 +11,17 @@
 // at byte i (In_i) iff  In_i = G_i | (X_i & In_{i-1}):  a G byte starts or
 // continues a match, a byte of X \ G (P) only continues one, any other byte
 // (K) ends it.  That is the carry recurrence of a binary adder (G = generate,
-// P = propagate), so In for a whole run of bytes is one integer addition: with
-// every byte encoded as X' = 0x7F | X << 7 and G' = G << 7, the carry out of
-// byte i of  S = X' + G' + carry_in  is In_i, and the byte (S ^ X' ^ G') is
-// 0xFF exactly where the carry INTO byte i (In_{i-1}) is set.  Then
-//   a match starts at i   <=>  G_i & !In_{i-1}
-//   sum len = #In bytes = sum over bytes of In_{i-1}, corrected at the ends.
-// Byte classes come from SWAR range tests on 4 bytes per dword (a host-built
-// program of at most 6 ranges, tables.cpp), the adds are v_add_co/v_addc
-// chains, the counts v_bcnt and v_dot4: about 5 VALU per byte, no LDS.
+// P = propagate), so In for a whole run of bytes is one integer addition.
+// Every byte is coded  e = 0xFF (G), 0xFE (P), 0x00 (K)  and added to 0x01:
+// 0xFF + 1 always carries out of the byte, 0xFE + 1 carries exactly when a
+// carry comes in, 0x00 + 1 never does.  So with  S = e + 0x01010101 + c_in
+// the carry out of byte i is In_i, and bit 0 of (S ^ e ^ 0x01010101) is the
+// carry INTO byte i, In_{i-1}.  Then
+//   a match starts at i   <=>  G_i & !In_{i-1}   (bit 0 of e & ~(S ^ e ^ 1))
+//   sum len = #In bytes   = sum over bytes of In_{i-1}, corrected at the ends.
+// The byte codes of two bytes at once come from one LDS lookup (a 64 Ki-entry
+// u16 pair table built from the 256 byte classes in the prologue), the adds
+// are v_add_co/v_addc chains, the counts v_bcnt and v_dot4.
 //
 // Layout.  Fully coalesced: a wave reads 1 KiB chunks, 16 bytes per lane
 // (lane l holds bytes [16 l, 16 l + 16)), four chunks in flight.  Lane
@@ -37,9 +39,9 @@
 // the starts and In bytes of its own byte range, so its record is
 // (entry = its first byte, exit = its end) and fix_kernel merges nothing.  The
 // wave holding the range end hi finds the chain exit: past hi no match starts
-// (G = 0), the match crossing hi runs on through X bytes, and the exit is the
-// first position >= hi whose carry-in is clear (capped at the readable end;
-// a match reaching a non-EOF readable end raises UGPU_FLAG_HALO).
+// (G becomes P), the match crossing hi runs on through X bytes, and the exit is
+// the first position >= hi outside a match (capped at the readable end; a
+// match reaching a non-EOF readable end raises UGPU_FLAG_HALO).
 #include "device_common.hpp"
 #include "tables.hpp"
 
@@ -47,17 +49,20 @@ namespace ugpu {
 
 namespace {
 
-constexpr int kCWaves = 4;             // waves per workgroup
-constexpr uint32_t kCChunk = 1024;     // one wave-load: 16 bytes per lane
 #ifndef UGPU_XC_ITER
 #define UGPU_XC_ITER 4
 #endif
-#ifndef UGPU_XC_MINW
-#define UGPU_XC_MINW 1  // waves per SIMD the register budget must allow
+#ifdef UGPU_XC_BYTE
+constexpr bool kCPair = false;  // byte-code lookups (4 per dword), measured against the pair table
+#else
+constexpr bool kCPair = true;   // pair-code lookups (2 per dword)
 #endif
-constexpr int kCIter = UGPU_XC_ITER;   // chunks per iteration (loads in flight per wave)
+constexpr int kCWaves = kCPair ? 16 : 4;  // waves per workgroup (the pair table takes 128 KiB of LDS per CU)
+constexpr uint32_t kCChunk = 1024;        // one wave-load: 16 bytes per lane
+constexpr int kCIter = UGPU_XC_ITER;      // chunks per iteration (loads in flight per wave)
 constexpr uint32_t kCTile = kCChunk * kCIter;
-constexpr int kCLook = 8;              // look-back chunks before giving up
+constexpr int kCLook = 8;                 // look-back chunks before giving up
+constexpr uint32_t kOnes = 0x01010101u;
 
 __device__ __forceinline__ uint4 cload(__amdgpu_buffer_rsrc_t rs, uint32_t off)
 {
@@ -75,54 +80,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t crsrc(const uint8_t* base, uin
                                            __builtin_amdgcn_readfirstlane((int)n), 0x00020000);
 }
 
-// The class program (tables.hpp XcProg): NF range tests on the case-folded
-// byte (b | 0x20) and NG on the byte itself give G, NP tests give X \ G.  A
-// test of [lo, hi] on 7-bit v is bit 7 of (v + (0x80 - lo)) & ~(v + (0x7f - hi));
-// bytes >= 0x80 are K.
-template <int NF, int NG, int NP>
-struct CProg {
-  uint32_t k[14];
-  __device__ __forceinline__ void operator()(uint32_t x, uint32_t& G, uint32_t& X) const
+// Byte codes of a dword (0xFF G, 0xFE P, 0x00 K per byte) from the LDS tables:
+// the pair table (u16 codes of every byte pair) or the byte table.
+struct CCodes {
+  const uint16_t* pair;
+  const uint8_t* byte;
+  __device__ __forceinline__ uint32_t operator()(uint32_t x) const
   {
-    const uint32_t x7 = x & 0x7f7f7f7fu;
-    uint32_t g = 0;
-    if constexpr (NF > 0) {
-      const uint32_t h = x7 | 0x20202020u;
-#pragma unroll
-      for (int i = 0; i < NF; ++i) g |= (h + k[2 * i]) & ~(h + k[2 * i + 1]);
+    if constexpr (kCPair) {
+      return (uint32_t)pair[x & 0xffffu] | ((uint32_t)pair[x >> 16] << 16);
+    } else {
+      const uint32_t r0 = byte[x & 0xffu] | ((uint32_t)byte[(x >> 16) & 0xffu] << 16);
+      const uint32_t r1 = byte[(x >> 8) & 0xffu] | ((uint32_t)byte[x >> 24] << 16);
+      return r0 | (r1 << 8);
     }
-#pragma unroll
-    for (int i = 0; i < NG; ++i) g |= (x7 + k[4 + 2 * i]) & ~(x7 + k[5 + 2 * i]);
-    G = g & ~x & 0x80808080u;
-    uint32_t p = 0;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) p |= (x7 + k[10 + 2 * i]) & ~(x7 + k[11 + 2 * i]);
-    X = (p & ~x) | G | 0x7f7f7f7fu;
   }
-};
-
-// The byte classes by lookup (the default): xc_cls[byte] = G << 7 | X << 6 in
-// LDS, four independent ds_read_u8 per dword (any byte sets, ASCII or not).
-// Text bytes < 0x80 sit in 32 dwords, one per bank: lanes never conflict.
-struct CLds {
-  const uint8_t* t;
-  __device__ __forceinline__ void operator()(uint32_t x, uint32_t& G, uint32_t& X) const
-  {
-    const uint32_t r0 = t[x & 0xffu] | ((uint32_t)t[(x >> 16) & 0xffu] << 16);
-    const uint32_t r1 = t[(x >> 8) & 0xffu] | ((uint32_t)t[x >> 24] << 16);
-    const uint32_t e = r0 | (r1 << 8);
-    G = e & 0x80808080u;
-    X = (e << 1) | 0x7f7f7f7fu;  // (bit 7 of a byte shifts into the next byte's bit 0, which is set anyway)
-  }
-};
-
-template <int NF, int NG, int NP>
-struct CSel {
-  typedef CProg<NF, NG, NP> type;
-};
-template <>
-struct CSel<-1, 0, 0> {
-  typedef CLds type;
 };
 
 // bytes of the dword at q that lie below lim (0xff per byte)
@@ -133,14 +105,9 @@ __device__ __forceinline__ uint32_t below(uint64_t q, uint64_t lim)
 }
 
 // Byte limits of a masked chunk: positions < qlo and >= qr are K, positions
-// >= qg start nothing.
+// >= qg start nothing (G becomes P).
 struct CLim {
   uint64_t qlo, qg, qr;
-};
-
-// Classes of one lane's 16 bytes and its adder inputs.
-struct CLane {
-  uint32_t G[4], X[4], S[4];
 };
 
 // Option W (ugrep -w) for tables whose X is exactly the ASCII word bytes
@@ -152,46 +119,51 @@ struct CLane {
 // UTF-8 decode (include/reflex/matcher.h:1194-1237): the wave flags any such
 // byte and the host redoes the range with wfind_kernel.
 struct CW {
-  uint32_t cx = 0;   // bit 31: the byte before the chunk is in X (uniform)
+  uint32_t cx = 0;   // byte 3: the code of the byte before the chunk (uniform)
   uint32_t hi = 0;   // lane: OR of the bytes seen (bit 7s: a byte >= 0x80)
   uint64_t bob = 0;  // buffer start (base coordinates): at_wb holds there
 };
 
-template <bool MASK, bool W, class PROG>
-__device__ __forceinline__ void cclass(const PROG& pr, const uint4& v, CLane& L, uint64_t q, const CLim& lim, CW& wc)
+// Codes and adder sums of one lane's 16 bytes.
+struct CLane {
+  uint32_t E[4], S[4];
+};
+
+template <bool MASK, bool W>
+__device__ __forceinline__ void ccodes(const CCodes& cc, const uint4& v, CLane& L, uint64_t q, const CLim& lim,
+                                       CW& wc)
 {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int d = 0; d < 4; ++d) pr(w[d], L.G[d], L.X[d]);
+  for (int d = 0; d < 4; ++d) L.E[d] = cc(w[d]);
   if constexpr (W) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       uint32_t m = 0xffffffffu;
-      if constexpr (MASK) {  // bytes before the buffer are neither word bytes nor seen
+      if constexpr (MASK) {  // bytes before the buffer are K and not seen
         m = ~below(q + 4 * d, wc.bob);
-        L.X[d] &= m | 0x7f7f7f7fu;
+        L.E[d] &= m;
       }
       wc.hi |= w[d] & m;
     }
-    // X of the byte before each byte: the previous dword, lane, or chunk
+    // a G byte whose previous byte is in X (code bit 1) becomes P
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t prev = __shfl_up(L.X[3], 1, 64);
+    uint32_t prev = __shfl_up(L.E[3], 1, 64);
     if (lane == 0) prev = wc.cx;
-    wc.cx = __shfl(L.X[3], 63, 64);
+    wc.cx = __shfl(L.E[3], 63, 64);
     uint32_t xp[4];
-    xp[0] = __builtin_amdgcn_alignbyte(L.X[0], prev, 3);
+    xp[0] = __builtin_amdgcn_alignbyte(L.E[0], prev, 3);
 #pragma unroll
-    for (int d = 1; d < 4; ++d) xp[d] = __builtin_amdgcn_alignbyte(L.X[d], L.X[d - 1], 3);
+    for (int d = 1; d < 4; ++d) xp[d] = __builtin_amdgcn_alignbyte(L.E[d], L.E[d - 1], 3);
 #pragma unroll
-    for (int d = 0; d < 4; ++d) L.G[d] &= ~xp[d];
+    for (int d = 0; d < 4; ++d) L.E[d] &= ~((xp[d] >> 1) & kOnes);
   }
+  if constexpr (MASK) {
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    if constexpr (MASK) {
+    for (int d = 0; d < 4; ++d) {
       const uint64_t qd = q + 4 * d;
       const uint32_t live = ~below(qd, lim.qlo) & below(qd, lim.qr);
-      L.G[d] &= live & below(qd, lim.qg);
-      L.X[d] &= live | 0x7f7f7f7fu;
+      L.E[d] &= live & (below(qd, lim.qg) | ~kOnes);
     }
   }
 }
@@ -200,10 +172,10 @@ __device__ __forceinline__ void cclass(const PROG& pr, const uint4& v, CLane& L,
 __device__ __forceinline__ bool cadd(CLane& L, bool& prop)
 {
   uint32_t k;
-  L.S[0] = __builtin_addc(L.X[0], L.G[0], 0u, &k);
-  L.S[1] = __builtin_addc(L.X[1], L.G[1], k, &k);
-  L.S[2] = __builtin_addc(L.X[2], L.G[2], k, &k);
-  L.S[3] = __builtin_addc(L.X[3], L.G[3], k, &k);
+  L.S[0] = __builtin_addc(L.E[0], kOnes, 0u, &k);
+  L.S[1] = __builtin_addc(L.E[1], kOnes, k, &k);
+  L.S[2] = __builtin_addc(L.E[2], kOnes, k, &k);
+  L.S[3] = __builtin_addc(L.E[3], kOnes, k, &k);
   prop = (L.S[0] & L.S[1] & L.S[2] & L.S[3]) == 0xffffffffu;
   return k != 0;
 }
@@ -218,15 +190,15 @@ __device__ __forceinline__ uint64_t clook(uint64_t gen, uint64_t prop, uint32_t 
   return cin;
 }
 
-// Per-iteration lane sums: starts per chunk, 128 x start offsets in the lane
-// (v_dot4 weights), carry-in bits (8 per In byte).
+// Per-iteration lane sums: starts per chunk, start offsets in the lane (v_dot4
+// weights), carry-in bits (one per In byte).
 struct CIt {
   uint32_t cs[kCIter] = {};
   uint32_t ws = 0, ls = 0;
 };
 
 // Finish one chunk: final adds with the lane carry-in, then the events.
-// Returns the lane's carry-in bytes (0xff where In_{i-1}) in cb.
+// cb = the lane's carry-in bits (bit 0 of each byte: In_{i-1}).
 __device__ __forceinline__ void cfinish(CLane& L, uint32_t ci, uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4])
 {
   uint32_t k;
@@ -236,8 +208,9 @@ __device__ __forceinline__ void cfinish(CLane& L, uint32_t ci, uint32_t& cs, uin
   L.S[3] = __builtin_addc(L.S[3], 0u, k, &k);
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    const uint32_t c = L.S[d] ^ L.X[d] ^ L.G[d];
-    const uint32_t st = L.G[d] & ~c;
+    const uint32_t x = L.S[d] ^ L.E[d] ^ kOnes;
+    const uint32_t c = x & kOnes;
+    const uint32_t st = L.E[d] & ~x & kOnes;
     cs = __builtin_popcount(st) + cs;
     ls = __builtin_popcount(c) + ls;
     const uint32_t wd = (4u * d) | ((4u * d + 1) << 8) | ((4u * d + 2) << 16) | ((4u * d + 3) << 24);
@@ -247,9 +220,9 @@ __device__ __forceinline__ void cfinish(CLane& L, uint32_t ci, uint32_t& cs, uin
 }
 
 // One chunk (16 bytes per lane at q = chunk base + 16 lane); cw = the wave's
-// carry, updated.  Returns the lane's carry-in bytes.
-template <bool MASK, bool W, class PROG>
-__device__ __forceinline__ void cchunk(const PROG& pr, const uint4& v, uint64_t q, const CLim& lim, uint32_t& cw,
+// carry, updated.  Returns the lane's carry-in bits.
+template <bool MASK, bool W>
+__device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_t q, const CLim& lim, uint32_t& cw,
                                        uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4], CW& wc)
 {
 #if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 1  // loads only (benchmarking; wrong counts)
@@ -259,31 +232,9 @@ __device__ __forceinline__ void cchunk(const PROG& pr, const uint4& v, uint64_t 
   }
 #endif
   CLane L;
-#if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 4  // trivial classes (benchmarking; wrong counts)
-  if (!MASK) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      L.G[d] = w[d] & 0x80808080u;
-      L.X[d] = w[d] | 0x7f7f7f7fu;
-    }
-  } else
-#endif
-  cclass<MASK, W>(pr, v, L, q, lim, wc);
+  ccodes<MASK, W>(cc, v, L, q, lim, wc);
   bool prop;
   const bool gen = cadd(L, prop);
-#if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 3  // no events (benchmarking; wrong counts)
-  if (!MASK) {
-    cs += L.S[0] ^ L.S[1] ^ L.S[2] ^ L.S[3] ^ (gen ? 1u : 0u) ^ (prop ? 2u : 0u);
-    return;
-  }
-#endif
-#if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 2  // no lane carry-lookahead (benchmarking; wrong counts)
-  if (!MASK) {
-    cfinish(L, gen ^ prop ? 1u : 0u, cs, ws, ls, cb);
-    return;
-  }
-#endif
   const uint64_t cin = clook(__ballot(gen), __ballot(prop), cw, cw);
   cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb);
 }
@@ -291,7 +242,7 @@ __device__ __forceinline__ void cchunk(const PROG& pr, const uint4& v, uint64_t 
 // Exit search after a masked chunk of the wave holding hi: the exit is the
 // first q >= hi with In_q clear (no match starts past hi, so q is the end of
 // the match crossing hi, or hi), i.e. the first p = q + 1 > hi whose carry-in
-// byte is clear; ~0 when there is none in this chunk.  Also flags a match that
+// bit is clear; ~0 when there is none in this chunk.  Also flags a match that
 // reaches the readable end rend (when not at EOF).
 __device__ __forceinline__ uint64_t cexit(const uint32_t cb[4], uint64_t q, uint64_t hi, uint64_t rend, bool at_eof,
                                           uint32_t& ovf)
@@ -300,9 +251,9 @@ __device__ __forceinline__ uint64_t cexit(const uint32_t cb[4], uint64_t q, uint
 #pragma unroll
   for (int d = 3; d >= 0; --d) {
     const uint64_t qd = q + 4 * d;
-    const uint32_t z = ~cb[d] & ~below(qd, hi + 1) & 0x80808080u;  // clear carry-in at a position > hi
+    const uint32_t z = ~cb[d] & ~below(qd, hi + 1) & kOnes;  // clear carry-in at a position > hi
     if (z) first = 4 * d + (__builtin_ctz(z) >> 3);
-    if (!at_eof && rend >= qd && rend < qd + 4 && ((cb[d] >> (8 * (rend - qd))) & 0x80u)) ovf = 1;
+    if (!at_eof && rend >= qd && rend < qd + 4 && ((cb[d] >> (8 * (rend - qd))) & 1u)) ovf = 1;
   }
   const uint64_t m = __ballot(first < 64);
   if (!m) return ~0ull;
@@ -312,21 +263,29 @@ __device__ __forceinline__ uint64_t cexit(const uint32_t cb[4], uint64_t q, uint
   return x < rend ? x : rend;
 }
 
+// code of a byte class (xc_cls: G << 7 | X << 6)
+__device__ __forceinline__ uint32_t ccode(uint32_t cls) { return cls & 0x80u ? 0xffu : (cls & 0x40u ? 0xfeu : 0u); }
+
 }  // namespace
 
-template <int NF, int NG, int NP, bool W>
-__global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanParams P)
+template <bool W>
+__global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
 {
-  typename CSel<NF, NG, NP>::type pr;
-  __shared__ uint32_t ctab[NF < 0 ? 64 : 1];
-  if constexpr (NF < 0) {
-    if (threadIdx.x < 64) ctab[threadIdx.x] = reinterpret_cast<const uint32_t*>(P.xc_cls)[threadIdx.x];
+  // LDS: byte codes, and (pair classifier) the codes of every byte pair
+  __shared__ __attribute__((aligned(16))) uint8_t bcode[256];
+  __shared__ __attribute__((aligned(16))) uint16_t pcode[kCPair ? 65536 : 8];
+  for (uint32_t i = threadIdx.x; i < 256; i += kCWaves * 64) bcode[i] = (uint8_t)ccode(P.xc_cls[i]);
+  __syncthreads();
+  if constexpr (kCPair) {
+    // pcode[b1 << 8 | b0] = code(b0) | code(b1) << 8, two entries (b0, b0 + 1) per store
+    for (uint32_t i = threadIdx.x; i < 65536u / 2; i += kCWaves * 64) {
+      const uint32_t b1 = i >> 7, b0 = (2 * i) & 0xffu;
+      const uint32_t hi = (uint32_t)bcode[b1] << 8;
+      reinterpret_cast<uint32_t*>(pcode)[i] = (hi | bcode[b0]) | ((hi | bcode[b0 + 1]) << 16);
+    }
     __syncthreads();
-    pr.t = reinterpret_cast<const uint8_t*>(ctab);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 14; ++i) pr.k[i] = P.xc[i];
   }
+  const CCodes cc{pcode, bcode};
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kCWaves + wid;
@@ -341,14 +300,8 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
   const uint32_t lo16 = 16u * (uint32_t)lane;
   CW wc;
   wc.bob = P.bob;
-  // option W: bit 31 = the byte before position p is in X (at_wb fails there)
-  auto xprev = [&](uint64_t p) -> uint32_t {
-    if constexpr (W) {
-      if (p <= P.bob) return 0u;
-      return (uint32_t)(pr.t[P.g[p - 1]] & 0x40u) << 25;
-    }
-    return 0u;
-  };
+  // option W: the code of the byte before position p (byte 3), 0 at the buffer start
+  auto xprev = [&](uint64_t p) -> uint32_t { return W && p > P.bob ? (uint32_t)bcode[P.g[p - 1]] << 24 : 0u; };
 
   // ---- the wave's carry-in: the chain enters P.lo fresh; other waves look back
   uint32_t cw = 0;
@@ -360,7 +313,7 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
       CLane L;
       const uint4 v = cload(crsrc(P.g + cb0, rend16 > cb0 ? rend16 - cb0 : 0), lo16);
       wc.cx = xprev(cb0);
-      cclass<true, W>(pr, v, L, cb0 + lo16, lim, wc);
+      ccodes<true, W>(cc, v, L, cb0 + lo16, lim, wc);
       bool prop;
       const bool gen = cadd(L, prop);
       const uint64_t g = __ballot(gen), p = __ballot(prop);
@@ -397,9 +350,9 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
   auto masked = [&](uint64_t q0) {
     const uint4 v = cload(crsrc(P.g + q0, rend16 > q0 ? rend16 - q0 : 0), lo16);
     uint32_t cs = 0, ws = 0, ls = 0, cb[4];
-    cchunk<true, W>(pr, v, q0 + lo16, lim, cw, cs, ws, ls, cb, wc);
+    cchunk<true, W>(cc, v, q0 + lo16, lim, cw, cs, ws, ls, cb, wc);
     cnt += cs;
-    pos += (uint64_t)cs * (q0 + lo16) + (ws >> 7);
+    pos += (uint64_t)cs * (q0 + lo16) + ws;
     lbits += ls;
     if (last_wave && !found && q0 + kCChunk > P.hi + 1) {
       const uint64_t x = cexit(cb, q0 + lo16, P.hi, P.rend, P.at_eof != 0, ovf);
@@ -410,12 +363,10 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
     }
   };
   uint64_t q0 = wlo & ~uint64_t(kCChunk - 1);
-  wc.cx = xprev(fte > ftb && q0 >= ftb * kCTile ? ftb * kCTile : q0);
+  wc.cx = xprev(q0);
   wc.hi = 0;
-#ifndef UGPU_XC_NOEDGE
   if (fte > ftb)
     for (; q0 < ftb * kCTile; q0 += kCChunk) masked(q0);
-#endif
 
   uint4 cur[kCIter], nxt[kCIter];
   if (fte > ftb) {
@@ -435,15 +386,15 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
     CIt a;
     uint32_t cb[4];
 #pragma unroll
-    for (int j = 0; j < kCIter; ++j) cchunk<false, W>(pr, cur[j], 0, lim, cw, a.cs[j], a.ws, a.ls, cb, wc);
-    uint32_t c = 0;
+    for (int j = 0; j < kCIter; ++j) cchunk<false, W>(cc, cur[j], 0, lim, cw, a.cs[j], a.ws, a.ls, cb, wc);
+    uint32_t c = 0, cj = 0;
 #pragma unroll
-    for (int j = 0; j < kCIter; ++j) c += a.cs[j];
+    for (int j = 0; j < kCIter; ++j) {
+      c += a.cs[j];
+      cj += j * a.cs[j];
+    }
     cnt += c;
-    uint32_t cj = 0;
-#pragma unroll
-    for (int j = 1; j < kCIter; ++j) cj += j * a.cs[j];
-    pos += (uint64_t)c * (ts + lo16) + (a.ws >> 7) + kCChunk * cj;
+    pos += (uint64_t)c * (ts + lo16) + a.ws + kCChunk * cj;
     lbits += a.ls;
 #pragma unroll
     for (int j = 0; j < kCIter; ++j) cur[j] = nxt[j];
@@ -453,10 +404,8 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
   // (the match crossing hi runs on through X bytes, no starts past hi).  Bytes
   // past the readable end are K, so the search ends at the latest in the chunk
   // after the one holding rend (its loads read nothing: the resource is empty).
-#ifndef UGPU_XC_NOEDGE
   if (n)
     for (; q0 < whi || (last_wave && !found); q0 += kCChunk) masked(q0);
-#endif
   if (found) cw = 0;  // past the exit every carry is clear
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
   if constexpr (W) {
@@ -464,9 +413,9 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
   }
   const uint64_t c = wave_sum(cnt), s = wave_sum(pos), lb = wave_sum(lbits);
   if (lane == 0) {
-    // In bytes = carry-in bits / 8, minus the carry into the first byte, plus
-    // the carry out of the last processed byte
-    const uint64_t len = n ? lb / 8 - cin0 + cw : 0;
+    // In bytes = carry-in bits, minus the carry into the first byte, plus the
+    // carry out of the last processed byte
+    const uint64_t len = n ? lb - cin0 + cw : 0;
     const uint64_t s_rep = s + c * (uint64_t)P.delta;  // reported starts
     BlockRec rec;
     rec.entry = wlo;
@@ -479,54 +428,18 @@ __global__ __launch_bounds__(kCWaves * 64, UGPU_XC_MINW) void xc_kernel(ScanPara
   }
 }
 
-namespace {
-template <int NF, int NG, int NP>
-hipError_t launch_shape(const ScanParams& P, hipStream_t stream)
-{
-  if (P.xc_w)
-    hipLaunchKernelGGL((xc_kernel<-1, 0, 0, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
-  else
-    hipLaunchKernelGGL((xc_kernel<NF, NG, NP, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
-  return hipGetLastError();
-}
-#ifdef UGPU_XC_SWAR
-template <int NF, int NG>
-hipError_t launch_np(const ScanParams& P, uint32_t np, hipStream_t stream)
-{
-  switch (np) {
-    case 0: return launch_shape<NF, NG, 0>(P, stream);
-    case 1: return launch_shape<NF, NG, 1>(P, stream);
-    default: return launch_shape<NF, NG, 2>(P, stream);
-  }
-}
-template <int NF>
-hipError_t launch_ng(const ScanParams& P, uint32_t ng, uint32_t np, hipStream_t stream)
-{
-  switch (ng) {
-    case 0: return launch_np<NF, 0>(P, np, stream);
-    case 1: return launch_np<NF, 1>(P, np, stream);
-    case 2: return launch_np<NF, 2>(P, np, stream);
-    default: return launch_np<NF, 3>(P, np, stream);
-  }
-}
-#endif
-}  // namespace
-
-// The SWAR classifier (range tests instead of the LDS lookup) is a build
-// option, UGPU_XC_SWAR (measured slower on C3: docs in DESIGN.md).
 hipError_t launch_xc(const ScanParams& P, hipStream_t stream)
 {
-#ifdef UGPU_XC_SWAR
-  const uint32_t nf = P.xc_shape & 15, ng = (P.xc_shape >> 4) & 15, np = (P.xc_shape >> 8) & 15;
-  if (nf <= 1 && ng <= 3 && np <= 2 && nf + ng > 0)
-    return nf ? launch_ng<1>(P, ng, np, stream) : launch_ng<0>(P, ng, np, stream);
-#endif
-  return launch_shape<-1, 0, 0>(P, stream);
+  if (P.xc_w)
+    hipLaunchKernelGGL(xc_kernel<true>, dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  else
+    hipLaunchKernelGGL(xc_kernel<false>, dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  return hipGetLastError();
 }
 
 hipError_t xc_occupancy(int* n)
 {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<-1, 0, 0, true>, kCWaves * 64, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<true>, kCWaves * 64, 0);
 }
 uint32_t xc_unit() { return kCTile; }
 uint32_t xc_waves() { return kCWaves; }

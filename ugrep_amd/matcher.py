@@ -127,17 +127,12 @@ def host_equivalent(opc_a, opc_b):
 
 
 def host_xc(opc):
-    """Byte classes of xc_kernel (two-state tables): (cls uint8[256] = G << 7 | X << 6,
-    SWAR range program shape (0: none), k uint32[14]) or None."""
-    a = np.ascontiguousarray(opc, dtype=np.uint32)
-    p = a.ctypes.data_as(_lib.c_u32p)
-    shape = ctypes.c_uint32(0)
+    """Byte classes of xc_kernel (two-state tables): cls uint8[256] = G << 7 | X << 6, or None."""
+    a, p = _as_u32(opc)
     ok = ctypes.c_int(0)
-    k = np.zeros(14, np.uint32)
     cls = np.zeros(256, np.uint8)
-    check(lib.ugpu_tables_xc_host(p, len(a), cls.ctypes.data_as(_lib.c_u8p), ctypes.byref(shape),
-                                  k.ctypes.data_as(_lib.c_u32p), ctypes.byref(ok)))
-    return (cls, shape.value, k) if ok.value else None
+    check(lib.ugpu_tables_xc_host(p, len(a), cls.ctypes.data_as(_lib.c_u8p), ctypes.byref(ok)))
+    return cls if ok.value else None
 
 
 class Pattern:
