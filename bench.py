@@ -257,6 +257,8 @@ def main():
     log("rank %d: shard [%d, %d) read_end %d, pattern %s: %s" % (rank, lo, hi, read_end, rx, info))
 
     sc = ugrep_amd.Scanner(pat)
+    if args.offsets:
+        sc.stage(True)  # single-pass OFFSETS (prefiltered tables): the COUNT pass stages the records
     ptr = buf.data_ptr()
     kms = []
 

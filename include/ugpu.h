@@ -191,6 +191,12 @@ int ugpu_scan_offsets(ugpu_scanner *sc, uint64_t *d_start, uint32_t *d_len, uint
    to the totals and the (possibly changed) exit.  Synchronous. */
 int ugpu_chain_fix(ugpu_scanner *sc, const uint8_t *dbuf, uint64_t lo, uint64_t hi, uint64_t read_end, int at_eof,
                    uint64_t bias, uint64_t old_entry, uint64_t new_entry, ugpu_totals *delta, void *stream);
+/* Single-pass OFFSETS: with on != 0, COUNT scans of prefiltered tables also
+   stage each wave's records, and ugpu_scan_offsets copies them to the output
+   (plus a WRITE pass over the waves whose speculative chain was not the true
+   one) instead of re-running the scan.  ugpu_find_all in OFFSETS mode does
+   this by itself.  Costs 16 B of staging per record (128 MiB per scanner). */
+int ugpu_scanner_stage(ugpu_scanner *sc, int on);
 /* Time (ms) of the scan kernel of the last ugpu_scan, measured with HIP events
    recorded on the scan stream around that launch. */
 int ugpu_scan_kernel_ms(ugpu_scanner *sc, float *ms);

@@ -119,6 +119,13 @@ struct ugpu_scanner {
   uint64_t* d_fent = nullptr;
   uint64_t* d_fsum = nullptr;
   uint64_t* d_fbase = nullptr;
+  // single-pass OFFSETS (sparse tables): the COUNT pass stages each wave's
+  // records (ugpu_scanner_stage, or a ugpu_find_all in OFFSETS mode)
+  bool stage = false, stage_once = false, staged_last = false;
+  uint64_t* d_st_start = nullptr;
+  uint32_t* d_st_len = nullptr;
+  uint32_t* d_st_cap = nullptr;
+  uint32_t* d_st_n = nullptr;
 };
 
 namespace {
@@ -757,6 +764,10 @@ int ugpu_scanner_destroy(ugpu_scanner* s)
   (void)hipHostFree(s->h_tot);
   (void)hipHostFree(s->h_flags);
   forest_free(s);
+  (void)hipFree(s->d_st_start);
+  (void)hipFree(s->d_st_len);
+  (void)hipFree(s->d_st_cap);
+  (void)hipFree(s->d_st_n);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   delete s;
@@ -803,6 +814,23 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   P.totals = s->d_tot;
   P.entries_out = s->d_entries;
   P.out_base_out = s->d_obase;
+  s->staged_last = false;
+  if (s->sparse && (s->stage || s->stage_once)) {
+    if (!s->d_st_n) {
+      const size_t n = (size_t)kMaxRec * kStagePer;
+      HIP_TRY(hipMalloc(&s->d_st_start, n * 8));
+      HIP_TRY(hipMalloc(&s->d_st_len, n * 4));
+      HIP_TRY(hipMalloc(&s->d_st_cap, n * 4));
+      HIP_TRY(hipMalloc(&s->d_st_n, kMaxRec * 4));
+    }
+    P.st_start = s->d_st_start;
+    P.st_len = s->d_st_len;
+    P.st_cap = s->d_st_cap;
+    P.st_n = s->d_st_n;
+    P.st_per = kStagePer;
+    s->staged_last = true;
+  }
+  s->stage_once = false;
   UGPU_TRACE("scan lo %llu hi %llu rend %llu eof %d grid %u xi %d xg %d sparse %d word %d\n", (unsigned long long)P.lo,
              (unsigned long long)P.hi, (unsigned long long)P.rend, at_eof, P.grid, (int)s->xi, (int)s->xg,
              (int)s->sparse, (int)s->word);
@@ -867,6 +895,13 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
   return UGPU_OK;
 }
 
+int ugpu_scanner_stage(ugpu_scanner* s, int on)
+{
+  if (!s) return fail(UGPU_INVAL, "NULL argument");
+  s->stage = on != 0;
+  return UGPU_OK;
+}
+
 int ugpu_scan_kernel_ms(ugpu_scanner* s, float* ms)
 {
   if (!s || !ms) return fail(UGPU_INVAL, "NULL argument");
@@ -912,7 +947,21 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
   P.out_len = d_len;
   P.out_cap = d_cap;
   P.out_capacity = capacity;
-  UGPU_TRACE("offsets forest %d capacity %llu\n", (int)forest, (unsigned long long)capacity);
+  UGPU_TRACE("offsets forest %d capacity %llu staged %d\n", (int)forest, (unsigned long long)capacity,
+             (int)s->staged_last);
+  if (!forest && s->staged_last && !s->last_xi) {
+    // single pass: copy the staged records of waves whose speculative chain was
+    // the true one; a WRITE pass (skipping the copied waves) covers the rest
+    HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
+    HIP_TRY(launch_stage_copy(P, st));
+    HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    s->staged_last = false;  // (the staging slots now say which waves are done)
+    if (*s->h_flags & UGPU_FLAG_CAPACITY) return fail(UGPU_CAPACITY, "output capacity exceeded");
+    if (!(*s->h_flags & UGPU_FLAG_NEEDWRITE)) return UGPU_OK;
+  } else {
+    P.st_n = nullptr;  // no staged records: every wave writes
+  }
   if (!forest) {
     HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
     HIP_TRY(launch_main(s, P, true, st));
@@ -1111,6 +1160,7 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
       rc = hip_fail(e, "input copy");
     dbuf = ws->d_in;
   }
+  s->stage_once = mode == UGPU_MODE_OFFSETS;  // single-pass OFFSETS for sparse tables
   if (!rc) rc = ugpu_scan(s, dbuf, start, len, len, 1, 0, ws->st);
   if (!rc) rc = ugpu_scan_totals(s, &tot);
   if (!rc) {

@@ -73,6 +73,11 @@ struct DevTotals {
 // option W on xc_kernel met a byte >= 0x80 (the W rules then need the UTF-8
 // decode): the host redoes the range with wfind_kernel
 #define UGPU_FLAG_WSLOW 32u
+// stage_copy_kernel left waves whose staged records were not the true chain's
+#define UGPU_FLAG_NEEDWRITE 64u
+constexpr uint32_t kStageOver = 0xffffffffu;
+constexpr uint32_t kStageDone = 0xfffffffeu;
+constexpr uint32_t kStagePer = 1024;  // staged records per wave (16 B each: 128 MiB for 8192 waves)
 
 struct ScanParams {
   const uint8_t* g;   // 16-byte aligned base of the scanned bytes
@@ -125,6 +130,14 @@ struct ScanParams {
   uint64_t merge_budget;
   // two-state tables (xc_kernel.hip)
   const uint8_t* xc_cls;  // byte classes G << 7 | X << 6 (256 B)
+  // single-pass OFFSETS (sparse_kernel): a COUNT pass with st_n set also stages
+  // each wave's records (st_per per wave); st_n[wave] = records staged, or
+  // kStageOver; stage_copy_kernel moves them and marks the wave kStageDone
+  uint64_t* st_start;
+  uint32_t* st_len;
+  uint32_t* st_cap;
+  uint32_t* st_n;
+  uint32_t st_per;
   uint32_t xc_w;          // option W on xc_kernel (X = the ASCII word bytes)
 };
 
@@ -152,6 +165,7 @@ hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_e
 hipError_t launch_gen(int kind, uint64_t seed, uint64_t off, uint8_t* dbuf, uint64_t len, hipStream_t stream);
 // sparse (prefiltered) wave-persistent kernel, sparse_kernel.hip
 hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream_t stream);
+hipError_t launch_stage_copy(const ScanParams& P, hipStream_t stream);
 hipError_t sparse_occupancy(const ScanParams& P, size_t smem, int* blocks_per_cu);
 size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates);
 // line-level consumers, lines.hip

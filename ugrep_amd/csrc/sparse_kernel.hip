@@ -134,10 +134,20 @@ static_assert(kDefer * 8 <= kAux && 64 * 32 <= kAux, "aux region too small");
 // match (Appendix A: a non-candidate position only steps p+1).  With the
 // exclusive prefix-max of match ends (relative to x) the rule is exact unless
 // two candidate matches overlap; those batches take a 64-step in-wave pass.
-template <bool WRITE>
+// Records staged by a COUNT pass for the OFFSETS pass (single-pass OFFSETS):
+// the wave's slice of the staging arrays, filled in chain order from index 0.
+struct Stage {
+  uint64_t* start = nullptr;
+  uint32_t* len = nullptr;
+  uint32_t* cap = nullptr;
+  uint64_t n = 0;       // records staged
+  uint32_t over = 0;    // the slice was too small
+};
+
+template <bool WRITE, bool STAGE = false>
 __device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, uint32_t le, int lane, const Ctx& C,
                                         const ScanParams& P, uint64_t& x, CountEm& acc, uint64_t& widx,
-                                        uint32_t& wover)
+                                        uint32_t& wover, Stage& sg)
 {
   const bool vm = valid && len != 0 && c >= x;
   const uint64_t endr = vm ? c + len - x : 0;  // > 0 for vm lanes
@@ -166,6 +176,12 @@ __device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, ui
     widx += __popcll(kb);
   } else {
     if (kept) acc.put(C, c, len, le, +1);
+    if constexpr (STAGE) {
+      WriteEm se{sg.n + lanes_below(kb), P.st_per, sg.start, sg.len, sg.cap};
+      if (kept) se.put(C, c, len, le, +1);
+      sg.over |= se.overflow;
+      sg.n += __popcll(kb);
+    }
   }
   // kept matches are disjoint and ordered: the last one ends last
   const int ll = 63 - __builtin_clzll(kb);
@@ -178,10 +194,10 @@ __device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, ui
 // Walk the deferred candidates (one per lane) and resolve them.  Each lane
 // copies the 32 bytes from c & ~15 into its LDS window (the tiles are gone
 // from registers); longer walks continue from global memory.
-template <bool WRITE, int ABL, bool W = false>
+template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
 __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr, uint32_t dn, int lane, const Tab<0>& T,
                                             const Ctx& C, const ScanParams& P, uint64_t& x, CountEm& acc,
-                                            uint64_t& widx, uint32_t& wover, uint32_t& ovf)
+                                            uint64_t& widx, uint32_t& wover, uint32_t& ovf, Stage& sg)
 {
   wave_lds_sync();
   const bool valid = (uint32_t)lane < dn;
@@ -210,7 +226,7 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
     // stay a superset (W only removes matches), so the prefilter is unchanged
     len = walk<0, W>(T, w, c, le, ovf);
   }
-  resolve<WRITE>(valid, c, len, le, lane, C, P, x, acc, widx, wover);
+  resolve<WRITE, STAGE>(valid, c, len, le, lane, C, P, x, acc, widx, wover, sg);
   wave_lds_sync();  // the aux region is reused
 }
 
@@ -222,6 +238,7 @@ struct WaveChain {
   uint32_t wover;  // output capacity exceeded
   uint32_t ovf;    // a walk ran past the read window
   CountEm acc;
+  Stage sg;        // COUNT pass with staging: the wave's staged records
 };
 
 // Prefilter one 4 KiB wave-tile held in registers (v_k = chunk k: bytes
@@ -231,7 +248,7 @@ struct WaveChain {
 // by the wave's range [wlo, whi).
 // ABL (benchmarking only; results are not matches): 1 loads alone, 2 loads +
 // prefilter, 3 everything but the walks.
-template <bool WRITE, int ABL, bool W = false>
+template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
 __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3,
                                           uint64_t ts, bool edge, uint64_t wlo, uint64_t whi, int lane,
                                           const FTab& F, const Tab<0>& T, const Ctx& C, const ScanParams& P,
@@ -310,7 +327,7 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
     const uint32_t rank = incl - cnt;
     for (uint32_t done = 0; done < tot;) {
       if (w.dn == (uint32_t)kDefer) {
-        flush_deferred<WRITE, ABL, W>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
+        flush_deferred<WRITE, ABL, W, STAGE>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf, w.sg);
         w.dn = 0;
       }
       const uint32_t take = tot - done < kDefer - w.dn ? tot - done : kDefer - w.dn;
@@ -341,7 +358,7 @@ __device__ __forceinline__ TileLoad wave_tile(const uint8_t* wbase, uint32_t i, 
 
 }  // namespace
 
-template <bool WRITE, int ABL, bool W = false>
+template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
 __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -377,6 +394,14 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
   w.widx = WRITE ? P.out_base[gw] : 0;
   w.wover = 0;
   w.ovf = 0;
+  if constexpr (WRITE) {  // single-pass OFFSETS: this wave's records were staged and copied already
+    if (P.st_n && P.st_n[gw] == kStageDone) return;
+  }
+  if constexpr (STAGE) {
+    w.sg.start = P.st_start + gw * P.st_per;
+    w.sg.len = P.st_len + gw * P.st_per;
+    w.sg.cap = P.st_cap + gw * P.st_per;
+  }
 
   // Tiles arrive by coalesced 16 B/lane loads into two register sets used in
   // turn (a* = tile i, b* = tile i+1): the load of the next tile is in flight
@@ -408,7 +433,7 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
   uint32_t i = 0;
   if (n >= 2) {
     do {
-      tile_pass<WRITE, ABL, W>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, i == 0 && clip_lo, wlo, whi, lane, F, T, C,
+      tile_pass<WRITE, ABL, W, STAGE>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, i == 0 && clip_lo, wlo, whi, lane, F, T, C,
                             P, dl, scr, w);
       {
         const TileLoad L = wave_tile(wbase, i + 2, rel);
@@ -417,7 +442,7 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
         a2 = stream16(L, lo16 + 2048);
         a3 = stream16(L, lo16 + 3072);
       }
-      tile_pass<WRITE, ABL, W>(b0, b1, b2, b3, wb + (uint64_t)(i + 1) * kWaveTile, i + 2 == n && clip_hi, wlo, whi,
+      tile_pass<WRITE, ABL, W, STAGE>(b0, b1, b2, b3, wb + (uint64_t)(i + 1) * kWaveTile, i + 2 == n && clip_hi, wlo, whi,
                             lane, F, T, C, P, dl, scr, w);
       {
         const TileLoad L = wave_tile(wbase, i + 3, rel);
@@ -430,9 +455,9 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
     } while (i + 1 < n);
   }
   if (i < n)  // a* holds tile i = n - 1
-    tile_pass<WRITE, ABL, W>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, (i == 0 && clip_lo) || clip_hi, wlo, whi,
+    tile_pass<WRITE, ABL, W, STAGE>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, (i == 0 && clip_lo) || clip_hi, wlo, whi,
                           lane, F, T, C, P, dl, scr, w);
-  if (w.dn) flush_deferred<WRITE, ABL, W>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf);
+  if (w.dn) flush_deferred<WRITE, ABL, W, STAGE>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf, w.sg);
   uint64_t x = w.x > whi ? w.x : whi;  // chain exit: the last kept match end or the range end
   if (tb == te) x = wlo;
 
@@ -440,6 +465,7 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
   if (w.wover) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
   if constexpr (!WRITE) {
     const uint64_t c = wave_sum(w.acc.cnt), d = wave_sum(w.acc.dg), dc = wave_sum(w.acc.dc);
+    if (STAGE && lane == 0) P.st_n[gw] = w.sg.over ? kStageOver : (uint32_t)w.sg.n;
     if (lane == 0) {
       BlockRec rec;
       rec.entry = wlo;
@@ -462,26 +488,68 @@ size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates)
 
 namespace {
 
-template <bool WRITE, int ABL, bool W = false>
+template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
 hipError_t sparse_one(const ScanParams& P, size_t smem, hipStream_t stream)
 {
   static size_t attr_smem = 65536;
   if (smem > attr_smem) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE, ABL, W>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE, ABL, W, STAGE>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_smem = smem;
   }
-  hipLaunchKernelGGL((sparse_kernel<WRITE, ABL, W>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream, P);
+  hipLaunchKernelGGL((sparse_kernel<WRITE, ABL, W, STAGE>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream, P);
   return hipGetLastError();
+}
+
+// Single-pass OFFSETS, second half: one workgroup per staged wave record
+// copies its records to their final slots (fix_kernel's output bases) when
+// the wave's speculative chain was the true one (its exact entry equals its
+// own) and its slice held them all; other waves are left to a WRITE pass
+// (UGPU_FLAG_NEEDWRITE), which skips the copied ones.
+__global__ __launch_bounds__(256) void stage_copy_kernel(ScanParams P)
+{
+  const uint32_t b = blockIdx.x;
+  if (b >= P.nrec) return;
+  const uint32_t n = P.st_n[b];
+  const uint64_t base = P.out_base[b];
+  const uint64_t next = b + 1 < P.nrec ? P.out_base[b + 1] : P.totals->count;
+  const bool ok = n != kStageOver && P.entries[b] == P.recs[b].entry && next - base == n;
+  __syncthreads();
+  if (!ok) {
+    if (threadIdx.x == 0) atomicOr(P.flags, UGPU_FLAG_NEEDWRITE);
+    return;
+  }
+  if (base + n > P.out_capacity) {
+    if (threadIdx.x == 0) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+    return;
+  }
+  const uint64_t s0 = (uint64_t)b * P.st_per;
+  for (uint32_t i = threadIdx.x; i < n; i += 256) {
+    P.out_start[base + i] = P.st_start[s0 + i];
+    P.out_len[base + i] = P.st_len[s0 + i];
+    P.out_cap[base + i] = P.st_cap[s0 + i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) P.st_n[b] = kStageDone;
 }
 
 }  // namespace
 
+hipError_t launch_stage_copy(const ScanParams& P, hipStream_t stream)
+{
+  hipLaunchKernelGGL(stage_copy_kernel, dim3(P.nrec), dim3(256), 0, stream, P);
+  return hipGetLastError();
+}
+
 hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream_t stream)
 {
-  if (P.wtab) return write ? sparse_one<true, 0, true>(P, smem, stream) : sparse_one<false, 0, true>(P, smem, stream);
+  if (P.wtab) {
+    if (write) return sparse_one<true, 0, true>(P, smem, stream);
+    return P.st_n ? sparse_one<false, 0, true, true>(P, smem, stream) : sparse_one<false, 0, true>(P, smem, stream);
+  }
   if (write) return sparse_one<true, 0>(P, smem, stream);
+  if (P.st_n) return sparse_one<false, 0, false, true>(P, smem, stream);
   switch (P.ablate) {  // benchmarking knob (UGPU_ABLATE): count pass only
     case 1: return sparse_one<false, 1>(P, smem, stream);
     case 2: return sparse_one<false, 2>(P, smem, stream);

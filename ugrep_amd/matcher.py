@@ -350,6 +350,10 @@ class Scanner:
         check(lib.ugpu_scan_totals(self._h, ctypes.byref(t)))
         return t
 
+    def stage(self, on=True):
+        """Single-pass OFFSETS: COUNT scans stage the records of prefiltered tables."""
+        check(lib.ugpu_scanner_stage(self._h, 1 if on else 0))
+
     def kernel_ms(self):
         ms = ctypes.c_float()
         check(lib.ugpu_scan_kernel_ms(self._h, ctypes.byref(ms)))
