@@ -221,3 +221,35 @@ def test_agrees_with_xi_kernel_256mib(U, pats):
         finally:
             os.environ.pop("UGPU_XC", None)
     assert res[:4] == res[4:], res
+
+
+def test_offsets_written_by_xc(U, pats, patterns, inputs):
+    """OFFSETS from xc_kernel's own WRITE pass (starts at exact indices, ends
+    paired by index, lengths by the subtraction pass): records of ranges
+    [lo, hi) equal the oracle's, over several grids."""
+    from oracle_lib import OracleDfa
+    opc = patterns["c3_ident"]["opc"]
+    st = torch.cuda.current_stream().cuda_stream
+    rng = np.random.default_rng(5)
+    for name in ("code", "long_words", "border_sync", "all_ident", "digits_noise"):
+        host = inputs[name]
+        n = host.size
+        t = _dev(host)
+        _, _, _, lst = OracleDfa(opc).find(host, want_list=True)
+        for lo, hi, g in ((0, n, ""), (0, n, "5"), (int(rng.integers(0, n // 2)), n - 3, "37"), (1, 5000, "")):
+            if g:
+                os.environ["UGPU_MAX_GRID"] = g
+            try:
+                sc = U.Scanner(pats["c3_ident"])
+            finally:
+                os.environ.pop("UGPU_MAX_GRID", None)
+            sc.scan(t.data_ptr(), lo, hi, n, True, 0, st)
+            cnt = sc.totals().count
+            s = torch.empty(cnt + 1, dtype=torch.int64, device="cuda")
+            ln = torch.empty(cnt + 1, dtype=torch.int32, device="cuda")
+            cp = torch.empty(cnt + 1, dtype=torch.int32, device="cuda")
+            sc.offsets(s.data_ptr(), ln.data_ptr(), cp.data_ptr(), cnt, st)
+            torch.cuda.synchronize()
+            got = list(zip(s[:cnt].cpu().tolist(), ln[:cnt].cpu().tolist(), cp[:cnt].cpu().tolist()))
+            want = [tuple(r) for r in OracleDfa(opc).find(host, start=lo, want_list=True)[3] if r[0] < hi]
+            assert got == want, (name, lo, hi, g)

@@ -297,7 +297,7 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
 hipError_t launch_main(const ugpu_scanner* s, const ScanParams& P, bool write, hipStream_t st, bool xi = false)
 {
   if (s->word) return launch_wfind(P, s->dfa->t.format, write, st);
-  if (xi && s->xc) return launch_xc(P, st);
+  if (xi && s->xc) return launch_xc(P, write, st);
   if (xi && s->xg) return launch_xg(P, st);
   if (xi) return launch_xi(P, s->xi_smem, st);
   if (s->sparse) return launch_sparse(P, write, s->smem, st);
@@ -918,7 +918,23 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
   HIP_TRY(hipStreamSynchronize(s->stream));
   ScanParams P = s->last;
   bool forest = s->forest || (*s->h_flags & UGPU_FLAG_BUDGET);
-  if (s->last_xi && s->wxc) s->word = true;  // the records of an xc W scan: wfind_kernel's passes
+  if (s->last_xi && s->xc && !forest) {
+    // xc_kernel writes its own records (starts, then lengths from the ends),
+    // at the output bases of the COUNT pass's exact records
+    P.out_base = s->d_obase;
+    P.out_start = d_start;
+    P.out_len = d_len;
+    P.out_cap = d_cap;
+    P.out_capacity = capacity;
+    HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
+    HIP_TRY(launch_xc(P, true, st, s->h_tot->count));
+    HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (*s->h_flags & UGPU_FLAG_CAPACITY) return fail(UGPU_CAPACITY, "output capacity exceeded");
+    if (*s->h_flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
+    return UGPU_OK;
+  }
+  if (s->last_xi && s->wxc) s->word = true;  // (not reached: xc writes its own W records)
   if (s->last_xi && !forest) {
     // xi_kernel has no record-writing pass: redo the chain records with the
     // dense kernel's geometry (COUNT + fix), then its WRITE pass

@@ -225,8 +225,9 @@ hipError_t xg_occupancy(uint32_t entries, int* blocks_per_cu);  // 0 blocks: the
 size_t xg_smem_bytes(uint32_t entries);
 uint32_t xg_unit();
 uint32_t xg_waves();
-// two-state carry-chain kernel, xc_kernel.hip (COUNT mode only)
-hipError_t launch_xc(const ScanParams& P, hipStream_t stream);
+// two-state carry-chain kernel, xc_kernel.hip (COUNT, or WRITE into P.out_*
+// at the output bases of the COUNT pass's records; out_capacity = the count)
+hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64_t count = 0);
 hipError_t xc_occupancy(int* blocks_per_cu);
 uint32_t xc_unit();
 uint32_t xc_waves();

@@ -199,7 +199,8 @@ struct CIt {
 
 // Finish one chunk: final adds with the lane carry-in, then the events.
 // cb = the lane's carry-in bits (bit 0 of each byte: In_{i-1}).
-__device__ __forceinline__ void cfinish(CLane& L, uint32_t ci, uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4])
+__device__ __forceinline__ void cfinish(CLane& L, uint32_t ci, uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4],
+                                        uint32_t sb[4])
 {
   uint32_t k;
   L.S[0] = __builtin_addc(L.S[0], ci, 0u, &k);
@@ -216,14 +217,76 @@ __device__ __forceinline__ void cfinish(CLane& L, uint32_t ci, uint32_t& cs, uin
     const uint32_t wd = (4u * d) | ((4u * d + 1) << 8) | ((4u * d + 2) << 16) | ((4u * d + 3) << 24);
     ws = __builtin_amdgcn_udot4(st, wd, ws, false);
     cb[d] = c;
+    sb[d] = st;
   }
+}
+
+// OFFSETS pass (WRITE): the wave's output cursor (index of its next match
+// start; fix_kernel's output base at the wave start) and the output arrays.
+struct COut {
+  uint64_t cur = 0;
+  uint64_t* start = nullptr;
+  uint32_t* len = nullptr;
+  uint32_t* cap = nullptr;
+  uint64_t capacity = 0;
+  int64_t delta = 0;
+  uint32_t cap1 = 0;
+  uint32_t over = 0;
+};
+
+// Write the chunk's match starts and ends.  Starts get consecutive indices in
+// chain order (the lane's offset is a wave scan of the lanes' start counts);
+// an end at position e (In_{e-1} set, In_e clear or a new start at e) closes
+// the match with the latest index before it, whose len slot temporarily gets
+// the end position (xc_len_kernel subtracts the start afterwards: the start
+// may lie in an earlier lane, chunk or wave).
+__device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], const uint32_t sb[4], uint64_t q, COut& o)
+{
+  const uint32_t ns = __builtin_popcount(sb[0]) + __builtin_popcount(sb[1]) + __builtin_popcount(sb[2]) +
+                      __builtin_popcount(sb[3]);
+  const int lane = threadIdx.x & 63;
+  uint32_t incl = ns;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const uint32_t y = __shfl_up(incl, s, 64);
+    if (lane >= s) incl += y;
+  }
+  uint64_t cur = o.cur + (incl - ns);
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t c = cb[d], st = sb[d];
+    const uint32_t in = (L.E[d] | ((L.E[d] >> 1) & c)) & kOnes;  // In_i = G_i | X_i & In_{i-1}
+    const uint32_t en = c & (~in | st);
+    uint32_t mm = en | st;
+    while (mm) {
+      const uint32_t j = (uint32_t)__builtin_ctz(mm) >> 3, bit = 1u << (8 * j);
+      const uint64_t pos = q + 4 * d + j + (uint64_t)o.delta;
+      if (en & bit) {
+        if (cur - 1 < o.capacity)
+          o.len[cur - 1] = (uint32_t)pos;
+        else
+          o.over = 1;
+      }
+      if (st & bit) {
+        if (cur < o.capacity) {
+          o.start[cur] = pos;
+          o.cap[cur] = o.cap1;
+        } else {
+          o.over = 1;
+        }
+        ++cur;
+      }
+      mm &= ~bit;
+    }
+  }
+  o.cur += (uint32_t)__shfl((int)incl, 63, 64);
 }
 
 // One chunk (16 bytes per lane at q = chunk base + 16 lane); cw = the wave's
 // carry, updated.  Returns the lane's carry-in bits.
-template <bool MASK, bool W>
+template <bool MASK, bool W, bool WR = false>
 __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_t q, const CLim& lim, uint32_t& cw,
-                                       uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4], CW& wc)
+                                       uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4], CW& wc, COut& o)
 {
 #if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 1  // loads only (benchmarking; wrong counts)
   if (!MASK) {
@@ -236,7 +299,9 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
   bool prop;
   const bool gen = cadd(L, prop);
   const uint64_t cin = clook(__ballot(gen), __ballot(prop), cw, cw);
-  cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb);
+  uint32_t sb[4];
+  cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb, sb);
+  if constexpr (WR) cwrite(L, cb, sb, q, o);
 }
 
 // Exit search after a masked chunk of the wave holding hi: the exit is the
@@ -268,7 +333,7 @@ __device__ __forceinline__ uint32_t ccode(uint32_t cls) { return cls & 0x80u ? 0
 
 }  // namespace
 
-template <bool W>
+template <bool W, bool WR>
 __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
 {
   // LDS: byte codes, and (pair classifier) the codes of every byte pair
@@ -300,6 +365,16 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   const uint32_t lo16 = 16u * (uint32_t)lane;
   CW wc;
   wc.bob = P.bob;
+  COut out;
+  if constexpr (WR) {
+    out.cur = n ? P.out_base[gw] : 0;
+    out.start = P.out_start;
+    out.len = P.out_len;
+    out.cap = P.out_cap;
+    out.capacity = P.out_capacity;
+    out.delta = P.delta;
+    out.cap1 = P.cap1;
+  }
   // option W: the code of the byte before position p (byte 3), 0 at the buffer start
   auto xprev = [&](uint64_t p) -> uint32_t { return W && p > P.bob ? (uint32_t)bcode[P.g[p - 1]] << 24 : 0u; };
 
@@ -350,7 +425,7 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   auto masked = [&](uint64_t q0) {
     const uint4 v = cload(crsrc(P.g + q0, rend16 > q0 ? rend16 - q0 : 0), lo16);
     uint32_t cs = 0, ws = 0, ls = 0, cb[4];
-    cchunk<true, W>(cc, v, q0 + lo16, lim, cw, cs, ws, ls, cb, wc);
+    cchunk<true, W, WR>(cc, v, q0 + lo16, lim, cw, cs, ws, ls, cb, wc, out);
     cnt += cs;
     pos += (uint64_t)cs * (q0 + lo16) + ws;
     lbits += ls;
@@ -386,7 +461,8 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
     CIt a;
     uint32_t cb[4];
 #pragma unroll
-    for (int j = 0; j < kCIter; ++j) cchunk<false, W>(cc, cur[j], 0, lim, cw, a.cs[j], a.ws, a.ls, cb, wc);
+    for (int j = 0; j < kCIter; ++j)
+      cchunk<false, W, WR>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out);
     uint32_t c = 0, cj = 0;
 #pragma unroll
     for (int j = 0; j < kCIter; ++j) {
@@ -408,6 +484,10 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
     for (; q0 < whi || (last_wave && !found); q0 += kCChunk) masked(q0);
   if (found) cw = 0;  // past the exit every carry is clear
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
+  if constexpr (WR) {
+    if (__ballot(out.over) && lane == 0) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+    return;  // (the records are the COUNT pass's)
+  }
   if constexpr (W) {
     if (__ballot((wc.hi & 0x80808080u) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_WSLOW);
   }
@@ -428,18 +508,40 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   }
 }
 
-hipError_t launch_xc(const ScanParams& P, hipStream_t stream)
+// OFFSETS, second step: len[k] held the end position (low 32 bits, reported
+// coordinates); subtract the start
+__global__ __launch_bounds__(256) void xc_len_kernel(uint64_t* start, uint32_t* len, uint64_t n)
 {
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256)
+    len[k] -= (uint32_t)start[k];
+}
+
+hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64_t count)
+{
+  if (write) {
+    if (P.xc_w)
+      hipLaunchKernelGGL((xc_kernel<true, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    else
+      hipLaunchKernelGGL((xc_kernel<false, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t n = count < P.out_capacity ? count : P.out_capacity;
+    if (n) {
+      const uint64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
+      hipLaunchKernelGGL(xc_len_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, P.out_start, P.out_len, n);
+    }
+    return hipGetLastError();
+  }
   if (P.xc_w)
-    hipLaunchKernelGGL(xc_kernel<true>, dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    hipLaunchKernelGGL((xc_kernel<true, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   else
-    hipLaunchKernelGGL(xc_kernel<false>, dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    hipLaunchKernelGGL((xc_kernel<false, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   return hipGetLastError();
 }
 
 hipError_t xc_occupancy(int* n)
 {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<true>, kCWaves * 64, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<true, true>, kCWaves * 64, 0);
 }
 uint32_t xc_unit() { return kCTile; }
 uint32_t xc_waves() { return kCWaves; }
