@@ -41,7 +41,7 @@
 //
 // Dispatch (tools/bench_adapter.py):
 //   * inputs shorter than UGPU_ADAPTER_MIN_BYTES (default 4 MiB for sparse
-//     tables, 256 KiB for dense ones; a stream counts when it ends before its
+//     tables, 64 KiB for dense ones; a stream counts when it ends before its
 //     first feed) stay on the CPU matcher: a device round trip costs more than
 //     the reference's scan of a small buffer;
 //   * patterns with a selective prefilter (sparse_kernel, e.g. foo|bar|baz) use
@@ -179,10 +179,10 @@ class GpuMatcher : public Matcher {
   }
   // smallest input for the GPU: measured crossover against one reference
   // matcher on a host buffer (profiles/r02_adapter_latency.jsonl): 4 MiB for
-  // C2-like sparse tables, 64-256 KiB for dense ones
+  // C2-like sparse tables, 64 KiB for dense ones (profiles/r02b_adapter_latency.jsonl)
   size_t min_bytes() const
   {
-    return min_bytes_ != ~static_cast<size_t>(0) ? min_bytes_ : (sparse_ ? (4u << 20) : (256u << 10));
+    return min_bytes_ != ~static_cast<size_t>(0) ? min_bytes_ : (sparse_ ? (4u << 20) : (64u << 10));
   }
   // live GpuMatchers of the process (ugrep: one per worker thread)
   static std::atomic<int>& live()
