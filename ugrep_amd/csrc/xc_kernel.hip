@@ -137,26 +137,28 @@ __device__ __forceinline__ void ccodes(const CCodes& cc, const uint4& v, CLane& 
 #pragma unroll
   for (int d = 0; d < 4; ++d) L.E[d] = cc(w[d]);
   if constexpr (W) {
+    if constexpr (MASK) {  // bytes before the buffer are K and not seen
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t m = 0xffffffffu;
-      if constexpr (MASK) {  // bytes before the buffer are K and not seen
-        m = ~below(q + 4 * d, wc.bob);
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t m = ~below(q + 4 * d, wc.bob);
         L.E[d] &= m;
+        wc.hi |= w[d] & m;
       }
-      wc.hi |= w[d] & m;
+    } else {
+      wc.hi |= w[0] | w[1] | w[2] | w[3];
     }
-    // a G byte whose previous byte is in X (code bit 1) becomes P
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t prev = __shfl_up(L.E[3], 1, 64);
-    if (lane == 0) prev = wc.cx;
-    wc.cx = __shfl(L.E[3], 63, 64);
+    // a G byte whose previous byte is in X (code bit 1) becomes P: bit 1 of the
+    // previous byte lands on bit 0 by one funnel shift (v_alignbit by 25)
+    // (DPP wave_shr:1: lane l gets lane l-1's last dword, lane 0 keeps the
+    // previous chunk's, held in wc.cx)
+    const uint32_t prev = __builtin_amdgcn_update_dpp(wc.cx, L.E[3], 0x138, 0xf, 0xf, false);
+    wc.cx = __builtin_amdgcn_readlane(L.E[3], 63);
     uint32_t xp[4];
-    xp[0] = __builtin_amdgcn_alignbyte(L.E[0], prev, 3);
+    xp[0] = __builtin_amdgcn_alignbit(L.E[0], prev, 25);
 #pragma unroll
-    for (int d = 1; d < 4; ++d) xp[d] = __builtin_amdgcn_alignbyte(L.E[d], L.E[d - 1], 3);
+    for (int d = 1; d < 4; ++d) xp[d] = __builtin_amdgcn_alignbit(L.E[d], L.E[d - 1], 25);
 #pragma unroll
-    for (int d = 0; d < 4; ++d) L.E[d] &= ~((xp[d] >> 1) & kOnes);
+    for (int d = 0; d < 4; ++d) L.E[d] &= ~(xp[d] & kOnes);
   }
   if constexpr (MASK) {
 #pragma unroll
