@@ -155,6 +155,14 @@ int ugpu_tables_gap_host(const uint32_t *opc, uint32_t nop, uint16_t *xg, uint32
    tables, the per-byte opcode scan of lib/matcher.cpp:460-545.) */
 int ugpu_tables_xc_host(const uint32_t *opc, uint32_t nop, uint8_t *cls, int *ok);
 
+/* Host-only: the code-point run tables of a table whose language is S+ for a
+   set S of single-code-point tokens (\w+, \S+, [[:alpha:]]+ over UTF-8;
+   ugrep_amd/csrc/tables.hpp xu_*): tab[256 + 64 * 256] token codes and
+   bm3[2048] third-byte bits (either may be NULL).  *ok = 0 when the table does
+   not qualify.  (Replaces, for these tables, the per-byte opcode scan of
+   lib/matcher.cpp:460-545.) */
+int ugpu_tables_xu_host(const uint32_t *opc, uint32_t nop, uint8_t *tab, uint32_t *bm3, int *ok);
+
 /* Host-only: *eq = 1 when two opcode tables accept the same strings with the
    same accept indices (so their FIND chains agree on every input).  The
    engine uses it to recognise \w+ under option W. */

@@ -19,8 +19,17 @@ torch = pytest.importorskip("torch")
 GAP = ("c4_word", "s_plus", "nonspace")
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _no_xu():
+    """These tables are also code-point run tables (xc_kernel U mode, tests/test_xu.py);
+    here they run xg_kernel."""
+    os.environ["UGPU_XU"] = "0"
+    yield
+    os.environ.pop("UGPU_XU", None)
+
+
 @pytest.fixture(scope="module")
-def gpats(U, patterns):  # noqa: F811
+def gpats(U, patterns, _no_xu):  # noqa: F811
     return {k: U.Pattern(patterns[k]["opc"]) for k in GAP}
 
 

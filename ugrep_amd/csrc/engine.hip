@@ -63,6 +63,7 @@ struct ugpu_dfa {
   uint16_t* d_xtrans = nullptr;  // FIND transducer (restart-local tables on the dense path)
   uint8_t* d_xid = nullptr;      // immediate transducer ids (xi_kernel), COUNT scans
   uint16_t* d_xg = nullptr;      // gap transducer (xg_kernel), COUNT scans
+  uint8_t* d_xu = nullptr;       // code-point run tables (xc_kernel U mode): kXuTab bytes, then kXuBm3 dwords
   uint8_t* d_xg_sync = nullptr;
   uint8_t* d_cls = nullptr;
   uint32_t* d_caps = nullptr;
@@ -87,7 +88,9 @@ struct ugpu_scanner {
   bool sparse = false;   // prefiltered wave-persistent kernel (sparse_kernel.hip)
   bool xi = false;       // COUNT scans run xi_kernel (immediate tables); OFFSETS use the dense kernel
   bool xg = false;       // COUNT scans run xg_kernel (gap tables); OFFSETS use the dense kernel
-  bool xc = false;       // COUNT scans run xc_kernel (two-state tables); OFFSETS use the dense kernel
+  bool xc = false;       // COUNT and OFFSETS scans run xc_kernel (two-state and, U mode, code-point run tables)
+  bool xu_xi = false, xu_xg = false;  // U mode: the kernels a range goes to when it flags UGPU_FLAG_USLOW
+  bool last_xc = false;  // the last ugpu_scan ran xc_kernel
   bool word = false;     // option W: every pass runs wfind_kernel (wfind.hip) (per scan when wfast)
   bool wfast = false;    // option W on a \w+ table: non-W kernels when the scanned bytes are valid UTF-8
   int word_rec = 0;      // chain records of a wfind scan
@@ -212,6 +215,14 @@ bool dfa_xc(const ugpu_dfa* d)
   return d->t.xc && !d->t.filter && d->t.cap1 != 0 && (!d->d_wtab || d->xcw) && !(env && env[0] == '0');
 }
 
+// code-point run tables run xc_kernel's U mode for COUNT and OFFSETS scans
+// (UGPU_XU=0: xg/xi/dense); under option W only on \w+ (the W fast path)
+bool dfa_xu(const ugpu_dfa* d)
+{
+  const char* env = std::getenv("UGPU_XU");
+  return d->d_xu && (!d->d_wtab || d->wplus) && !(env && env[0] == '0');
+}
+
 void fill_tables(ScanParams& P, const ugpu_dfa* d)
 {
   P.trans = d->d_trans;
@@ -235,6 +246,9 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.nwtab = d->nwtab;
   P.xc_cls = d->d_cls + 256;
   P.xc_w = d->xcw ? 1u : 0u;
+  P.xu_tab = dfa_xu(d) ? d->d_xu : nullptr;
+  P.xu_bm3 = d->d_xu ? reinterpret_cast<const uint32_t*>(d->d_xu + kXuTab) : nullptr;
+  P.xu_null = d->t.xu_null;
   // chain bytes one stitch merge may cross before the chains count as not
   // resynchronising (two chains of a resynchronising table meet within a match
   // or two; longer merges go to the forest FIND)
@@ -439,6 +453,14 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       return hip_fail(e, "immediate transducer upload");
     }
   }
+  if (d->t.xu && !d->t.filter && d->t.cap1 != 0) {
+    if ((e = hipMalloc(&d->d_xu, kXuTab + 4 * kXuBm3)) != hipSuccess ||
+        (e = hipMemcpy(d->d_xu, d->t.xu_tab.data(), kXuTab, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(d->d_xu + kXuTab, d->t.xu_bm3.data(), 4 * kXuBm3, hipMemcpyHostToDevice)) != hipSuccess) {
+      ugpu_dfa_destroy(d);
+      return hip_fail(e, "code-point run table upload");
+    }
+  }
   if (d->t.gap && !d->t.filter && d->t.cap1 != 0) {
     // device form: the class-major product table (tables.hpp xg2), padded to 8 entries
     std::vector<uint16_t> xg((d->t.xg2.size() + 7) & ~size_t(7), 0);
@@ -465,6 +487,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   if (d->d_wtab) (void)hipFree(d->d_wtab);
   if (d->d_xid) (void)hipFree(d->d_xid);
   if (d->d_xg) (void)hipFree(d->d_xg);
+  if (d->d_xu) (void)hipFree(d->d_xu);
   if (d->d_xg_sync) (void)hipFree(d->d_xg_sync);
   if (d->d_cls) (void)hipFree(d->d_cls);
   if (d->d_caps) (void)hipFree(d->d_caps);
@@ -488,6 +511,7 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->kernel = (d->d_wtab && !d->wplus && !d->xcw && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
                  : (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
                  : dfa_xc(d)                                   ? 5u
+                 : dfa_xu(d)                                   ? 6u
                  : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u
                  : (d->d_xg && !(genv && genv[0] == '0'))  ? 3u
                                                            : 1u;
@@ -513,6 +537,7 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   info->accepting = t.accepting;
   info->kernel = (t.filter && t.format == FMT_BYTE) ? 0u
                  : (t.xc && t.cap1 != 0)             ? 5u
+                 : (t.xu && t.cap1 != 0)             ? 6u
                  : (t.immediate && t.cap1 != 0)      ? 2u
                  : (t.gap && t.cap1 != 0)            ? 3u
                                                      : 1u;
@@ -597,6 +622,19 @@ int ugpu_tables_xc_host(const uint32_t* opc, uint32_t nop, uint8_t* cls, int* ok
   if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
   *ok = t.xc ? 1 : 0;
   if (cls && t.xc) std::copy(t.xc_tab.begin(), t.xc_tab.end(), cls);
+  return UGPU_OK;
+}
+
+int ugpu_tables_xu_host(const uint32_t* opc, uint32_t nop, uint8_t* tab, uint32_t* bm3, int* ok)
+{
+  if (!ok) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *ok = t.xu ? 1 : 0;
+  if (tab && t.xu) std::copy(t.xu_tab.begin(), t.xu_tab.end(), tab);
+  if (bm3 && t.xu) std::copy(t.xu_bm3.begin(), t.xu_bm3.end(), bm3);
   return UGPU_OK;
 }
 
@@ -725,11 +763,13 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   }
   // two-state tables: COUNT scans on xc_kernel, ahead of xi/xg (UGPU_XC=0
   // keeps those)
-  if (!s->sparse && dfa_xc(dfa)) {
+  if (!s->sparse && (dfa_xc(dfa) || dfa_xu(dfa))) {
     int cpc = 0;
     HIP_TRY_S(xc_occupancy(&cpc));
     if (cpc >= 1) {
       s->xc = true;
+      s->xu_xi = s->xi;
+      s->xu_xg = s->xg;
       s->xi = s->xg = false;
       const int cg = prop.multiProcessorCount * cpc * (int)xc_waves();
       s->xi_rec = cg > kMaxRec ? kMaxRec : cg;
@@ -843,6 +883,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   s->last = P;
   s->last_xi = !s->word && (s->xi || s->xg || s->xc);
+  s->last_xc = !s->word && s->xc;
   s->last_buf = dbuf;
   s->last_args[0] = lo;
   s->last_args[1] = hi;
@@ -868,6 +909,19 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
     const int rc = ugpu_scan(s, s->last_buf, s->last_args[0], s->last_args[1], s->last_args[2],
                              (int)s->last_args[3], s->last_args[4], s->stream);
     s->wxc = true;
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+  }
+  if (s->last_xc && (*s->h_flags & UGPU_FLAG_USLOW)) {
+    // U mode met a lead byte of a 4-byte token: redo the range with the
+    // table's next kernel (xg / xi / dense)
+    s->xc = false;
+    s->xi = s->xu_xi;
+    s->xg = s->xu_xg;
+    const int rc = ugpu_scan(s, s->last_buf, s->last_args[0], s->last_args[1], s->last_args[2],
+                             (int)s->last_args[3], s->last_args[4], s->stream);
+    s->xc = true;
+    s->xi = s->xg = false;
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
   }
@@ -918,7 +972,7 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
   HIP_TRY(hipStreamSynchronize(s->stream));
   ScanParams P = s->last;
   bool forest = s->forest || (*s->h_flags & UGPU_FLAG_BUDGET);
-  if (s->last_xi && s->xc && !forest) {
+  if (s->last_xc && !forest) {
     // xc_kernel writes its own records (starts, then lengths from the ends),
     // at the output bases of the COUNT pass's exact records
     P.out_base = s->d_obase;

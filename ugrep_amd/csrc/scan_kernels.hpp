@@ -75,6 +75,9 @@ struct DevTotals {
 #define UGPU_FLAG_WSLOW 32u
 // stage_copy_kernel left waves whose staged records were not the true chain's
 #define UGPU_FLAG_NEEDWRITE 64u
+// xc_kernel's U mode met a lead byte of a 4-byte token (tables.hpp XU_SLOW):
+// the host redoes the range with the table's next kernel
+#define UGPU_FLAG_USLOW 128u
 constexpr uint32_t kStageOver = 0xffffffffu;
 constexpr uint32_t kStageDone = 0xfffffffeu;
 constexpr uint32_t kStagePer = 1024;  // staged records per wave (16 B each: 128 MiB for 8192 waves)
@@ -139,6 +142,10 @@ struct ScanParams {
   uint32_t* st_n;
   uint32_t st_per;
   uint32_t xc_w;          // option W on xc_kernel (X = the ASCII word bytes)
+  // code-point run tables (xc_kernel U mode, tables.hpp xu_*) or NULL
+  const uint8_t* xu_tab;  // kXuTab bytes (4-byte aligned)
+  const uint32_t* xu_bm3; // kXuBm3 dwords
+  uint32_t xu_null;       // the fill byte
 };
 
 // Forest FIND (forest.hip): exact for every table, no resynchronisation

@@ -171,6 +171,120 @@ bool restart_local(const std::vector<uint32_t>& nxt, uint32_t start, uint32_t fi
   return true;
 }
 
+// Code-point run tables (tables.hpp xu_*).  Tokens are the strings that take
+// the start state to its first accepting state; they must be single code
+// points (ASCII x, or x >= 0xC0 followed by continuation bytes), which also
+// makes the set prefix-free and the tokens non-overlapping.  The language is
+// then S+ exactly when every state a a token ends in accepts, after one byte
+// or more, the same strings as the start state (then a word of the language
+// splits greedily into tokens, and the longest match at p is the longest run
+// of consecutive tokens from p).
+void build_xu(const std::vector<uint32_t>& nxt, uint32_t S, uint32_t first_acc, uint32_t start_sid, DfaTables& t)
+{
+  auto acc = [&](uint32_t s) { return s >= first_acc; };
+  auto go = [&](uint32_t s, int c) { return nxt[(size_t)s * 256 + c]; };
+  auto cont = [](int c) { return (c & 0xc0) == 0x80; };
+  std::vector<uint8_t> tab(kXuTab, 0);
+  std::vector<uint32_t> bm3(kXuBm3, 0);
+  std::set<uint32_t> ends;  // states a token ends in
+  std::map<uint32_t, int> s3_ok;  // states after 3 bytes of a 4-byte token: 1 = every continuation ends a token
+  for (int x = 0; x < 256; ++x) {
+    const uint32_t s1 = go(start_sid, x);
+    if (!s1) continue;
+    if (cont(x)) return;  // a token may not start with a continuation byte
+    if (acc(s1)) {
+      ends.insert(s1);
+      if (x < 0x80)
+        tab[x] = 0x01;
+      else
+        for (int y = 0; y < 256; ++y) tab[256 + (x & 63) * 256 + y] = 0x01;
+      continue;
+    }
+    if (x < 0xc0) return;  // ASCII bytes are whole code points
+    for (int y = 0; y < 256; ++y) {
+      const uint32_t s2 = go(s1, y);
+      if (!s2) continue;
+      if (!cont(y)) return;
+      uint8_t& e = tab[256 + (x & 63) * 256 + y];
+      if (acc(s2)) {
+        ends.insert(s2);
+        e = 0x03;
+        continue;
+      }
+      int nacc = 0, nlive = 0;
+      for (int z = 0; z < 256; ++z) {
+        const uint32_t s3 = go(s2, z);
+        if (!s3) continue;
+        if (!cont(z)) return;
+        if (acc(s3)) {
+          ends.insert(s3);
+          ++nacc;
+          continue;
+        }
+        ++nlive;
+        auto it = s3_ok.find(s3);
+        if (it == s3_ok.end()) {
+          int ok = 1;
+          for (int w = 0; w < 256 && ok; ++w) {
+            const uint32_t s4 = go(s3, w);
+            if (!s4) continue;
+            if (!cont(w) || !acc(s4)) ok = 0;
+            else ends.insert(s4);
+          }
+          it = s3_ok.emplace(s3, ok).first;
+        }
+        if (!it->second) return;
+      }
+      if (nacc && nlive) return;  // 3- and 4-byte tokens sharing two bytes: not UTF-8
+      if (nlive) {
+        e = XU_SLOW;
+      } else if (nacc == 64) {
+        e = 0x07 | XU_T3;
+      } else if (nacc) {
+        if (x < 0xe0 || x > 0xef) return;
+        e = XU_T3 | XU_MIX;
+        for (int z = 0x80; z < 0xc0; ++z)
+          if (acc(go(s2, z))) {
+            const uint32_t i = (uint32_t)(x & 15) << 12 | (uint32_t)(y & 63) << 6 | (uint32_t)(z & 63);
+            bm3[i >> 5] |= 1u << (i & 31);
+          }
+      }
+    }
+  }
+  if (ends.empty()) return;
+  // the fill byte for positions outside [lo, readable end): starts no token
+  // and continues none
+  int null = -1;
+  for (int b = 255; b >= 0 && null < 0; --b)
+    if (!cont(b) && !go(start_sid, b)) null = b;
+  if (null < 0) return;
+  // every token end behaves like the start state on non-empty strings
+  for (uint32_t a : ends) {
+    std::set<std::pair<uint32_t, uint32_t> > seen;
+    std::vector<std::pair<uint32_t, uint32_t> > work;
+    work.emplace_back(a, start_sid);
+    while (!work.empty()) {
+      const auto pq = work.back();
+      work.pop_back();
+      for (int c = 0; c < 256; ++c) {
+        const uint32_t p = go(pq.first, c), q = go(pq.second, c);
+        if (acc(p) != acc(q)) return;
+        if ((p == 0) != (q == 0)) return;  // (minimised tables: a live state can accept)
+        if (p && seen.insert(std::make_pair(p, q)).second) {
+          if (seen.size() > 100000) return;
+          work.emplace_back(p, q);
+        }
+      }
+    }
+  }
+  (void)S;
+  t.xu = true;
+  t.xu_null = (uint8_t)null;
+  tab[129] = (uint8_t)null;  // (an unused slot: exported with the table)
+  t.xu_tab = std::move(tab);
+  t.xu_bm3 = std::move(bm3);
+}
+
 }  // namespace
 
 // Language equivalence with accept indices (tables.hpp): breadth-first over
@@ -612,6 +726,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
     else if (caps[s] != t.cap1)
       t.cap1 = 0;
   }
+  if (!t.xc && t.cap1 != 0 && start_sid < first_acc) build_xu(nxt, S, first_acc, start_sid, t);
   // prefilter (see tables.hpp): per first byte c, the bytes that can follow
   // it (second) and follow those (third); "all" once a prefix accepts
   std::vector<Lead> leads;

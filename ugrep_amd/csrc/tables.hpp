@@ -94,7 +94,32 @@ struct DfaTables {
   // [0-9A-Za-z_] (option W on xc_kernel).
   bool xc = false, xc_w = false;
   std::vector<uint8_t> xc_tab;
+  // Code-point runs (xc_kernel U mode): the language is S+ for a prefix-free
+  // set S of tokens (one UTF-8 code point each: an ASCII byte, or a lead byte
+  // >= 0xC0 followed by 1-3 continuation bytes 80-BF, and no token starts with
+  // a continuation byte).  Tokens then never overlap, so the FIND matches are
+  // exactly the maximal runs of bytes that lie inside some token, and "byte i
+  // lies inside a token" (M_i) is a local property of bytes i-3 .. i+3.  The
+  // token starting at byte x (next byte y) is coded XU_* (see below):
+  //   xu_tab[x]                            x < 0x80 (y is irrelevant)
+  //   xu_tab[128]                          continuation bytes: 0
+  //   xu_tab[256 + (x & 63) * 256 + y]     lead bytes x >= 0xC0
+  // xu_bm3: for 3-byte tokens whose completion depends on the third byte z
+  // (XU_MIX), bit ((x & 15) << 12 | (y & 63) << 6 | (z & 63)).
+  // xu_null: a byte that starts no token and is no continuation byte; the
+  // kernel reads it in place of bytes outside [lo, readable end).
+  bool xu = false;
+  uint8_t xu_null = 0;
+  std::vector<uint8_t> xu_tab;    // kXuTab bytes
+  std::vector<uint32_t> xu_bm3;   // kXuBm3 dwords
 };
+
+// xu codes: bits 0-3 a thermometer of the token's bytes (bit k: the token
+// covers byte x + k), XU_T3 the token needs a continuation byte at x + 2,
+// XU_MIX the third byte decides (xu_bm3), XU_SLOW a 4-byte token may start
+// here (the kernel flags the range and the host scans it with another kernel).
+constexpr uint8_t XU_T3 = 0x10, XU_MIX = 0x20, XU_SLOW = 0x40;
+constexpr uint32_t kXuTab = 256 + 64 * 256, kXuBm3 = 2048;
 
 // True when the two tables accept the same strings with the same accept
 // indices (so the FIND chains agree on every input).

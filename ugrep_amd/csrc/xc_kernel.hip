@@ -45,6 +45,8 @@
 #include "device_common.hpp"
 #include "tables.hpp"
 
+#include <type_traits>
+
 namespace ugpu {
 
 namespace {
@@ -159,6 +161,136 @@ __device__ __forceinline__ void ccodes(const CCodes& cc, const uint4& v, CLane& 
     for (int d = 1; d < 4; ++d) xp[d] = __builtin_amdgcn_alignbit(L.E[d], L.E[d - 1], 25);
 #pragma unroll
     for (int d = 0; d < 4; ++d) L.E[d] &= ~(xp[d] & kOnes);
+  }
+  if constexpr (MASK) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint64_t qd = q + 4 * d;
+      const uint32_t live = ~below(qd, lim.qlo) & below(qd, lim.qr);
+      L.E[d] &= live & (below(qd, lim.qg) | ~kOnes);
+    }
+  }
+}
+
+// ---- U mode: code-point runs (tables.hpp xu_*) ----------------------------
+// The language is S+ for single-code-point tokens, so the FIND matches are the
+// maximal runs of bytes inside a token (M bytes).  Each byte gets the code of
+// the token starting at it (a thermometer of the bytes it covers, from one
+// LDS byte lookup: ASCII bytes by themselves, continuation bytes all to one
+// entry, lead bytes by (lead, next byte)); M_i = OR_k bit k of code_{i-k} by
+// three funnel shifts; then e = 0xFF * M feeds the same adder as the two-state
+// tables (past hi the M bytes become P: they only continue the match crossing
+// hi).  Context: byte i's code reads bytes i+1, i+2 (the next lane's first
+// dword by DPP wave_shl:1, lane 63 the next chunk's), M_i reads codes i-3..i-1
+// (the previous lane's last code dword by DPP wave_shr:1, lane 0 the previous
+// chunk's).  Bytes outside [lo, readable end) read as the table's fill byte.
+struct CU {
+  const uint8_t* tab = nullptr;   // LDS: kXuTab token codes
+  const uint32_t* bm3 = nullptr;  // LDS: 3-byte completion bits
+  uint32_t null4 = 0;             // the fill byte, in every byte
+  uint64_t lo = 0, rend = 0;      // the bytes read as themselves
+  uint32_t nx0 = 0;               // (uniform) the dword after the chunk, filled
+  uint32_t cprev = 0;             // (uniform) codes of the 4 bytes before the chunk
+  uint32_t slow = 0;              // lane: OR of the codes (XU_SLOW: a 4-byte token)
+};
+
+// bytes of the dword at q inside [lo, rend) (0xff per byte)
+__device__ __forceinline__ uint32_t uinside(const CU& u, uint64_t q) { return ~below(q, u.lo) & below(q, u.rend); }
+
+// token codes of the 4 bytes of x (the next 4 bytes in nx); c7 = bit 7 of
+// each continuation byte of x
+__device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t nx, uint32_t& c7)
+{
+  const uint32_t t = x << 1;
+  const uint32_t l7 = x & t & 0x80808080u;  // lead bytes (>= 0xC0)
+  c7 = x & ~t & 0x80808080u;                // continuation bytes (80-BF)
+  const uint32_t lm = (l7 << 1) - (l7 >> 7);  // 0xff per lead byte
+  const uint32_t cm = (c7 << 1) - (c7 >> 7);
+  const uint32_t h = ((x & 0x3f3f3f3fu) + 0x01010101u) & lm;     // lead: (x & 63) + 1
+  const uint32_t y = __builtin_amdgcn_alignbit(nx, x, 8);          // the byte after each byte
+  uint32_t l = (y & lm) | (x & ~lm);
+  l = (l & ~cm) | (0x80808080u & cm);                              // continuation: entry 128
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t a = __builtin_amdgcn_perm(h, l, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
+    r |= (uint32_t)u.tab[a] << (8 * k);
+  }
+  return r;
+}
+
+// resolve the 3-byte tokens of code dword c (bytes x, next nx; continuation
+// bits c7 of x and c7n of nx): XU_MIX by the third byte, then every XU_T3
+// token needs a continuation byte at +2
+__device__ __forceinline__ uint32_t ucode_fix(const CU& u, uint32_t c, uint32_t x, uint32_t nx, uint32_t c7,
+                                              uint32_t c7n)
+{
+  uint32_t mm = c & 0x20202020u;
+  if (mm) {
+    do {
+      const uint32_t j = (uint32_t)__builtin_ctz(mm) >> 3;
+      const uint32_t b = __builtin_amdgcn_alignbit(nx, x, 8 * j);  // bytes x+j .. x+j+3
+      const uint32_t i = (b & 15u) << 12 | ((b >> 8) & 63u) << 6 | ((b >> 16) & 63u);
+      if ((u.bm3[i >> 5] >> (i & 31)) & 1u) c |= 7u << (8 * j);
+      mm &= ~(0xffu << (8 * j));
+    } while (mm);
+  }
+  const uint32_t bad = c & 0x10101010u & ~(__builtin_amdgcn_alignbit(c7n, c7, 16) >> 3);
+  return c & ~(bad - (bad >> 4));
+}
+
+// codes of the dword at q - 4 (for the chunk at q): every lane the same
+__device__ __forceinline__ uint32_t ucode_before(const CU& u, const uint8_t* g, uint64_t q)
+{
+  if (q < 4) return 0;  // (the fill byte starts no token)
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(g + q - 4);
+  const uint32_t x = (p[0] & uinside(u, q - 4)) | (u.null4 & ~uinside(u, q - 4));
+  const uint32_t nx = q < u.rend ? (p[1] & uinside(u, q)) | (u.null4 & ~uinside(u, q)) : u.null4;
+  uint32_t c7, c7n;
+  const uint32_t c = ucode_dw(u, x, nx, c7);
+  (void)ucode_dw(u, nx, u.null4, c7n);
+  return ucode_fix(u, c, x, nx, c7, c7n);
+}
+
+// the filled dword at q (uniform)
+__device__ __forceinline__ uint32_t uload_dw(const CU& u, const uint8_t* g, uint64_t q)
+{
+  if (q >= u.rend) return u.null4;
+  const uint32_t x = *reinterpret_cast<const uint32_t*>(g + q);
+  return (x & uinside(u, q)) | (u.null4 & ~uinside(u, q));
+}
+
+// One lane's 16 bytes at q: the adder codes e = 0xFF * M (limits as ccodes)
+template <bool MASK>
+__device__ __forceinline__ void ucodes(CU& u, const uint4& v, CLane& L, uint64_t q, const CLim& lim)
+{
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  if constexpr (MASK) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t in = uinside(u, q + 4 * d);
+      w[d] = (w[d] & in) | (u.null4 & ~in);
+    }
+  }
+  const uint32_t nx = __builtin_amdgcn_update_dpp(u.nx0, w[0], 0x130, 0xf, 0xf, false);  // wave_shl:1
+  uint32_t c[4], c7[5];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) c[d] = ucode_dw(u, w[d], d < 3 ? w[d + 1] : nx, c7[d]);
+  {
+    const uint32_t t = nx << 1;
+    c7[4] = nx & ~t & 0x80808080u;
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d) c[d] = ucode_fix(u, c[d], w[d], d < 3 ? w[d + 1] : nx, c7[d], c7[d + 1]);
+  u.slow |= c[0] | c[1] | c[2] | c[3];
+  const uint32_t cp = __builtin_amdgcn_update_dpp(u.cprev, c[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
+  u.cprev = __builtin_amdgcn_readlane(c[3], 63);
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t pv = d ? c[d - 1] : cp;
+    const uint32_t m = (c[d] | __builtin_amdgcn_alignbit(c[d], pv, 25) | __builtin_amdgcn_alignbit(c[d], pv, 18) |
+                        __builtin_amdgcn_alignbit(c[d], pv, 11)) & kOnes;
+    L.E[d] = (m << 8) - m;  // 0xff per M byte
   }
   if constexpr (MASK) {
 #pragma unroll
@@ -286,9 +418,10 @@ __device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], con
 
 // One chunk (16 bytes per lane at q = chunk base + 16 lane); cw = the wave's
 // carry, updated.  Returns the lane's carry-in bits.
-template <bool MASK, bool W, bool WR = false>
+template <bool MASK, bool W, bool WR = false, bool U = false>
 __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_t q, const CLim& lim, uint32_t& cw,
-                                       uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4], CW& wc, COut& o)
+                                       uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4], CW& wc, COut& o,
+                                       CU& u)
 {
 #if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 1  // loads only (benchmarking; wrong counts)
   if (!MASK) {
@@ -297,7 +430,10 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
   }
 #endif
   CLane L;
-  ccodes<MASK, W>(cc, v, L, q, lim, wc);
+  if constexpr (U)
+    ucodes<MASK>(u, v, L, q, lim);
+  else
+    ccodes<MASK, W>(cc, v, L, q, lim, wc);
   bool prop;
   const bool gen = cadd(L, prop);
   const uint64_t cin = clook(__ballot(gen), __ballot(prop), cw, cw);
@@ -335,15 +471,31 @@ __device__ __forceinline__ uint32_t ccode(uint32_t cls) { return cls & 0x80u ? 0
 
 }  // namespace
 
-template <bool W, bool WR>
+template <bool W, bool WR, bool U>
 __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
 {
-  // LDS: byte codes, and (pair classifier) the codes of every byte pair
+  // LDS: byte codes, and (pair classifier) the codes of every byte pair; U
+  // mode: the token codes and 3-byte completion bits
   __shared__ __attribute__((aligned(16))) uint8_t bcode[256];
-  __shared__ __attribute__((aligned(16))) uint16_t pcode[kCPair ? 65536 : 8];
-  for (uint32_t i = threadIdx.x; i < 256; i += kCWaves * 64) bcode[i] = (uint8_t)ccode(P.xc_cls[i]);
-  __syncthreads();
-  if constexpr (kCPair) {
+  __shared__ __attribute__((aligned(16))) uint16_t pcode[(kCPair && !U) ? 65536 : 8];
+  __shared__ __attribute__((aligned(16))) uint32_t utab[U ? kXuTab / 4 : 1];
+  __shared__ __attribute__((aligned(16))) uint32_t ubm3[U ? kXuBm3 : 1];
+  CU u;
+  if constexpr (U) {
+    const uint32_t* gt = reinterpret_cast<const uint32_t*>(P.xu_tab);
+    for (uint32_t i = threadIdx.x; i < kXuTab / 4; i += kCWaves * 64) utab[i] = gt[i];
+    for (uint32_t i = threadIdx.x; i < kXuBm3; i += kCWaves * 64) ubm3[i] = P.xu_bm3[i];
+    __syncthreads();
+    u.tab = reinterpret_cast<const uint8_t*>(utab);
+    u.bm3 = ubm3;
+    u.null4 = P.xu_null * 0x01010101u;
+    u.lo = P.lo;
+    u.rend = P.rend;
+  } else {
+    for (uint32_t i = threadIdx.x; i < 256; i += kCWaves * 64) bcode[i] = (uint8_t)ccode(P.xc_cls[i]);
+    __syncthreads();
+  }
+  if constexpr (kCPair && !U) {
     // pcode[b1 << 8 | b0] = code(b0) | code(b1) << 8, two entries (b0, b0 + 1) per store
     for (uint32_t i = threadIdx.x; i < 65536u / 2; i += kCWaves * 64) {
       const uint32_t b1 = i >> 7, b0 = (2 * i) & 0xffu;
@@ -390,7 +542,13 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
       CLane L;
       const uint4 v = cload(crsrc(P.g + cb0, rend16 > cb0 ? rend16 - cb0 : 0), lo16);
       wc.cx = xprev(cb0);
-      ccodes<true, W>(cc, v, L, cb0 + lo16, lim, wc);
+      if constexpr (U) {
+        u.nx0 = uload_dw(u, P.g, cb0 + kCChunk);
+        u.cprev = ucode_before(u, P.g, cb0);
+        ucodes<true>(u, v, L, cb0 + lo16, lim);
+      } else {
+        ccodes<true, W>(cc, v, L, cb0 + lo16, lim, wc);
+      }
       bool prop;
       const bool gen = cadd(L, prop);
       const uint64_t g = __ballot(gen), p = __ballot(prop);
@@ -424,10 +582,11 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   uint64_t ftb = (wlo + kCTile - 1) / kCTile, fte = whi / kCTile;
   if (!n || ftb >= fte) ftb = fte = 0;
   // one masked chunk at q0 (exit search on chunks reaching past hi)
-  auto masked = [&](uint64_t q0) {
+  auto masked = [&](uint64_t q0) __attribute__((always_inline)) {
     const uint4 v = cload(crsrc(P.g + q0, rend16 > q0 ? rend16 - q0 : 0), lo16);
     uint32_t cs = 0, ws = 0, ls = 0, cb[4];
-    cchunk<true, W, WR>(cc, v, q0 + lo16, lim, cw, cs, ws, ls, cb, wc, out);
+    if constexpr (U) u.nx0 = uload_dw(u, P.g, q0 + kCChunk);
+    cchunk<true, W, WR, U>(cc, v, q0 + lo16, lim, cw, cs, ws, ls, cb, wc, out, u);
     cnt += cs;
     pos += (uint64_t)cs * (q0 + lo16) + ws;
     lbits += ls;
@@ -441,6 +600,7 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   };
   uint64_t q0 = wlo & ~uint64_t(kCChunk - 1);
   wc.cx = xprev(q0);
+  if constexpr (U) u.cprev = ucode_before(u, P.g, q0);
   wc.hi = 0;
   if (fte > ftb)
     for (; q0 < ftb * kCTile; q0 += kCChunk) masked(q0);
@@ -455,16 +615,35 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   for (uint64_t t = ftb; t < fte; ++t) {
     const uint64_t ts = t * kCTile;
     {
-      const uint64_t tn = t + 1 < fte ? ts + kCTile : ts;
+      // (U mode reads the next tile also after the last: its first dword is
+      // the last chunk's context)
+      const uint64_t tn = (U || t + 1 < fte) ? ts + kCTile : ts;
       const __amdgpu_buffer_rsrc_t rn = crsrc(P.g + tn, rend16 > tn ? rend16 - tn : 0);
 #pragma unroll
       for (int j = 0; j < kCIter; ++j) nxt[j] = cload(rn, j * kCChunk + lo16);
     }
     CIt a;
     uint32_t cb[4];
-#pragma unroll
-    for (int j = 0; j < kCIter; ++j)
-      cchunk<false, W, WR>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out);
+    // (chunk indices are compile-time constants, so cur[] and nxt[] stay in
+    // registers also when the body is too large for the loop unroller)
+    auto chunk = [&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      if constexpr (U) {
+        if constexpr (j + 1 < kCIter) {
+          u.nx0 = __builtin_amdgcn_readlane(cur[j + 1].x, 0);
+        } else {
+          const uint64_t qn = ts + kCTile;
+          const uint32_t x = __builtin_amdgcn_readlane(nxt[0].x, 0), in = uinside(u, qn);
+          u.nx0 = (x & in) | (u.null4 & ~in);
+        }
+      }
+      cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u);
+    };
+    static_assert(kCIter == 4, "the chunk calls below");
+    chunk(std::integral_constant<int, 0>{});
+    chunk(std::integral_constant<int, 1>{});
+    chunk(std::integral_constant<int, 2>{});
+    chunk(std::integral_constant<int, 3>{});
     uint32_t c = 0, cj = 0;
 #pragma unroll
     for (int j = 0; j < kCIter; ++j) {
@@ -485,7 +664,13 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   if (n)
     for (; q0 < whi || (last_wave && !found); q0 += kCChunk) masked(q0);
   if (found) cw = 0;  // past the exit every carry is clear
+  // U mode: the codes of the last 3 bytes before a non-EOF readable end
+  // depend on bytes not read yet
+  if (U && last_wave && !P.at_eof && exit + 3 >= P.rend) ovf = 1;
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
+  if constexpr (U) {
+    if (__ballot((u.slow & 0x40404040u) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_USLOW);
+  }
   if constexpr (WR) {
     if (__ballot(out.over) && lane == 0) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
     return;  // (the records are the COUNT pass's)
@@ -521,10 +706,12 @@ __global__ __launch_bounds__(256) void xc_len_kernel(uint64_t* start, uint32_t* 
 hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64_t count)
 {
   if (write) {
-    if (P.xc_w)
-      hipLaunchKernelGGL((xc_kernel<true, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    if (P.xu_tab)
+      hipLaunchKernelGGL((xc_kernel<false, true, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    else if (P.xc_w)
+      hipLaunchKernelGGL((xc_kernel<true, true, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
     else
-      hipLaunchKernelGGL((xc_kernel<false, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+      hipLaunchKernelGGL((xc_kernel<false, true, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t n = count < P.out_capacity ? count : P.out_capacity;
@@ -534,16 +721,18 @@ hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64
     }
     return hipGetLastError();
   }
-  if (P.xc_w)
-    hipLaunchKernelGGL((xc_kernel<true, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  if (P.xu_tab)
+    hipLaunchKernelGGL((xc_kernel<false, false, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  else if (P.xc_w)
+    hipLaunchKernelGGL((xc_kernel<true, false, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   else
-    hipLaunchKernelGGL((xc_kernel<false, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    hipLaunchKernelGGL((xc_kernel<false, false, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   return hipGetLastError();
 }
 
 hipError_t xc_occupancy(int* n)
 {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<true, true>, kCWaves * 64, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<true, true, false>, kCWaves * 64, 0);
 }
 uint32_t xc_unit() { return kCTile; }
 uint32_t xc_waves() { return kCWaves; }
