@@ -110,7 +110,7 @@ def test_gpu_w_word_plus_fast_path():
     bad[(5 << 20) + 2] = ord("a")
     for opc in (ref, U.compile_regex(r"\w+")):
         pat = U.Pattern(opc, word=True)
-        assert pat.info()["kernel"] == 6  # (the non-W kernel: xc_kernel U mode)
+        assert pat.info()["kernel"] == 3  # (the non-W kernel: xg_kernel)
         for data, fast in ((host, True), (bad, False)):
             dev = torch.from_numpy(data).to("cuda")
             torch.cuda.synchronize()

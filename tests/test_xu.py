@@ -10,16 +10,26 @@ import os
 import numpy as np
 import pytest
 
-from test_xi import U, _dev, _oracle_range, _scan  # noqa: F401  (fixtures and helpers)
+from test_xc import _scan  # noqa: F401  (with ptr_off)
+from test_xi import U, _dev, _oracle_range  # noqa: F401  (fixtures and helpers)
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
-RUNS = ("c4_word", "s_plus", "nonspace", "wide_class")
+RUNS = ("c4_word", "s_plus", "nonspace")  # (wide_class qualifies too, but is prefiltered: sparse_kernel)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _prefer_xu():
+    """These tables also have a gap transducer (xg_kernel, the default for them);
+    UGPU_XU=1 runs U mode."""
+    os.environ["UGPU_XU"] = "1"
+    yield
+    os.environ.pop("UGPU_XU", None)
 
 
 @pytest.fixture(scope="module")
-def upats(U, patterns):  # noqa: F811
+def upats(U, patterns, _prefer_xu):  # noqa: F811
     return {k: U.Pattern(patterns[k]["opc"]) for k in RUNS}
 
 
@@ -152,5 +162,5 @@ def test_agrees_with_xg_at_scale(U, patterns):  # noqa: F811
         assert pat.info()["kernel"] == 3
         b = U.find_all(pat, buf[:n])
     finally:
-        os.environ.pop("UGPU_XU", None)
+        os.environ["UGPU_XU"] = "1"
     assert (a.count, a.digest, a.dcap) == (b.count, b.digest, b.dcap)

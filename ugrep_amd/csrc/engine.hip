@@ -216,11 +216,14 @@ bool dfa_xc(const ugpu_dfa* d)
 }
 
 // code-point run tables run xc_kernel's U mode for COUNT and OFFSETS scans
-// (UGPU_XU=0: xg/xi/dense); under option W only on \w+ (the W fast path)
+// when they have no gap transducer: on C4 (\w+) xg_kernel measured 3.0 ms
+// against U mode's 3.56.  UGPU_XU=1 prefers U mode, UGPU_XU=0
+// never takes it.  Under option W only on \w+ (the W fast path).
 bool dfa_xu(const ugpu_dfa* d)
 {
   const char* env = std::getenv("UGPU_XU");
-  return d->d_xu && (!d->d_wtab || d->wplus) && !(env && env[0] == '0');
+  const bool force = env && env[0] == '1', off = env && env[0] == '0';
+  return d->d_xu && (!d->d_wtab || d->wplus) && !off && (force || !d->d_xg);
 }
 
 void fill_tables(ScanParams& P, const ugpu_dfa* d)

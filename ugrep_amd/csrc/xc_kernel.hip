@@ -260,9 +260,9 @@ __device__ __forceinline__ uint32_t uload_dw(const CU& u, const uint8_t* g, uint
   return (x & uinside(u, q)) | (u.null4 & ~uinside(u, q));
 }
 
-// One lane's 16 bytes at q: the adder codes e = 0xFF * M (limits as ccodes)
+// One lane's 16 bytes at q: M (bit 0 of each byte: the byte lies inside a token)
 template <bool MASK>
-__device__ __forceinline__ void ucodes(CU& u, const uint4& v, CLane& L, uint64_t q, const CLim& lim)
+__device__ __forceinline__ void umask(CU& u, const uint4& v, uint64_t q, uint32_t m[4])
 {
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
   if constexpr (MASK) {
@@ -288,10 +288,19 @@ __device__ __forceinline__ void ucodes(CU& u, const uint4& v, CLane& L, uint64_t
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t pv = d ? c[d - 1] : cp;
-    const uint32_t m = (c[d] | __builtin_amdgcn_alignbit(c[d], pv, 25) | __builtin_amdgcn_alignbit(c[d], pv, 18) |
-                        __builtin_amdgcn_alignbit(c[d], pv, 11)) & kOnes;
-    L.E[d] = (m << 8) - m;  // 0xff per M byte
+    m[d] = (c[d] | __builtin_amdgcn_alignbit(c[d], pv, 25) | __builtin_amdgcn_alignbit(c[d], pv, 18) |
+            __builtin_amdgcn_alignbit(c[d], pv, 11)) & kOnes;
   }
+}
+
+// ... as the adder codes e = 0xFF * M (limits as ccodes)
+template <bool MASK>
+__device__ __forceinline__ void ucodes(CU& u, const uint4& v, CLane& L, uint64_t q, const CLim& lim)
+{
+  uint32_t m[4];
+  umask<MASK>(u, v, q, m);
+#pragma unroll
+  for (int d = 0; d < 4; ++d) L.E[d] = (m[d] << 8) - m[d];  // 0xff per M byte
   if constexpr (MASK) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -440,6 +449,28 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
   uint32_t sb[4];
   cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb, sb);
   if constexpr (WR) cwrite(L, cb, sb, q, o);
+}
+
+// U mode, COUNT, a chunk wholly inside [wlo, hi): no byte only continues a
+// match, so In = M and no carry chain is needed: starts M & !M_prev, In bytes
+// counted directly (ls counts In_i here, not In_{i-1}; the caller corrects the
+// difference at the main loop's ends).  mprev (uniform): M of the 4 bytes
+// before the chunk (bit 24: the byte just before).
+__device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q, uint32_t& mprev, uint32_t& cs,
+                                              uint32_t& ws, uint32_t& ls)
+{
+  uint32_t m[4];
+  umask<false>(u, v, q, m);
+  const uint32_t mp = __builtin_amdgcn_update_dpp(mprev, m[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
+  mprev = __builtin_amdgcn_readlane(m[3], 63);
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t st = m[d] & ~__builtin_amdgcn_alignbit(m[d], d ? m[d - 1] : mp, 24);
+    cs = __builtin_popcount(st) + cs;
+    ls = __builtin_popcount(m[d]) + ls;
+    const uint32_t wd = (4u * d) | ((4u * d + 1) << 8) | ((4u * d + 2) << 16) | ((4u * d + 3) << 24);
+    ws = __builtin_amdgcn_udot4(st, wd, ws, false);
+  }
 }
 
 // Exit search after a masked chunk of the wave holding hi: the exit is the
@@ -606,11 +637,17 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
     for (; q0 < ftb * kCTile; q0 += kCChunk) masked(q0);
 
   uint4 cur[kCIter], nxt[kCIter];
+  // U mode: the first dword of the tile after the current one (the last
+  // chunk's context), loaded one tile ahead; M of the byte before the chunk
+  uint32_t nfc = 0, nfn = 0, mprev = 0;
+  const uint32_t cw_main = cw;
   if (fte > ftb) {
     const uint64_t ts = ftb * kCTile;
     const __amdgpu_buffer_rsrc_t rs = crsrc(P.g + ts, rend16 > ts ? rend16 - ts : 0);
 #pragma unroll
     for (int j = 0; j < kCIter; ++j) cur[j] = cload(rs, j * kCChunk + lo16);
+    if constexpr (U) nfc = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)kCTile, 0, 0);
+    mprev = cw << 24;
   }
   for (uint64_t t = ftb; t < fte; ++t) {
     const uint64_t ts = t * kCTile;
@@ -621,6 +658,7 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
       const __amdgpu_buffer_rsrc_t rn = crsrc(P.g + tn, rend16 > tn ? rend16 - tn : 0);
 #pragma unroll
       for (int j = 0; j < kCIter; ++j) nxt[j] = cload(rn, j * kCChunk + lo16);
+      if constexpr (U) nfn = __builtin_amdgcn_raw_buffer_load_b32(rn, (int)kCTile, 0, 0);
     }
     CIt a;
     uint32_t cb[4];
@@ -633,11 +671,14 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
           u.nx0 = __builtin_amdgcn_readlane(cur[j + 1].x, 0);
         } else {
           const uint64_t qn = ts + kCTile;
-          const uint32_t x = __builtin_amdgcn_readlane(nxt[0].x, 0), in = uinside(u, qn);
-          u.nx0 = (x & in) | (u.null4 & ~in);
+          const uint32_t in = uinside(u, qn);
+          u.nx0 = (__builtin_amdgcn_readfirstlane(nfc) & in) | (u.null4 & ~in);
         }
       }
-      cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u);
+      if constexpr (U && !WR)
+        uchunk_direct(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls);
+      else
+        cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u);
     };
     static_assert(kCIter == 4, "the chunk calls below");
     chunk(std::integral_constant<int, 0>{});
@@ -655,8 +696,17 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
     lbits += a.ls;
 #pragma unroll
     for (int j = 0; j < kCIter; ++j) cur[j] = nxt[j];
+    nfc = nfn;
   }
   if (fte > ftb) q0 = fte * kCTile;
+  if constexpr (U && !WR) {
+    if (fte > ftb) {
+      // the wave carry after the main loop, and ls's In_i -> In_{i-1} form:
+      // sum In_{i-1} over [a, b) = sum In_i + In_{a-1} - In_{b-1}
+      cw = (mprev >> 24) & 1u;
+      if (lane == 0) lbits += (uint64_t)cw_main - (uint64_t)cw;
+    }
+  }
   // the rest of the wave's range; the wave holding hi goes on until the exit
   // (the match crossing hi runs on through X bytes, no starts past hi).  Bytes
   // past the readable end are K, so the search ends at the latest in the chunk
