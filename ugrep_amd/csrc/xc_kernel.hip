@@ -201,6 +201,20 @@ __device__ __forceinline__ uint32_t uinside(const CU& u, uint64_t q) { return ~b
 // each continuation byte of x
 __device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t nx, uint32_t& c7)
 {
+#ifdef UGPU_XU_PAIR
+  // (variant: a 64 KiB table of every byte pair, entry (x, y) at
+  // x << 8 | (y ^ (x << 2 & 0xfc)) -- fewer VALU, more bank conflicts)
+  const uint32_t y = __builtin_amdgcn_alignbit(nx, x, 8);
+  const uint32_t sw = y ^ ((x << 2) & 0xfcfcfcfcu);
+  c7 = x & ~(x << 1) & 0x80808080u;
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t a = __builtin_amdgcn_perm(x, sw, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
+    r |= (uint32_t)u.tab[a] << (8 * k);
+  }
+  return r;
+#else
   const uint32_t t = x << 1;
   const uint32_t l7 = x & t & 0x80808080u;  // lead bytes (>= 0xC0)
   c7 = x & ~t & 0x80808080u;                // continuation bytes (80-BF)
@@ -217,6 +231,7 @@ __device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t n
     r |= (uint32_t)u.tab[a] << (8 * k);
   }
   return r;
+#endif
 }
 
 // resolve the 3-byte tokens of code dword c (bytes x, next nx; continuation
@@ -509,12 +524,28 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   // mode: the token codes and 3-byte completion bits
   __shared__ __attribute__((aligned(16))) uint8_t bcode[256];
   __shared__ __attribute__((aligned(16))) uint16_t pcode[(kCPair && !U) ? 65536 : 8];
+#ifdef UGPU_XU_PAIR
+  __shared__ __attribute__((aligned(16))) uint32_t utab[U ? 65536 / 4 : 1];
+#else
   __shared__ __attribute__((aligned(16))) uint32_t utab[U ? kXuTab / 4 : 1];
+#endif
   __shared__ __attribute__((aligned(16))) uint32_t ubm3[U ? kXuBm3 : 1];
   CU u;
   if constexpr (U) {
+#ifdef UGPU_XU_PAIR
+    for (uint32_t i = threadIdx.x; i < 65536 / 4; i += kCWaves * 64) {
+      uint32_t w = 0;
+      for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t a = 4 * i + b, x = a >> 8, y = (a & 0xffu) ^ ((x << 2) & 0xfcu);
+        const uint32_t e = x < 0x80 ? P.xu_tab[x] : x < 0xc0 ? 0u : P.xu_tab[256 + (x & 63) * 256 + y];
+        w |= e << (8 * b);
+      }
+      utab[i] = w;
+    }
+#else
     const uint32_t* gt = reinterpret_cast<const uint32_t*>(P.xu_tab);
     for (uint32_t i = threadIdx.x; i < kXuTab / 4; i += kCWaves * 64) utab[i] = gt[i];
+#endif
     for (uint32_t i = threadIdx.x; i < kXuBm3; i += kCWaves * 64) ubm3[i] = P.xu_bm3[i];
     __syncthreads();
     u.tab = reinterpret_cast<const uint8_t*>(utab);
