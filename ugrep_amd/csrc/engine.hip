@@ -217,7 +217,7 @@ bool dfa_xc(const ugpu_dfa* d)
 
 // code-point run tables run xc_kernel's U mode for COUNT and OFFSETS scans
 // when they have no gap transducer: on C4 (\w+) xg_kernel measured 3.0 ms
-// against U mode's 3.56.  UGPU_XU=1 prefers U mode, UGPU_XU=0
+// against U mode's 3.17.  UGPU_XU=1 prefers U mode, UGPU_XU=0
 // never takes it.  Under option W only on \w+ (the W fast path).
 bool dfa_xu(const ugpu_dfa* d)
 {
