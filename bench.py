@@ -41,7 +41,12 @@ CONFIGS = {
     "c3": ("c3_ident", "re", "[A-Za-z_][A-Za-z0-9_]*", 3, 16 << 30,
            "identifier ERE over 16 GiB synthetic source-code corpus"),
     "c4": ("c4_word", "re", r"\w+", 4, 8 << 30, "Unicode \\w+ over 8 GiB synthetic UTF-8 words"),
+    # C5's whole stream: 128 GiB in total, cut into one shard per rank (strong
+    # scaling; with --gpus 8 each rank scans 16 GiB, as the weak-scaling c2 line)
+    "c5": ("c2_foobarbaz", "re", "foo|bar|baz", 1, 128 << 30,
+           "'foo|bar|baz' over one 128 GiB synthetic ASCII stream, sharded across the ranks"),
 }
+STRONG = {"c5"}  # configs whose size is the whole job's, not per GPU
 
 
 def log(msg):
@@ -234,6 +239,8 @@ def main():
 
     pkey, mode, rx, kind, size, desc = CONFIGS[args.config]
     per_gpu = args.bytes or size
+    if args.config in STRONG and not args.bytes:
+        per_gpu = size // world
     total = per_gpu * world
     lo, hi, read_end, eof = shard_bounds(total, world, rank, args.halo)
     n_read = read_end - lo
@@ -356,7 +363,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config in STRONG else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
