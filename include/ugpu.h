@@ -157,7 +157,7 @@ int ugpu_tables_xc_host(const uint32_t *opc, uint32_t nop, uint8_t *cls, int *ok
 
 /* Host-only: the code-point run tables of a table whose language is S+ for a
    set S of single-code-point tokens (\w+, \S+, [[:alpha:]]+ over UTF-8;
-   ugrep_amd/csrc/tables.hpp xu_*): tab[256 + 64 * 256] token codes and
+   ugrep_amd/csrc/tables.hpp xu_*): tab[256 + 64 * 256 + 256] token codes and
    bm3[2048] third-byte bits (either may be NULL).  *ok = 0 when the table does
    not qualify.  (Replaces, for these tables, the per-byte opcode scan of
    lib/matcher.cpp:460-545.) */

@@ -26,19 +26,24 @@ def _xu(opc):
     return host_xu(opc)
 
 
+KXU_CLS = 256 + 64 * 256  # tables.hpp kXuCls
+
+
 def xu_codes(tab, bm3, b):
-    """Per-byte token codes of the padded stream b (the kernel's lookups)."""
+    """Per-byte token codes of the padded stream b (the kernel's lookups and
+    its 3-byte resolution: the classes of the byte after, else the bitmap)."""
     n = b.size - 3
-    x, y, z = b[:n].astype(np.int64), b[1:n + 1].astype(np.int64), b[2:n + 2].astype(np.int64)
+    x, y, z = b[:n + 1].astype(np.int64), b[1:n + 2].astype(np.int64), b[2:n + 3].astype(np.int64)
     code = np.where(x < 0x80, tab[np.minimum(x, 127)],
-                    np.where(x < 0xC0, tab[128], tab[256 + (x & 63) * 256 + y])).astype(np.int64)
-    mix = (code & 0x20) != 0
+                    np.where(x < 0xC0, tab[KXU_CLS + y], tab[256 + (x & 63) * 256 + y])).astype(np.int64)
+    cy = np.concatenate([code[1:], [0]])
+    l3 = (code & 0x80) != 0
+    ok = l3 & ((code & cy & 0x70) != 0)
     idx = ((x & 15) << 12) | ((y & 63) << 6) | (z & 63)
     bit = (bm3[idx >> 5].astype(np.int64) >> (idx & 31)) & 1
-    code = np.where(mix & (bit == 1), code | 7, code)
-    t3bad = ((code & 0x10) != 0) & ((z & 0xC0) != 0x80)
-    code = np.where(t3bad, code & ~0xF, code)
-    return code
+    mix = l3 & ((code & 0x70) == 0) & (bit == 1) & ((z & 0xC0) == 0x80)
+    code = np.where(ok | mix, code | 7, code)
+    return code[:n]
 
 
 def xu_restated(tab, bm3, cap, data, lo, hi, rend, at_eof):
@@ -47,7 +52,7 @@ def xu_restated(tab, bm3, cap, data, lo, hi, rend, at_eof):
     b = np.full(rend + 3, null, np.uint8)
     b[lo:rend] = data[lo:rend]
     code = xu_codes(tab, bm3, b)
-    slow = bool((code[lo:rend] & 0x40).any())
+    slow = bool((code[lo:rend] & 0x08).any())  # (XU_SLOW = 0x0F: only 4-byte leads have bit 3)
     m = np.zeros(rend, bool)
     for k in range(4):
         m[k:] |= ((code[:rend - k] >> k) & 1) != 0

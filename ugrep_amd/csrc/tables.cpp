@@ -188,6 +188,7 @@ void build_xu(const std::vector<uint32_t>& nxt, uint32_t S, uint32_t first_acc, 
   std::vector<uint32_t> bm3(kXuBm3, 0);
   std::set<uint32_t> ends;  // states a token ends in
   std::map<uint32_t, int> s3_ok;  // states after 3 bytes of a 4-byte token: 1 = every continuation ends a token
+  std::vector<std::pair<uint32_t, uint64_t> > l3;  // 3-byte leads (x << 8 | y) and their third-byte sets
   for (int x = 0; x < 256; ++x) {
     const uint32_t s1 = go(start_sid, x);
     if (!s1) continue;
@@ -212,6 +213,7 @@ void build_xu(const std::vector<uint32_t>& nxt, uint32_t S, uint32_t first_acc, 
         continue;
       }
       int nacc = 0, nlive = 0;
+      uint64_t zset = 0;  // continuation bytes z completing a 3-byte token
       for (int z = 0; z < 256; ++z) {
         const uint32_t s3 = go(s2, z);
         if (!s3) continue;
@@ -219,6 +221,7 @@ void build_xu(const std::vector<uint32_t>& nxt, uint32_t S, uint32_t first_acc, 
         if (acc(s3)) {
           ends.insert(s3);
           ++nacc;
+          zset |= 1ull << (z & 63);
           continue;
         }
         ++nlive;
@@ -238,17 +241,53 @@ void build_xu(const std::vector<uint32_t>& nxt, uint32_t S, uint32_t first_acc, 
       if (nacc && nlive) return;  // 3- and 4-byte tokens sharing two bytes: not UTF-8
       if (nlive) {
         e = XU_SLOW;
-      } else if (nacc == 64) {
-        e = 0x07 | XU_T3;
       } else if (nacc) {
-        if (x < 0xe0 || x > 0xef) return;
-        e = XU_T3 | XU_MIX;
-        for (int z = 0x80; z < 0xc0; ++z)
-          if (acc(go(s2, z))) {
-            const uint32_t i = (uint32_t)(x & 15) << 12 | (uint32_t)(y & 63) << 6 | (uint32_t)(z & 63);
-            bm3[i >> 5] |= 1u << (i & 31);
-          }
+        if (x < 0xe0 || x > 0xef) return;  // (the bitmap index assumes a 3-byte lead)
+        e = XU_L3;
+        l3.emplace_back((uint32_t)x << 8 | (uint32_t)y, zset);
       }
+    }
+  }
+  // classes of continuation bytes: refine {all 64} by the third-byte sets of
+  // the 3-byte leads while at most 3 classes result -- General Punctuation
+  // and Currency Symbols (E2 80-82) first, then by code point; the leads whose
+  // set is a union of classes get the class bits, the rest go to xu_bm3
+  std::vector<std::pair<uint32_t, uint64_t> > order = l3;
+  std::stable_sort(order.begin(), order.end(), [](const std::pair<uint32_t, uint64_t>& a,
+                                                  const std::pair<uint32_t, uint64_t>& b) {
+    const bool pa = a.first >= 0xe280 && a.first <= 0xe282, pb = b.first >= 0xe280 && b.first <= 0xe282;
+    return pa != pb ? pa : a.first < b.first;
+  });
+  std::vector<uint64_t> parts(1, ~0ull);
+  for (const auto& l : order) {
+    std::vector<uint64_t> np;
+    for (uint64_t q : parts) {
+      if (q & l.second) np.push_back(q & l.second);
+      if (q & ~l.second) np.push_back(q & ~l.second);
+    }
+    if (np.size() <= 3) parts = np;
+  }
+  for (int z = 0x80; z < 0xc0; ++z)
+    for (size_t k = 0; k < parts.size(); ++k)
+      if (parts[k] >> (z & 63) & 1) tab[kXuCls + z] = (uint8_t)(0x10u << k);
+  for (const auto& l : l3) {
+    const int x = (int)(l.first >> 8), y = (int)(l.first & 0xff);
+    uint8_t m = 0;
+    uint64_t cover = 0;
+    for (size_t k = 0; k < parts.size(); ++k)
+      if ((parts[k] & l.second) == parts[k]) {
+        m |= (uint8_t)(0x10u << k);
+        cover |= parts[k];
+      }
+    if (cover == l.second) {
+      tab[256 + (x & 63) * 256 + y] = (uint8_t)(XU_L3 | m);
+    } else {
+      tab[256 + (x & 63) * 256 + y] = XU_MIX;
+      for (int z = 0x80; z < 0xc0; ++z)
+        if (l.second >> (z & 63) & 1) {
+          const uint32_t i = (uint32_t)(x & 15) << 12 | (uint32_t)(y & 63) << 6 | (uint32_t)(z & 63);
+          bm3[i >> 5] |= 1u << (i & 31);
+        }
     }
   }
   if (ends.empty()) return;

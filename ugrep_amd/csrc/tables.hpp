@@ -100,11 +100,11 @@ struct DfaTables {
   // a continuation byte).  Tokens then never overlap, so the FIND matches are
   // exactly the maximal runs of bytes that lie inside some token, and "byte i
   // lies inside a token" (M_i) is a local property of bytes i-3 .. i+3.  The
-  // token starting at byte x (next byte y) is coded XU_* (see below):
+  // code of byte x (next byte y) is (see XU_* below)
   //   xu_tab[x]                            x < 0x80 (y is irrelevant)
-  //   xu_tab[128]                          continuation bytes: 0
+  //   xu_tab[kXuCls + y]                   x a continuation byte: y's class
   //   xu_tab[256 + (x & 63) * 256 + y]     lead bytes x >= 0xC0
-  // xu_bm3: for 3-byte tokens whose completion depends on the third byte z
+  // xu_bm3: for 3-byte tokens whose third byte z decides beyond the classes
   // (XU_MIX), bit ((x & 15) << 12 | (y & 63) << 6 | (z & 63)).
   // xu_null: a byte that starts no token and is no continuation byte; the
   // kernel reads it in place of bytes outside [lo, readable end).
@@ -114,12 +114,19 @@ struct DfaTables {
   std::vector<uint32_t> xu_bm3;   // kXuBm3 dwords
 };
 
-// xu codes: bits 0-3 a thermometer of the token's bytes (bit k: the token
-// covers byte x + k), XU_T3 the token needs a continuation byte at x + 2,
-// XU_MIX the third byte decides (xu_bm3), XU_SLOW a 4-byte token may start
-// here (the kernel flags the range and the host scans it with another kernel).
-constexpr uint8_t XU_T3 = 0x10, XU_MIX = 0x20, XU_SLOW = 0x40;
-constexpr uint32_t kXuTab = 256 + 64 * 256, kXuBm3 = 2048;
+// xu codes.  Bits 0-3: a thermometer of the token's bytes (bit k: the token
+// covers byte x + k; 0x0F = a 4-byte token may start here, XU_SLOW: the kernel
+// flags the range and the host scans it with another kernel).  A 3-byte lead
+// (x, y) has bit 7 (XU_L3) and in bits 4-6 the continuation-byte classes z
+// that complete a token; a continuation byte's code carries the one-hot class
+// of the byte after it in bits 4-6 (0 when that is no continuation byte).  So
+// the token at x exists iff code(x) & code(x + 1) & 0x70, one AND per dword
+// for every byte.  XU_L3 with no class bits (XU_MIX): z decides through xu_bm3.
+// The 64 continuation bytes fall into at most 3 classes, chosen so that the
+// common mixed blocks (General Punctuation, Currency Symbols first) are unions.
+constexpr uint8_t XU_SLOW = 0x0F, XU_L3 = 0x80, XU_MIX = 0x80, XU_CLS = 0x70;
+constexpr uint32_t kXuCls = 256 + 64 * 256;               // continuation classes, 256 bytes
+constexpr uint32_t kXuTab = kXuCls + 256, kXuBm3 = 2048;
 
 // True when the two tables accept the same strings with the same accept
 // indices (so the FIND chains agree on every input).

@@ -191,7 +191,7 @@ struct CU {
   uint64_t lo = 0, rend = 0;      // the bytes read as themselves
   uint32_t nx0 = 0;               // (uniform) the dword after the chunk, filled
   uint32_t cprev = 0;             // (uniform) codes of the 4 bytes before the chunk
-  uint32_t slow = 0;              // lane: OR of the codes (XU_SLOW: a 4-byte token)
+  uint32_t slow = 0;              // lane: OR of the codes (bit 3: XU_SLOW, a 4-byte token)
 };
 
 // bytes of the dword at q inside [lo, rend) (0xff per byte)
@@ -199,18 +199,15 @@ __device__ __forceinline__ uint32_t uinside(const CU& u, uint64_t q) { return ~b
 
 // token codes of the 4 bytes of x (the next 4 bytes in nx); c7 = bit 7 of
 // each continuation byte of x
-__device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t nx, uint32_t& c7)
+__device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t nx)
 {
-#ifndef UGPU_XU_SPLIT
   // a 64 KiB table of every byte pair (built in the prologue from the host's
-  // 16.25 KiB table), entry (x, y) at x << 8 | (y ^ (x << 2 & 0xfc)): the
-  // swizzle spreads the lanes of ASCII text over the banks.  11 VALU per
-  // dword; the UGPU_XU_SPLIT build instead addresses the host table itself
-  // (ASCII and continuation lanes on few dwords: fewer bank conflicts, 26
-  // VALU per dword) and measured 3.57 against 3.17 ms on C4.
+  // tables), entry (x, y) at x << 8 | (y ^ (x << 2 & 0xfc)): the swizzle
+  // spreads the lanes of ASCII text over the banks.  (Addressing the host
+  // tables directly, ASCII and continuation lanes on few dwords, had fewer
+  // bank conflicts but 26 instead of 11 VALU per dword: 3.57 vs 3.17 ms on C4.)
   const uint32_t y = __builtin_amdgcn_alignbit(nx, x, 8);
   const uint32_t sw = y ^ ((x << 2) & 0xfcfcfcfcu);
-  c7 = x & ~(x << 1) & 0x80808080u;
   uint32_t r = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -218,44 +215,36 @@ __device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t n
     r |= (uint32_t)u.tab[a] << (8 * k);
   }
   return r;
-#else
-  const uint32_t t = x << 1;
-  const uint32_t l7 = x & t & 0x80808080u;  // lead bytes (>= 0xC0)
-  c7 = x & ~t & 0x80808080u;                // continuation bytes (80-BF)
-  const uint32_t lm = (l7 << 1) - (l7 >> 7);  // 0xff per lead byte
-  const uint32_t cm = (c7 << 1) - (c7 >> 7);
-  const uint32_t h = ((x & 0x3f3f3f3fu) + 0x01010101u) & lm;     // lead: (x & 63) + 1
-  const uint32_t y = __builtin_amdgcn_alignbit(nx, x, 8);          // the byte after each byte
-  uint32_t l = (y & lm) | (x & ~lm);
-  l = (l & ~cm) | (0x80808080u & cm);                              // continuation: entry 128
-  uint32_t r = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t a = __builtin_amdgcn_perm(h, l, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
-    r |= (uint32_t)u.tab[a] << (8 * k);
-  }
-  return r;
-#endif
 }
 
-// resolve the 3-byte tokens of code dword c (bytes x, next nx; continuation
-// bits c7 of x and c7n of nx): XU_MIX by the third byte, then every XU_T3
-// token needs a continuation byte at +2
-__device__ __forceinline__ uint32_t ucode_fix(const CU& u, uint32_t c, uint32_t x, uint32_t nx, uint32_t c7,
-                                              uint32_t c7n)
+// the code of byte 0 of x (byte 1 of x follows it)
+__device__ __forceinline__ uint32_t ucode_b0(const CU& u, uint32_t x)
 {
-  uint32_t mm = c & 0x20202020u;
+  const uint32_t a = ((x & 0xffu) << 8) | (((x >> 8) & 0xffu) ^ ((x << 2) & 0xfcu));
+  return u.tab[a];
+}
+
+// resolve the 3-byte tokens of code dword c (bytes x, next bytes nx; cn =
+// the codes of the next 4 bytes): a 3-byte lead (XU_L3) shares a class bit
+// with the code of the byte after it (which carries the class of the third
+// byte) -- one AND for all 4 bytes; leads without class bits (XU_MIX) ask the
+// bitmap (rare: the divergent loop)
+__device__ __forceinline__ uint32_t ucode_fix(const CU& u, uint32_t c, uint32_t x, uint32_t nx, uint32_t cn)
+{
+  const uint32_t cy = __builtin_amdgcn_alignbit(cn, c, 8);  // code of byte k + 1, in byte k
+  const uint32_t v7 = c & ((c & cy & 0x70707070u) + 0x70707070u) & 0x80808080u;
+  uint32_t mm = c & ~((c & 0x70707070u) + 0x70707070u) & 0x80808080u;  // XU_MIX
+  c |= (v7 >> 4) - (v7 >> 7);  // 0x07: the token covers x .. x + 2
   if (mm) {
     do {
       const uint32_t j = (uint32_t)__builtin_ctz(mm) >> 3;
       const uint32_t b = __builtin_amdgcn_alignbit(nx, x, 8 * j);  // bytes x+j .. x+j+3
       const uint32_t i = (b & 15u) << 12 | ((b >> 8) & 63u) << 6 | ((b >> 16) & 63u);
-      if ((u.bm3[i >> 5] >> (i & 31)) & 1u) c |= 7u << (8 * j);
+      if (((u.bm3[i >> 5] >> (i & 31)) & 1u) && ((b >> 16) & 0xc0u) == 0x80u) c |= 7u << (8 * j);
       mm &= ~(0xffu << (8 * j));
     } while (mm);
   }
-  const uint32_t bad = c & 0x10101010u & ~(__builtin_amdgcn_alignbit(c7n, c7, 16) >> 3);
-  return c & ~(bad - (bad >> 4));
+  return c;
 }
 
 // codes of the dword at q - 4 (for the chunk at q): every lane the same
@@ -265,10 +254,7 @@ __device__ __forceinline__ uint32_t ucode_before(const CU& u, const uint8_t* g, 
   const uint32_t* p = reinterpret_cast<const uint32_t*>(g + q - 4);
   const uint32_t x = (p[0] & uinside(u, q - 4)) | (u.null4 & ~uinside(u, q - 4));
   const uint32_t nx = q < u.rend ? (p[1] & uinside(u, q)) | (u.null4 & ~uinside(u, q)) : u.null4;
-  uint32_t c7, c7n;
-  const uint32_t c = ucode_dw(u, x, nx, c7);
-  (void)ucode_dw(u, nx, u.null4, c7n);
-  return ucode_fix(u, c, x, nx, c7, c7n);
+  return ucode_fix(u, ucode_dw(u, x, nx), x, nx, ucode_dw(u, nx, u.null4));
 }
 
 // the filled dword at q (uniform)
@@ -292,15 +278,13 @@ __device__ __forceinline__ void umask(CU& u, const uint4& v, uint64_t q, uint32_
     }
   }
   const uint32_t nx = __builtin_amdgcn_update_dpp(u.nx0, w[0], 0x130, 0xf, 0xf, false);  // wave_shl:1
-  uint32_t c[4], c7[5];
+  uint32_t c[4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) c[d] = ucode_dw(u, w[d], d < 3 ? w[d + 1] : nx, c7[d]);
-  {
-    const uint32_t t = nx << 1;
-    c7[4] = nx & ~t & 0x80808080u;
-  }
+  for (int d = 0; d < 4; ++d) c[d] = ucode_dw(u, w[d], d < 3 ? w[d + 1] : nx);
+  // the code of the byte after the lane (only its first byte is used)
+  const uint32_t cn = __builtin_amdgcn_update_dpp(ucode_b0(u, u.nx0), c[0], 0x130, 0xf, 0xf, false);
 #pragma unroll
-  for (int d = 0; d < 4; ++d) c[d] = ucode_fix(u, c[d], w[d], d < 3 ? w[d + 1] : nx, c7[d], c7[d + 1]);
+  for (int d = 0; d < 4; ++d) c[d] = ucode_fix(u, c[d], w[d], d < 3 ? w[d + 1] : nx, d < 3 ? c[d + 1] : cn);
   u.slow |= c[0] | c[1] | c[2] | c[3];
   const uint32_t cp = __builtin_amdgcn_update_dpp(u.cprev, c[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
   u.cprev = __builtin_amdgcn_readlane(c[3], 63);
@@ -528,28 +512,22 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   // mode: the token codes and 3-byte completion bits
   __shared__ __attribute__((aligned(16))) uint8_t bcode[256];
   __shared__ __attribute__((aligned(16))) uint16_t pcode[(kCPair && !U) ? 65536 : 8];
-#ifndef UGPU_XU_SPLIT
   __shared__ __attribute__((aligned(16))) uint32_t utab[U ? 65536 / 4 : 1];
-#else
-  __shared__ __attribute__((aligned(16))) uint32_t utab[U ? kXuTab / 4 : 1];
-#endif
   __shared__ __attribute__((aligned(16))) uint32_t ubm3[U ? kXuBm3 : 1];
   CU u;
   if constexpr (U) {
-#ifndef UGPU_XU_SPLIT
+    // the pair table: entry (x, y) at x << 8 | (y ^ (x << 2 & 0xfc))
     for (uint32_t i = threadIdx.x; i < 65536 / 4; i += kCWaves * 64) {
       uint32_t w = 0;
       for (uint32_t b = 0; b < 4; ++b) {
         const uint32_t a = 4 * i + b, x = a >> 8, y = (a & 0xffu) ^ ((x << 2) & 0xfcu);
-        const uint32_t e = x < 0x80 ? P.xu_tab[x] : x < 0xc0 ? 0u : P.xu_tab[256 + (x & 63) * 256 + y];
+        const uint32_t e = x < 0x80   ? P.xu_tab[x]
+                           : x < 0xc0 ? P.xu_tab[kXuCls + y]
+                                      : P.xu_tab[256 + (x & 63) * 256 + y];
         w |= e << (8 * b);
       }
       utab[i] = w;
     }
-#else
-    const uint32_t* gt = reinterpret_cast<const uint32_t*>(P.xu_tab);
-    for (uint32_t i = threadIdx.x; i < kXuTab / 4; i += kCWaves * 64) utab[i] = gt[i];
-#endif
     for (uint32_t i = threadIdx.x; i < kXuBm3; i += kCWaves * 64) ubm3[i] = P.xu_bm3[i];
     __syncthreads();
     u.tab = reinterpret_cast<const uint8_t*>(utab);
@@ -754,7 +732,7 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   if (U && last_wave && !P.at_eof && exit + 3 >= P.rend) ovf = 1;
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
   if constexpr (U) {
-    if (__ballot((u.slow & 0x40404040u) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_USLOW);
+    if (__ballot((u.slow & 0x08080808u) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_USLOW);
   }
   if constexpr (WR) {
     if (__ballot(out.over) && lane == 0) atomicOr(P.flags, UGPU_FLAG_CAPACITY);

@@ -136,10 +136,10 @@ def host_xc(opc):
 
 
 def host_xu(opc):
-    """Code-point run tables of xc_kernel's U mode: (tab uint8[16640], bm3 uint32[2048]), or None."""
+    """Code-point run tables of xc_kernel's U mode: (tab uint8[16896], bm3 uint32[2048]), or None."""
     a, p = _as_u32(opc)
     ok = ctypes.c_int(0)
-    tab = np.zeros(256 + 64 * 256, np.uint8)
+    tab = np.zeros(256 + 64 * 256 + 256, np.uint8)  # (tables.hpp kXuTab)
     bm3 = np.zeros(2048, np.uint32)
     check(lib.ugpu_tables_xu_host(p, len(a), tab.ctypes.data_as(_lib.c_u8p), bm3.ctypes.data_as(_lib.c_u32p),
                                   ctypes.byref(ok)))
