@@ -65,7 +65,9 @@ typedef struct ugpu_dfa_info
   uint32_t accepting;   /* accepting states */
   uint32_t kernel;      /* kernel of a COUNT scan: 0 sparse (prefiltered), 1 dense, 2 xi (immediate
                            transducer; UGPU_XI=0 selects dense), 3 xg (gap transducer; UGPU_XG=0),
-                           4 wfind (option W, UGPU_PAT_WORD) */
+                           4 wfind (option W, UGPU_PAT_WORD), 5 xc (two-state carry chain; UGPU_XC=0),
+                           6 xc U mode (code-point runs without a gap transducer; UGPU_XU=1 prefers it,
+                           UGPU_XU=0 never) */
 } ugpu_dfa_info;
 
 /* Totals of one scan.  digest = sum(start*31 + len), dcap = sum((start+1)*cap),
