@@ -229,7 +229,12 @@ int ugpu_stream_create(const ugpu_dfa *dfa, uint64_t keep, ugpu_stream **out);
 int ugpu_stream_destroy(ugpu_stream *st);
 
 /* Feed host bytes; *out (free with ugpu_result_free) gets the newly final
-   matches (records in OFFSETS mode) and their count/digest/dcap. */
+   matches (records in OFFSETS mode) and their count/digest/dcap.
+   final: 1 = the input ends with this chunk; UGPU_FEED_FLUSH = more input may
+   follow, but settle every match the bytes so far decide (the input would
+   block: a slow pipe or a TTY, whose reference matcher reports those matches
+   before it waits, include/reflex/input.h:716-731); 0 = hold back `keep`. */
+#define UGPU_FEED_FLUSH 2
 int ugpu_stream_feed(ugpu_stream *st, const uint8_t *chunk, uint64_t len, int final, uint32_t mode,
                      ugpu_result **out);
 

@@ -61,6 +61,8 @@
 #include <memory>
 #include <string>
 
+#include <poll.h>
+
 #include <reflex/matcher.h>
 
 #include "ugpu.h"
@@ -277,16 +279,32 @@ class GpuMatcher : public Matcher {
         gcur_abs_ = num_ + cur_;
         return r;
       }
-      // read until chunk_ unfed bytes are buffered or the input ends, then feed
+      // read until chunk_ unfed bytes are buffered or the input ends, then
+      // feed.  A short read with nothing more ready (a slow pipe or a TTY that
+      // ugrep set non-blocking, src/ugrep.cpp:3956-3966; Input::get returns what
+      // has arrived, include/reflex/input.h:716-731) feeds at once: the next
+      // get() would block, and the reference matcher reports the matches in the
+      // bytes it already has before it blocks.
+      bool flush = false;
       while (!eof_ && num_ + end_ - sfed_ < chunk_)
       {
         if (end_ + blk_ + 1 >= max_)
           (void)grow(chunk_ > Const::BLOCK ? chunk_ : Const::BLOCK);
-        const size_t n = get(buf_ + end_, blk_ > 0 ? blk_ : max_ - end_ - 1);
+        const size_t want = blk_ > 0 ? blk_ : max_ - end_ - 1;
+        const size_t n = get(buf_ + end_, want);
         if (n == 0)
+        {
           eof_ = !wrap();
+        }
         else
+        {
           end_ += n;
+          if (n < want && !input_ready())
+          {
+            flush = true;
+            break;
+          }
+        }
       }
       if (eof_ && scans_at_restart_ == scans_ && num_ + end_ - sbase_ < min_bytes())
       {
@@ -298,8 +316,8 @@ class GpuMatcher : public Matcher {
       }
       const size_t from = static_cast<size_t>(sfed_ - num_);
       drop_records();
-      if (ugpu_stream_feed(gst_, reinterpret_cast<const uint8_t*>(buf_ + from), end_ - from, eof_ ? 1 : 0,
-                           UGPU_MODE_OFFSETS, &gres_) != UGPU_OK)
+      if (ugpu_stream_feed(gst_, reinterpret_cast<const uint8_t*>(buf_ + from), end_ - from,
+                           eof_ ? 1 : flush ? UGPU_FEED_FLUSH : 0, UGPU_MODE_OFFSETS, &gres_) != UGPU_OK)
       {
         // engine unavailable for this input: the CPU matcher takes over at the cursor
         cpu_stream_ = true;
@@ -311,6 +329,19 @@ class GpuMatcher : public Matcher {
       sfed_ = num_ + end_;
       sdone_ = eof_;
     }
+  }
+  // more input can be read without blocking (memory and std::istream sources
+  // never block; for a FILE*, poll its descriptor)
+  bool input_ready()
+  {
+    FILE* f = in.file();
+    if (f == NULL)
+      return true;
+    struct pollfd p;
+    p.fd = fileno(f);
+    p.events = POLLIN;
+    p.revents = 0;
+    return ::poll(&p, 1, 0) > 0;  // data, EOF or an error: get() returns at once
   }
   bool stream_inside(uint64_t at)
   {

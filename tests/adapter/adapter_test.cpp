@@ -15,6 +15,9 @@
 //                     UGPU_ADAPTER_CHUNK bytes, set small here), plain loop
 //   5. stream -c    : the same with skip('\n') after each hit
 //   in every loop lineno(), columno() after each hit and at_end() at the end agree
+// Then the slow-pipe case: stdin is a non-blocking pipe (as ugrep sets it,
+// src/ugrep.cpp:3956-3966) whose writer stalls after its first line; the first
+// match must be reported before the writer continues, as the reference does.
 // INPUT as in oracle/ref_harness.cpp (file:, gen:, hex:).  Prints one line
 // per case; exit status 1 if any case differs.
 #include <stdint.h>
@@ -22,8 +25,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <fstream>
+#include <thread>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -129,6 +138,50 @@ static std::vector<Hit> run(M& m, std::vector<char>& buf, int kind, bool& at_end
   return out;
 }
 
+// The writer sends one line with a match, then waits (up to 5 s) until the
+// reader has reported it, then sends the rest.  Returns 1 on failure.
+static int slow_pipe()
+{
+  const std::string part1 = "alpha foo beta\n", part2 = "gamma bar delta baz\n";
+  int fds[2];
+  if (pipe(fds) != 0)
+    return 1;
+  const int saved = dup(0);
+  dup2(fds[0], 0);
+  close(fds[0]);
+  fcntl(0, F_SETFL, fcntl(0, F_GETFL) | O_NONBLOCK);
+  clearerr(stdin);
+  std::atomic<bool> got_first(false);
+  bool timely = false;
+  std::thread writer([&] {
+    (void)!write(fds[1], part1.data(), part1.size());
+    for (int i = 0; i < 500 && !got_first.load(); ++i)
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    timely = got_first.load();
+    (void)!write(fds[1], part2.data(), part2.size());
+    close(fds[1]);
+  });
+  reflex::Pattern pat(build_regex("re", "foo|bar|baz"), "r");
+  reflex::GpuMatcher gpu(pat, reflex::Input(stdin), NULL);
+  gpu.gpu_min_bytes(0);
+  gpu.gpu_sparse_max(1 << 30);
+  std::vector<size_t> got;
+  while (gpu.find())
+  {
+    got.push_back(gpu.first());
+    got_first = true;
+  }
+  writer.join();
+  dup2(saved, 0);
+  close(saved);
+  clearerr(stdin);
+  const std::vector<size_t> want = {6, 21, 31};
+  const bool ok = timely && got == want && gpu.gpu_scans() > 0;
+  printf("%s gpu slow-pipe: first match before the writer continued: %s, %zu matches, gpu scans %zu\n",
+         ok ? "ok" : "FAIL", timely ? "yes" : "no", got.size(), gpu.gpu_scans());
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv)
 {
   if (argc < 2)
@@ -190,6 +243,8 @@ int main(int argc, char** argv)
       ++n;
     }
   }
+  bad += slow_pipe();
+  ++n;
   printf("%d cases, %d failed\n", n, bad);
   return bad ? 1 : 0;
 }

@@ -108,3 +108,30 @@ def test_stream_forest_fallback(U, patterns):
     finally:
         os.environ.pop("UGPU_FIX_BUDGET", None)
         os.environ.pop("UGPU_MERGE_BUDGET", None)
+
+
+def test_stream_flush_settles_decided_matches(U, patterns):
+    """UGPU_FEED_FLUSH (an input that would block): every match the fed bytes
+    decide comes back from that feed -- all of them when the bytes end at a
+    separator -- and the concatenation over any chunking still equals the
+    oracle's FIND over the whole input."""
+    from oracle_lib import gen
+    for pname, kind in (("c2_foobarbaz", 1), ("c4_word", 4)):
+        data = gen(kind, 5, 0, 1 << 20)
+        pat = U.Pattern(patterns[pname]["opc"])
+        want = _whole(U, pat, data)
+        rng = np.random.default_rng(kind)
+        st = U.Stream(pat)
+        trip, i = [], 0
+        cuts = sorted(set(int(x) for x in rng.integers(1, data.size, 40)))
+        for c in cuts + [data.size]:
+            chunk = data[i:c]
+            r = st.feed(chunk.tobytes(), final=c == data.size, flush=c < data.size)
+            trip += r.triples()
+            i = c
+            if c < data.size:
+                # every match that ends before the last separator of the bytes so
+                # far is final after this feed
+                sep = int(np.nonzero(np.isin(data[:c], np.frombuffer(b" \n", np.uint8)))[0][-1])
+                assert [t for t in want[0] if t[0] + t[1] <= sep] == [t for t in trip if t[0] + t[1] <= sep], (pname, c)
+        assert trip == want[0], pname

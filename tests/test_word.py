@@ -171,3 +171,21 @@ def test_gpu_w_identifiers_on_xc():
         cnt, dg, dc, lst = OracleDfa(ref).find_w(data, want_list=True)
         assert (res.count, res.digest, res.dcap) == (cnt, dg, dc)
         assert res.triples() == lst
+    # a range starting on a 1024-byte chunk border right after a multi-byte
+    # character: at_wb there decodes that character (word: no match starts at
+    # the border; non-word: one does), which xc_kernel's chunks never see
+    base = gen(3, 23, 0, 1 << 20)
+    for ch in ("\u00e9", "\u20ac", "\u00d7"):
+        data = base.copy()
+        enc = np.frombuffer(ch.encode(), np.uint8)
+        for border in (2048, 4096, 65536):
+            data[border - enc.size:border] = enc
+            data[border:border + 5] = np.frombuffer(b"abcde", np.uint8)
+        dev = torch.from_numpy(data).to("cuda")
+        torch.cuda.synchronize()
+        for border in (2048, 4096, 65536):
+            res = U.find_all(pat, dev, start=border, offsets=True)
+            cnt, dg, dc, lst = OracleDfa(ref).find_w(data, start=border, want_list=True)
+            assert (res.count, res.digest, res.dcap) == (cnt, dg, dc), (ch, border)
+            assert res.triples() == lst, (ch, border)
+            assert (lst[0][0] == border) == (ch != "\u00e9"), (ch, border, lst[:2])

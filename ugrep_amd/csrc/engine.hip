@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <string>
@@ -31,13 +32,16 @@ void ugpu_word_ranges(std::vector<uint32_t>& out);
 // Geometry of a UTF-8 / NUL scan of the device bytes dbuf[0, len) (U.out unset).
 ugpu::Utf8Params utf8_params(const uint8_t* dbuf, uint64_t len)
 {
-  static int cus = [] {
-    int dev = 0, n = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n = 256;
-    return n;
-  }();
+  // CU count of the calling thread's device (cached per device id)
+  static std::atomic<int> cached[64];
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  if (dev < 64 && cached[dev].load(std::memory_order_relaxed) > 0) {
+    cus = cached[dev].load(std::memory_order_relaxed);
+  } else {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    if (dev < 64) cached[dev].store(cus, std::memory_order_relaxed);
+  }
   ugpu::Utf8Params U{};
   U.head = reinterpret_cast<uintptr_t>(dbuf) & 15u;
   U.g = dbuf - U.head;
@@ -300,7 +304,7 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
   if (s->word)
     geometry(P, dbuf, lo, hi, read_end, s->word_rec, wfind_unit(), wfind_waves(), off);
   else if (xi && s->xc)
-    geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xc_unit(), xc_waves(), off);
+    geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xc_unit(dfa_xu(s->dfa)), xc_waves(), off);
   else if (xi && s->xg)
     geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xg_unit(), xg_waves(), off);
   else if (xi)
@@ -768,7 +772,7 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   // keeps those)
   if (!s->sparse && (dfa_xc(dfa) || dfa_xu(dfa))) {
     int cpc = 0;
-    HIP_TRY_S(xc_occupancy(&cpc));
+    HIP_TRY_S(xc_occupancy(dfa_xu(dfa), &cpc));
     if (cpc >= 1) {
       s->xc = true;
       s->xu_xi = s->xi;
@@ -860,11 +864,26 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   s->staged_last = false;
   if (s->sparse && (s->stage || s->stage_once)) {
     if (!s->d_st_n) {
+      // all four or none (a partial failure frees what it got)
       const size_t n = (size_t)kMaxRec * kStagePer;
-      HIP_TRY(hipMalloc(&s->d_st_start, n * 8));
-      HIP_TRY(hipMalloc(&s->d_st_len, n * 4));
-      HIP_TRY(hipMalloc(&s->d_st_cap, n * 4));
-      HIP_TRY(hipMalloc(&s->d_st_n, kMaxRec * 4));
+      uint64_t* a = nullptr;
+      uint32_t *b = nullptr, *c = nullptr, *d = nullptr;
+      hipError_t e = hipMalloc(&a, n * 8);
+      if (e == hipSuccess) e = hipMalloc(&b, n * 4);
+      if (e == hipSuccess) e = hipMalloc(&c, n * 4);
+      if (e == hipSuccess) e = hipMalloc(&d, kMaxRec * 4);
+      if (e != hipSuccess) {
+        (void)hipFree(a);
+        (void)hipFree(b);
+        (void)hipFree(c);
+        (void)hipFree(d);
+        (void)hipGetLastError();
+        return fail(UGPU_NOMEM, "staging buffers");
+      }
+      s->d_st_start = a;
+      s->d_st_len = b;
+      s->d_st_cap = c;
+      s->d_st_n = d;
     }
     P.st_start = s->d_st_start;
     P.st_len = s->d_st_len;
@@ -1633,6 +1652,9 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
 {
   if (!st || !out || (!chunk && len)) return fail(UGPU_INVAL, "NULL argument");
   if (st->done) return fail(UGPU_INVAL, "stream already ended (final chunk fed)");
+  if (final != 0 && final != 1 && final != UGPU_FEED_FLUSH) return fail(UGPU_INVAL, "final: 0, 1 or UGPU_FEED_FLUSH");
+  const bool flush = final == UGPU_FEED_FLUSH;
+  final = final == 1;
   *out = nullptr;
   const uint64_t n = st->carry + len;
   int rc = stream_grow(st, n);
@@ -1646,7 +1668,55 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
   uint64_t hi = final ? n : (n > st->keep ? n - st->keep : 0);
   uint64_t exit = 0;
   ugpu_totals tot{};
-  while (hi > 0) {
+  if (flush && !final) {
+    // settle as far as the bytes decide: the largest hi whose chain has no walk
+    // open at the end (the start of the last, still open match) -- step back
+    // from the end by 16, 64, 256, ... bytes, then bisect between the last hi
+    // that was too close and the first that was not
+    auto try_hi = [&](uint64_t h) -> int {
+      int c = ugpu_scan(st->sc, b, 0, h, n, 0, st->base, nullptr);
+      if (!c) c = ugpu_scan_totals(st->sc, &tot);
+      return c;
+    };
+    uint64_t good = 0, bad = n + 1, h = n, back = 16, last = ~0ull;
+    while (h > 0) {
+      rc = try_hi(h);
+      last = h;
+      if (rc == UGPU_OK) {
+        good = h;
+        break;
+      }
+      if (rc != UGPU_HALO) {
+        std::free(r);
+        return rc;
+      }
+      bad = h;
+      h = n > back ? n - back : 0;
+      back *= 4;
+    }
+    while (bad - good > 1) {
+      const uint64_t mid = good + (bad - good) / 2;
+      rc = try_hi(mid);
+      last = mid;
+      if (rc == UGPU_OK) {
+        good = mid;
+      } else if (rc == UGPU_HALO) {
+        bad = mid;
+      } else {
+        std::free(r);
+        return rc;
+      }
+    }
+    hi = good;
+    rc = UGPU_OK;
+    if (hi > 0 && last != hi) rc = try_hi(hi);  // (the scanner holds the last scan)
+    if (rc) {
+      std::free(r);
+      return rc;
+    }
+    exit = hi > 0 ? tot.exit : 0;
+  }
+  while (hi > 0 && !(flush && !final)) {
     rc = ugpu_scan(st->sc, b, 0, hi, n, final ? 1 : 0, st->base, nullptr);
     if (!rc) rc = ugpu_scan_totals(st->sc, &tot);
     if (rc == UGPU_HALO && !final) {

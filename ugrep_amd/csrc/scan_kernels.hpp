@@ -235,8 +235,8 @@ uint32_t xg_waves();
 // two-state carry-chain kernel, xc_kernel.hip (COUNT, or WRITE into P.out_*
 // at the output bases of the COUNT pass's records; out_capacity = the count)
 hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64_t count = 0);
-hipError_t xc_occupancy(int* blocks_per_cu);
-uint32_t xc_unit();
+hipError_t xc_occupancy(bool u, int* blocks_per_cu);  // u: the U-mode COUNT kernel
+uint32_t xc_unit(bool u);  // wave-tile bytes (u: U mode)
 uint32_t xc_waves();
 // dense wave-persistent kernel, dense_kernel.hip
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);

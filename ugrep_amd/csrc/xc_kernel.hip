@@ -63,6 +63,11 @@ constexpr int kCWaves = kCPair ? 16 : 4;  // waves per workgroup (the pair table
 constexpr uint32_t kCChunk = 1024;        // one wave-load: 16 bytes per lane
 constexpr int kCIter = UGPU_XC_ITER;      // chunks per iteration (loads in flight per wave)
 constexpr uint32_t kCTile = kCChunk * kCIter;
+#ifndef UGPU_XU_ITER
+#define UGPU_XU_ITER 2
+#endif
+constexpr int kUIter = UGPU_XU_ITER;  // U mode: fewer chunks in flight per wave, twice the waves
+static_assert(kCIter <= 4 && kUIter <= 4, "CIt");
 constexpr int kCLook = 8;                 // look-back chunks before giving up
 constexpr uint32_t kOnes = 0x01010101u;
 
@@ -212,7 +217,13 @@ __device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t n
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t a = __builtin_amdgcn_perm(x, sw, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
+#if defined(UGPU_XU_ABL) && UGPU_XU_ABL == 1  // broadcast lookups: no bank conflicts (benchmarking; wrong counts)
+    r |= (uint32_t)u.tab[a & 3u] << (8 * k);
+#elif defined(UGPU_XU_ABL) && UGPU_XU_ABL == 2  // no LDS lookups (benchmarking; wrong counts)
+    r |= ((a >> 13) & 1u) << (8 * k);
+#else
     r |= (uint32_t)u.tab[a] << (8 * k);
+#endif
   }
   return r;
 }
@@ -339,7 +350,7 @@ __device__ __forceinline__ uint64_t clook(uint64_t gen, uint64_t prop, uint32_t 
 // Per-iteration lane sums: starts per chunk, start offsets in the lane (v_dot4
 // weights), carry-in bits (one per In byte).
 struct CIt {
-  uint32_t cs[kCIter] = {};
+  uint32_t cs[4] = {};
   uint32_t ws = 0, ls = 0;
 };
 
@@ -462,6 +473,10 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
 __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q, uint32_t& mprev, uint32_t& cs,
                                               uint32_t& ws, uint32_t& ls)
 {
+#if defined(UGPU_XU_ABL) && UGPU_XU_ABL == 3  // loads only (benchmarking; wrong counts)
+  cs += v.x ^ v.y ^ v.z ^ v.w;
+  return;
+#endif
   uint32_t m[4];
   umask<false>(u, v, q, m);
   const uint32_t mp = __builtin_amdgcn_update_dpp(mprev, m[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
@@ -500,14 +515,27 @@ __device__ __forceinline__ uint64_t cexit(const uint32_t cb[4], uint64_t q, uint
   return x < rend ? x : rend;
 }
 
+// f(integral_constant<J>) for J = I .. N-1 (compile-time chunk indices)
+template <int I, int N, class F>
+__device__ __forceinline__ void cunroll(F& f)
+{
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    cunroll<I + 1, N>(f);
+  }
+}
+
 // code of a byte class (xc_cls: G << 7 | X << 6)
 __device__ __forceinline__ uint32_t ccode(uint32_t cls) { return cls & 0x80u ? 0xffu : (cls & 0x40u ? 0xfeu : 0u); }
 
 }  // namespace
 
+// (the body of the kernels below)
 template <bool W, bool WR, bool U>
-__global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
+__device__ __forceinline__ void xc_body(const ScanParams& P)
 {
+  constexpr int kIt = U ? kUIter : kCIter;  // chunks per iteration
+  constexpr uint32_t kTile = kCChunk * kIt;
   // LDS: byte codes, and (pair classifier) the codes of every byte pair; U
   // mode: the token codes and 3-byte completion bits
   __shared__ __attribute__((aligned(16))) uint8_t bcode[256];
@@ -555,8 +583,8 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   uint64_t tb = P.t0 + gw * P.tpb;
   uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
   if (tb > te) tb = te;
-  const uint64_t wlo = clampu(tb * kCTile, P.lo, P.hi);
-  const uint64_t whi = clampu(te * kCTile, P.lo, P.hi);
+  const uint64_t wlo = clampu(tb * kTile, P.lo, P.hi);
+  const uint64_t whi = clampu(te * kTile, P.lo, P.hi);
   const uint32_t n = (uint32_t)(te - tb);
   const bool last_wave = n && whi == P.hi;
   const uint64_t rend16 = (P.rend + 15) & ~uint64_t(15);
@@ -623,7 +651,7 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   // (the first wave, lo not tile aligned) and after them (the wave holding hi,
   // then on past hi until the exit) run one masked chunk at a time, outside
   // the main loop's register budget.
-  uint64_t ftb = (wlo + kCTile - 1) / kCTile, fte = whi / kCTile;
+  uint64_t ftb = (wlo + kTile - 1) / kTile, fte = whi / kTile;
   if (!n || ftb >= fte) ftb = fte = 0;
   // one masked chunk at q0 (exit search on chunks reaching past hi)
   auto masked = [&](uint64_t q0) __attribute__((always_inline)) {
@@ -646,32 +674,38 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   wc.cx = xprev(q0);
   if constexpr (U) u.cprev = ucode_before(u, P.g, q0);
   wc.hi = 0;
+  // option W: at_wb at the range start decodes the character before it; when
+  // lo is chunk aligned no chunk holds that byte, so it is seen here (>= 0x80:
+  // the host redoes the range with wfind_kernel)
+  if constexpr (W) {
+    if (n && wlo == P.lo && P.lo > P.bob) wc.hi |= (uint32_t)P.g[P.lo - 1];
+  }
   if (fte > ftb)
-    for (; q0 < ftb * kCTile; q0 += kCChunk) masked(q0);
+    for (; q0 < ftb * kTile; q0 += kCChunk) masked(q0);
 
-  uint4 cur[kCIter], nxt[kCIter];
+  uint4 cur[kIt], nxt[kIt];
   // U mode: the first dword of the tile after the current one (the last
   // chunk's context), loaded one tile ahead; M of the byte before the chunk
   uint32_t nfc = 0, nfn = 0, mprev = 0;
   const uint32_t cw_main = cw;
   if (fte > ftb) {
-    const uint64_t ts = ftb * kCTile;
+    const uint64_t ts = ftb * kTile;
     const __amdgpu_buffer_rsrc_t rs = crsrc(P.g + ts, rend16 > ts ? rend16 - ts : 0);
 #pragma unroll
-    for (int j = 0; j < kCIter; ++j) cur[j] = cload(rs, j * kCChunk + lo16);
-    if constexpr (U) nfc = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)kCTile, 0, 0);
+    for (int j = 0; j < kIt; ++j) cur[j] = cload(rs, j * kCChunk + lo16);
+    if constexpr (U) nfc = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)kTile, 0, 0);
     mprev = cw << 24;
   }
   for (uint64_t t = ftb; t < fte; ++t) {
-    const uint64_t ts = t * kCTile;
+    const uint64_t ts = t * kTile;
     {
       // (U mode reads the next tile also after the last: its first dword is
       // the last chunk's context)
-      const uint64_t tn = (U || t + 1 < fte) ? ts + kCTile : ts;
+      const uint64_t tn = (U || t + 1 < fte) ? ts + kTile : ts;
       const __amdgpu_buffer_rsrc_t rn = crsrc(P.g + tn, rend16 > tn ? rend16 - tn : 0);
 #pragma unroll
-      for (int j = 0; j < kCIter; ++j) nxt[j] = cload(rn, j * kCChunk + lo16);
-      if constexpr (U) nfn = __builtin_amdgcn_raw_buffer_load_b32(rn, (int)kCTile, 0, 0);
+      for (int j = 0; j < kIt; ++j) nxt[j] = cload(rn, j * kCChunk + lo16);
+      if constexpr (U) nfn = __builtin_amdgcn_raw_buffer_load_b32(rn, (int)kTile, 0, 0);
     }
     CIt a;
     uint32_t cb[4];
@@ -680,10 +714,10 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
     auto chunk = [&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       if constexpr (U) {
-        if constexpr (j + 1 < kCIter) {
+        if constexpr (j + 1 < kIt) {
           u.nx0 = __builtin_amdgcn_readlane(cur[j + 1].x, 0);
         } else {
-          const uint64_t qn = ts + kCTile;
+          const uint64_t qn = ts + kTile;
           const uint32_t in = uinside(u, qn);
           u.nx0 = (__builtin_amdgcn_readfirstlane(nfc) & in) | (u.null4 & ~in);
         }
@@ -693,14 +727,10 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
       else
         cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u);
     };
-    static_assert(kCIter == 4, "the chunk calls below");
-    chunk(std::integral_constant<int, 0>{});
-    chunk(std::integral_constant<int, 1>{});
-    chunk(std::integral_constant<int, 2>{});
-    chunk(std::integral_constant<int, 3>{});
+    cunroll<0, kIt>(chunk);
     uint32_t c = 0, cj = 0;
 #pragma unroll
-    for (int j = 0; j < kCIter; ++j) {
+    for (int j = 0; j < kIt; ++j) {
       c += a.cs[j];
       cj += j * a.cs[j];
     }
@@ -708,10 +738,10 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
     pos += (uint64_t)c * (ts + lo16) + a.ws + kCChunk * cj;
     lbits += a.ls;
 #pragma unroll
-    for (int j = 0; j < kCIter; ++j) cur[j] = nxt[j];
+    for (int j = 0; j < kIt; ++j) cur[j] = nxt[j];
     nfc = nfn;
   }
-  if (fte > ftb) q0 = fte * kCTile;
+  if (fte > ftb) q0 = fte * kTile;
   if constexpr (U && !WR) {
     if (fte > ftb) {
       // the wave carry after the main loop, and ls's In_i -> In_{i-1} form:
@@ -758,6 +788,23 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   }
 }
 
+template <bool W, bool WR, bool U>
+__global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
+{
+  xc_body<W, WR, U>(P);
+}
+
+// U mode COUNT: LDS-latency bound (its byte lookups), so two workgroups per CU
+// (8 waves per SIMD, at most 64 VGPRs; the tables take 72 KiB per workgroup)
+#ifndef UGPU_XU_WAVES_PER_EU
+#define UGPU_XU_WAVES_PER_EU 8
+#endif
+__global__ __launch_bounds__(kCWaves * 64) __attribute__((amdgpu_waves_per_eu(UGPU_XU_WAVES_PER_EU)))
+void xu_kernel(ScanParams P)
+{
+  xc_body<false, false, true>(P);
+}
+
 // OFFSETS, second step: len[k] held the end position (low 32 bits, reported
 // coordinates); subtract the start
 __global__ __launch_bounds__(256) void xc_len_kernel(uint64_t* start, uint32_t* len, uint64_t n)
@@ -785,7 +832,7 @@ hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64
     return hipGetLastError();
   }
   if (P.xu_tab)
-    hipLaunchKernelGGL((xc_kernel<false, false, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    hipLaunchKernelGGL(xu_kernel, dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   else if (P.xc_w)
     hipLaunchKernelGGL((xc_kernel<true, false, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   else
@@ -793,11 +840,12 @@ hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64
   return hipGetLastError();
 }
 
-hipError_t xc_occupancy(int* n)
+hipError_t xc_occupancy(bool u, int* n)
 {
+  if (u) return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xu_kernel, kCWaves * 64, 0);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<true, true, false>, kCWaves * 64, 0);
 }
-uint32_t xc_unit() { return kCTile; }
+uint32_t xc_unit(bool u) { return u ? kCChunk * kUIter : kCTile; }
 uint32_t xc_waves() { return kCWaves; }
 
 }  // namespace ugpu

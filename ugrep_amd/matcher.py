@@ -242,10 +242,12 @@ class Stream:
         check(lib.ugpu_stream_create(pattern.handle, keep, ctypes.byref(h)))
         self._h = h
 
-    def feed(self, chunk, final=False, offsets=True):
+    def feed(self, chunk, final=False, offsets=True, flush=False):
+        """final: the input ends here; flush: more may follow, but settle every
+        match the bytes so far decide (UGPU_FEED_FLUSH: an input that would block)."""
         ptr, n, keep = _buffer_ptr(chunk)
         res = ctypes.POINTER(_lib.Result)()
-        check(lib.ugpu_stream_feed(self._h, ctypes.c_void_p(ptr), n, 1 if final else 0,
+        check(lib.ugpu_stream_feed(self._h, ctypes.c_void_p(ptr), n, 1 if final else (2 if flush else 0),
                                    _lib.MODE_OFFSETS if offsets else _lib.MODE_COUNT, ctypes.byref(res)))
         out = _take_result(res, offsets)
         del keep
