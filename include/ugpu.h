@@ -178,6 +178,23 @@ int ugpu_find_all(const ugpu_dfa *dfa, const uint8_t *buf, uint64_t len, uint64_
                   ugpu_result **out);
 int ugpu_result_free(ugpu_result *res);
 
+/* Multi-device FIND (the reference has no counterpart: one
+   buffer is always scanned by one thread, src/ugrep.cpp:4118-4480).  One
+   process drives the devices: [start, len) is cut into `ndev` contiguous
+   shards at arbitrary byte offsets; shard k runs on device k mod
+   hipGetDeviceCount() (so ndev may exceed the devices: virtual shards share a
+   card), each with its own table copy, its own input copy (host buffers: H2D
+   over that device's PCIe link; a device buffer: a peer copy over xGMI for
+   the shards on other devices) plus a 1 MiB halo, and its own stream.  The
+   shards' FIND chains are then resolved left to right on the host
+   (ugpu_chain_fix on the owning device when a chain enters a shard elsewhere
+   than at its start), and OFFSETS records are copied straight from each
+   device into their slice of the result.  Same result as ugpu_find_all.
+   Option W tables run ugpu_find_all on one device (at_wb at a shard start
+   needs the previous shard's bytes).  ndev <= 0: one shard per device. */
+int ugpu_find_all_multi(const ugpu_dfa *dfa, const uint8_t *buf, uint64_t len, uint64_t start, uint32_t mode,
+                        int ndev, ugpu_result **out);
+
 /* --- device-resident scanning (benchmarks, multi-GPU shards) --- */
 
 /* Workspace for scans of device buffers on the current device. */

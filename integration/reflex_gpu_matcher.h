@@ -93,7 +93,17 @@ class GpuMatcher : public Matcher {
   {
     const char* st = std::getenv("UGPU_ADAPTER_STATS");
     if (st != NULL && *st == '1')
-      std::fprintf(stderr, "[ugpu-adapter] scans=%zu\n", scans_);
+    {
+      // one line per matcher: GPU scans, FIND calls answered from GPU records,
+      // FIND calls the CPU matcher answered and why (UGPU_ADAPTER_STATS=1)
+      std::string why;
+      for (int r = 0; r < kReasons; ++r)
+        if (cpu_why_[r] != 0)
+          why += std::string(why.empty() ? "" : ",") + reason_name(r) + ":" + std::to_string(cpu_why_[r]);
+      std::fprintf(stderr, "[ugpu-adapter] scans=%zu gpu_finds=%zu cpu_finds=%zu table=%s cpu_why=%s\n", scans_,
+                   gpu_finds_, cpu_finds(), tab_pat_ == NULL ? "none" : tab_ ? "gpu" : "unsupported",
+                   why.empty() ? "-" : why.c_str());
+    }
     ugpu_result_free(gres_);
     ugpu_stream_destroy(gst_);
     --live();
@@ -110,6 +120,15 @@ class GpuMatcher : public Matcher {
 
   /// GPU scans (whole-buffer scans and stream feeds) issued so far (tests).
   size_t gpu_scans() const { return scans_; }
+  /// FIND calls answered from GPU records, and by the CPU matcher (tests).
+  size_t gpu_finds() const { return gpu_finds_; }
+  size_t cpu_finds() const
+  {
+    size_t n = 0;
+    for (int r = 0; r < kReasons; ++r)
+      n += cpu_why_[r];
+    return n;
+  }
   /// Whether the engine supports this pattern (builds the tables if needed).
   bool gpu_ready() { return tables() != NULL; }
   /// Smallest input sent to the GPU (0: every input).
@@ -120,12 +139,22 @@ class GpuMatcher : public Matcher {
  protected:
   virtual size_t match(Method method)
   {
-    if (method != Const::FIND || opt_.A || opt_.N || tables() == NULL || (sparse_ && live() > sparse_max_))
-      return Matcher::match(method);
+    if (method != Const::FIND)
+      return cpu(method, R_METHOD);
+    if (opt_.A)
+      return cpu(method, R_OPT_A);
+    if (opt_.N)
+      return cpu(method, R_OPT_N);
+    if (tables() == NULL)
+      return cpu(method, R_TABLE);
+    if (sparse_ && live() > sparse_max_)
+      return cpu(method, R_SPARSE);
     if (own_)
       return stream_match();
-    if (!eof_ || end_ < min_bytes())
-      return Matcher::match(method);
+    if (!eof_)
+      return cpu(method, R_PARTIAL);
+    if (end_ < min_bytes())
+      return cpu(method, R_SMALL);
     reset_text();
     // buffer() is non-virtual and rewinds cur_ without telling this class
     // (absmatcher.h:542-591), and the caller may hand over new bytes at the
@@ -134,7 +163,8 @@ class GpuMatcher : public Matcher {
     // means the records may be stale, so scan again
     if (gres_ == NULL || gbuf_ != buf_ || gend_ != end_ || cur_ < gcur_ || inside_match())
       if (!rescan())
-        return Matcher::match(method);
+        return cpu(method, R_ENGINE);
+    ++gpu_finds_;
     while (gi_ < gres_->count && gres_->start[gi_] < cur_)
       ++gi_;
     if (gi_ >= gres_->count)
@@ -147,6 +177,19 @@ class GpuMatcher : public Matcher {
   }
 
  private:
+  // why the CPU matcher answered a call (adapter statistics)
+  enum Reason { R_METHOD, R_OPT_A, R_OPT_N, R_TABLE, R_SPARSE, R_PARTIAL, R_SMALL, R_ENGINE, R_W_STREAM, kReasons };
+  static const char* reason_name(int r)
+  {
+    static const char* const n[kReasons] = {"method", "option_A", "option_N", "table",         "sparse_limit",
+                                            "partial", "small",    "engine",   "option_W_stream"};
+    return n[r];
+  }
+  size_t cpu(Method method, int why)
+  {
+    ++cpu_why_[why];
+    return Matcher::match(method);
+  }
   // device tables of (pattern, option W), shared with clones; NULL when the
   // engine does not support the pattern
   const ugpu_dfa* tables()
@@ -252,14 +295,17 @@ class GpuMatcher : public Matcher {
   // stream was started at absolute offset sbase_ and has been fed up to sfed_.
   size_t stream_match()
   {
-    if (opt_.W || cpu_stream_)
-      return Matcher::match(Const::FIND);  // (W: at_wb at a window start needs the bytes before it)
+    if (opt_.W)
+      return cpu(Const::FIND, R_W_STREAM);  // (at_wb at a window start needs the bytes before it)
+    if (cpu_stream_)
+      return cpu(Const::FIND, cpu_stream_why_);
     reset_text();
     txt_ = buf_ + cur_;  // bytes before the cursor may be shifted out (as lib/matcher.cpp:51)
     const uint64_t at = static_cast<uint64_t>(num_ + cur_);
     if (gst_ == NULL || at < gcur_abs_ || at > sfed_ || stream_inside(at))
       if (!stream_restart(at))
-        return Matcher::match(Const::FIND);
+        return cpu(Const::FIND, cpu_stream_why_);
+    ++gpu_finds_;
     for (;;)
     {
       while (gres_ != NULL && gi_ < gres_->count && sbase_ + gres_->start[gi_] < at)
@@ -310,9 +356,11 @@ class GpuMatcher : public Matcher {
       {
         // a small input, all of it read before any feed: the CPU matcher is faster
         cpu_stream_ = true;
+        cpu_stream_why_ = R_SMALL;
         ugpu_stream_destroy(gst_);
         gst_ = NULL;
-        return Matcher::match(Const::FIND);
+        --gpu_finds_;
+        return cpu(Const::FIND, R_SMALL);
       }
       const size_t from = static_cast<size_t>(sfed_ - num_);
       drop_records();
@@ -321,9 +369,11 @@ class GpuMatcher : public Matcher {
       {
         // engine unavailable for this input: the CPU matcher takes over at the cursor
         cpu_stream_ = true;
+        cpu_stream_why_ = R_ENGINE;
         ugpu_stream_destroy(gst_);
         gst_ = NULL;
-        return Matcher::match(Const::FIND);
+        --gpu_finds_;
+        return cpu(Const::FIND, R_ENGINE);
       }
       ++scans_;
       sfed_ = num_ + end_;
@@ -366,6 +416,7 @@ class GpuMatcher : public Matcher {
     if (ugpu_stream_create(tables(), 0, &gst_) != UGPU_OK)
     {
       cpu_stream_ = true;
+      cpu_stream_why_ = R_ENGINE;
       return false;
     }
     sbase_ = at;
@@ -389,6 +440,9 @@ class GpuMatcher : public Matcher {
   ugpu_stream* gst_ = NULL;
   uint64_t sbase_ = 0, sfed_ = 0, gcur_abs_ = 0;
   bool sdone_ = false, cpu_stream_ = false;
+  int cpu_stream_why_ = R_ENGINE;
+  size_t gpu_finds_ = 0;
+  size_t cpu_why_[kReasons] = {};
 };
 
 }  // namespace reflex

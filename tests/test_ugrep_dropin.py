@@ -25,20 +25,39 @@ CWD = os.path.join(ROOT, "tests", "golden", "verify")
 SPEC = json.load(open(os.path.join(ROOT, "tests", "golden", "verify_cases.json")))
 
 
+def _stats(stderr):
+    """The adapter's per-matcher statistics lines (UGPU_ADAPTER_STATS=1):
+    scans, FIND calls answered from GPU records, FIND calls the CPU matcher
+    answered, whether the engine took the table, and the CPU calls by reason."""
+    out = []
+    for ln in stderr.decode(errors="replace").splitlines():
+        if ln.startswith("[ugpu-adapter] "):
+            kv = dict(f.split("=", 1) for f in ln.split()[1:])
+            why = {} if kv["cpu_why"] == "-" else {k: int(v) for k, v in (w.split(":") for w in kv["cpu_why"].split(","))}
+            out.append(dict(scans=int(kv["scans"]), gpu=int(kv["gpu_finds"]), cpu=int(kv["cpu_finds"]),
+                            table=kv["table"], why=why))
+    return out
+
+
 def _run_all(exe, env):
     env = dict(env, **SPEC["env"])
     env.pop("UGREP_COLORS", None)
-    bad, scans = [], 0
+    bad, ledger = [], []
     for c in SPEC["cases"]:
         r = subprocess.run([exe] + c["args"], cwd=CWD, env=env, capture_output=True, timeout=60,
                            input=open(os.path.join(CWD, c["stdin"]), "rb").read() if c["stdin"] else None)
         h = hashlib.sha256(r.stdout).hexdigest()
         if h != c["sha256"]:
             bad.append((c["args"], c["expect"], len(r.stdout), c["size"]))
-        for ln in r.stderr.decode(errors="replace").splitlines():
-            if ln.startswith("[ugpu-adapter] scans="):
-                scans += int(ln.split("=")[1])
-    return bad, scans
+        ledger.append(dict(expect=c["expect"], args=c["args"], matchers=_stats(r.stderr)))
+    return bad, ledger
+
+
+# CPU answers that are by design: option N (ugrep -Y / empty-matching
+# patterns) is not on the GPU path, nor option W on streamed input (at_wb at a
+# window start needs the bytes before the window)
+BY_DESIGN = {"option_N", "option_W_stream"}
+LEDGER = os.path.join(ROOT, "tests", "golden", "dropin_fallbacks.json")
 
 
 def test_fixture_size():
@@ -53,12 +72,51 @@ def test_reference_ugrep_reproduces_goldens():
     assert not bad, bad[:5]
 
 
+def test_fallback_ledger_is_consistent():
+    """The committed ledger of cases in which the CPU matcher answered FIND
+    calls names a reason for each, and only reasons of the adapter."""
+    if not os.path.exists(LEDGER):
+        pytest.skip("no ledger yet")
+    led = json.load(open(LEDGER))
+    known = {"method", "option_A", "option_N", "table", "sparse_limit", "partial", "small", "engine",
+             "option_W_stream"}
+    expects = {c["expect"] for c in SPEC["cases"]}
+    for e, why in led["cpu_cases"].items():
+        assert e in expects, e
+        assert why and set(why) <= known, (e, why)
+
+
 @pytest.mark.gpu
 def test_dropin_ugrep_reproduces_goldens():
     exe = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")
     if not os.path.exists(exe):
         pytest.skip("ugrep_gpu not built (make -C oracle ref, build container)")
     env = dict(os.environ, UGPU_ADAPTER_MIN_BYTES="0", UGPU_ADAPTER_SPARSE_MAX="1000000", UGPU_ADAPTER_STATS="1")
-    bad, scans = _run_all(exe, env)
+    bad, ledger = _run_all(exe, env)
     assert not bad, bad[:5]
-    assert scans > 100, scans
+    # attribution: per case, which FIND calls the GPU answered and why the CPU
+    # answered the others
+    cpu_cases, served, leaks = {}, 0, []
+    for c in ledger:
+        why = {}
+        for m in c["matchers"]:
+            for k, v in m["why"].items():
+                why[k] = why.get(k, 0) + v
+            # a table the engine accepted: every FIND call not excluded by design ran on the GPU
+            if m["table"] == "gpu" and set(m["why"]) - BY_DESIGN:
+                leaks.append((c["expect"], m))
+        if any(m["gpu"] for m in c["matchers"]):
+            served += 1
+        if why:
+            cpu_cases[c["expect"]] = sorted(why)
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "dropin_ledger.json"), "w") as f:
+        json.dump(dict(served_by_gpu=served, cases=len(ledger), cpu_cases=cpu_cases, detail=ledger), f, indent=1)
+    assert not leaks, leaks[:5]
+    assert served > 100, served
+    if os.path.exists(LEDGER):  # the committed list of cases the CPU (partly) answered, and why
+        want = json.load(open(LEDGER))
+        diff = sorted(k for k in set(cpu_cases) | set(want["cpu_cases"]) if cpu_cases.get(k) != want["cpu_cases"].get(k))
+        assert not diff, [(k, cpu_cases.get(k), want["cpu_cases"].get(k)) for k in diff[:10]]
+        assert served == want["served_by_gpu"]

@@ -84,6 +84,8 @@ def _load():
         "ugpu_tables_xc_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, c_u8p, P(ctypes.c_int)]),
         "ugpu_tables_xu_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, c_u8p, c_u32p, P(ctypes.c_int)]),
         "ugpu_find_all": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P(P(Result))]),
+        "ugpu_find_all_multi": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int,
+                                               P(P(Result))]),
         "ugpu_result_free": (ctypes.c_int, [P(Result)]),
         "ugpu_scanner_create": (ctypes.c_int, [V, P(V)]),
         "ugpu_scanner_destroy": (ctypes.c_int, [V]),

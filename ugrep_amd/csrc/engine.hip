@@ -21,6 +21,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ugpu.h"
@@ -83,6 +84,12 @@ struct ugpu_dfa {
   // costs device allocations and property queries)
   std::mutex pool_mu;
   std::vector<ugpu_scanner*> pool;
+  // the opcode words and flags it was built from, and its copies on other
+  // devices (ugpu_find_all_multi), created on first use
+  std::vector<uint32_t> opc;
+  uint32_t pflags = 0;
+  std::mutex rep_mu;
+  std::vector<ugpu_dfa*> reps;
 };
 
 struct ugpu_scanner {
@@ -412,6 +419,8 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     delete d;
     return hip_fail(e, "hipGetDevice");
   }
+  d->opc.assign(opc, opc + nop);
+  d->pflags = pattern_flags;
   const size_t n = d->t.trans.size();
   d->ntrans_pad = (uint32_t)((n + 7) & ~size_t(7));
   std::vector<uint16_t> tr(d->ntrans_pad, 0);
@@ -488,6 +497,15 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
 int ugpu_dfa_destroy(ugpu_dfa* d)
 {
   if (!d) return UGPU_OK;
+  for (ugpu_dfa* r : d->reps) {
+    if (r) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(r->device);
+      ugpu_dfa_destroy(r);
+      (void)hipSetDevice(cur);
+    }
+  }
   for (ugpu_scanner* s : d->pool) ugpu_scanner_destroy(s);
   if (d->d_trans) (void)hipFree(d->d_trans);
   if (d->d_xtrans) (void)hipFree(d->d_xtrans);
@@ -1285,6 +1303,245 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
   }
   *out = r;
   return UGPU_OK;
+}
+
+// ---------------------------------------------------------------- multi-device
+namespace {
+
+// the table copy of d on device dev (d itself on its own device); the caller
+// has made dev current
+int dfa_on(const ugpu_dfa* d, int dev, const ugpu_dfa** out)
+{
+  if (dev == d->device) {
+    *out = d;
+    return UGPU_OK;
+  }
+  ugpu_dfa* m = const_cast<ugpu_dfa*>(d);
+  std::lock_guard<std::mutex> lk(m->rep_mu);
+  if (m->reps.size() <= (size_t)dev) m->reps.resize((size_t)dev + 1, nullptr);
+  if (!m->reps[dev]) {
+    ugpu_dfa* r = nullptr;
+    const int rc = ugpu_dfa_create(m->opc.data(), (uint32_t)m->opc.size(), m->pflags, &r);
+    if (rc) return rc;
+    m->reps[dev] = r;
+  }
+  *out = m->reps[dev];
+  return UGPU_OK;
+}
+
+// One shard of ugpu_find_all_multi: [lo, hi) of the caller's buffer, scanned on
+// device dev from its own copy of [lo, rend).
+struct Shard {
+  int dev = 0;
+  uint64_t lo = 0, hi = 0, rend = 0;
+  const ugpu_dfa* tab = nullptr;
+  ugpu_scanner* sc = nullptr;
+  FindWs* ws = nullptr;
+  const uint8_t* dbuf = nullptr;  // the shard's bytes on its device (dbuf[0] = buffer byte lo)
+  ugpu_totals tot{};
+  uint64_t entry = 0, exit = 0;   // global chain entry / exit (entry = lo speculatively)
+  uint64_t base = 0;              // first record index (OFFSETS)
+  int rc = UGPU_OK;
+};
+
+// bytes [lo, rend) of the caller's buffer onto the shard's device
+int shard_load(Shard& sh, const uint8_t* buf, bool host, int src_dev)
+{
+  const uint64_t n = sh.rend - sh.lo;
+  hipError_t e;
+  if (!host && src_dev == sh.dev) {
+    sh.dbuf = buf + sh.lo;
+    return UGPU_OK;
+  }
+  if ((e = sh.ws->reserve_in(n)) != hipSuccess) return hip_fail(e, "shard input");
+  if (host)
+    e = hipMemcpyAsync(sh.ws->d_in, buf + sh.lo, n, hipMemcpyHostToDevice, sh.ws->st);
+  else
+    e = hipMemcpyPeerAsync(sh.ws->d_in, sh.dev, buf + sh.lo, src_dev, n, sh.ws->st);
+  if (e != hipSuccess) return hip_fail(e, "shard input copy");
+  sh.dbuf = sh.ws->d_in;
+  return UGPU_OK;
+}
+
+// speculative COUNT scan of the shard from its start (a match that walks past
+// the halo: again with the rest of the buffer readable)
+void shard_scan(Shard& sh, const uint8_t* buf, uint64_t len, bool host, int src_dev, uint32_t mode)
+{
+  if ((sh.rc = hipSetDevice(sh.dev)) != hipSuccess) {
+    sh.rc = hip_fail((hipError_t)sh.rc, "hipSetDevice");
+    return;
+  }
+  if ((sh.rc = dfa_on(sh.tab, sh.dev, &sh.tab)) != UGPU_OK) return;
+  if ((sh.rc = scanner_acquire(sh.tab, &sh.sc)) != UGPU_OK) return;
+  if (!(sh.ws = find_ws_acquire(sh.dev))) {
+    sh.rc = fail(UGPU_NOMEM, "find workspace");
+    return;
+  }
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if ((sh.rc = shard_load(sh, buf, host, src_dev)) != UGPU_OK) return;
+    sh.sc->stage_once = mode == UGPU_MODE_OFFSETS;
+    sh.rc = ugpu_scan(sh.sc, sh.dbuf, 0, sh.hi - sh.lo, sh.rend - sh.lo, sh.rend == len, sh.lo, sh.ws->st);
+    if (!sh.rc) sh.rc = ugpu_scan_totals(sh.sc, &sh.tot);
+    if (sh.rc != UGPU_HALO || sh.rend == len) break;
+    sh.rend = len;
+  }
+  if (sh.rc) return;
+  sh.entry = sh.lo;
+  sh.exit = sh.tot.exit + sh.lo;
+}
+
+// the shard's records into r at its base (a shard whose chain entry moved
+// is scanned again from the true entry first)
+void shard_records(Shard& sh, uint64_t len, ugpu_result* r)
+{
+  if ((sh.rc = hipSetDevice(sh.dev)) != hipSuccess) {
+    sh.rc = hip_fail((hipError_t)sh.rc, "hipSetDevice");
+    return;
+  }
+  const uint64_t n = sh.tot.count;
+  if (n == 0) return;
+  if (sh.entry != sh.lo) {
+    ugpu_totals t{};
+    sh.rc = ugpu_scan(sh.sc, sh.dbuf, sh.entry - sh.lo, sh.hi - sh.lo, sh.rend - sh.lo, sh.rend == len, sh.lo,
+                      sh.ws->st);
+    if (!sh.rc) sh.rc = ugpu_scan_totals(sh.sc, &t);
+    if (sh.rc) return;
+    if (t.count != n) {
+      sh.rc = fail(UGPU_DEVICE, "shard re-scan disagrees with the stitched count");
+      return;
+    }
+  }
+  hipError_t e;
+  if ((e = sh.ws->reserve_out(n)) != hipSuccess) {
+    sh.rc = hip_fail(e, "match list");
+    return;
+  }
+  if ((sh.rc = ugpu_scan_offsets(sh.sc, sh.ws->d_start, sh.ws->d_len, sh.ws->d_cap, n, sh.ws->st)) != UGPU_OK) return;
+  if ((e = hipMemcpyAsync(r->start + sh.base, sh.ws->d_start, n * 8, hipMemcpyDeviceToHost, sh.ws->st)) != hipSuccess ||
+      (e = hipMemcpyAsync(r->len + sh.base, sh.ws->d_len, n * 4, hipMemcpyDeviceToHost, sh.ws->st)) != hipSuccess ||
+      (e = hipMemcpyAsync(r->cap + sh.base, sh.ws->d_cap, n * 4, hipMemcpyDeviceToHost, sh.ws->st)) != hipSuccess ||
+      (e = hipStreamSynchronize(sh.ws->st)) != hipSuccess)
+    sh.rc = hip_fail(e, "hipMemcpy matches");
+}
+
+}  // namespace
+}  // extern "C"
+namespace {
+// f(shard) on one host thread per shard
+template <class F>
+void each_shard(std::vector<Shard>& shards, F f)
+{
+  std::vector<std::thread> th;
+  th.reserve(shards.size());
+  for (Shard& sh : shards) th.emplace_back([&sh, &f] { f(sh); });
+  for (std::thread& t : th) t.join();
+}
+}  // namespace
+extern "C" {
+
+int ugpu_find_all_multi(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_t start, uint32_t mode,
+                        int ndev, ugpu_result** out)
+{
+  if (!dfa || !out || (!buf && len)) return fail(UGPU_INVAL, "NULL argument");
+  if (mode != UGPU_MODE_COUNT && mode != UGPU_MODE_OFFSETS) return fail(UGPU_INVAL, "unknown mode");
+  *out = nullptr;
+  if (start > len) start = len;
+  int devices = 0, cur = 0;
+  HIP_TRY(hipGetDeviceCount(&devices));
+  HIP_TRY(hipGetDevice(&cur));
+  if (devices < 1) return fail(UGPU_DEVICE, "no device");
+  if (ndev <= 0) ndev = devices;
+  // tiny ranges and option W (at_wb at a shard start needs the previous
+  // shard's bytes): one device
+  const uint64_t span = len - start;
+  if (ndev == 1 || dfa->d_wtab || span < (uint64_t)ndev * 4096) return ugpu_find_all(dfa, buf, len, start, mode, out);
+  bool host = true;
+  int src_dev = cur;
+  {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, buf) == hipSuccess && a.type == hipMemoryTypeDevice) {
+      host = false;
+      src_dev = a.device;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  const uint64_t halo = env_u64("UGPU_MULTI_HALO", 1ull << 20);
+  std::vector<Shard> shards((size_t)ndev);
+  for (int k = 0; k < ndev; ++k) {
+    Shard& sh = shards[(size_t)k];
+    sh.dev = k % devices;
+    sh.lo = start + span * (uint64_t)k / (uint64_t)ndev;
+    sh.hi = start + span * (uint64_t)(k + 1) / (uint64_t)ndev;
+    sh.rend = sh.hi + halo < len ? sh.hi + halo : len;
+    sh.tab = dfa;
+  }
+  int rc = UGPU_OK;
+  auto finish = [&](int code) {
+    for (Shard& sh : shards) {
+      if (sh.ws) {
+        (void)hipSetDevice(sh.dev);
+        (void)hipStreamSynchronize(sh.ws->st);
+        find_ws_release(sh.ws);
+      }
+      if (sh.sc) scanner_release(sh.tab, sh.sc);
+    }
+    (void)hipSetDevice(cur);
+    return code;
+  };
+  each_shard(shards, [&](Shard& sh) { shard_scan(sh, buf, len, host, src_dev, mode); });
+  for (Shard& sh : shards)
+    if (sh.rc) return finish(sh.rc);
+  // resolve the chains left to right: shard k's speculative entry (its start)
+  // is right iff shard k-1's exit is there; otherwise re-enter it at that exit
+  for (size_t k = 1; k < shards.size(); ++k) {
+    Shard& sh = shards[k];
+    const uint64_t e = shards[k - 1].exit;
+    if (e == sh.entry) continue;
+    if (e >= sh.hi) {  // the previous shard's last match covers this whole shard
+      sh.tot.count = sh.tot.digest = sh.tot.dcap = 0;
+      sh.entry = e;
+      sh.exit = e;
+      continue;
+    }
+    ugpu_totals d{};
+    const hipError_t he = hipSetDevice(sh.dev);
+    if (he != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
+    rc = ugpu_chain_fix(sh.sc, sh.dbuf, 0, sh.hi - sh.lo, sh.rend - sh.lo, sh.rend == len, sh.lo, sh.entry - sh.lo,
+                        e - sh.lo, &d, sh.ws->st);
+    if (rc) return finish(rc);
+    sh.tot.count += d.count;
+    sh.tot.digest += d.digest;
+    sh.tot.dcap += d.dcap;
+    sh.entry = e;
+    if (d.exit != ~0ull) sh.exit = d.exit + sh.lo;
+  }
+  ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
+  if (!r) return finish(fail(UGPU_NOMEM, "host allocation"));
+  for (Shard& sh : shards) {
+    sh.base = r->count;
+    r->count += sh.tot.count;
+    r->digest += sh.tot.digest;
+    r->dcap += sh.tot.dcap;
+  }
+  if (mode == UGPU_MODE_OFFSETS && r->count > 0) {
+    const uint64_t n = r->count;
+    r->start = static_cast<uint64_t*>(std::malloc(n * 8));
+    r->len = static_cast<uint32_t*>(std::malloc(n * 4));
+    r->cap = static_cast<uint32_t*>(std::malloc(n * 4));
+    if (!r->start || !r->len || !r->cap) {
+      ugpu_result_free(r);
+      return finish(fail(UGPU_NOMEM, "match list allocation"));
+    }
+    each_shard(shards, [&](Shard& sh) { shard_records(sh, len, r); });
+    for (Shard& sh : shards)
+      if (sh.rc) {
+        ugpu_result_free(r);
+        return finish(sh.rc);
+      }
+  }
+  *out = r;
+  return finish(UGPU_OK);
 }
 
 // ---------------------------------------------------------------- lines

@@ -238,22 +238,28 @@ __device__ __forceinline__ uint32_t ucode_b0(const CU& u, uint32_t x)
 // resolve the 3-byte tokens of code dword c (bytes x, next bytes nx; cn =
 // the codes of the next 4 bytes): a 3-byte lead (XU_L3) shares a class bit
 // with the code of the byte after it (which carries the class of the third
-// byte) -- one AND for all 4 bytes; leads without class bits (XU_MIX) ask the
-// bitmap (rare: the divergent loop)
+// byte) -- one AND for all 4 bytes.  EXACT: leads whose third bytes are no
+// union of classes (XU_MIX, kernel code kUMix) ask the bitmap (the divergent
+// loop); otherwise the caller knows that the dword has none.
+constexpr uint32_t kUMix = 0xF8u;  // XU_MIX in the LDS table: bit 3 without bit 0 (XU_SLOW = 0x0F)
+template <bool EXACT = true>
 __device__ __forceinline__ uint32_t ucode_fix(const CU& u, uint32_t c, uint32_t x, uint32_t nx, uint32_t cn)
 {
   const uint32_t cy = __builtin_amdgcn_alignbit(cn, c, 8);  // code of byte k + 1, in byte k
-  const uint32_t v7 = c & ((c & cy & 0x70707070u) + 0x70707070u) & 0x80808080u;
-  uint32_t mm = c & ~((c & 0x70707070u) + 0x70707070u) & 0x80808080u;  // XU_MIX
-  c |= (v7 >> 4) - (v7 >> 7);  // 0x07: the token covers x .. x + 2
-  if (mm) {
-    do {
-      const uint32_t j = (uint32_t)__builtin_ctz(mm) >> 3;
-      const uint32_t b = __builtin_amdgcn_alignbit(nx, x, 8 * j);  // bytes x+j .. x+j+3
-      const uint32_t i = (b & 15u) << 12 | ((b >> 8) & 63u) << 6 | ((b >> 16) & 63u);
-      if (((u.bm3[i >> 5] >> (i & 31)) & 1u) && ((b >> 16) & 0xc0u) == 0x80u) c |= 7u << (8 * j);
-      mm &= ~(0xffu << (8 * j));
-    } while (mm);
+  uint32_t v7 = c & ((c & cy & 0x70707070u) + 0x70707070u) & 0x80808080u;
+  if constexpr (!EXACT) {
+    c |= (v7 >> 4) - (v7 >> 7);  // 0x07: the token covers x .. x + 2
+    return c;
+  }
+  uint32_t mm = c & ~(c << 3) & 0x08080808u;  // XU_MIX leads
+  v7 &= ~(mm << 4);
+  c |= (v7 >> 4) - (v7 >> 7);
+  while (mm) {
+    const uint32_t j = (uint32_t)__builtin_ctz(mm) >> 3;
+    const uint32_t b = __builtin_amdgcn_alignbit(nx, x, 8 * j);  // bytes x+j .. x+j+3
+    const uint32_t i = (b & 15u) << 12 | ((b >> 8) & 63u) << 6 | ((b >> 16) & 63u);
+    if (((u.bm3[i >> 5] >> (i & 31)) & 1u) && ((b >> 16) & 0xc0u) == 0x80u) c |= 7u << (8 * j);
+    mm &= ~(0xffu << (8 * j));
   }
   return c;
 }
@@ -276,8 +282,11 @@ __device__ __forceinline__ uint32_t uload_dw(const CU& u, const uint8_t* g, uint
   return (x & uinside(u, q)) | (u.null4 & ~uinside(u, q));
 }
 
-// One lane's 16 bytes at q: M (bit 0 of each byte: the byte lies inside a token)
-template <bool MASK>
+// One lane's 16 bytes at q: M (bit 0 of each byte: the byte lies inside a
+// token).  FAST (the unmasked COUNT main loop): the 3-byte test runs without
+// the XU_MIX bitmap unless some lane of the wave met a code with bit 3 (an
+// XU_MIX lead or an XU_SLOW 4-byte lead) in this chunk.
+template <bool MASK, bool FAST = false>
 __device__ __forceinline__ void umask(CU& u, const uint4& v, uint64_t q, uint32_t m[4])
 {
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -294,16 +303,25 @@ __device__ __forceinline__ void umask(CU& u, const uint4& v, uint64_t q, uint32_
   for (int d = 0; d < 4; ++d) c[d] = ucode_dw(u, w[d], d < 3 ? w[d + 1] : nx);
   // the code of the byte after the lane (only its first byte is used)
   const uint32_t cn = __builtin_amdgcn_update_dpp(ucode_b0(u, u.nx0), c[0], 0x130, 0xf, 0xf, false);
+  bool exact = !FAST;
+  if constexpr (FAST) exact = __ballot(((c[0] | c[1] | c[2] | c[3]) & 0x08080808u) != 0) != 0;
+  if (exact) {
 #pragma unroll
-  for (int d = 0; d < 4; ++d) c[d] = ucode_fix(u, c[d], w[d], d < 3 ? w[d + 1] : nx, d < 3 ? c[d + 1] : cn);
-  u.slow |= c[0] | c[1] | c[2] | c[3];
+    for (int d = 0; d < 4; ++d) u.slow |= c[d] & (c[d] << 3);  // bit 3: XU_SLOW
+#pragma unroll
+    for (int d = 0; d < 4; ++d) c[d] = ucode_fix<true>(u, c[d], w[d], d < 3 ? w[d + 1] : nx, d < 3 ? c[d + 1] : cn);
+  } else {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) c[d] = ucode_fix<false>(u, c[d], w[d], d < 3 ? w[d + 1] : nx, d < 3 ? c[d + 1] : cn);
+  }
   const uint32_t cp = __builtin_amdgcn_update_dpp(u.cprev, c[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
   u.cprev = __builtin_amdgcn_readlane(c[3], 63);
+  // (bit 3, a 4-byte token's fourth byte, is not needed: XU_SLOW hands the
+  // whole range to another kernel)
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t pv = d ? c[d - 1] : cp;
-    m[d] = (c[d] | __builtin_amdgcn_alignbit(c[d], pv, 25) | __builtin_amdgcn_alignbit(c[d], pv, 18) |
-            __builtin_amdgcn_alignbit(c[d], pv, 11)) & kOnes;
+    m[d] = (c[d] | __builtin_amdgcn_alignbit(c[d], pv, 25) | __builtin_amdgcn_alignbit(c[d], pv, 18)) & kOnes;
   }
 }
 
@@ -478,7 +496,7 @@ __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q,
   return;
 #endif
   uint32_t m[4];
-  umask<false>(u, v, q, m);
+  umask<false, true>(u, v, q, m);
   const uint32_t mp = __builtin_amdgcn_update_dpp(mprev, m[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
   mprev = __builtin_amdgcn_readlane(m[3], 63);
 #pragma unroll
@@ -549,9 +567,10 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
       uint32_t w = 0;
       for (uint32_t b = 0; b < 4; ++b) {
         const uint32_t a = 4 * i + b, x = a >> 8, y = (a & 0xffu) ^ ((x << 2) & 0xfcu);
-        const uint32_t e = x < 0x80   ? P.xu_tab[x]
-                           : x < 0xc0 ? P.xu_tab[kXuCls + y]
-                                      : P.xu_tab[256 + (x & 63) * 256 + y];
+        uint32_t e = x < 0x80   ? P.xu_tab[x]
+                     : x < 0xc0 ? P.xu_tab[kXuCls + y]
+                                : P.xu_tab[256 + (x & 63) * 256 + y];
+        if (e == XU_MIX) e = kUMix;
         w |= e << (8 * b);
       }
       utab[i] = w;

@@ -232,6 +232,19 @@ def find_all(pattern, data, start=0, offsets=True):
     return out
 
 
+def find_all_multi(pattern, data, ndev=0, start=0, offsets=True):
+    """ugpu_find_all_multi: as find_all, with [start, len) cut into ndev shards
+    at arbitrary offsets, shard k on device k mod the visible devices (ndev 0:
+    one per device), chains resolved across the cuts."""
+    ptr, n, keep = _buffer_ptr(data)
+    res = ctypes.POINTER(_lib.Result)()
+    check(lib.ugpu_find_all_multi(pattern.handle, ctypes.c_void_p(ptr), n, start,
+                                  _lib.MODE_OFFSETS if offsets else _lib.MODE_COUNT, ndev, ctypes.byref(res)))
+    out = _take_result(res, offsets)
+    del keep
+    return out
+
+
 class Stream:
     """Streaming FIND over input fed in chunks (ugpu_stream):
     feed() returns the matches that became final, with absolute offsets."""
