@@ -110,8 +110,20 @@ typedef struct ugpu_result
    lib/matcher.cpp:107, :142, :208, include/reflex/matcher.h:1194-1237); W scans
    run wfind_kernel on whole buffers (ugpu_find_all, ugpu_scan with the buffer
    start at dbuf[0]); ugpu_chain_fix and the stream API return UGPU_UNSUPPORTED
-   for W patterns. */
+   for W patterns.  UGPU_PAT_EMPTY: Matcher option N (ugrep -Y, and -x:
+   src/ugrep.cpp:8381-8386, :8612-8613), empty matches are reported
+   (lib/matcher.cpp:682-728; never at the end of the input).  Tables with line
+   anchors (META_BOL ^, META_EOL $ edges, include/reflex/pattern.h:942-943, as
+   ugrep -x makes, src/cnf.hpp:167-185) are accepted; other meta edges (word
+   boundaries, \A, \Z, indent) return UGPU_UNSUPPORTED.  Anchored tables, and
+   tables that match the empty string under option N, scan on the exact context
+   walk (wfind_kernel; its W rules replaced by the anchor rules): bol at a walk
+   start is "the byte before is '\n' or the position is the buffer begin"
+   (see ugpu_scanner_context for buffers that do not begin the input), eol is
+   "the next byte is '\n', EOF, or '\r' before '\n'".  W together with anchors
+   or empty matches returns UGPU_UNSUPPORTED. */
 #define UGPU_PAT_WORD 1u
+#define UGPU_PAT_EMPTY 2u
 int ugpu_dfa_create(const uint32_t *opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa **out);
 int ugpu_dfa_destroy(ugpu_dfa *dfa);
 int ugpu_dfa_info_get(const ugpu_dfa *dfa, ugpu_dfa_info *info);
@@ -165,6 +177,13 @@ int ugpu_tables_xc_host(const uint32_t *opc, uint32_t nop, uint8_t *cls, int *ok
    lib/matcher.cpp:460-545.) */
 int ugpu_tables_xu_host(const uint32_t *opc, uint32_t nop, uint8_t *tab, uint32_t *bm3, int *ok);
 
+/* Host-only: the per-context accept indices of the dense tables (states * 4
+   u32: acap[state * 4 + bol * 2 + eol], state numbering as
+   ugpu_tables_build_host), whether the table has line anchors, and whether its
+   start state accepts in some context (empty matches). */
+int ugpu_tables_context_host(const uint32_t *opc, uint32_t nop, uint32_t *acap, uint32_t acap_cap, int *anchored,
+                             int *start_acc);
+
 /* Host-only: *eq = 1 when two opcode tables accept the same strings with the
    same accept indices (so their FIND chains agree on every input).  The
    engine uses it to recognise \w+ under option W. */
@@ -207,6 +226,11 @@ int ugpu_scanner_destroy(ugpu_scanner *sc);
    Asynchronous: results are read with ugpu_scan_totals. */
 int ugpu_scan(ugpu_scanner *sc, const uint8_t *dbuf, uint64_t lo, uint64_t hi, uint64_t read_end, int at_eof,
               uint64_t bias, void *stream);
+/* Context of the scanner's next scans: bol0 != 0 when dbuf[0] begins a line
+   (it is the first byte of the input, or the byte before it is '\n'); the
+   default is 1.  Only line-anchored tables read it (a shard or stream window
+   that starts inside the input sets it from the byte before). */
+int ugpu_scanner_context(ugpu_scanner *sc, int bol0);
 /* Synchronize the scanner's stream and return the totals of the last scan. */
 int ugpu_scan_totals(ugpu_scanner *sc, ugpu_totals *out);
 /* After ugpu_scan + ugpu_scan_totals: write the match records of the last scan

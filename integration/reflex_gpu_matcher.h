@@ -49,15 +49,26 @@
 //     exist: host buffers cross PCIe at ~55 GB/s, which a few reference AVX2
 //     cores match on such patterns (11 GB/s each), while dense patterns (C3/C4
 //     class, ~0.2-2 GB/s per core) always gain.  UGPU_ADAPTER_STATS=1 prints each
-// matcher's GPU scan count to stderr when it is destroyed.  Everything else --
-// SCAN/SPLIT/MATCH, options A/N, option W on streams, tables the engine rejects
-// (anchors, \b, lookahead: UGPU_UNSUPPORTED) -- stays on the CPU matcher.
+// matcher's GPU scan count to stderr when it is destroyed.
+//
+// Option N (ugrep -Y, and -x / patterns that start with ^ or end with $, which
+// turn it on: src/ugrep.cpp:8381-8386, src/cnf.hpp:201-206) runs on the GPU
+// (UGPU_PAT_EMPTY), and so do line anchors when N is on and they are only a
+// leading ^ and/or a trailing $ of the whole regex (anchors_outer).  Other
+// anchored tables stay on the CPU: there the reference's match predictor
+// (lib/pattern.cpp:4342-4430) can skip positions its DFA matches at -- ugrep -c
+// 'a$|ab' prints 0 on "xa\nb\nzzzz\n", and '^\w+' without N finds nothing --
+// and the GPU walks the DFA (tests/test_anchor.py records both).  Everything
+// else -- SCAN/SPLIT/MATCH, option A, option W on streams, tables the engine
+// rejects (\b, lookahead, W with anchors or N: UGPU_UNSUPPORTED) -- stays on the
+// CPU matcher.
 #ifndef REFLEX_GPU_MATCHER_H
 #define REFLEX_GPU_MATCHER_H
 
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <memory>
 #include <string>
 
@@ -83,7 +94,8 @@ class GpuMatcher : public Matcher {
   /// Clones (ugrep's worker threads, src/ugrep.cpp:4146, :9006) share the
   /// device tables; per-input state starts empty.
   GpuMatcher(const GpuMatcher& m)
-      : Matcher(m), tab_(m.tab_), tab_pat_(m.tab_pat_), tab_w_(m.tab_w_), sparse_(m.sparse_),
+      : Matcher(m), tab_(m.tab_), tab_pat_(m.tab_pat_), tab_w_(m.tab_w_), tab_n_(m.tab_n_),
+        tab_anchor_(m.tab_anchor_), sparse_(m.sparse_),
         min_bytes_(m.min_bytes_), chunk_(m.chunk_), sparse_max_(m.sparse_max_)
   {
     ++live();
@@ -143,10 +155,8 @@ class GpuMatcher : public Matcher {
       return cpu(method, R_METHOD);
     if (opt_.A)
       return cpu(method, R_OPT_A);
-    if (opt_.N)
-      return cpu(method, R_OPT_N);
     if (tables() == NULL)
-      return cpu(method, R_TABLE);
+      return cpu(method, tab_anchor_ ? R_ANCHOR : R_TABLE);
     if (sparse_ && live() > sparse_max_)
       return cpu(method, R_SPARSE);
     if (own_)
@@ -178,11 +188,11 @@ class GpuMatcher : public Matcher {
 
  private:
   // why the CPU matcher answered a call (adapter statistics)
-  enum Reason { R_METHOD, R_OPT_A, R_OPT_N, R_TABLE, R_SPARSE, R_PARTIAL, R_SMALL, R_ENGINE, R_W_STREAM, kReasons };
+  enum Reason { R_METHOD, R_OPT_A, R_ANCHOR, R_TABLE, R_SPARSE, R_PARTIAL, R_SMALL, R_ENGINE, R_W_STREAM, kReasons };
   static const char* reason_name(int r)
   {
-    static const char* const n[kReasons] = {"method", "option_A", "option_N", "table",         "sparse_limit",
-                                            "partial", "small",    "engine",   "option_W_stream"};
+    static const char* const n[kReasons] = {"method", "option_A", "anchor_predictor", "table",         "sparse_limit",
+                                            "partial", "small",    "engine",           "option_W_stream"};
     return n[r];
   }
   size_t cpu(Method method, int why)
@@ -190,15 +200,18 @@ class GpuMatcher : public Matcher {
     ++cpu_why_[why];
     return Matcher::match(method);
   }
-  // device tables of (pattern, option W), shared with clones; NULL when the
-  // engine does not support the pattern
+  // device tables of (pattern, option W, option N), shared with clones; NULL
+  // when the engine does not support the pattern or its anchors are left to the
+  // reference's predictor (tab_anchor_)
   const ugpu_dfa* tables()
   {
-    if (!tab_pat_ || tab_pat_ != pat_ || tab_w_ != opt_.W)
+    if (!tab_pat_ || tab_pat_ != pat_ || tab_w_ != opt_.W || tab_n_ != opt_.N)
     {
       tab_.reset();
       tab_pat_ = pat_;
       tab_w_ = opt_.W;
+      tab_n_ = opt_.N;
+      tab_anchor_ = false;
       if (pat_ != NULL)
       {
         const std::string rx = (*pat_)[0];
@@ -207,10 +220,23 @@ class GpuMatcher : public Matcher {
         ugpu_dfa* d = NULL;
         if (ugpu_compile(rx.data(), rx.size(), UGPU_RX_REFLEX, &opc, &nop) == UGPU_OK)
         {
-          if (ugpu_dfa_create(opc, nop, opt_.W ? UGPU_PAT_WORD : 0u, &d) != UGPU_OK)
+          int anchored = 0;
+          if (ugpu_tables_context_host(opc, nop, NULL, 0, &anchored, NULL) == UGPU_OK && anchored &&
+              !(opt_.N && anchors_outer(rx)))
+            tab_anchor_ = true;
+          else if (ugpu_dfa_create(opc, nop, (opt_.W ? UGPU_PAT_WORD : 0u) | (opt_.N ? UGPU_PAT_EMPTY : 0u), &d) !=
+                   UGPU_OK)
             d = NULL;
           ugpu_opc_free(opc);
         }
+        if (tab_anchor_)
+          tab_err_ = "line anchors without option N or inside the regex (the reference's predictor decides there)";
+        else if (d == NULL)
+          tab_err_ = ugpu_last_error();
+        const char* dump = std::getenv("UGPU_ADAPTER_DUMP");
+        if (dump != NULL && *dump == '1')
+          std::fprintf(stderr, "[ugpu-adapter] regex=%s tables=%s%s\n", rx.c_str(), d ? "gpu" : "unsupported: ",
+                       d ? "" : tab_err_.c_str());
         if (d != NULL)
         {
           tab_.reset(d, ugpu_dfa_destroy);
@@ -221,6 +247,55 @@ class GpuMatcher : public Matcher {
       }
     }
     return tab_.get();
+  }
+  // the regex's line anchors are at most a leading ^ (after the (?m...) prefix
+  // ugrep puts first, src/ugrep.cpp:8586-8604) and a trailing $: ^ and $ in
+  // bracket expressions, escaped or inside \Q...\E are literals
+  static bool anchors_outer(const std::string& rx)
+  {
+    size_t i = 0;
+    const size_t n = rx.size();
+    while (i + 1 < n && rx[i] == '(' && rx[i + 1] == '?')
+    {
+      size_t q = i + 2;
+      while (q < n && std::strchr("imsx-", rx[q]) != NULL)
+        ++q;
+      if (q >= n || rx[q] != ')')
+        break;
+      i = q + 1;
+    }
+    const size_t first = i;
+    while (i < n)
+    {
+      const char c = rx[i];
+      if (c == '\\')
+      {
+        if (i + 1 < n && rx[i + 1] == 'Q')
+        {
+          const size_t e = rx.find("\\E", i + 2);
+          i = e == std::string::npos ? n : e + 2;
+        }
+        else
+          i += 2;
+        continue;
+      }
+      if (c == '[')
+      {
+        size_t j = i + 1;
+        if (j < n && rx[j] == '^')
+          ++j;
+        if (j < n && rx[j] == ']')
+          ++j;
+        while (j < n && rx[j] != ']')
+          j += rx[j] == '\\' ? 2 : 1;
+        i = j + 1;
+        continue;
+      }
+      if ((c == '^' && i != first) || (c == '$' && i + 1 != n))
+        return false;
+      ++i;
+    }
+    return true;
   }
   // smallest input for the GPU: measured crossover against one reference
   // matcher on a host buffer (profiles/r02_adapter_latency.jsonl): 4 MiB for
@@ -246,7 +321,9 @@ class GpuMatcher : public Matcher {
     txt_ = buf_ + start;
     len_ = len;
     cap_ = cap;
-    set_current(start + len);
+    // an empty match (option N) leaves the cursor one past it, as
+    // lib/matcher.cpp:715-719 does ("advance one char ... when we return")
+    set_current(start + len + (len == 0 && start < end_ ? 1 : 0));
     gcur_ = cur_;
     return cap_;
   }
@@ -429,7 +506,8 @@ class GpuMatcher : public Matcher {
 
   std::shared_ptr<ugpu_dfa> tab_;
   const Pattern* tab_pat_ = NULL;
-  bool tab_w_ = false;
+  bool tab_w_ = false, tab_n_ = false;
+  bool tab_anchor_ = false;  // anchored table left to the CPU matcher (see anchors_outer)
   bool sparse_ = false;  // the table has a selective prefilter (sparse_kernel)
   ugpu_result* gres_ = NULL;
   const char* gbuf_ = NULL;
@@ -441,6 +519,7 @@ class GpuMatcher : public Matcher {
   uint64_t sbase_ = 0, sfed_ = 0, gcur_abs_ = 0;
   bool sdone_ = false, cpu_stream_ = false;
   int cpu_stream_why_ = R_ENGINE;
+  std::string tab_err_;  // why the engine rejected the table (ugpu_last_error)
   size_t gpu_finds_ = 0;
   size_t cpu_why_[kReasons] = {};
 };

@@ -125,14 +125,50 @@ struct Tally
   uint64_t count = 0, digest = 0, dcap = 0;
 };
 
-// matcher options (mode suffix "W" = ugrep -w: Matcher option W, src/ugrep.cpp:8616-8618)
+// matcher options (mode suffixes "W" = ugrep -w: option W, src/ugrep.cpp:8616-8618; "N" = ugrep -Y / -x: option N, :8612-8613)
 static std::string g_matcher_opt;
+// mode suffix "P": the same Matcher with its match predictor switched off.
+// FIND normally jumps between candidate positions the Pattern's predictor
+// (bitap/hash tables, lib/pattern.cpp:4342-4430, lib/matcher.cpp:797-950)
+// accepts; with "P" every position is a candidate, which leaves the DFA's own
+// semantics (lib/matcher.cpp:125-546).  The two differ where the predictor
+// rejects a position at which the DFA matches through a meta edge (e.g.
+// "a$|ab" before "\n" followed by more text, or "^\w+" without option N):
+// tests/golden/make_anchor_golden.py records both.
+static bool g_no_predict = false;
+
+struct Unpredicted : public reflex::Matcher {
+  Unpredicted(const reflex::Pattern& pat, const char *opt) : reflex::Matcher(pat, reflex::Input(), opt) { }
+  bool advance_each(size_t loc)
+  {
+    if (loc >= end_)
+    {
+      set_current(end_);
+      return false;
+    }
+    set_current(loc);
+    return true;
+  }
+  void unpredict()
+  {
+    adv_ = static_cast<bool (reflex::Matcher::*)(size_t)>(&Unpredicted::advance_each);
+  }
+};
 
 static Tally scan(const reflex::Pattern& pat, char *base, size_t n, size_t bias, std::vector<uint64_t> *list)
 {
   Tally t;
-  reflex::Matcher m(pat, reflex::Input(), g_matcher_opt.empty() ? NULL : g_matcher_opt.c_str());
+  Unpredicted m(pat, g_matcher_opt.empty() ? NULL : g_matcher_opt.c_str());
   m.buffer(base, n + 1);
+  if (g_no_predict)
+  {
+    if (pat.one_)
+    {
+      fprintf(stderr, "mode P: single-string pattern, nothing to switch off\n");
+      exit(2);
+    }
+    m.unpredict();
+  }
   while (size_t cap = m.find())
   {
     uint64_t st = m.first() + bias;
@@ -174,9 +210,14 @@ int main(int argc, char **argv)
     return 0;
   }
   std::string cmd = argv[1], mode = argv[2], rx = argv[3];
-  if (mode.size() > 1 && mode[mode.size() - 1] == 'W')
+  // mode suffixes: W = Matcher option W (ugrep -w), N = option N (ugrep -Y, and -x)
+  // P = predictor off (see Unpredicted above)
+  while (mode.size() > 1 && (mode[mode.size() - 1] == 'W' || mode[mode.size() - 1] == 'N' || mode[mode.size() - 1] == 'P'))
   {
-    g_matcher_opt = "W";
+    if (mode[mode.size() - 1] == 'P')
+      g_no_predict = true;
+    else
+      g_matcher_opt.push_back(mode[mode.size() - 1]);
     mode.erase(mode.size() - 1);
   }
   std::string conv = build_regex(mode, rx);

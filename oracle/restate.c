@@ -16,14 +16,21 @@
  *     include/reflex/pattern.h:1155-1247 (GOTO lo<<24|hi<<16|idx, HALT
  *     0x00FFFFFF, LONG idx 0xFFFE + next word, TAKE 0xFE..).  TAKE at the head
  *     of a block (lib/pattern.cpp:2945-2952) makes the state accepting.
- *     REDO/TAIL/HEAD and meta edges are rejected (ORC_UNSUPPORTED).
+ *     REDO/TAIL/HEAD and meta edges other than META_BOL / META_EOL are
+ *     rejected (ORC_UNSUPPORTED); BOL/EOL edges are kept per state in block
+ *     order (orc_find_a).
  *   orc_find -- the FIND driver of Matcher::match (lib/matcher.cpp:42-750) for
  *     tables without meta/lookahead, options A/N/W off: from p walk the DFA,
  *     remember the last TAKE (:139-150, :207-217), stop on HALT/EOF (:448-459,
  *     :528-541); emit the longest non-empty match and resume at its end
  *     (:681, :735-737), otherwise retry at p+1 (:635-661, :692-713).  The adv_
  *     prefilters (lib/matcher.cpp:797-954, lib/matcher_avx2.cpp) only skip
- *     positions that cannot start a match and are not restated.
+ *     positions that cannot start a match and are not restated -- except for
+ *     tables with meta edges, where the Pattern's predictor can also reject
+ *     positions the DFA matches at (anchored patterns without option N, "a$|ab";
+ *     oracle/ref_harness.cpp mode "P", tests/golden/make_anchor_golden.py):
+ *     orc_find_a restates the DFA semantics (the reference with its predictor
+ *     off), and the golden fixtures record both.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -36,12 +43,15 @@
 #define ORC_INVAL 2
 #define ORC_NOMEM 3
 
+#define ORC_MAXMETA 4
 typedef struct orc_dfa
 {
   uint32_t nstates; /* including dead state 0 */
   uint32_t start;
   uint32_t *next;   /* [nstates][256] */
   uint32_t *accept; /* [nstates], 0 = not accepting */
+  uint32_t *meta;   /* [nstates][ORC_MAXMETA]: (META - META_MIN) << 24 | target state, in block order; 0 = none */
+  int anchored;     /* some state has a meta edge */
 } orc_dfa;
 
 static int is_goto(uint32_t w) { return (uint32_t)(w << 8) >= (w & 0xff000000u); }
@@ -53,6 +63,7 @@ void orc_dfa_free(orc_dfa *d)
     return;
   free(d->next);
   free(d->accept);
+  free(d->meta);
   free(d);
 }
 
@@ -70,7 +81,8 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
     goto nomem;
   d->next = (uint32_t *)calloc((size_t)cap * 256, sizeof(uint32_t));
   d->accept = (uint32_t *)calloc(cap, sizeof(uint32_t));
-  if (!d->next || !d->accept)
+  d->meta = (uint32_t *)calloc((size_t)cap * ORC_MAXMETA, sizeof(uint32_t));
+  if (!d->next || !d->accept || !d->meta)
     goto nomem;
   id[0] = ns++;
   queue[nq++] = 0;
@@ -93,19 +105,47 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
       if (!na)
         goto nomem;
       d->accept = na;
+      {
+        uint32_t *nm = (uint32_t *)realloc(d->meta, (size_t)ncap * ORC_MAXMETA * sizeof(uint32_t));
+        if (!nm)
+          goto nomem;
+        d->meta = nm;
+        memset(d->meta + (size_t)cap * ORC_MAXMETA, 0, (size_t)(ncap - cap) * ORC_MAXMETA * sizeof(uint32_t));
+      }
       memset(d->next + (size_t)cap * 256, 0, (size_t)(ncap - cap) * 256 * sizeof(uint32_t));
       memset(d->accept + cap, 0, (ncap - cap) * sizeof(uint32_t));
       cap = ncap;
     }
-    /* block header: [REDO|TAKE]? TAIL* HEAD* */
-    while (g < nop && !is_goto(opc[g]))
+    /* block header: [REDO|TAKE]? TAIL* HEAD*, then meta edges (not goto
+       words: the interpreter tests them in block order before the byte edges,
+       lib/matcher.cpp:193-450); only META_BOL (0x109) and META_EOL (0x10a),
+       include/reflex/pattern.h:942-943 */
     {
-      uint32_t op = opc[g] >> 24;
-      if (op == 0xfe)
-        d->accept[s] = opc[g] & 0xffffff;
-      else
-        goto unsupported; /* REDO, TAIL, HEAD, indent metas */
-      ++g;
+      uint32_t nm = 0;
+      while (g < nop && !is_goto(opc[g]))
+      {
+        uint32_t w = opc[g], op = w >> 24;
+        if (op == 0xfe)
+          d->accept[s] = w & 0xffffff;
+        else if (is_meta(w) && (op == 0x09 || op == 0x0a) && nm < ORC_MAXMETA)
+        {
+          uint32_t idx = w & 0xffff, tgt = idx == 0xfffe ? (g + 1 < nop ? opc[g + 1] & 0xffffff : nop) : idx;
+          if (idx == 0xffff || tgt >= nop)
+            goto inval;
+          if (id[tgt] == 0)
+          {
+            id[tgt] = ns++;
+            queue[nq++] = tgt;
+          }
+          d->meta[(size_t)s * ORC_MAXMETA + nm++] = op << 24 | id[tgt];
+          d->anchored = 1;
+          if (idx == 0xfffe)
+            ++g;
+        }
+        else
+          goto unsupported; /* REDO, TAIL, HEAD, other metas */
+        ++g;
+      }
     }
     if (g >= nop)
       goto inval;
@@ -154,6 +194,24 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
     }
   }
   d->nstates = ns;
+  /* a meta edge whose target consumes bytes: the interpreter then tries the
+     target's byte edges on the next byte first and falls back to the state's
+     own through its backtrack point (lib/matcher.cpp:405-423, :513-523) -- two
+     walks at once, outside this restatement's (and the engine's) one-state
+     model.  Targets without byte edges only contribute accepts. */
+  {
+    uint32_t s, k, b;
+    for (s = 1; s < ns; ++s)
+      for (k = 0; k < ORC_MAXMETA; ++k)
+      {
+        uint32_t e = d->meta[(size_t)s * ORC_MAXMETA + k], t = e & 0xffffff;
+        if (e == 0)
+          break;
+        for (b = 0; b < 256; ++b)
+          if (d->next[(size_t)t * 256 + b] != 0)
+            goto unsupported;
+      }
+  }
   free(id);
   free(queue);
   *out = d;
@@ -380,6 +438,100 @@ uint64_t orc_find_w(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t s
     }
     else
       ++p;
+  }
+  if (digest)
+    *digest = dg;
+  if (dcap)
+    *dcap = dc;
+  return cnt;
+}
+
+/* ---- line anchors (META_BOL ^, META_EOL $) and option N (empty matches) ----
+ * The interpreter (lib/matcher.cpp:42-750) fixes `bol` at the walk start
+ * (:93, at_bol(): the byte before is '\n', or the position is the buffer
+ * begin, where got_ is '\n' under WITH_SPAN, include/reflex/absmatcher.h:1571-1580)
+ * and, at each state, fetches the next byte ch and tests the state's meta edges
+ * in block order (:294-316): META_BOL holds when bol, META_EOL when ch is
+ * '\n', EOF, or '\r' followed by '\n'.  The first edge that holds is followed
+ * without consuming ch (at most 5 in a row); a TAKE met there is an accept at
+ * the current position (:207-217); then the walk goes on with the byte edges
+ * (the backtrack point, :405-440).  Empty matches (:682-728): without option N
+ * the search moves to p+1; with N the empty match is reported and the search
+ * moves to p+1, except at the end of the input. */
+static uint32_t orc_accept_at(const orc_dfa *d, uint32_t s, int bol, const uint8_t *buf, uint64_t n, uint64_t q)
+{
+  uint32_t cap = d->accept[s];
+  int eol = q >= n || buf[q] == '\n' || (buf[q] == '\r' && q + 1 < n && buf[q + 1] == '\n');
+  int jumps;
+  for (jumps = 0; jumps < 5; ++jumps)
+  {
+    uint32_t t = 0, k;
+    for (k = 0; k < ORC_MAXMETA; ++k)
+    {
+      uint32_t e = d->meta[(size_t)s * ORC_MAXMETA + k], m = e >> 24;
+      if (e == 0)
+        break;
+      if ((m == 0x09 && bol) || (m == 0x0a && eol))
+      {
+        t = e & 0xffffff;
+        break;
+      }
+    }
+    if (t == 0)
+      break;
+    if (d->accept[t])
+      cap = d->accept[t];
+    s = t;
+  }
+  return cap;
+}
+
+int orc_dfa_anchored(const orc_dfa *d) { return d->anchored; }
+
+/* orc_find for tables with ^ / $ edges, with option N (nul) on or off; the
+   buffer begin (position 0) is a begin of line */
+uint64_t orc_find_a(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t start, int nul, uint64_t *digest,
+                    uint64_t *dcap, uint64_t *list, uint64_t list_cap)
+{
+  uint64_t p = start, cnt = 0, dg = 0, dc = 0;
+  while (p < n)
+  {
+    int bol = p == 0 || buf[p - 1] == '\n';
+    uint32_t s = d->start, a = 0, c;
+    uint64_t q = p, last = p;
+    int hit = 0;
+    if ((c = orc_accept_at(d, s, bol, buf, n, q)) != 0)
+    {
+      hit = 1;
+      a = c;
+    }
+    while (q < n)
+    {
+      uint32_t t = d->next[(size_t)s * 256 + buf[q]];
+      if (t == 0)
+        break;
+      s = t;
+      ++q;
+      if ((c = orc_accept_at(d, s, bol, buf, n, q)) != 0)
+      {
+        hit = 1;
+        last = q;
+        a = c;
+      }
+    }
+    if (hit && (last > p || nul))
+    {
+      if (list && cnt < list_cap)
+      {
+        list[3 * cnt] = p;
+        list[3 * cnt + 1] = last - p;
+        list[3 * cnt + 2] = a;
+      }
+      ++cnt;
+      dg += p * 31 + (last - p);
+      dc += (p + 1) * a;
+    }
+    p = last > p ? last : p + 1;
   }
   if (digest)
     *digest = dg;

@@ -32,6 +32,10 @@ def _load():
     L.orc_find_mt.restype = U64
     L.orc_find_w.argtypes = [V, V, U64, U64, P64, P64, V, U64]
     L.orc_find_w.restype = U64
+    L.orc_find_a.argtypes = [V, V, U64, U64, ctypes.c_int, P64, P64, V, U64]
+    L.orc_find_a.restype = U64
+    L.orc_dfa_anchored.argtypes = [V]
+    L.orc_dfa_anchored.restype = ctypes.c_int
     L.orc_chain_exit.argtypes = [V, V, U64, U64, U64]
     L.orc_chain_exit.restype = U64
     L.orc_gen.argtypes = [ctypes.c_int, U64, U64, V, U64]
@@ -61,8 +65,25 @@ class OracleDfa:
     def nstates(self):
         return L.orc_dfa_nstates(self.h)
 
-    def find(self, data, start=0, bias=0, want_list=False):
+    @property
+    def anchored(self):
+        return bool(L.orc_dfa_anchored(self.h))
+
+    def find(self, data, start=0, bias=0, want_list=False, nul=False):
+        """FIND over data[start:] (orc_find; orc_find_a for tables with ^/$
+        edges or with option N, nul=True): (count, digest, dcap, list|None)."""
         buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+        if nul or self.anchored:
+            assert bias == 0
+            dg, dc = ctypes.c_uint64(), ctypes.c_uint64()
+            cnt = L.orc_find_a(self.h, buf.ctypes.data, buf.size, start, int(nul), ctypes.byref(dg), ctypes.byref(dc),
+                               None, 0)
+            lst = None
+            if want_list:
+                arr = np.zeros(3 * max(cnt, 1), np.uint64)
+                L.orc_find_a(self.h, buf.ctypes.data, buf.size, start, int(nul), None, None, arr.ctypes.data, cnt)
+                lst = arr[:3 * cnt].reshape(-1, 3).tolist()
+            return cnt, dg.value, dc.value, lst
         dg, dc = ctypes.c_uint64(), ctypes.c_uint64()
         cnt = L.orc_find(self.h, buf.ctypes.data, buf.size, start, bias, ctypes.byref(dg), ctypes.byref(dc), None, 0)
         lst = None

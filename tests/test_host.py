@@ -10,7 +10,10 @@ import ugrep_amd
 from ugrep_amd import _lib
 from oracle_lib import case_input
 
-UNSUPPORTED = {"anchor_bol", "anchor_eol", "word_boundary", "lookahead"}
+# line anchors (anchor_bol, anchor_eol) are supported since round 3: per-context
+# accepts, tests/test_anchor.py; word boundaries and lookahead are not
+UNSUPPORTED = {"word_boundary", "lookahead"}
+ANCHORED = {"anchor_bol", "anchor_eol"}
 
 
 def test_exports_every_declared_symbol():
@@ -28,6 +31,8 @@ def test_unsupported_patterns(patterns):
                 ugrep_amd.host_tables(p["opc"])
         else:
             ugrep_amd.host_tables(p["opc"])
+            from ugrep_amd.matcher import host_context
+            assert host_context(p["opc"])[1] == (name in ANCHORED), name
 
 
 def test_malformed_table_rejected():
@@ -78,8 +83,8 @@ def _py_find(t, data):
 def test_host_tables_reproduce_reference_matches(patterns, cases):
     done = 0
     for c in cases:
-        if c["input"]["type"] != "hex" or c["pattern"] in UNSUPPORTED:
-            continue
+        if c["input"]["type"] != "hex" or c["pattern"] in UNSUPPORTED | ANCHORED:
+            continue  # (anchored tables: the context walk of tests/test_anchor.py)
         t = ugrep_amd.host_tables(patterns[c["pattern"]]["opc"])
         data = case_input(c["input"]).tolist()
         assert _py_find(t, data) == c["matches"], (c["pattern"], c["input"]["name"])

@@ -69,7 +69,7 @@ def test_multi_records_equal_single_device(U, patterns):
             for ndev in (2, 5, 16):
                 r = U.find_all_multi(pat, host, ndev=ndev, start=start, offsets=True)
                 assert (r.count, r.digest, r.dcap) == (one.count, one.digest, one.dcap), (pname, ndev, start)
-                assert np.array_equal(r.start, one.start) and np.array_equal(r.len, one.len), (pname, ndev)
+                assert np.array_equal(r.start, one.start) and np.array_equal(r.length, one.length), (pname, ndev)
                 assert np.array_equal(r.cap, one.cap), (pname, ndev)
 
 

@@ -9,13 +9,15 @@ import pytest
 
 from oracle_lib import OracleDfa, case_input, gen
 
-UNSUPPORTED = {"anchor_bol", "anchor_eol", "word_boundary", "lookahead"}
+UNSUPPORTED = {"word_boundary", "lookahead"}
+ANCHORED = {"anchor_bol", "anchor_eol"}  # restated by orc_find_a (tests/test_anchor.py)
 
 
 def test_unsupported_tables_rejected(patterns):
     for name, p in patterns.items():
         d = OracleDfa(p["opc"])
         assert d.supported == (name not in UNSUPPORTED), name
+        assert d.supported is False or d.anchored == (name in ANCHORED), name
 
 
 def test_refgold_hello_offsets(patterns, refgold):
@@ -38,7 +40,7 @@ def test_c1_anchor_64mib(patterns):
 def test_small_cases_full_lists(patterns, cases):
     n = 0
     for c in cases:
-        if c.get("big") or c["pattern"] in UNSUPPORTED:
+        if c.get("big") or c["pattern"] in UNSUPPORTED | ANCHORED:
             continue
         d = OracleDfa(patterns[c["pattern"]]["opc"])
         data = case_input(c["input"])

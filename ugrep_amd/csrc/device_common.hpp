@@ -28,11 +28,41 @@ struct Win {
   const uint8_t* g;
   uint64_t rend;
   uint32_t eof;
-  // option W only (walk<FMT, true>): Word ranges and the buffer's first byte
+  // option W only (walk<FMT, 1>): Word ranges and the buffer's first byte
   const uint32_t* wtab = nullptr;
   uint32_t nwtab = 0;
   uint64_t bob = 0;
+  // line anchors / option N only (walk<FMT, 2>): per-context accept indices
+  // (tables.hpp acap), the row shift of the table's entries, whether position
+  // bob starts a line, option N
+  const uint32_t* acap = nullptr;
+  uint32_t log_row = 0;
+  uint32_t bol0 = 1;
+  uint32_t nul = 0;
 };
+
+// Walk modes (template argument W of walk / chain_step / merge)
+constexpr int kWalkPlain = 0, kWalkWord = 1, kWalkCtx = 2;
+
+// The window of a scan: bytes from global memory, W / anchor context from P.
+__device__ __forceinline__ Win win_of(const ScanParams& P)
+{
+  Win w;
+  w.lds = nullptr;
+  w.base = 0;
+  w.lend = 0;
+  w.g = P.g;
+  w.rend = P.rend;
+  w.eof = P.at_eof;
+  w.wtab = P.wtab;
+  w.nwtab = P.nwtab;
+  w.bob = P.bob;
+  w.acap = P.acap;
+  w.log_row = P.log_row;
+  w.bol0 = P.bol0;
+  w.nul = P.nul;
+  return w;
+}
 
 // ---------------------------------------------------------------- option W
 // Matcher option W (ugrep -w): a walk starts only where at_wb() holds and a
@@ -108,17 +138,72 @@ __device__ __forceinline__ bool at_we(const Win& w, uint64_t q, uint32_t& ovf)
   return !walnum(c);
 }
 
+// ---------------------------------------------------------------- anchors
+// Line anchors (META_BOL `^`, META_EOL `$`) and option N.  The reference fixes
+// `bol` at the walk start (lib/matcher.cpp:93: at_bol(), the byte before is
+// '\n' or the position is the buffer begin) and tests `$` on the byte after
+// the current position (:294-316: '\n', EOF, or '\r' before '\n'); the
+// accept at a state is tables.hpp acap[sid * 4 + bol * 2 + eol].
+// eol at q (q at the end of the stream: EOF; at a readable end that is not
+// EOF the answer depends on bytes not read yet: ovf)
+__device__ __forceinline__ uint32_t at_eol(const Win& w, uint64_t q, uint32_t& ovf)
+{
+  if (q >= w.rend) {
+    if (!w.eof) ovf = 1;
+    return 1u;
+  }
+  const uint32_t c = w.g[q];
+  if (c == '\n') return 1u;
+  if (c != '\r') return 0u;
+  if (q + 1 >= w.rend) {
+    if (!w.eof) ovf = 1;
+    return 0u;
+  }
+  return w.g[q + 1] == '\n' ? 1u : 0u;
+}
+
+// accept at q in the state of entry e: the acap index (0 = none; index 0..3
+// is the dead state, which never accepts)
+__device__ __forceinline__ uint32_t ctx_accept(const Win& w, uint32_t e, uint32_t bol, uint64_t q, uint32_t& ovf)
+{
+  const uint32_t b = ((e >> w.log_row) << 2) | (bol << 1);
+  const uint32_t a0 = w.acap[b], a1 = w.acap[b + 1];
+  if (a0 == a1) return a0 ? b : 0u;
+  const uint32_t k = b + at_eol(w, q, ovf);
+  return w.acap[k] ? k : 0u;
+}
+
 // Longest match starting at p (0 = none).  `le` = entry of the last accepting
 // state (its row identifies the accept index).  Mirrors the reference walk:
 // TAKE on entering an accepting state (lib/matcher.cpp:207-217), stop on HALT
-// (:528-541) or EOF (:460-465).
-template <int FMT, bool W = false>
+// (:528-541) or EOF (:460-465).  Mode kWalkCtx: `le` = the acap index of the
+// last accept (also for an empty match at p: then le != 0 and 0 is returned).
+template <int FMT, int W = kWalkPlain>
 __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64_t p, uint32_t& le, uint32_t& ovf)
 {
   uint32_t s = T.start;
   uint64_t q = p, last = p;
   le = 0;
-  if constexpr (W) {
+  if constexpr (W == kWalkCtx) {
+    const uint32_t bol = p <= w.bob ? w.bol0 : (w.g[p - 1] == '\n' ? 1u : 0u);
+    le = ctx_accept(w, s, bol, q, ovf);
+    while (q < w.rend) {
+      const uint32_t e = T.step(s, w.g[q]);
+      if (e == 0) return last - p;
+      s = e;
+      ++q;
+      if (e >= T.accb) {
+        const uint32_t a = ctx_accept(w, e, bol, q, ovf);
+        if (a) {
+          last = q;
+          le = a;
+        }
+      }
+    }
+    if (!w.eof) ovf = 1;
+    return last - p;
+  }
+  if constexpr (W == kWalkWord) {
     if (!at_wb(w, p)) return 0;
     while (q < w.rend) {
       const uint32_t e = T.step(s, w.g[q]);
@@ -205,7 +290,9 @@ struct WriteEm {
 
 // One step of the FIND chain from p: the longest match at p (emitted with
 // `sign`, then the chain continues at its end) or p+1.
-template <int FMT, class Em, bool W = false>
+// Mode kWalkCtx with option N: an empty match at p is reported (the chain
+// still moves to p+1, lib/matcher.cpp:682-728).
+template <int FMT, class Em, int W = kWalkPlain>
 __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t p, Em& em,
                                                int sign, uint32_t& ovf)
 {
@@ -215,6 +302,9 @@ __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, 
     em.put(c, p, len, le, sign);
     return p + len;
   }
+  if constexpr (W == kWalkCtx) {
+    if (le && w.nul) em.put(c, p, 0, le, sign);
+  }
   return p + 1;
 }
 
@@ -222,7 +312,7 @@ __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, 
 // Returns true if the chains met (exit unchanged), else sets nexit.  A merge
 // whose chains cross more than `budget` bytes without meeting sets `over` and
 // stops (the result is then invalid: UGPU_FLAG_BUDGET).
-template <int FMT, bool W = false>
+template <int FMT, int W = kWalkPlain>
 __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t xo, uint64_t xn,
                                       uint64_t e, CountEm& em, uint64_t& nexit, uint32_t& ovf,
                                       uint64_t budget = ~0ull, uint32_t* over = nullptr)

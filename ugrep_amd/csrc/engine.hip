@@ -80,6 +80,11 @@ struct ugpu_dfa {
   // option W on a two-state table whose X is the ASCII word bytes: xc_kernel
   // applies the W rules itself (non-ASCII input falls back to wfind_kernel)
   bool xcw = false;
+  // line anchors / option N (UGPU_PAT_EMPTY): amode = the table has anchors,
+  // or matches the empty string under N; its scans run the context walk
+  // (wfind_kernel, device_common.hpp kWalkCtx) on the per-context accepts
+  bool nul = false, amode = false;
+  uint32_t* d_acap = nullptr;
   // idle scanners of ugpu_find_all calls on this table (reused: creating one
   // costs device allocations and property queries)
   std::mutex pool_mu;
@@ -106,6 +111,7 @@ struct ugpu_scanner {
   bool wfast = false;    // option W on a \w+ table: non-W kernels when the scanned bytes are valid UTF-8
   int word_rec = 0;      // chain records of a wfind scan
   bool wxc = false;      // option W on xc_kernel (dfa->xcw), wfind_kernel when it flags UGPU_FLAG_WSLOW
+  uint32_t bol0 = 1;     // dbuf[0] begins a line (ugpu_scanner_context; anchored tables)
   size_t smem = 0;       // sparse / dense kernel
   size_t xi_smem = 0;
   int xi_rec = 0;        // chain records of an xi scan
@@ -263,6 +269,9 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.xu_tab = dfa_xu(d) ? d->d_xu : nullptr;
   P.xu_bm3 = d->d_xu ? reinterpret_cast<const uint32_t*>(d->d_xu + kXuTab) : nullptr;
   P.xu_null = d->t.xu_null;
+  P.acap = d->amode ? d->d_acap : nullptr;
+  P.nul = d->nul ? 1u : 0u;
+  P.bol0 = 1;
   // chain bytes one stitch merge may cross before the chains count as not
   // resynchronising (two chains of a resynchronising table meet within a match
   // or two; longer merges go to the forest FIND)
@@ -404,7 +413,7 @@ const char* ugpu_version(void) { return "ugrep_amd 0.1 (gfx950)"; }
 int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa** out)
 {
   if (!out) return fail(UGPU_INVAL, "out is NULL");
-  if (pattern_flags & ~UGPU_PAT_WORD) return fail(UGPU_INVAL, "unknown pattern flags");
+  if (pattern_flags & ~(UGPU_PAT_WORD | UGPU_PAT_EMPTY)) return fail(UGPU_INVAL, "unknown pattern flags");
   *out = nullptr;
   ugpu_dfa* d = new (std::nothrow) ugpu_dfa();
   if (!d) return fail(UGPU_NOMEM, "host allocation");
@@ -435,6 +444,22 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       (e = hipMemcpy(d->d_caps, d->t.caps.data(), d->t.caps.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
     ugpu_dfa_destroy(d);
     return hip_fail(e, "table upload");
+  }
+  d->nul = (pattern_flags & UGPU_PAT_EMPTY) != 0;
+  d->amode = d->t.anchored || (d->nul && d->t.start_acc);
+  if (d->amode) {
+    if (pattern_flags & UGPU_PAT_WORD) {
+      ugpu_dfa_destroy(d);
+      return fail(UGPU_UNSUPPORTED, "option W with line anchors or empty matches");
+    }
+    // the per-context accepts; every scan runs the context walk (no transducers)
+    if ((e = hipMalloc(&d->d_acap, d->t.acap.size() * 4)) != hipSuccess ||
+        (e = hipMemcpy(d->d_acap, d->t.acap.data(), d->t.acap.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+      ugpu_dfa_destroy(d);
+      return hip_fail(e, "context accept upload");
+    }
+    *out = d;
+    return UGPU_OK;
   }
   if (pattern_flags & UGPU_PAT_WORD) {
     std::vector<uint32_t> wt;
@@ -516,6 +541,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   if (d->d_xg_sync) (void)hipFree(d->d_xg_sync);
   if (d->d_cls) (void)hipFree(d->d_cls);
   if (d->d_caps) (void)hipFree(d->d_caps);
+  if (d->d_acap) (void)hipFree(d->d_acap);
   delete d;
   return UGPU_OK;
 }
@@ -533,7 +559,7 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->accepting = d->t.accepting;
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
-  info->kernel = (d->d_wtab && !d->wplus && !d->xcw && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
+  info->kernel = d->amode || (d->d_wtab && !d->wplus && !d->xcw && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
                  : (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
                  : dfa_xc(d)                                   ? 5u
                  : dfa_xu(d)                                   ? 6u
@@ -663,6 +689,20 @@ int ugpu_tables_xu_host(const uint32_t* opc, uint32_t nop, uint8_t* tab, uint32_
   return UGPU_OK;
 }
 
+int ugpu_tables_context_host(const uint32_t* opc, uint32_t nop, uint32_t* acap, uint32_t acap_cap, int* anchored,
+                             int* start_acc)
+{
+  DfaTables t;
+  std::string err;
+  const int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  if (acap && acap_cap < t.acap.size()) return fail(UGPU_INVAL, "acap too small");
+  if (acap) std::copy(t.acap.begin(), t.acap.end(), acap);
+  if (anchored) *anchored = t.anchored ? 1 : 0;
+  if (start_acc) *start_acc = t.start_acc ? 1 : 0;
+  return UGPU_OK;
+}
+
 int ugpu_tables_equivalent_host(const uint32_t* opc_a, uint32_t nop_a, const uint32_t* opc_b, uint32_t nop_b, int* eq)
 {
   if (!eq) return fail(UGPU_INVAL, "NULL argument");
@@ -695,8 +735,9 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   HIP_TRY_S(hipGetDevice(&s->device));
   // option W: prefiltered tables keep sparse_kernel (its candidate walks check
   // the W rules); every other table runs wfind_kernel (tables through the caches)
-  if (dfa->d_wtab && !(dfa->t.filter && dfa->t.format == FMT_BYTE)) {
-    if (wfind_smem_bytes(dfa->ntrans_pad, dfa->t.states, dfa->nwtab) > 160 * 1024) {
+  // line anchors / option N: every scan runs the context walk on wfind_kernel
+  if (dfa->amode || (dfa->d_wtab && !(dfa->t.filter && dfa->t.format == FMT_BYTE))) {
+    if (wfind_smem_bytes(dfa->ntrans_pad, dfa->t.states, dfa->nwtab, dfa->amode) > 160 * 1024) {
       delete s;
       return fail(UGPU_UNSUPPORTED, "tables do not fit in LDS");
     }
@@ -869,6 +910,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   }
   ScanParams P{};
   fill_tables(P, s->dfa);
+  P.bol0 = s->bol0;
   if (s->wfast && !s->word) P.wtab = nullptr, P.nwtab = 0;  // the non-W kernels, stitches and forest
   geometry_for(P, s, dbuf, lo, hi, read_end, s->off, s->xi || s->xg || s->xc);
   P.delta = (int64_t)bias - (int64_t)s->off;
@@ -933,6 +975,13 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   s->stream = st;
   s->have_scan = true;
   s->forest = false;
+  return UGPU_OK;
+}
+
+int ugpu_scanner_context(ugpu_scanner* s, int bol0)
+{
+  if (!s) return fail(UGPU_INVAL, "NULL argument");
+  s->bol0 = bol0 ? 1u : 0u;
   return UGPU_OK;
 }
 
@@ -1034,6 +1083,7 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
     // dense kernel's geometry (COUNT + fix), then its WRITE pass
     P = ScanParams{};
     fill_tables(P, s->dfa);
+    P.bol0 = s->bol0;
     if (s->wfast) P.wtab = nullptr, P.nwtab = 0;  // (only a non-W scan gets here)
     uint64_t off = 0;
     geometry_for(P, s, s->last_buf, s->last_args[0], s->last_args[1], s->last_args[2], off, false);
@@ -1096,6 +1146,7 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P{};
   fill_tables(P, s->dfa);
+  P.bol0 = s->bol0;
   uint64_t off = 0;
   geometry_for(P, s, dbuf, lo, hi, read_end, off);
   P.delta = (int64_t)bias - (int64_t)off;
@@ -1217,6 +1268,7 @@ int scanner_acquire(const ugpu_dfa* dfa, ugpu_scanner** out)
     if (!d->pool.empty()) {
       *out = d->pool.back();
       d->pool.pop_back();
+      (*out)->bol0 = 1;  // (a pooled scanner may have served a shard)
       return UGPU_OK;
     }
   }
@@ -1377,6 +1429,20 @@ void shard_scan(Shard& sh, const uint8_t* buf, uint64_t len, bool host, int src_
     sh.rc = fail(UGPU_NOMEM, "find workspace");
     return;
   }
+  // (anchored tables: does the shard's first byte begin a line?)
+  uint8_t prev = '\n';
+  if (sh.lo > 0) {
+    if (host) {
+      prev = buf[sh.lo - 1];
+    } else {
+      const hipError_t e = hipMemcpy(&prev, buf + sh.lo - 1, 1, hipMemcpyDeviceToHost);
+      if (e != hipSuccess) {
+        sh.rc = hip_fail(e, "shard context byte");
+        return;
+      }
+    }
+  }
+  ugpu_scanner_context(sh.sc, prev == '\n');
   for (int attempt = 0; attempt < 2; ++attempt) {
     if ((sh.rc = shard_load(sh, buf, host, src_dev)) != UGPU_OK) return;
     sh.sc->stage_once = mode == UGPU_MODE_OFFSETS;
@@ -1836,6 +1902,7 @@ struct ugpu_stream {
   uint64_t carry = 0;  // unsettled bytes at buf[cur][0..carry)
   uint64_t base = 0;   // absolute offset of buf[cur][0] = the settled chain position
   bool done = false;
+  uint32_t bol0 = 1;   // buf[cur][0] begins a line (anchored tables: the byte before it is '\n')
 };
 
 namespace {
@@ -1920,6 +1987,7 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
   if (len) HIP_TRY(hipMemcpy(b + st->carry, chunk, len, hipMemcpyHostToDevice));
   ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
   if (!r) return fail(UGPU_NOMEM, "host allocation");
+  ugpu_scanner_context(st->sc, (int)st->bol0);
   // settle the chain up to `keep` bytes before the end (all of it when final);
   // a walk still open at the end of the bytes so far means hi was too close
   uint64_t hi = final ? n : (n > st->keep ? n - st->keep : 0);
@@ -2017,6 +2085,12 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
     }
   }
   // carry [exit, n) to the other buffer; the chain resumes at its first byte
+  // (an anchored table also needs to know whether the byte before it is '\n')
+  if (st->dfa->amode && exit > 0) {
+    uint8_t prev = 0;
+    HIP_TRY(hipMemcpy(&prev, b + exit - 1, 1, hipMemcpyDeviceToHost));
+    st->bol0 = prev == '\n' ? 1u : 0u;
+  }
   const uint64_t keep_n = n - exit;
   if (keep_n) HIP_TRY(hipMemcpy(st->buf[1 - st->cur], b + exit, keep_n, hipMemcpyDeviceToDevice));
   st->cur = 1 - st->cur;

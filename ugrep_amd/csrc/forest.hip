@@ -66,44 +66,40 @@ __device__ __forceinline__ Win fstage_bytes(const ScanParams& P, uint8_t* dst, u
   const uint64_t lend = bs + kFStage < P.rend ? bs + kFStage : (P.rend > bs ? P.rend : bs);
   const uint32_t n = (uint32_t)(lend - bs);
   for (uint32_t i = tid; i < n; i += nthr) dst[i] = P.g[bs + i];
-  Win w;
+  Win w = win_of(P);
   w.lds = dst;
   w.base = bs;
   w.lend = lend;
-  w.g = P.g;
-  w.rend = P.rend;
-  w.eof = P.at_eof;
-  w.wtab = P.wtab;
-  w.nwtab = P.nwtab;
-  w.bob = P.bob;
   return w;
 }
 
 constexpr uint32_t kFMatch = 0x80000000u;  // N entry: a match starts here (else N = p + 1)
 constexpr uint32_t kFOvf = 0x40000000u;    // N entry: the walk reached the readable end before EOF
-constexpr uint32_t kFNMask = 0x3fffffffu;  // N entry: N(p) - block start
+constexpr uint32_t kFEmpty = 0x20000000u;  // N entry: the match is empty (option N; N = p + 1)
+constexpr uint32_t kFNMask = 0x1fffffffu;  // N entry: N(p) - block start
 constexpr int kFSub = 64;                  // forest_walk_kernel: positions per lane sub-block
 
 // N(p) - bs (with the flags above) for the block's positions, and the walk's
 // last accepting entry (its row gives the accept index) when LE is set.
 // Neighbouring threads walk neighbouring positions: similar bytes, similar rows.
-template <int FMT, bool W, bool LE>
+template <int FMT, int W, bool LE>
 __device__ __forceinline__ void forest_n(const Tab<FMT>& T, const Win& w, uint64_t bs, uint32_t nb, uint32_t* N,
-                                         uint16_t* le_out, int tid, int nthr)
+                                         uint32_t* le_out, int tid, int nthr)
 {
   for (uint32_t r = tid; r < nb; r += nthr) {
     uint32_t le, ovf = 0;
     const uint64_t len = walk<FMT, W>(T, w, bs + r, le, ovf);
     uint64_t nx = (uint64_t)r + (len ? len : 1);
-    if (nx > kFNMask) nx = kFNMask;  // (a match longer than 1 GiB)
-    N[r] = (uint32_t)nx | (len ? kFMatch : 0u) | (ovf ? kFOvf : 0u);
-    if constexpr (LE) le_out[r] = (uint16_t)le;
+    if (nx > kFNMask) nx = kFNMask;  // (a match longer than 512 MiB)
+    const bool empty = W == kWalkCtx && !len && le && w.nul;  // option N: the empty match at p
+    N[r] = (uint32_t)nx | (len || empty ? kFMatch : 0u) | (empty ? kFEmpty : 0u) | (ovf ? kFOvf : 0u);
+    if constexpr (LE) le_out[r] = le;
   }
 }
 
 }  // namespace
 
-template <int FMT, bool W>
+template <int FMT, int W>
 __global__ __launch_bounds__(kFThreads) void forest_exit_kernel(ScanParams P, ForestArgs A)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
@@ -203,7 +199,7 @@ __global__ __launch_bounds__(kFThreads) void forest_stitch_kernel(ForestArgs A)
 // dependent LDS reads), and lane i walks sub-block i from its entry along N,
 // summing matches (COUNT) or writing them from the block's output base plus
 // the lane prefix (WRITE).
-template <int FMT, bool W, bool WRITE>
+template <int FMT, int W, bool WRITE>
 __global__ __launch_bounds__(kFThreads) void forest_walk_kernel(ScanParams P, ForestArgs A)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
@@ -213,7 +209,7 @@ __global__ __launch_bounds__(kFThreads) void forest_walk_kernel(ScanParams P, Fo
   uint8_t* bytes = fsm + ftab_bytes(P);
   uint32_t* N = reinterpret_cast<uint32_t*>(bytes + kFStage);
   uint32_t* J = N + kFB;
-  uint16_t* LE = reinterpret_cast<uint16_t*>(J + kFB);
+  uint32_t* LE = J + kFB;
   const uint64_t k = blockIdx.x;
   const uint64_t bs = A.c_lo + k * kFB;
   const uint64_t be = bs + kFB < A.c_hi ? bs + kFB : A.c_hi;
@@ -255,13 +251,13 @@ __global__ __launch_bounds__(kFThreads) void forest_walk_kernel(ScanParams P, Fo
   // lane = sub-block
   const uint64_t sa = bs + (uint64_t)lane * kFSub;
   const uint64_t sb = sa + kFSub < be ? sa + kFSub : be;
-  const Ctx C{P.caps, P.log_row, P.delta};
+  const Ctx C = W == kWalkCtx ? Ctx{P.acap, 0u, P.delta} : Ctx{P.caps, P.log_row, P.delta};
   uint32_t ovf = 0;
   CountEm em;
   for (uint64_t p = sent[lane]; p < sb;) {
     const uint32_t nv = N[p - bs];
     const uint64_t q = bs + (nv & kFNMask);
-    if (nv & kFMatch) em.put(C, p, q - p, LE[p - bs], +1);
+    if (nv & kFMatch) em.put(C, p, nv & kFEmpty ? 0 : q - p, LE[p - bs], +1);
     ovf |= nv & kFOvf;
     p = q;
   }
@@ -276,7 +272,7 @@ __global__ __launch_bounds__(kFThreads) void forest_walk_kernel(ScanParams P, Fo
     for (uint64_t p = sent[lane]; p < sb;) {
       const uint32_t nv = N[p - bs];
       const uint64_t q = bs + (nv & kFNMask);
-      if (nv & kFMatch) we.put(C, p, q - p, LE[p - bs], +1);
+      if (nv & kFMatch) we.put(C, p, nv & kFEmpty ? 0 : q - p, LE[p - bs], +1);
       p = q;
     }
     if (__ballot(we.overflow) && lane == 0) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
@@ -360,13 +356,13 @@ __global__ void forest_init_kernel(ForestArgs A, uint64_t entry)
 // ---------------------------------------------------------------- launcher
 namespace {
 
-template <int FMT, bool W>
+template <int FMT, int W>
 hipError_t forest_fmt(const ScanParams& P, ForestArgs A, uint64_t entry, bool write, DevTotals* tot,
                       hipStream_t st)
 {
   const size_t tab = ((2 * (size_t)P.ntrans_pad + 256) + 15) & ~size_t(15);
   const size_t sm1 = tab + kFStage + 4 * (size_t)kFB;
-  const size_t sm2 = tab + kFStage + 10 * (size_t)kFB;
+  const size_t sm2 = tab + kFStage + 12 * (size_t)kFB;
   hipError_t e;
   if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(forest_exit_kernel<FMT, W>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm1)) != hipSuccess)
@@ -407,10 +403,14 @@ uint64_t forest_block() { return kFB; }
 hipError_t launch_forest(const ScanParams& P, uint32_t format, const ForestArgs& A, uint64_t entry, bool write,
                          DevTotals* tot, hipStream_t st)
 {
-  const bool w = P.wtab != nullptr;
-  if (format == 0)
-    return w ? forest_fmt<0, true>(P, A, entry, write, tot, st) : forest_fmt<0, false>(P, A, entry, write, tot, st);
-  return w ? forest_fmt<1, true>(P, A, entry, write, tot, st) : forest_fmt<1, false>(P, A, entry, write, tot, st);
+  if (P.acap)
+    return format == 0 ? forest_fmt<0, kWalkCtx>(P, A, entry, write, tot, st)
+                       : forest_fmt<1, kWalkCtx>(P, A, entry, write, tot, st);
+  if (P.wtab)
+    return format == 0 ? forest_fmt<0, kWalkWord>(P, A, entry, write, tot, st)
+                       : forest_fmt<1, kWalkWord>(P, A, entry, write, tot, st);
+  return format == 0 ? forest_fmt<0, kWalkPlain>(P, A, entry, write, tot, st)
+                     : forest_fmt<1, kWalkPlain>(P, A, entry, write, tot, st);
 }
 
 }  // namespace ugpu

@@ -21,8 +21,14 @@
 // \p{NAME} \P{NAME} \pL (general categories and their long names, common
 // scripts, POSIX-style names), groups ( ) (?: ), alternation,
 // * + ? {n} {n,} {n,m}, -F literal mode, and -i (ASCII plus case_fold.inc pairs).
+// Line anchors: a ^ that starts a top-level alternative and a $ that ends one
+// (ugrep's -x wrapper ^(?:P)$, src/cnf.hpp:167-185, and ^P / P$ / ^a|b$),
+// under (?m) (ugrep's pattern prefix, src/ugrep.cpp:8586) or in the ERE mode;
+// they become per-context accepts encoded as META_BOL / META_EOL edges to
+// accept-only states (include/reflex/pattern.h:942-943), the shape the
+// reference's Pattern gives them (^ moved to the accept side).
 // Returns UGPU_UNSUPPORTED for what the GPU tables cannot express or this
-// compiler does not cover (anchors, word boundaries, lazy quantifiers,
+// compiler does not cover (other anchors, word boundaries, lazy quantifiers,
 // lookaround, backreferences, other \p names, \p{Lu} under -i): the caller keeps
 // the CPU matcher for those, as for any unsupported opcode table.
 #include <stdint.h>
@@ -31,6 +37,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <bitset>
 #include <map>
 #include <string>
@@ -405,16 +412,22 @@ class Parser
     }
     if (!s_.empty() && s_[0] == '|')
       fail(UGPU_INVAL, "empty first alternative");  // the reference rejects "|a" (but not "a|")
-    alts.push_back(parse_concat());
-    while (p_ < s_.size() && s_[p_] == '|')
+    for (;;)
     {
+      bol_ = eol_ = false;
+      alts.push_back(parse_concat(true));
+      anchors.push_back((bol_ ? 1 : 0) | (eol_ ? 2 : 0));
+      if (p_ >= s_.size() || s_[p_] != '|')
+        break;
       ++p_;
-      alts.push_back(parse_concat());
     }
     if (p_ != s_.size())
       fail(UGPU_INVAL, "unbalanced ')'");
     return alts;
   }
+
+  // per top-level alternative: 1 = starts with ^, 2 = ends with $
+  std::vector<int> anchors;
 
  private:
   const std::string &s_;
@@ -423,6 +436,8 @@ class Parser
   size_t p_ = 0;
   bool ic_;             // case-insensitive (flag, or RE/flex (?i) in REFLEX mode)
   bool dotall_ = false;  // REFLEX mode (?s): '.' matches '\n'
+  bool multiline_ = false;  // REFLEX mode (?m): ^ and $ are line anchors
+  bool bol_ = false, eol_ = false;  // anchors of the top-level alternative being parsed
 
   bool icase() const { return ic_; }
   bool reflex() const { return (flags_ & UGPU_RX_REFLEX) != 0; }
@@ -454,12 +469,27 @@ class Parser
     return alts.size() == 1 ? alts[0] : t_.add(ALT, alts);
   }
 
-  int parse_concat()
+  int parse_concat(bool top = false)
   {
     std::vector<int> seq;
     bool atoms = false;
     while (p_ < s_.size() && s_[p_] != '|' && s_[p_] != ')')
     {
+      // line anchors of a top-level alternative: ^ before its first atom, $
+      // as its last character (anything else stays UNSUPPORTED in parse_atom)
+      if (top && (s_[p_] == '^' || s_[p_] == '$') && (multiline_ || !reflex()))
+      {
+        const bool first = s_[p_] == '^' && !atoms;
+        const bool last = s_[p_] == '$' && (p_ + 1 == s_.size() || s_[p_ + 1] == '|');
+        if (first || last)
+        {
+          if (p_ + 1 < s_.size() && strchr("*+?{", s_[p_ + 1]) != NULL)
+            fail(UGPU_UNSUPPORTED, "repeated anchor");
+          (first ? bol_ : eol_) = true;
+          ++p_;
+          continue;
+        }
+      }
       // REFLEX mode: a (?imsx) modifier after atoms of its branch opens a group
       // that runs to the end of the enclosing group, later alternatives
       // included ("x(?i)ab|cd" is x(?i:ab|cd)); a leading one just sets the
@@ -471,6 +501,8 @@ class Parser
         seq.push_back(p_ >= s_.size() || s_[p_] == ')' ? t_.add(EMPTY) : parse_alt());
         break;
       }
+      if (eol_)
+        fail(UGPU_UNSUPPORTED, "anchor");  // (unreachable: $ ends the alternative)
       atoms = atoms || !(reflex() && modifier_at(p_));
       seq.push_back(parse_repeat());
     }
@@ -879,6 +911,57 @@ class Parser
     return static_cast<uint8_t>(c);
   }
 
+  // class escapes the Pattern itself resolves in a byte-mode regex (ugrep -U
+  // leaves them to it: Matcher::convert without the unicode flag):
+  // \s \S \h \H \d \D \l \L \u \U \w \W are the POSIX classes Space, Blank,
+  // Digit, Lower, Upper, Word and their 256-byte complements (lib/pattern.cpp
+  // :1660-1676 with its posix table :2714-2735; the complements include '\n')
+  bool pattern_class_escape(char c, ByteSet &b)
+  {
+    const char *lower = "shdluw";
+    const char *k = strchr(lower, c | 0x20);
+    if (k == NULL || c == '\0')
+      return false;
+    if ((c | 0x20) == 'u' && p_ < s_.size() && s_[p_] == '{')
+      return false;  // \u{...}: a code point
+    if (icase() && ((c | 0x20) == 'l' || (c | 0x20) == 'u'))
+      fail(UGPU_UNSUPPORTED, std::string("escape \\") + c + " under (?i)");
+    ByteSet x;
+    switch (c | 0x20)
+    {
+      case 's':
+        for (unsigned v = '\t'; v <= '\r'; ++v)
+          x.set(v);
+        x.set(' ');
+        break;
+      case 'h':
+        x.set('\t');
+        x.set(' ');
+        break;
+      case 'd':
+        for (unsigned v = '0'; v <= '9'; ++v)
+          x.set(v);
+        break;
+      case 'l':
+        for (unsigned v = 'a'; v <= 'z'; ++v)
+          x.set(v);
+        break;
+      case 'u':
+        for (unsigned v = 'A'; v <= 'Z'; ++v)
+          x.set(v);
+        break;
+      case 'w':
+        for (unsigned v = 0; v < 256; ++v)
+          if ((v >= '0' && v <= '9') || (v >= 'A' && v <= 'Z') || (v >= 'a' && v <= 'z') || v == '_')
+            x.set(v);
+        break;
+    }
+    if (c >= 'A' && c <= 'Z')
+      x.flip();
+    b |= x;
+    return true;
+  }
+
   // "(?imsx-imsx)" starts at q
   bool modifier_at(size_t q) const
   {
@@ -926,6 +1009,13 @@ class Parser
         fail(UGPU_UNSUPPORTED, "POSIX bracket in byte mode");
       uint8_t lo, hi;
       ++p_;
+      if (c == '\\' && p_ < s_.size())
+      {
+        const char e = s_[p_++];
+        if (pattern_class_escape(e, b))
+          continue;
+        --p_;
+      }
       lo = c == '\\' ? reflex_escape_byte() : static_cast<uint8_t>(c);
       hi = lo;
       if (p_ + 1 < s_.size() && s_[p_] == '-' && s_[p_ + 1] != ']')
@@ -960,7 +1050,7 @@ class Parser
           // (?imsx-imsx) modifies the rest of the enclosing group,
           // (?imsx-imsx:...) just the group; anything else ((?=, (?^ ...) is not a DFA
           size_t q = p_ + 1;
-          bool on = true, i = ic_, d = dotall_;
+          bool on = true, i = ic_, d = dotall_, m = multiline_;
           while (q < s_.size() && strchr("imsx-", s_[q]) != NULL)
           {
             switch (s_[q])
@@ -969,7 +1059,8 @@ class Parser
               case 'i': i = on; break;
               case 's': d = on; break;
               case 'x': if (on) fail(UGPU_UNSUPPORTED, "free-space mode"); break;
-              default: break;  // m: multiline anchors (anchors are not supported anyway)
+              case 'm': m = on; break;
+              default: break;
             }
             ++q;
           }
@@ -978,6 +1069,7 @@ class Parser
             p_ = q + 1;
             ic_ = i;
             dotall_ = d;
+            multiline_ = m;
             return t_.add(EMPTY);
           }
           if (q >= s_.size() || s_[q] != ':')
@@ -1030,6 +1122,14 @@ class Parser
           if (seq.empty())
             return t_.add(EMPTY);
           return seq.size() == 1 ? seq[0] : t_.add(CAT, seq);
+        }
+        if (p_ < s_.size())
+        {
+          ByteSet cls;
+          const char e = s_[p_++];
+          if (pattern_class_escape(e, cls))
+            return t_.leaf(cls);
+          --p_;
         }
         if (p_ < s_.size() && strchr("bBAzZ<>`'GkKEXRNuUcCldDwWsShHpPiIjJ", s_[p_]) != NULL)
           fail(UGPU_UNSUPPORTED, std::string("escape \\") + s_[p_] + " in byte mode");
@@ -1140,6 +1240,7 @@ struct Glushkov
   std::vector<ByteSet> bytes;            // position -> bytes
   std::vector<std::vector<int>> follow;  // position -> follow positions
   std::vector<int> accept;               // position -> accept index (end markers), 0 otherwise
+  std::vector<int> anchor;               // end marker -> 1: needs a walk begun at a line begin, 2: needs a line end next
 
   struct Info
   {
@@ -1167,6 +1268,7 @@ struct Glushkov
     bytes.push_back(b);
     follow.emplace_back();
     accept.push_back(acc);
+    anchor.push_back(0);
     return static_cast<int>(bytes.size() - 1);
   }
 
@@ -1227,10 +1329,16 @@ struct Glushkov
   }
 };
 
+// accept index per line context (bit 0: the walk began at a line begin, bit 1:
+// a line end follows), the lowest satisfied top-level alternative, 0 = none
+typedef std::array<uint32_t, 4> Ctx4;
+
 struct Dfa
 {
   std::vector<std::vector<uint32_t>> next;  // state -> 256 targets (0 = dead state)
-  std::vector<uint32_t> acc;                // accept index, 0 = none
+  std::vector<uint32_t> acc;                // accept index without line context (cx[s][0]), 0 = none
+  std::vector<Ctx4> cx;                     // accept index per line context
+  bool anchored = false;                    // some accept depends on the context
 };
 
 Dfa subsets(Glushkov &g, const std::vector<int> &start)
@@ -1272,11 +1380,14 @@ Dfa subsets(Glushkov &g, const std::vector<int> &start)
   for (size_t k = 0; k < sets.size(); ++k)
   {
     std::vector<int> cur = sets[k];  // copy: sets grows
-    uint32_t a = 0;
-    for (int p : cur)
-      if (g.accept[p] && (a == 0 || static_cast<uint32_t>(g.accept[p]) < a))
-        a = g.accept[p];
-    d.acc.push_back(a);
+    Ctx4 cx = {0, 0, 0, 0};
+    for (int ctx = 0; ctx < 4; ++ctx)
+      for (int p : cur)
+        if (g.accept[p] && (g.anchor[p] & ~ctx) == 0 && (cx[ctx] == 0 || static_cast<uint32_t>(g.accept[p]) < cx[ctx]))
+          cx[ctx] = g.accept[p];
+    d.acc.push_back(cx[0]);
+    d.cx.push_back(cx);
+    d.anchored = d.anchored || cx[1] != cx[0] || cx[2] != cx[0] || cx[3] != cx[0];
     std::vector<uint32_t> row(256, 0);
     std::vector<uint32_t> by_cls(ncls, 0);
     for (int c = 0; c < ncls; ++c)
@@ -1301,9 +1412,9 @@ Dfa minimize(const Dfa &d, uint32_t start)
   size_t n = d.acc.size();
   std::vector<uint32_t> part(n);
   {
-    std::map<uint32_t, uint32_t> m;
+    std::map<Ctx4, uint32_t> m;
     for (size_t s = 0; s < n; ++s)
-      part[s] = m.emplace(d.acc[s], static_cast<uint32_t>(m.size())).first->second;
+      part[s] = m.emplace(d.cx[s], static_cast<uint32_t>(m.size())).first->second;
   }
   size_t nparts = 0;
   for (;;)
@@ -1331,8 +1442,10 @@ Dfa minimize(const Dfa &d, uint32_t start)
   for (size_t s = n; s-- > 0;)
     rep[part[s]] = static_cast<uint32_t>(s);
   Dfa out;
+  out.anchored = d.anchored;
   newid[dead] = 0;
   out.acc.push_back(0);
+  out.cx.push_back(Ctx4{0, 0, 0, 0});
   out.next.push_back(std::vector<uint32_t>(256, 0));
   std::vector<uint32_t> order{part[start]};
   if (part[start] != dead)
@@ -1355,6 +1468,7 @@ Dfa minimize(const Dfa &d, uint32_t start)
       row[b] = static_cast<uint32_t>(newid[tb]);
     }
     out.acc.push_back(d.acc[s]);
+    out.cx.push_back(d.cx[s]);
     out.next.push_back(row);
   }
   return out;
@@ -1371,8 +1485,8 @@ Dfa unfold_gaps(const Dfa &d)
 {
   const int kMaxGap = 6;
   size_t n = d.acc.size();
-  if (n < 2)
-    return d;
+  if (n < 2 || d.anchored)
+    return d;  // (no gap transducer for context-dependent accepts: tables.cpp)
   std::map<std::pair<uint32_t, int>, uint32_t> id;
   std::vector<std::pair<uint32_t, int>> order{{0, -1}, {1, 0}};
   id[order[0]] = 0;
@@ -1405,6 +1519,7 @@ Dfa unfold_gaps(const Dfa &d)
       }
     out.next.push_back(row);
     out.acc.push_back(d.acc[s]);
+    out.cx.push_back(d.cx[s]);
   }
   return out;
 }
@@ -1413,7 +1528,9 @@ Dfa unfold_gaps(const Dfa &d)
 
 std::vector<uint32_t> encode(const Dfa &d)
 {
-  // states 1..n-1 are emitted in order; state 1 (start) at word 0
+  // states 1..n-1 are emitted in order as blocks 0..n-2 (state 1, the start,
+  // at word 0), then the accept-only blocks that context-dependent accepts
+  // point at through META_BOL / META_EOL words
   size_t n = d.acc.size();
   if (n < 2)
   {
@@ -1423,9 +1540,16 @@ std::vector<uint32_t> encode(const Dfa &d)
   struct Run
   {
     unsigned lo, hi;
-    uint32_t target;
+    uint32_t target;  // block index + 1, 0 = HALT
   };
-  std::vector<std::vector<Run>> runs(n);
+  struct Block
+  {
+    uint32_t take = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> metas;  // (META - META_MIN, block index + 1)
+    std::vector<Run> runs;
+  };
+  const uint32_t kBol = 0x09, kEol = 0x0a;  // META_BOL, META_EOL - META_MIN (pattern.h:942-943)
+  std::vector<Block> blocks(n - 1);
   for (size_t s = 1; s < n; ++s)
   {
     int b = 255;
@@ -1437,20 +1561,85 @@ std::vector<uint32_t> encode(const Dfa &d)
         --e;
       // dead runs become HALT words: every byte of a state block is covered
       // and its last word has lo == 0, as encode_dfa emits them
-      runs[s].push_back(Run{static_cast<unsigned>(e), static_cast<unsigned>(b), t});
+      blocks[s - 1].runs.push_back(Run{static_cast<unsigned>(e), static_cast<unsigned>(b), t});
       b = e - 1;
     }
   }
+  // accept-only blocks: P(v) = TAKE v; Q(a, b) = TAKE a, then META_EOL -> P(b)
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> extra;
+  auto accept_only = [&](uint32_t a, uint32_t b) -> uint32_t {
+    auto key = std::make_pair(a, b);
+    auto it = extra.find(key);
+    if (it != extra.end())
+      return it->second;
+    Block k;
+    k.take = a;
+    if (b != a)
+    {
+      uint32_t pb = 0;
+      {
+        auto key2 = std::make_pair(b, b);
+        auto it2 = extra.find(key2);
+        if (it2 == extra.end())
+        {
+          Block pk;
+          pk.take = b;
+          pk.runs.push_back(Run{0, 255, 0});
+          blocks.push_back(pk);
+          it2 = extra.emplace(key2, static_cast<uint32_t>(blocks.size())).first;
+        }
+        pb = it2->second;
+      }
+      k.metas.push_back(std::make_pair(kEol, pb));
+    }
+    k.runs.push_back(Run{0, 255, 0});
+    blocks.push_back(k);
+    return extra.emplace(key, static_cast<uint32_t>(blocks.size())).first->second;
+  };
+  // a state's accept per line context f = cx[s] (bit 0 bol, bit 1 eol) as the
+  // reference evaluates it (lib/matcher.cpp:193-450): its TAKE f[0], then the
+  // first meta edge that holds -- BOL to Q(f[1], f[3]) (whose EOL edge gives
+  // f[3]), else EOL to P(f[2])
+  for (size_t s = 1; s < n; ++s)
+  {
+    const Ctx4 &f = d.cx[s];
+    Block &k = blocks[s - 1];
+    k.take = f[0];
+    const bool by_bol = f[1] != f[0] || f[3] != f[2];
+    const bool by_eol = f[2] != f[0] || f[3] != f[1];
+    if (by_bol && by_eol)
+    {
+      const uint32_t q = accept_only(f[1], f[3]);
+      blocks[s - 1].metas.push_back(std::make_pair(kBol, q));
+      if (f[2] != f[0])
+      {
+        const uint32_t pe = accept_only(f[2], f[2]);
+        blocks[s - 1].metas.push_back(std::make_pair(kEol, pe));
+      }
+    }
+    else if (by_bol)
+    {
+      const uint32_t pb = accept_only(f[1], f[1]);
+      blocks[s - 1].metas.push_back(std::make_pair(kBol, pb));
+    }
+    else if (by_eol)
+    {
+      const uint32_t pe = accept_only(f[2], f[2]);
+      blocks[s - 1].metas.push_back(std::make_pair(kEol, pe));
+    }
+  }
+  const size_t nb = blocks.size();
   for (int pass = 0; pass < 2; ++pass)
   {
     bool lng = pass == 1;
-    std::vector<uint32_t> at(n, 0);
+    std::vector<uint32_t> at(nb + 1, 0);
     uint32_t w = 0;
-    for (size_t s = 1; s < n; ++s)
+    for (size_t i = 0; i < nb; ++i)
     {
-      at[s] = w;
-      w += d.acc[s] ? 1 : 0;
-      for (auto &r : runs[s])
+      at[i + 1] = w;
+      w += blocks[i].take ? 1 : 0;
+      w += static_cast<uint32_t>(blocks[i].metas.size()) * (lng ? 2 : 1);
+      for (auto &r : blocks[i].runs)
         w += (lng && r.target != 0) ? 2 : 1;
     }
     if (!lng && w >= 0xFFFE)
@@ -1459,11 +1648,22 @@ std::vector<uint32_t> encode(const Dfa &d)
       fail(UGPU_UNSUPPORTED, "opcode table too large");
     std::vector<uint32_t> out;
     out.reserve(w);
-    for (size_t s = 1; s < n; ++s)
+    for (size_t i = 0; i < nb; ++i)
     {
-      if (d.acc[s])
-        out.push_back(0xFE000000u | d.acc[s]);
-      for (auto &r : runs[s])
+      const Block &k = blocks[i];
+      if (k.take)
+        out.push_back(0xFE000000u | k.take);
+      for (auto &m : k.metas)
+      {
+        if (lng)
+        {
+          out.push_back(m.first << 24 | 0xFFFEu);
+          out.push_back(0xFF000000u | at[m.second]);
+        }
+        else
+          out.push_back(m.first << 24 | at[m.second]);
+      }
+      for (auto &r : k.runs)
       {
         if (r.target == 0)
           out.push_back(r.lo << 24 | r.hi << 16 | 0xFFFFu);
@@ -1513,11 +1713,11 @@ int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, 
     std::vector<int> alts = parser.parse_top();
     Glushkov g(tree);
     std::vector<int> start;
-    std::vector<std::pair<std::vector<int>, int>> ends;
     for (size_t k = 0; k < alts.size(); ++k)
     {
       Glushkov::Info info = g.walk(alts[k]);
       int end = g.new_pos(ByteSet(), static_cast<int>(k + 1));
+      g.anchor[end] = k < parser.anchors.size() ? parser.anchors[k] : 0;
       g.link(info.last, std::vector<int>{end});
       Glushkov::merge(start, info.first);
       if (info.nullable)

@@ -21,17 +21,8 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int G = (int)P.nrec;
   const Tab<FMT> T{P.trans, P.cls, P.start, P.accb};
-  const Ctx C{P.caps, P.log_row, P.delta};
-  Win w;
-  w.lds = nullptr;
-  w.base = 0;
-  w.lend = 0;
-  w.g = P.g;
-  w.rend = P.rend;
-  w.eof = P.at_eof;
-  w.wtab = P.wtab;
-  w.nwtab = P.nwtab;
-  w.bob = P.bob;
+  const Ctx C = P.acap ? Ctx{P.acap, 0u, P.delta} : Ctx{P.caps, P.log_row, P.delta};
+  const Win w = win_of(P);
   uint32_t ovf = 0, over = 0;
   // the scan kernel already gave up on these chains (UGPU_FLAG_BUDGET): the host
   // resolves the range with the forest FIND, nothing to stitch
@@ -78,8 +69,10 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
       const uint64_t bhi = clampu(te * P.unit, P.lo, P.hi);
       CountEm d;
       uint64_t ne;
-      const bool met = P.wtab ? merge<FMT, true>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over)
-                              : merge<FMT>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over);
+      const bool met =
+          P.acap   ? merge<FMT, kWalkCtx>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over)
+          : P.wtab ? merge<FMT, kWalkWord>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over)
+                   : merge<FMT>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over);
       if (!met) exi[b] = ne;
       ent[b] = nx[j];
       cnt[j] += d.cnt;
@@ -155,18 +148,14 @@ __global__ void chain_fix_kernel(ScanParams P, uint64_t old_entry, uint64_t new_
 {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const Tab<FMT> T{P.trans, P.cls, P.start, P.accb};
-  const Ctx C{P.caps, P.log_row, P.delta};
-  Win w;
-  w.lds = nullptr;
-  w.base = 0;
-  w.lend = 0;
-  w.g = P.g;
-  w.rend = P.rend;
-  w.eof = P.at_eof;
+  const Ctx C = P.acap ? Ctx{P.acap, 0u, P.delta} : Ctx{P.caps, P.log_row, P.delta};
+  Win w = win_of(P);
+  w.wtab = nullptr;  // (option W is not stitched across shards: the host refuses it)
   uint32_t ovf = 0, over = 0;
   CountEm d;
   uint64_t ne = 0;
-  bool met = merge<FMT>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over);
+  bool met = P.acap ? merge<FMT, kWalkCtx>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over)
+                    : merge<FMT>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over);
   DevTotals* t = P.totals;
   t->count = d.cnt;
   t->digest = d.dg;

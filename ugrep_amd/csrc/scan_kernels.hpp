@@ -146,6 +146,13 @@ struct ScanParams {
   const uint8_t* xu_tab;  // kXuTab bytes (4-byte aligned)
   const uint32_t* xu_bm3; // kXuBm3 dwords
   uint32_t xu_null;       // the fill byte
+  // line anchors / option N (tables.hpp acap): per-context accept indices
+  // (sid * 4 + bol * 2 + eol) or NULL; bol0: the position bob starts a line
+  // (the byte before the buffer is '\n', or the buffer begins the input);
+  // nul: option N, empty matches are reported
+  const uint32_t* acap;
+  uint32_t bol0;
+  uint32_t nul;
 };
 
 // Forest FIND (forest.hip): exact for every table, no resynchronisation
@@ -220,7 +227,7 @@ uint32_t utf8_tile();
 hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream);
 uint32_t wfind_unit();
 uint32_t wfind_waves();
-size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab);
+size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, bool ctx);  // ctx: anchors / N
 // immediate-transducer kernel, xi_kernel.hip (COUNT mode only)
 hipError_t launch_xi(const ScanParams& P, size_t smem, hipStream_t stream);
 hipError_t xi_occupancy(size_t smem, int* blocks_per_cu);

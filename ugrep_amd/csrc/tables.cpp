@@ -32,7 +32,10 @@ struct RawState {
   uint32_t pc;
   uint32_t cap;
   int64_t target_pc[256];
+  std::vector<std::pair<uint32_t, uint32_t> > metas;  // (META code - 0x100, target pc) in block order
 };
+
+constexpr uint32_t kMetaBol = 0x09, kMetaEol = 0x0a;  // META_BOL / META_EOL - META_MIN (pattern.h:942-943)
 
 // Bucket approximation used by the GPU prefilter: the bytes whose 3-bit
 // fields (lo3, mid3, hi2) each occur among the members' fields.
@@ -390,17 +393,42 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   std::vector<RawState> raw;
   std::unordered_map<uint32_t, uint32_t> index_of_pc;  // pc -> raw index
   raw.reserve(64);
-  raw.push_back(RawState{0, 0, {}});
+  raw.push_back(RawState{0, 0, {}, {}});
   index_of_pc[0] = 0;
   for (size_t qi = 0; qi < raw.size(); ++qi) {
     uint32_t pc = raw[qi].pc;
     uint32_t k = pc;
     uint32_t cap = 0;
-    // block header
+    // block header: TAKE, then meta edges (no goto words: the interpreter
+    // tests them in block order before the byte edges, lib/matcher.cpp:193-450)
     while (k < nop && !word_is_goto(opc[k])) {
-      uint32_t op = opc[k] >> 24;
+      const uint32_t w = opc[k], op = w >> 24;
       if (op == 0xfe) {
-        cap = opc[k] & 0xffffff;
+        cap = w & 0xffffff;
+      } else if (word_is_meta(w)) {
+        const uint32_t idx = w & 0xffff;
+        if (op != kMetaBol && op != kMetaEol) {
+          err = "opcode table uses meta edges other than ^ and $ (word boundaries, \\A, \\Z, indent)";
+          return 1;
+        }
+        uint64_t t = idx;
+        if (idx == kLong) {
+          if (k + 1 >= nop) {
+            err = "LONG meta goto without index word";
+            return 2;
+          }
+          t = opc[k + 1] & 0xffffff;
+          ++k;
+        }
+        if (idx == kHalt || t >= nop) {
+          err = "meta goto target out of range";
+          return 2;
+        }
+        raw[qi].metas.emplace_back(op, (uint32_t)t);
+        if (index_of_pc.find((uint32_t)t) == index_of_pc.end()) {
+          index_of_pc[(uint32_t)t] = (uint32_t)raw.size();
+          raw.push_back(RawState{(uint32_t)t, 0, {}, {}});
+        }
       } else {
         err = "opcode table uses REDO/TAIL/HEAD/indent words";
         return 1;
@@ -422,7 +450,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
         return 2;
       }
       if (word_is_meta(w)) {
-        err = "opcode table uses meta edges (anchors / word boundaries)";
+        err = "meta edge after a byte edge";
         return 1;
       }
       uint32_t lo = w >> 24, hi = (w >> 16) & 0xff, idx = w & 0xffff;
@@ -454,29 +482,68 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       int64_t t = tgt[c];
       if (t != kDead && index_of_pc.find((uint32_t)t) == index_of_pc.end()) {
         index_of_pc[(uint32_t)t] = (uint32_t)raw.size();
-        raw.push_back(RawState{(uint32_t)t, 0, {}});
+        raw.push_back(RawState{(uint32_t)t, 0, {}, {}});
       }
     }
     raw[qi].cap = cap;
     std::copy(tgt, tgt + 256, raw[qi].target_pc);
   }
 
-  // renumber: dead = 0, non-accepting states, then accepting states
+  // acceptance per (bol, eol) context: the reference's meta evaluation at a
+  // state (lib/matcher.cpp:193-450): its own TAKE, then the first meta edge
+  // that holds, that target's TAKE, its first meta edge that holds, ... (at
+  // most 5 meta jumps); a meta target that goes on with byte edges is not
+  // supported (the reference would continue that walk from the same byte)
   const uint32_t n = (uint32_t)raw.size();
+  bool anchored = false;
+  std::vector<uint32_t> acc4((size_t)n * 4, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    anchored = anchored || !raw[i].metas.empty();
+    for (uint32_t ctx = 0; ctx < 4; ++ctx) {
+      const bool bol = ctx & 2, eol = ctx & 1;
+      uint32_t cap = raw[i].cap, cur = i;
+      for (int jumps = 0; jumps < 5; ++jumps) {
+        uint32_t to = ~0u;
+        for (const auto& m : raw[cur].metas)
+          if ((m.first == kMetaBol && bol) || (m.first == kMetaEol && eol)) {
+            to = index_of_pc[m.second];
+            break;
+          }
+        if (to == ~0u) break;
+        for (int c = 0; c < 256; ++c)
+          if (raw[to].target_pc[c] != kDead) {
+            err = "a meta edge's target state goes on with byte edges";
+            return 1;
+          }
+        if (raw[to].cap) cap = raw[to].cap;
+        cur = to;
+      }
+      acc4[(size_t)i * 4 + ctx] = cap;
+    }
+  }
+  auto accepts = [&](uint32_t i) {
+    return acc4[(size_t)i * 4] | acc4[(size_t)i * 4 + 1] | acc4[(size_t)i * 4 + 2] | acc4[(size_t)i * 4 + 3];
+  };
+  // renumber: dead = 0, non-accepting states, then accepting states (for an
+  // anchored table: accepting in some context)
   std::vector<uint32_t> sid(n);
   uint32_t next_id = 1;
   for (uint32_t i = 0; i < n; ++i)
-    if (raw[i].cap == 0) sid[i] = next_id++;
+    if (!accepts(i)) sid[i] = next_id++;
   const uint32_t first_acc = next_id;
   for (uint32_t i = 0; i < n; ++i)
-    if (raw[i].cap != 0) sid[i] = next_id++;
+    if (accepts(i)) sid[i] = next_id++;
   const uint32_t S = next_id;
 
   // dense next[sid][byte] in new ids
   std::vector<uint32_t> nxt((size_t)S * 256, 0);
-  std::vector<uint32_t> caps(S, 0);
+  std::vector<uint32_t> caps(S, 0), acap((size_t)S * 4, 0);
   for (uint32_t i = 0; i < n; ++i) {
     caps[sid[i]] = raw[i].cap;
+    for (uint32_t ctx = 0; ctx < 4; ++ctx) acap[(size_t)sid[i] * 4 + ctx] = acc4[(size_t)i * 4 + ctx];
+    if (anchored && !raw[i].cap) {  // (caps: the state's accept in some context, for the prefilter's superset)
+      for (uint32_t ctx = 0; ctx < 4 && !caps[sid[i]]; ++ctx) caps[sid[i]] = acc4[(size_t)i * 4 + ctx];
+    }
     for (int c = 0; c < 256; ++c) {
       int64_t t = raw[i].target_pc[c];
       nxt[(size_t)sid[i] * 256 + c] = (t == kDead) ? 0 : sid[index_of_pc[(uint32_t)t]];
@@ -528,9 +595,13 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       for (int c = 0; c < 256; ++c) t.trans[(size_t)s * R + cls[c]] = (uint16_t)(nxt[(size_t)s * 256 + c] * R);
   }
   t.caps = caps;
+  t.acap = acap;
+  t.anchored = anchored;
   const uint32_t start_sid = sid[0];
-  // FIND transducer for restart-local tables (tables.hpp)
-  if (R >= 4) {
+  t.start_acc = start_sid >= first_acc;
+  // FIND transducer for restart-local tables (tables.hpp); none of the
+  // transducer forms below holds for conditional acceptance (anchored tables)
+  if (R >= 4 && !anchored) {
     std::vector<int> reps;  // one byte per column class
     {
       std::vector<bool> seen_cls(256, false);
@@ -727,7 +798,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   }
   // two-state tables (tables.hpp XcProg, xc_kernel.hip): start --G--> A,
   // A --X--> A, G a subset of X, both sets inside ASCII
-  if (start_sid < first_acc) {
+  if (start_sid < first_acc && !anchored) {
     uint32_t A = 0;
     bool ok = true;
     for (int c = 0; c < 256 && ok; ++c) {
@@ -765,6 +836,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
     else if (caps[s] != t.cap1)
       t.cap1 = 0;
   }
+  if (anchored) t.cap1 = 0;  // (conditional accepts: the accept index comes from acap)
   if (!t.xc && t.cap1 != 0 && start_sid < first_acc) build_xu(nxt, S, first_acc, start_sid, t);
   // prefilter (see tables.hpp): per first byte c, the bytes that can follow
   // it (second) and follow those (third); "all" once a prefix accepts
@@ -808,7 +880,8 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
     }
   }
   // the sparse kernel pays off when few positions survive the prefilter
-  t.filter = t.format == FMT_BYTE && !leads.empty() && t.fdensity <= 0.15;
+  // (a start state that accepts: empty matches anywhere, no candidate filter)
+  t.filter = t.format == FMT_BYTE && !leads.empty() && t.fdensity <= 0.15 && start_sid < first_acc;
   out = std::move(t);
   return 0;
 }

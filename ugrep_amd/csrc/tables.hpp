@@ -112,6 +112,21 @@ struct DfaTables {
   uint8_t xu_null = 0;
   std::vector<uint8_t> xu_tab;    // kXuTab bytes
   std::vector<uint32_t> xu_bm3;   // kXuBm3 dwords
+  // Line anchors (META_BOL `^`, META_EOL `$`, include/reflex/pattern.h:942-943)
+  // and option N (empty matches).  The reference tests meta edges when it has
+  // fetched the byte after the current position (lib/matcher.cpp:294-316): a
+  // META_BOL edge holds when the walk started at the begin of a line (`bol`,
+  // fixed at the walk start, :93), a META_EOL edge when that byte is '\n', EOF,
+  // or '\r' before '\n'; the first edge that holds is followed (to at most 5
+  // chained meta targets), and a TAKE met on the way is the accept at the
+  // current position.  So acceptance is a function of (state, bol, eol):
+  //   acap[sid * 4 + bol * 2 + eol] = accept index, 0 = none
+  // (also for tables without meta edges: the state's TAKE in all four).
+  // anchored: the table has meta edges, so its acceptance is conditional and
+  // only the context walk (device_common.hpp walk mode 2) may scan it.
+  // start_acc: the start state accepts in some context (empty matches).
+  bool anchored = false, start_acc = false;
+  std::vector<uint32_t> acap;  // states * 4
 };
 
 // xu codes.  Bits 0-3: a thermometer of the token's bytes (bit k: the token

@@ -33,33 +33,39 @@ constexpr uint32_t kWUnit = 4096;   // bytes per tile (records hold whole tiles)
 #endif
 constexpr int kWWaves = UGPU_WF_WAVES;  // waves (records) per workgroup: one staged table copy
 
-// LDS image: transitions (u16, ntrans_pad), accept indices (u32 per state),
-// Word ranges (2 x u32 each), class bytes (256)
-__host__ __device__ inline size_t wfind_smem(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab)
+// LDS image: transitions (u16, ntrans_pad), accept indices (u32 per state;
+// mode kWalkCtx: 4 per state, tables.hpp acap), Word ranges (2 x u32 each),
+// class bytes (256)
+__host__ __device__ inline size_t wfind_smem(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, bool ctx)
 {
-  return 2 * (size_t)ntrans_pad + 4 * (size_t)nstates + 8 * (size_t)nwtab + 256;
+  return 2 * (size_t)ntrans_pad + 4 * (size_t)nstates * (ctx ? 4 : 1) + 8 * (size_t)nwtab + 256;
 }
 
-template <int FMT, bool WRITE>
+// M: kWalkWord (option W) or kWalkCtx (line anchors / option N): the same
+// exact chain machinery, with that mode's walk rules
+template <int FMT, bool WRITE, int M>
 __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
+  const uint32_t ncaps = M == kWalkCtx ? 4 * P.nstates : P.nstates;
+  const uint32_t nwt = M == kWalkCtx ? 0u : P.nwtab;
   {
     // stage the tables once per workgroup (the walks look them up per byte)
     uint16_t* tr = reinterpret_cast<uint16_t*>(wsm);
     uint32_t* cp = reinterpret_cast<uint32_t*>(wsm + 2 * (size_t)P.ntrans_pad);
-    uint32_t* wt = cp + P.nstates;
-    uint8_t* cl = reinterpret_cast<uint8_t*>(wt + 2 * P.nwtab);
+    uint32_t* wt = cp + ncaps;
+    uint8_t* cl = reinterpret_cast<uint8_t*>(wt + 2 * nwt);
+    const uint32_t* caps = M == kWalkCtx ? P.acap : P.caps;
     for (uint32_t i = threadIdx.x; i < P.ntrans_pad; i += blockDim.x) tr[i] = P.trans[i];
-    for (uint32_t i = threadIdx.x; i < P.nstates; i += blockDim.x) cp[i] = P.caps[i];
-    for (uint32_t i = threadIdx.x; i < 2 * P.nwtab; i += blockDim.x) wt[i] = P.wtab[i];
+    for (uint32_t i = threadIdx.x; i < ncaps; i += blockDim.x) cp[i] = caps[i];
+    for (uint32_t i = threadIdx.x; i < 2 * nwt; i += blockDim.x) wt[i] = P.wtab[i];
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) cl[i] = P.cls[i];
     __syncthreads();
   }
   const uint16_t* s_trans = reinterpret_cast<const uint16_t*>(wsm);
   const uint32_t* s_caps = reinterpret_cast<const uint32_t*>(wsm + 2 * (size_t)P.ntrans_pad);
-  const uint32_t* s_wtab = s_caps + P.nstates;
-  const uint8_t* s_cls = reinterpret_cast<const uint8_t*>(s_wtab + 2 * P.nwtab);
+  const uint32_t* s_wtab = s_caps + ncaps;
+  const uint8_t* s_cls = reinterpret_cast<const uint8_t*>(s_wtab + 2 * nwt);
   const int lane = threadIdx.x & 63;
   const uint64_t r = (uint64_t)blockIdx.x * kWWaves + (threadIdx.x >> 6);
   if (r >= P.nrec) return;  // wave-uniform
@@ -72,24 +78,17 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
   const uint64_t slo = wlo + seg * lane < whi ? wlo + seg * lane : whi;
   const uint64_t shi = slo + seg < whi ? slo + seg : whi;
   const Tab<FMT> T{s_trans, s_cls, P.start, P.accb};
-  const Ctx C{s_caps, P.log_row, P.delta};
-  Win w;
-  w.lds = nullptr;
-  w.base = 0;
-  w.lend = 0;
-  w.g = P.g;
-  w.rend = P.rend;
-  w.eof = P.at_eof;
+  const Ctx C{s_caps, M == kWalkCtx ? 0u : P.log_row, P.delta};
+  Win w = win_of(P);
   w.wtab = s_wtab;
-  w.nwtab = P.nwtab;
-  w.bob = P.bob;
+  w.acap = s_caps;
   uint32_t ovf = 0;
 
   // speculative lane chains (lane 0 enters at the record's entry)
   uint64_t ent = (WRITE && lane == 0) ? P.entries[r] : slo;
   CountEm acc;
   uint64_t p = ent;
-  while (p < shi) p = chain_step<FMT, CountEm, true>(T, w, C, p, acc, +1, ovf);
+  while (p < shi) p = chain_step<FMT, CountEm, M>(T, w, C, p, acc, +1, ovf);
   uint64_t exi = p;  // first chain position >= shi (the entry itself when it lies beyond)
   // lane stitch rounds (a wrong entry moves one lane per round; chains that do
   // not resynchronise give up after 24 rounds: UGPU_FLAG_BUDGET, and the host
@@ -104,7 +103,7 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
     }
     if (ch) {
       uint64_t ne;
-      if (!merge<FMT, true>(T, w, C, ent, nx, shi, acc, ne, ovf)) exi = ne;
+      if (!merge<FMT, M>(T, w, C, ent, nx, shi, acc, ne, ovf)) exi = ne;
       ent = nx;
     }
   }
@@ -118,7 +117,7 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
     }
     WriteEm em{P.out_base[r] + incl - acc.cnt, P.out_capacity, P.out_start, P.out_len, P.out_cap};
     uint64_t q = ent;
-    while (q < shi) q = chain_step<FMT, WriteEm, true>(T, w, C, q, em, +1, ovf);
+    while (q < shi) q = chain_step<FMT, WriteEm, M>(T, w, C, q, em, +1, ovf);
     if (em.overflow) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
   } else {
     const uint64_t c = wave_sum(acc.cnt), d = wave_sum(acc.dg), dc = wave_sum(acc.dc);
@@ -137,34 +136,41 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
 }
 
-template <int FMT, bool WRITE>
+template <int FMT, bool WRITE, int M>
 hipError_t wfind_one(const ScanParams& P, hipStream_t stream)
 {
-  const size_t smem = wfind_smem(P.ntrans_pad, P.nstates, P.nwtab);
+  const size_t smem = wfind_smem(P.ntrans_pad, P.nstates, P.nwtab, M == kWalkCtx);
   static size_t attr_smem = 65536;
   if (smem > attr_smem) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wfind_kernel<FMT, WRITE>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wfind_kernel<FMT, WRITE, M>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_smem = smem;
   }
-  hipLaunchKernelGGL((wfind_kernel<FMT, WRITE>), dim3(P.grid), dim3(kWWaves * 64), smem, stream, P);
+  hipLaunchKernelGGL((wfind_kernel<FMT, WRITE, M>), dim3(P.grid), dim3(kWWaves * 64), smem, stream, P);
   return hipGetLastError();
+}
+
+template <int M>
+hipError_t wfind_mode(const ScanParams& P, uint32_t format, bool write, hipStream_t stream)
+{
+  if (format == 0) return write ? wfind_one<0, true, M>(P, stream) : wfind_one<0, false, M>(P, stream);
+  return write ? wfind_one<1, true, M>(P, stream) : wfind_one<1, false, M>(P, stream);
 }
 
 }  // namespace
 
 uint32_t wfind_unit() { return kWUnit; }
 uint32_t wfind_waves() { return kWWaves; }
-size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab)
+size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, bool ctx)
 {
-  return wfind_smem(ntrans_pad, nstates, nwtab);
+  return wfind_smem(ntrans_pad, nstates, nwtab, ctx);
 }
 
+// option W (P.wtab) or line anchors / option N (P.acap)
 hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream)
 {
-  if (format == 0) return write ? wfind_one<0, true>(P, stream) : wfind_one<0, false>(P, stream);
-  return write ? wfind_one<1, true>(P, stream) : wfind_one<1, false>(P, stream);
+  return P.acap ? wfind_mode<kWalkCtx>(P, format, write, stream) : wfind_mode<kWalkWord>(P, format, write, stream);
 }
 
 }  // namespace ugpu

@@ -29,6 +29,7 @@ RX_FIXED = 1
 RX_ICASE = 2
 RX_REFLEX = 4
 PAT_WORD = 1  # ugpu_dfa_create pattern_flags: option W
+PAT_EMPTY = 2  # ugpu_dfa_create pattern_flags: option N (empty matches)
 
 
 def compile_regex(regex, fixed=False, icase=False, reflex=False):
@@ -70,6 +71,19 @@ def host_tables(opc):
                                      ctypes.byref(start), ctypes.byref(accb)))
     return dict(info={f: getattr(info, f) for f, _ in _lib.DfaInfo._fields_}, trans=trans, cls=cls, caps=caps,
                 start=start.value, accb=accb.value)
+
+
+def host_context(opc):
+    """(acap u32[states * 4], anchored, start_acc): the per-context accept
+    indices acap[state * 4 + bol * 2 + eol] of the dense tables (tables.hpp)."""
+    a, p = _as_u32(opc)
+    info = _lib.DfaInfo()
+    check(lib.ugpu_tables_build_host(p, len(a), ctypes.byref(info), None, 0, None, None, 0, None, None))
+    acap = np.zeros(info.states * 4, np.uint32)
+    an, sa = ctypes.c_int(), ctypes.c_int()
+    check(lib.ugpu_tables_context_host(p, len(a), acap.ctypes.data_as(_lib.c_u32p), len(acap), ctypes.byref(an),
+                                       ctypes.byref(sa)))
+    return acap, bool(an.value), bool(sa.value)
 
 
 def host_prefilter(opc):
@@ -149,16 +163,19 @@ def host_xu(opc):
 class Pattern:
     """Compiled pattern (opcode words) with its device tables."""
 
-    def __init__(self, opc, word=False):
+    def __init__(self, opc, word=False, empty=False):
         """opc: opcode words (or a regex for compile_regex).  word=True is
         Matcher option W (ugrep -w, reflex::Matcher(pat, input, "W"),
-        src/ugrep.cpp:8616-8618): whole-buffer scans on wfind_kernel."""
+        src/ugrep.cpp:8616-8618): whole-buffer scans on wfind_kernel.
+        empty=True is option N (ugrep -Y, -x): empty matches are reported."""
         if isinstance(opc, (str, bytes)):
             opc = compile_regex(opc)
         self.opc, p = _as_u32(opc)
         self.word = bool(word)
+        self.empty = bool(empty)
         h = ctypes.c_void_p()
-        check(lib.ugpu_dfa_create(p, len(self.opc), PAT_WORD if word else 0, ctypes.byref(h)))
+        check(lib.ugpu_dfa_create(p, len(self.opc), (PAT_WORD if word else 0) | (PAT_EMPTY if empty else 0),
+                                  ctypes.byref(h)))
         self._h = h
 
     @property
@@ -375,6 +392,10 @@ class Scanner:
         t = _lib.Totals()
         check(lib.ugpu_scan_totals(self._h, ctypes.byref(t)))
         return t
+
+    def context(self, bol0):
+        """ugpu_scanner_context: whether dbuf[0] begins a line (anchored tables)."""
+        check(lib.ugpu_scanner_context(self._h, 1 if bol0 else 0))
 
     def stage(self, on=True):
         """Single-pass OFFSETS: COUNT scans stage the records of prefiltered tables."""
