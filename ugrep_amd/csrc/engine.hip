@@ -1142,7 +1142,10 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
                    uint64_t bias, uint64_t old_entry, uint64_t new_entry, ugpu_totals* delta, void* stream)
 {
   if (!s || !dbuf || !delta) return fail(UGPU_INVAL, "NULL argument");
-  if (s->word || s->wfast || s->wxc) return fail(UGPU_UNSUPPORTED, "option W across shards (at_wb needs the previous shard's bytes)");
+  // (anchored / option N tables also run wfind_kernel, s->word, but carry their
+  // line context in s->bol0: ugpu_scanner_context)
+  if ((s->word && !s->dfa->amode) || s->wfast || s->wxc)
+    return fail(UGPU_UNSUPPORTED, "option W across shards (at_wb needs the previous shard's bytes)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ScanParams P{};
   fill_tables(P, s->dfa);
