@@ -107,10 +107,11 @@ typedef struct ugpu_result
 /* Build the dense device tables from opcode words and upload them once to the
    current device.  pattern_flags: 0, or UGPU_PAT_WORD for Matcher option W
    (ugrep -w: matches bounded by word boundaries, src/ugrep.cpp:8616-8618,
-   lib/matcher.cpp:107, :142, :208, include/reflex/matcher.h:1194-1237); W scans
-   run wfind_kernel on whole buffers (ugpu_find_all, ugpu_scan with the buffer
-   start at dbuf[0]); ugpu_chain_fix and the stream API return UGPU_UNSUPPORTED
-   for W patterns.  UGPU_PAT_EMPTY: Matcher option N (ugrep -Y, and -x:
+   lib/matcher.cpp:107, :142, :208, include/reflex/matcher.h:1194-1237); at_wb
+   at a walk start reads the code point before it, so dbuf[0] counts as the
+   begin of the input and a scan that starts inside the input passes the bytes
+   before lo in dbuf (4 suffice; ugpu_find_all_multi and the stream API do).
+   UGPU_PAT_EMPTY: Matcher option N (ugrep -Y, and -x:
    src/ugrep.cpp:8381-8386, :8612-8613), empty matches are reported
    (lib/matcher.cpp:682-728; never at the end of the input).  Tables with line
    anchors (META_BOL ^, META_EOL $ edges, include/reflex/pattern.h:942-943, as
@@ -209,8 +210,9 @@ int ugpu_result_free(ugpu_result *res);
    (ugpu_chain_fix on the owning device when a chain enters a shard elsewhere
    than at its start), and OFFSETS records are copied straight from each
    device into their slice of the result.  Same result as ugpu_find_all.
-   Option W tables run ugpu_find_all on one device (at_wb at a shard start
-   needs the previous shard's bytes).  ndev <= 0: one shard per device. */
+   Each shard's copy starts 4 bytes before it (the code point at_wb reads for
+   option W, the byte at_bol reads for line anchors).  ndev <= 0: one shard per
+   device. */
 int ugpu_find_all_multi(const ugpu_dfa *dfa, const uint8_t *buf, uint64_t len, uint64_t start, uint32_t mode,
                         int ndev, ugpu_result **out);
 
@@ -228,8 +230,9 @@ int ugpu_scan(ugpu_scanner *sc, const uint8_t *dbuf, uint64_t lo, uint64_t hi, u
               uint64_t bias, void *stream);
 /* Context of the scanner's next scans: bol0 != 0 when dbuf[0] begins a line
    (it is the first byte of the input, or the byte before it is '\n'); the
-   default is 1.  Only line-anchored tables read it (a shard or stream window
-   that starts inside the input sets it from the byte before). */
+   default is 1.  Only line-anchored tables read it, for a walk at dbuf[0];
+   walks after dbuf[0] read the byte before them (the library's own shards and
+   streams keep 4 bytes before their range in dbuf instead). */
 int ugpu_scanner_context(ugpu_scanner *sc, int bol0);
 /* Synchronize the scanner's stream and return the totals of the last scan. */
 int ugpu_scan_totals(ugpu_scanner *sc, ugpu_totals *out);
@@ -261,7 +264,9 @@ int ugpu_scan_kernel_ms(ugpu_scanner *sc, float *ms);
    FIND chain is settled up to a point `keep` bytes before the end (or the end
    when `final`), the rest is carried to the next call.  Offsets are absolute
    (from the first byte ever fed); a match may span any number of chunks.  The
-   concatenation of all results equals ugpu_find_all over the whole input. */
+   concatenation of all results equals ugpu_find_all over the whole input
+   (also for option W and line anchors: the carry keeps the 4 bytes before the
+   settled position, the code point at_wb and the byte at_bol read). */
 typedef struct ugpu_stream ugpu_stream;
 
 /* keep: bytes held back from each non-final scan (a match that is still open
@@ -355,6 +360,15 @@ const char *ugpu_compile_error(void);
 
 const char *ugpu_last_error(void);
 const char *ugpu_version(void);
+
+/* Devices (no reference counterpart: its matchers are CPU threads).
+   ugpu_select_device makes `dev` the calling thread's device (hipSetDevice):
+   ugpu_find_all, ugpu_stream_create and scanners created afterwards on this
+   thread run there, with the table copy a ugpu_dfa keeps per device (uploaded
+   at the first use).  The drop-in adapter spreads ugrep's worker matchers over
+   the devices this way. */
+int ugpu_device_count(int *n);
+int ugpu_select_device(int dev);
 
 #ifdef __cplusplus
 }

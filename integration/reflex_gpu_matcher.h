@@ -46,9 +46,13 @@
 //     the reference's scan of a small buffer;
 //   * patterns with a selective prefilter (sparse_kernel, e.g. foo|bar|baz) use
 //     the GPU only while at most UGPU_ADAPTER_SPARSE_MAX (default 4) GpuMatchers
-//     exist: host buffers cross PCIe at ~55 GB/s, which a few reference AVX2
-//     cores match on such patterns (11 GB/s each), while dense patterns (C3/C4
-//     class, ~0.2-2 GB/s per core) always gain.  UGPU_ADAPTER_STATS=1 prints each
+//     per device exist: host buffers cross PCIe at ~55 GB/s per device link,
+//     which a few reference AVX2 cores match on such patterns (11 GB/s each),
+//     while dense patterns (C3/C4 class, ~0.2-2 GB/s per core) always gain;
+//   * devices: matchers are dealt round-robin over the visible devices
+//     (ugpu_select_device before every engine call), and a buffer of at least
+//     UGPU_ADAPTER_MULTI_MIN bytes (default 64 MiB) is cut over all of them
+//     (ugpu_find_all_multi: one H2D per device link).  UGPU_ADAPTER_STATS=1 prints each
 // matcher's GPU scan count to stderr when it is destroyed.
 //
 // Option N (ugrep -Y, and -x / patterns that start with ^ or end with $, which
@@ -59,9 +63,8 @@
 // (lib/pattern.cpp:4342-4430) can skip positions its DFA matches at -- ugrep -c
 // 'a$|ab' prints 0 on "xa\nb\nzzzz\n", and '^\w+' without N finds nothing --
 // and the GPU walks the DFA (tests/test_anchor.py records both).  Everything
-// else -- SCAN/SPLIT/MATCH, option A, option W on streams, tables the engine
-// rejects (\b, lookahead, W with anchors or N: UGPU_UNSUPPORTED) -- stays on the
-// CPU matcher.
+// else -- SCAN/SPLIT/MATCH, option A, tables the engine rejects (\b,
+// lookahead, W with anchors or N: UGPU_UNSUPPORTED) -- stays on the CPU matcher.
 #ifndef REFLEX_GPU_MATCHER_H
 #define REFLEX_GPU_MATCHER_H
 
@@ -89,6 +92,7 @@ class GpuMatcher : public Matcher {
       : Matcher(pattern, input, opt)
   {
     init_policy();
+    dev_ = next_device();
     ++live();
   }
   /// Clones (ugrep's worker threads, src/ugrep.cpp:4146, :9006) share the
@@ -96,8 +100,9 @@ class GpuMatcher : public Matcher {
   GpuMatcher(const GpuMatcher& m)
       : Matcher(m), tab_(m.tab_), tab_pat_(m.tab_pat_), tab_w_(m.tab_w_), tab_n_(m.tab_n_),
         tab_anchor_(m.tab_anchor_), sparse_(m.sparse_),
-        min_bytes_(m.min_bytes_), chunk_(m.chunk_), sparse_max_(m.sparse_max_)
+        min_bytes_(m.min_bytes_), chunk_(m.chunk_), multi_min_(m.multi_min_), sparse_max_(m.sparse_max_)
   {
+    dev_ = next_device();
     ++live();
   }
   virtual GpuMatcher* clone() { return new GpuMatcher(*this); }
@@ -117,6 +122,8 @@ class GpuMatcher : public Matcher {
                    why.empty() ? "-" : why.c_str());
     }
     ugpu_result_free(gres_);
+    if (gst_ != NULL)
+      on_device();
     ugpu_stream_destroy(gst_);
     --live();
   }
@@ -125,6 +132,8 @@ class GpuMatcher : public Matcher {
   {
     Matcher::reset(opt);
     drop_records();
+    if (gst_ != NULL)
+      on_device();
     ugpu_stream_destroy(gst_);
     gst_ = NULL;
     cpu_stream_ = false;
@@ -157,7 +166,7 @@ class GpuMatcher : public Matcher {
       return cpu(method, R_OPT_A);
     if (tables() == NULL)
       return cpu(method, tab_anchor_ ? R_ANCHOR : R_TABLE);
-    if (sparse_ && live() > sparse_max_)
+    if (sparse_ && live() > sparse_max_ * devices())
       return cpu(method, R_SPARSE);
     if (own_)
       return stream_match();
@@ -188,11 +197,11 @@ class GpuMatcher : public Matcher {
 
  private:
   // why the CPU matcher answered a call (adapter statistics)
-  enum Reason { R_METHOD, R_OPT_A, R_ANCHOR, R_TABLE, R_SPARSE, R_PARTIAL, R_SMALL, R_ENGINE, R_W_STREAM, kReasons };
+  enum Reason { R_METHOD, R_OPT_A, R_ANCHOR, R_TABLE, R_SPARSE, R_PARTIAL, R_SMALL, R_ENGINE, kReasons };
   static const char* reason_name(int r)
   {
-    static const char* const n[kReasons] = {"method", "option_A", "anchor_predictor", "table",         "sparse_limit",
-                                            "partial", "small",    "engine",           "option_W_stream"};
+    static const char* const n[kReasons] = {"method",  "option_A", "anchor_predictor", "table",
+                                            "sparse_limit", "partial",  "small",            "engine"};
     return n[r];
   }
   size_t cpu(Method method, int why)
@@ -310,6 +319,23 @@ class GpuMatcher : public Matcher {
     static std::atomic<int> n(0);
     return n;
   }
+  // visible devices (at least 1), and the next matcher's device
+  static int devices()
+  {
+    static const int n = [] {
+      int k = 0;
+      return ugpu_device_count(&k) == UGPU_OK && k > 0 ? k : 1;
+    }();
+    return n;
+  }
+  static int next_device()
+  {
+    static std::atomic<int> k(0);
+    return k++ % devices();
+  }
+  // this matcher's device current on the calling thread (ugrep calls a matcher
+  // from the worker thread that owns it, but clones are made elsewhere)
+  void on_device() const { (void)ugpu_select_device(dev_); }
   void drop_records()
   {
     ugpu_result_free(gres_);
@@ -341,6 +367,8 @@ class GpuMatcher : public Matcher {
     min_bytes_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : ~static_cast<size_t>(0);  // ~0: per table
     e = std::getenv("UGPU_ADAPTER_SPARSE_MAX");
     sparse_max_ = e && *e ? std::atoi(e) : 4;
+    e = std::getenv("UGPU_ADAPTER_MULTI_MIN");
+    multi_min_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (64u << 20);
     e = std::getenv("UGPU_ADAPTER_CHUNK");
     chunk_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (8u << 20);
     if (chunk_ == 0)
@@ -357,8 +385,12 @@ class GpuMatcher : public Matcher {
   bool rescan()
   {
     drop_records();
-    if (ugpu_find_all(tables(), reinterpret_cast<const uint8_t*>(buf_), end_, cur_, UGPU_MODE_OFFSETS, &gres_) !=
-        UGPU_OK)
+    on_device();
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(buf_);
+    const int rc = devices() > 1 && end_ - cur_ >= multi_min_
+                       ? ugpu_find_all_multi(tables(), b, end_, cur_, UGPU_MODE_OFFSETS, 0, &gres_)
+                       : ugpu_find_all(tables(), b, end_, cur_, UGPU_MODE_OFFSETS, &gres_);
+    if (rc != UGPU_OK)
       return false;  // (this input stays on the CPU matcher)
     ++scans_;
     gbuf_ = buf_;
@@ -372,8 +404,6 @@ class GpuMatcher : public Matcher {
   // stream was started at absolute offset sbase_ and has been fed up to sfed_.
   size_t stream_match()
   {
-    if (opt_.W)
-      return cpu(Const::FIND, R_W_STREAM);  // (at_wb at a window start needs the bytes before it)
     if (cpu_stream_)
       return cpu(Const::FIND, cpu_stream_why_);
     reset_text();
@@ -441,6 +471,7 @@ class GpuMatcher : public Matcher {
       }
       const size_t from = static_cast<size_t>(sfed_ - num_);
       drop_records();
+      on_device();
       if (ugpu_stream_feed(gst_, reinterpret_cast<const uint8_t*>(buf_ + from), end_ - from,
                            eof_ ? 1 : flush ? UGPU_FEED_FLUSH : 0, UGPU_MODE_OFFSETS, &gres_) != UGPU_OK)
       {
@@ -490,6 +521,7 @@ class GpuMatcher : public Matcher {
     drop_records();
     ugpu_stream_destroy(gst_);
     gst_ = NULL;
+    on_device();
     if (ugpu_stream_create(tables(), 0, &gst_) != UGPU_OK)
     {
       cpu_stream_ = true;
@@ -513,7 +545,8 @@ class GpuMatcher : public Matcher {
   const char* gbuf_ = NULL;
   // gcur_: the cursor this class left behind (after the scan or the last hit)
   size_t gend_ = 0, gcur_ = 0, gi_ = 0, scans_ = 0, scans_at_restart_ = 0;
-  size_t min_bytes_ = 0, chunk_ = 0;
+  size_t min_bytes_ = 0, chunk_ = 0, multi_min_ = 0;
+  int dev_ = 0;  // this matcher's device
   int sparse_max_ = 4;
   ugpu_stream* gst_ = NULL;
   uint64_t sbase_ = 0, sfed_ = 0, gcur_abs_ = 0;

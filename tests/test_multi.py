@@ -97,12 +97,36 @@ def test_multi_long_matches_and_unsynchronised_chains(U):
         assert (r.count, r.digest, r.dcap) == want, ndev
 
 
-def test_multi_option_w_runs_single_device(U):
-    """Option W: at_wb at a shard start needs the previous shard's bytes, so
-    the call runs one device; same result as ugpu_find_all."""
-    from oracle_lib import OracleDfa, gen
-    host = gen(4, 8, 0, 4 << 20)
-    opc = U.compile_regex(r"\w+")
-    pat = U.Pattern(opc, word=True)
-    r = U.find_all_multi(pat, host, ndev=4, offsets=False)
-    assert (r.count, r.digest, r.dcap) == OracleDfa(opc).find_w(host)[:3]
+W_PATTERNS = [r"\w+", r"[A-Za-z_][A-Za-z0-9_]*", "foo|bar|baz", r"\p{L}+\d*", "de|dei|é"]
+
+
+def _w_corpus(n):
+    """Mixed ASCII / 2-, 3- and 4-byte UTF-8 words, so that shard cuts land
+    inside code points and inside words."""
+    from oracle_lib import gen
+    data = gen(4, 8, 0, n).copy()
+    rng = np.random.default_rng(11)
+    pieces = ["é".encode(), "日本".encode(), "𝔘x".encode(), b"foo_bar", b" de ", b"dei\n"]
+    for at in rng.integers(0, n - 16, n // 64):
+        p = pieces[int(at) % len(pieces)]
+        data[int(at):int(at) + len(p)] = np.frombuffer(p, np.uint8)
+    return data
+
+
+def test_multi_option_w_shards(U):
+    """Option W across shard cuts: each shard's copy begins 4 bytes before it,
+    so at_wb at the cut reads the true code point before it; the stitch walks
+    with the W rules.  Records equal the oracle's option-W FIND and
+    ugpu_find_all."""
+    from oracle_lib import OracleDfa
+    host = _w_corpus(3 << 20)
+    for rx in W_PATTERNS:
+        opc = U.compile_regex(rx)
+        pat = U.Pattern(opc, word=True)
+        want = OracleDfa(opc).find_w(host, want_list=True)
+        one = U.find_all(pat, torch.from_numpy(host).cuda(), offsets=True)
+        assert (one.count, one.digest, one.dcap) == want[:3], rx
+        for ndev in (3, 7, 16):
+            r = U.find_all_multi(pat, host, ndev=ndev, offsets=True)
+            assert (r.count, r.digest, r.dcap) == want[:3], (rx, ndev)
+            assert r.triples() == want[3], (rx, ndev)

@@ -135,3 +135,27 @@ def test_stream_flush_settles_decided_matches(U, patterns):
                 sep = int(np.nonzero(np.isin(data[:c], np.frombuffer(b" \n", np.uint8)))[0][-1])
                 assert [t for t in want[0] if t[0] + t[1] <= sep] == [t for t in trip if t[0] + t[1] <= sep], (pname, c)
         assert trip == want[0], pname
+
+
+def test_stream_option_w(U):
+    """Option W on streamed input: the carry keeps the 4 bytes before the
+    settled position, so at_wb at a chunk start reads the true code point
+    before it; chunk cuts inside code points and words, flushed and plain
+    feeds -- the concatenation equals the oracle's option-W FIND."""
+    from oracle_lib import OracleDfa
+    from test_multi import W_PATTERNS, _w_corpus
+    data = _w_corpus(1 << 20)
+    rng = np.random.default_rng(5)
+    for rx in W_PATTERNS:
+        opc = U.compile_regex(rx)
+        pat = U.Pattern(opc, word=True)
+        want = OracleDfa(opc).find_w(data, want_list=True)
+        for flush in (False, True):
+            st = U.Stream(pat, keep=4096)
+            trip, i = [], 0
+            cuts = sorted(set(int(x) for x in rng.integers(1, data.size, 60)))
+            for c in cuts + [data.size]:
+                r = st.feed(data[i:c].tobytes(), final=c == data.size, flush=flush and c < data.size)
+                trip += r.triples()
+                i = c
+            assert trip == want[3], (rx, flush)

@@ -53,11 +53,10 @@ def _run_all(exe, env):
     return bad, ledger
 
 
-# CPU answers that are by design: option W on streamed input (at_wb at a
-# window start needs the bytes before the window), and line anchors the
-# reference's match predictor decides (anchored tables without option N or with
-# anchors inside the regex: tests/test_anchor.py)
-BY_DESIGN = {"anchor_predictor", "option_W_stream"}
+# CPU answers that are by design: line anchors the reference's match predictor
+# decides (anchored tables without option N or with anchors inside the regex:
+# tests/test_anchor.py)
+BY_DESIGN = {"anchor_predictor"}
 LEDGER = os.path.join(ROOT, "tests", "golden", "dropin_fallbacks.json")
 
 
@@ -79,8 +78,7 @@ def test_fallback_ledger_is_consistent():
     if not os.path.exists(LEDGER):
         pytest.skip("no ledger yet")
     led = json.load(open(LEDGER))
-    known = {"method", "option_A", "anchor_predictor", "table", "sparse_limit", "partial", "small", "engine",
-             "option_W_stream"}
+    known = {"method", "option_A", "anchor_predictor", "table", "sparse_limit", "partial", "small", "engine"}
     expects = {c["expect"] for c in SPEC["cases"]}
     for e, why in led["cpu_cases"].items():
         assert e in expects, e

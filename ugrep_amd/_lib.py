@@ -116,6 +116,8 @@ def _load():
         "ugpu_compile_error": (ctypes.c_char_p, []),
         "ugpu_last_error": (ctypes.c_char_p, []),
         "ugpu_version": (ctypes.c_char_p, []),
+        "ugpu_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "ugpu_select_device": (ctypes.c_int, [ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -134,7 +134,13 @@ __device__ __forceinline__ bool at_we(const Win& w, uint64_t q, uint32_t& ovf)
   }
   const uint32_t c = w.g[q];
   if (c == '_') return false;
-  if ((c & 0xC0) == 0xC0) return !wisword(w, wutf8(w, q));
+  if ((c & 0xC0) == 0xC0) {
+    // the code point after the match decides; when its bytes run past a readable
+    // end that is not EOF, so does the next chunk (a stream feed, a shard halo)
+    const uint64_t need = c >= 0xF0 ? 4u : c >= 0xE0 ? 3u : 2u;
+    if (q + need > w.rend && !w.eof) ovf = 1;
+    return !wisword(w, wutf8(w, q));
+  }
   return !walnum(c);
 }
 

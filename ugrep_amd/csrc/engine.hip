@@ -402,6 +402,8 @@ int forest_run(ugpu_scanner* s, ScanParams P, uint64_t entry, bool write, hipStr
   return UGPU_OK;
 }
 
+int dfa_on(const ugpu_dfa* d, int dev, const ugpu_dfa** out);
+
 }  // namespace
 
 extern "C" {
@@ -409,6 +411,23 @@ extern "C" {
 const char* ugpu_last_error(void) { return g_err.c_str(); }
 
 const char* ugpu_version(void) { return "ugrep_amd 0.1 (gfx950)"; }
+
+int ugpu_device_count(int* n)
+{
+  if (!n) return fail(UGPU_INVAL, "NULL argument");
+  *n = 0;
+  HIP_TRY(hipGetDeviceCount(n));
+  return UGPU_OK;
+}
+
+int ugpu_select_device(int dev)
+{
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (dev < 0 || dev >= n) return fail(UGPU_INVAL, "no such device");
+  HIP_TRY(hipSetDevice(dev));
+  return UGPU_OK;
+}
 
 int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa** out)
 {
@@ -719,6 +738,13 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
 {
   if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
   *out = nullptr;
+  {
+    // the table copy on the calling thread's device (ugpu_select_device)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(UGPU_DEVICE, "hipGetDevice");
+    const int rc = dfa_on(dfa, dev, &dfa);
+    if (rc) return rc;
+  }
   ugpu_scanner* s = new (std::nothrow) ugpu_scanner();
   if (!s) return fail(UGPU_NOMEM, "host allocation");
   s->dfa = dfa;
@@ -1142,11 +1168,9 @@ int ugpu_chain_fix(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t h
                    uint64_t bias, uint64_t old_entry, uint64_t new_entry, ugpu_totals* delta, void* stream)
 {
   if (!s || !dbuf || !delta) return fail(UGPU_INVAL, "NULL argument");
-  // (anchored / option N tables also run wfind_kernel, s->word, but carry their
-  // line context in s->bol0: ugpu_scanner_context)
-  if ((s->word && !s->dfa->amode) || s->wfast || s->wxc)
-    return fail(UGPU_UNSUPPORTED, "option W across shards (at_wb needs the previous shard's bytes)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // (option W: the exact W walk -- also for scanners whose scans take the
+  // non-W kernels, wfast / wxc; at_wb at lo reads dbuf[lo - 4 .. lo))
   ScanParams P{};
   fill_tables(P, s->dfa);
   P.bol0 = s->bol0;
@@ -1305,8 +1329,14 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
     std::free(r);
     return hip_fail(e, "hipGetDevice");
   }
+  // (the calling thread's device: the table copy there, ugpu_select_device)
+  int rc = dfa_on(dfa, dev, &dfa);
+  if (rc) {
+    std::free(r);
+    return rc;
+  }
   ugpu_scanner* s = nullptr;
-  int rc = scanner_acquire(dfa, &s);
+  rc = scanner_acquire(dfa, &s);
   if (rc) {
     std::free(r);
     return rc;
@@ -1389,30 +1419,32 @@ int dfa_on(const ugpu_dfa* d, int dev, const ugpu_dfa** out)
 struct Shard {
   int dev = 0;
   uint64_t lo = 0, hi = 0, rend = 0;
+  uint64_t org = 0;  // buffer offset of dbuf[0]: lo minus the context prefix (at most 4 bytes: at_wb's code
+                     // point before lo, at_bol's byte)
   const ugpu_dfa* tab = nullptr;
   ugpu_scanner* sc = nullptr;
   FindWs* ws = nullptr;
-  const uint8_t* dbuf = nullptr;  // the shard's bytes on its device (dbuf[0] = buffer byte lo)
+  const uint8_t* dbuf = nullptr;  // the shard's bytes on its device (dbuf[0] = buffer byte org)
   ugpu_totals tot{};
   uint64_t entry = 0, exit = 0;   // global chain entry / exit (entry = lo speculatively)
   uint64_t base = 0;              // first record index (OFFSETS)
   int rc = UGPU_OK;
 };
 
-// bytes [lo, rend) of the caller's buffer onto the shard's device
+// bytes [org, rend) of the caller's buffer onto the shard's device
 int shard_load(Shard& sh, const uint8_t* buf, bool host, int src_dev)
 {
-  const uint64_t n = sh.rend - sh.lo;
+  const uint64_t n = sh.rend - sh.org;
   hipError_t e;
   if (!host && src_dev == sh.dev) {
-    sh.dbuf = buf + sh.lo;
+    sh.dbuf = buf + sh.org;
     return UGPU_OK;
   }
   if ((e = sh.ws->reserve_in(n)) != hipSuccess) return hip_fail(e, "shard input");
   if (host)
-    e = hipMemcpyAsync(sh.ws->d_in, buf + sh.lo, n, hipMemcpyHostToDevice, sh.ws->st);
+    e = hipMemcpyAsync(sh.ws->d_in, buf + sh.org, n, hipMemcpyHostToDevice, sh.ws->st);
   else
-    e = hipMemcpyPeerAsync(sh.ws->d_in, sh.dev, buf + sh.lo, src_dev, n, sh.ws->st);
+    e = hipMemcpyPeerAsync(sh.ws->d_in, sh.dev, buf + sh.org, src_dev, n, sh.ws->st);
   if (e != hipSuccess) return hip_fail(e, "shard input copy");
   sh.dbuf = sh.ws->d_in;
   return UGPU_OK;
@@ -1432,31 +1464,21 @@ void shard_scan(Shard& sh, const uint8_t* buf, uint64_t len, bool host, int src_
     sh.rc = fail(UGPU_NOMEM, "find workspace");
     return;
   }
-  // (anchored tables: does the shard's first byte begin a line?)
-  uint8_t prev = '\n';
-  if (sh.lo > 0) {
-    if (host) {
-      prev = buf[sh.lo - 1];
-    } else {
-      const hipError_t e = hipMemcpy(&prev, buf + sh.lo - 1, 1, hipMemcpyDeviceToHost);
-      if (e != hipSuccess) {
-        sh.rc = hip_fail(e, "shard context byte");
-        return;
-      }
-    }
-  }
-  ugpu_scanner_context(sh.sc, prev == '\n');
+  // the shard's line context and the code point before it come with its bytes:
+  // dbuf[0] is the buffer's first byte (BOB) or 4 bytes before lo
+  ugpu_scanner_context(sh.sc, 1);
+  const uint64_t o = sh.org;
   for (int attempt = 0; attempt < 2; ++attempt) {
     if ((sh.rc = shard_load(sh, buf, host, src_dev)) != UGPU_OK) return;
     sh.sc->stage_once = mode == UGPU_MODE_OFFSETS;
-    sh.rc = ugpu_scan(sh.sc, sh.dbuf, 0, sh.hi - sh.lo, sh.rend - sh.lo, sh.rend == len, sh.lo, sh.ws->st);
+    sh.rc = ugpu_scan(sh.sc, sh.dbuf, sh.lo - o, sh.hi - o, sh.rend - o, sh.rend == len, o, sh.ws->st);
     if (!sh.rc) sh.rc = ugpu_scan_totals(sh.sc, &sh.tot);
     if (sh.rc != UGPU_HALO || sh.rend == len) break;
     sh.rend = len;
   }
   if (sh.rc) return;
   sh.entry = sh.lo;
-  sh.exit = sh.tot.exit + sh.lo;
+  sh.exit = sh.tot.exit + o;
 }
 
 // the shard's records into r at its base (a shard whose chain entry moved
@@ -1471,7 +1493,7 @@ void shard_records(Shard& sh, uint64_t len, ugpu_result* r)
   if (n == 0) return;
   if (sh.entry != sh.lo) {
     ugpu_totals t{};
-    sh.rc = ugpu_scan(sh.sc, sh.dbuf, sh.entry - sh.lo, sh.hi - sh.lo, sh.rend - sh.lo, sh.rend == len, sh.lo,
+    sh.rc = ugpu_scan(sh.sc, sh.dbuf, sh.entry - sh.org, sh.hi - sh.org, sh.rend - sh.org, sh.rend == len, sh.org,
                       sh.ws->st);
     if (!sh.rc) sh.rc = ugpu_scan_totals(sh.sc, &t);
     if (sh.rc) return;
@@ -1520,10 +1542,9 @@ int ugpu_find_all_multi(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, u
   HIP_TRY(hipGetDevice(&cur));
   if (devices < 1) return fail(UGPU_DEVICE, "no device");
   if (ndev <= 0) ndev = devices;
-  // tiny ranges and option W (at_wb at a shard start needs the previous
-  // shard's bytes): one device
+  // tiny ranges: one device
   const uint64_t span = len - start;
-  if (ndev == 1 || dfa->d_wtab || span < (uint64_t)ndev * 4096) return ugpu_find_all(dfa, buf, len, start, mode, out);
+  if (ndev == 1 || span < (uint64_t)ndev * 4096) return ugpu_find_all(dfa, buf, len, start, mode, out);
   bool host = true;
   int src_dev = cur;
   {
@@ -1542,6 +1563,7 @@ int ugpu_find_all_multi(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, u
     sh.dev = k % devices;
     sh.lo = start + span * (uint64_t)k / (uint64_t)ndev;
     sh.hi = start + span * (uint64_t)(k + 1) / (uint64_t)ndev;
+    sh.org = sh.lo > 4 ? sh.lo - 4 : 0;
     sh.rend = sh.hi + halo < len ? sh.hi + halo : len;
     sh.tab = dfa;
   }
@@ -1576,14 +1598,14 @@ int ugpu_find_all_multi(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, u
     ugpu_totals d{};
     const hipError_t he = hipSetDevice(sh.dev);
     if (he != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
-    rc = ugpu_chain_fix(sh.sc, sh.dbuf, 0, sh.hi - sh.lo, sh.rend - sh.lo, sh.rend == len, sh.lo, sh.entry - sh.lo,
-                        e - sh.lo, &d, sh.ws->st);
+    rc = ugpu_chain_fix(sh.sc, sh.dbuf, sh.lo - sh.org, sh.hi - sh.org, sh.rend - sh.org, sh.rend == len, sh.org,
+                        sh.entry - sh.org, e - sh.org, &d, sh.ws->st);
     if (rc) return finish(rc);
     sh.tot.count += d.count;
     sh.tot.digest += d.digest;
     sh.tot.dcap += d.dcap;
     sh.entry = e;
-    if (d.exit != ~0ull) sh.exit = d.exit + sh.lo;
+    if (d.exit != ~0ull) sh.exit = d.exit + sh.org;
   }
   ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
   if (!r) return finish(fail(UGPU_NOMEM, "host allocation"));
@@ -1892,9 +1914,11 @@ int ugpu_is_binary(const uint8_t* dbuf, uint64_t len, uint32_t flags, int* binar
 }
 
 // ---------------------------------------------------------------- streaming
-// Device buffer holds the unsettled carry followed by the new chunk; each feed
-// scans [0, hi) of it with the chain entering at 0 (the previous settled
-// exit), readable to the end, and carries [exit, n) into the other buffer.
+// Device buffer holds a context prefix (the up to 4 bytes before the settled
+// chain position: at_wb's code point for option W, at_bol's byte for line
+// anchors), the unsettled carry and the new chunk; each feed scans [ctx, hi)
+// of it with the chain entering at ctx (the previous settled exit), readable
+// to the end, and carries [exit - 4, n) into the other buffer.
 struct ugpu_stream {
   const ugpu_dfa* dfa = nullptr;
   ugpu_scanner* sc = nullptr;
@@ -1902,10 +1926,10 @@ struct ugpu_stream {
   uint8_t* buf[2] = {nullptr, nullptr};
   uint64_t cap = 0;    // capacity of each buffer (bytes, + 16 padding allocated)
   int cur = 0;         // buffer holding the carry
-  uint64_t carry = 0;  // unsettled bytes at buf[cur][0..carry)
-  uint64_t base = 0;   // absolute offset of buf[cur][0] = the settled chain position
+  uint64_t carry = 0;  // bytes at buf[cur][0..carry): the prefix, then the unsettled bytes
+  uint64_t ctx = 0;    // prefix bytes (4, or fewer at the stream's start: buf[cur][0] is its first byte)
+  uint64_t base = 0;   // absolute offset of buf[cur][ctx] = the settled chain position
   bool done = false;
-  uint32_t bol0 = 1;   // buf[cur][0] begins a line (anchored tables: the byte before it is '\n')
 };
 
 namespace {
@@ -1948,13 +1972,15 @@ int ugpu_stream_create(const ugpu_dfa* dfa, uint64_t keep, ugpu_stream** out)
   *out = nullptr;
   ugpu_stream* st = new (std::nothrow) ugpu_stream();
   if (!st) return fail(UGPU_NOMEM, "host allocation");
-  if (dfa->d_wtab) {
+  int dev = 0;
+  int rc = hipGetDevice(&dev) == hipSuccess ? dfa_on(dfa, dev, &dfa) : fail(UGPU_DEVICE, "hipGetDevice");
+  if (rc) {
     delete st;
-    return fail(UGPU_UNSUPPORTED, "option W on streamed input");
+    return rc;
   }
   st->dfa = dfa;
   st->keep = keep ? keep : (64ull << 10);
-  int rc = ugpu_scanner_create(dfa, &st->sc);
+  rc = ugpu_scanner_create(dfa, &st->sc);
   if (rc) {
     delete st;
     return rc;
@@ -1990,11 +2016,12 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
   if (len) HIP_TRY(hipMemcpy(b + st->carry, chunk, len, hipMemcpyHostToDevice));
   ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
   if (!r) return fail(UGPU_NOMEM, "host allocation");
-  ugpu_scanner_context(st->sc, (int)st->bol0);
+  ugpu_scanner_context(st->sc, 1);  // (buf[cur][0] is the stream's first byte or 4 bytes before lo)
+  const uint64_t lo = st->ctx, bias = st->base - lo;
   // settle the chain up to `keep` bytes before the end (all of it when final);
   // a walk still open at the end of the bytes so far means hi was too close
-  uint64_t hi = final ? n : (n > st->keep ? n - st->keep : 0);
-  uint64_t exit = 0;
+  uint64_t hi = final ? n : (n > lo + st->keep ? n - st->keep : lo);
+  uint64_t exit = lo;
   ugpu_totals tot{};
   if (flush && !final) {
     // settle as far as the bytes decide: the largest hi whose chain has no walk
@@ -2002,12 +2029,12 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
     // from the end by 16, 64, 256, ... bytes, then bisect between the last hi
     // that was too close and the first that was not
     auto try_hi = [&](uint64_t h) -> int {
-      int c = ugpu_scan(st->sc, b, 0, h, n, 0, st->base, nullptr);
+      int c = ugpu_scan(st->sc, b, lo, h, n, 0, bias, nullptr);
       if (!c) c = ugpu_scan_totals(st->sc, &tot);
       return c;
     };
-    uint64_t good = 0, bad = n + 1, h = n, back = 16, last = ~0ull;
-    while (h > 0) {
+    uint64_t good = lo, bad = n + 1, h = n, back = 16, last = ~0ull;
+    while (h > lo) {
       rc = try_hi(h);
       last = h;
       if (rc == UGPU_OK) {
@@ -2019,7 +2046,7 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
         return rc;
       }
       bad = h;
-      h = n > back ? n - back : 0;
+      h = n > lo + back ? n - back : lo;
       back *= 4;
     }
     while (bad - good > 1) {
@@ -2037,18 +2064,18 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
     }
     hi = good;
     rc = UGPU_OK;
-    if (hi > 0 && last != hi) rc = try_hi(hi);  // (the scanner holds the last scan)
+    if (hi > lo && last != hi) rc = try_hi(hi);  // (the scanner holds the last scan)
     if (rc) {
       std::free(r);
       return rc;
     }
-    exit = hi > 0 ? tot.exit : 0;
+    exit = hi > lo ? tot.exit : lo;
   }
-  while (hi > 0 && !(flush && !final)) {
-    rc = ugpu_scan(st->sc, b, 0, hi, n, final ? 1 : 0, st->base, nullptr);
+  while (hi > lo && !(flush && !final)) {
+    rc = ugpu_scan(st->sc, b, lo, hi, n, final ? 1 : 0, bias, nullptr);
     if (!rc) rc = ugpu_scan_totals(st->sc, &tot);
     if (rc == UGPU_HALO && !final) {
-      hi /= 2;
+      hi = lo + (hi - lo) / 2;
       continue;
     }
     if (rc) {
@@ -2058,7 +2085,7 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
     exit = final ? n : tot.exit;
     break;
   }
-  if (hi > 0) {
+  if (hi > lo) {
     r->count = tot.count;
     r->digest = tot.digest;
     r->dcap = tot.dcap;
@@ -2087,18 +2114,16 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
       }
     }
   }
-  // carry [exit, n) to the other buffer; the chain resumes at its first byte
-  // (an anchored table also needs to know whether the byte before it is '\n')
-  if (st->dfa->amode && exit > 0) {
-    uint8_t prev = 0;
-    HIP_TRY(hipMemcpy(&prev, b + exit - 1, 1, hipMemcpyDeviceToHost));
-    st->bol0 = prev == '\n' ? 1u : 0u;
-  }
-  const uint64_t keep_n = n - exit;
-  if (keep_n) HIP_TRY(hipMemcpy(st->buf[1 - st->cur], b + exit, keep_n, hipMemcpyDeviceToDevice));
+  // carry [exit - ctx', n) to the other buffer, ctx' = the up to 4 bytes before
+  // the exit (fewer only when they reach the stream's first byte); the chain
+  // resumes at the byte after them
+  const uint64_t nctx = exit < 4 ? exit : 4;  // (exit >= lo: buf[cur][0] is the first byte when exit < 4)
+  const uint64_t keep_n = n - exit + nctx;
+  if (keep_n) HIP_TRY(hipMemcpy(st->buf[1 - st->cur], b + exit - nctx, keep_n, hipMemcpyDeviceToDevice));
   st->cur = 1 - st->cur;
   st->carry = keep_n;
-  st->base += exit;
+  st->ctx = nctx;
+  st->base += exit - lo;
   if (final) st->done = true;
   *out = r;
   return UGPU_OK;

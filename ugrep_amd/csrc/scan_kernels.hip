@@ -149,13 +149,15 @@ __global__ void chain_fix_kernel(ScanParams P, uint64_t old_entry, uint64_t new_
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const Tab<FMT> T{P.trans, P.cls, P.start, P.accb};
   const Ctx C = P.acap ? Ctx{P.acap, 0u, P.delta} : Ctx{P.caps, P.log_row, P.delta};
-  Win w = win_of(P);
-  w.wtab = nullptr;  // (option W is not stitched across shards: the host refuses it)
+  // (option W: at_wb reads the bytes before a walk start; the caller's buffer
+  // holds the code point before lo -- shard and stream prefixes, engine.hip)
+  const Win w = win_of(P);
   uint32_t ovf = 0, over = 0;
   CountEm d;
   uint64_t ne = 0;
-  bool met = P.acap ? merge<FMT, kWalkCtx>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over)
-                    : merge<FMT>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over);
+  bool met = P.acap   ? merge<FMT, kWalkCtx>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over)
+             : P.wtab ? merge<FMT, kWalkWord>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over)
+                      : merge<FMT>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over);
   DevTotals* t = P.totals;
   t->count = d.cnt;
   t->digest = d.dg;

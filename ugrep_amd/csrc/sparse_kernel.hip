@@ -304,13 +304,23 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
   }
   const uint32_t any0 = X[0][0] | X[0][1] | X[0][2] | X[0][3], any1 = X[1][0] | X[1][1] | X[1][2] | X[1][3];
   const uint32_t any2 = X[2][0] | X[2][1] | X[2][2] | X[2][3], any3 = X[3][0] | X[3][1] | X[3][2] | X[3][3];
-  if (!__ballot((any0 | any1 | any2 | any3) != 0)) return;  // the common case: no candidate in the tile
+  // (tail: the tile holds the last two readable positions of a non-final range)
+  const bool tail = !P.at_eof && ts + kWaveTile + 2 > P.rend && ts < P.rend;
+  if (!tail && !__ballot((any0 | any1 | any2 | any3) != 0)) return;  // the common case: no candidate in the tile
   const uint32_t anyk[4] = {any0, any1, any2, any3};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    if (!__ballot(anyk[k] != 0)) continue;
+    if (!tail && !__ballot(anyk[k] != 0)) continue;
     uint32_t mk = flags4(X[k][0]) | (flags4(X[k][1]) << 4) | (flags4(X[k][2]) << 8) | (flags4(X[k][3]) << 12);
     const uint64_t p0 = ts + 1024u * k + 16u * lane;
+    if (!P.at_eof && p0 + 18 > P.rend && p0 < P.rend) {
+      // the last two readable positions of a non-final range: their prefilter
+      // window reaches bytes not read yet (past rend the granule holds stale
+      // bytes), so they stay candidates and their walks report HALO
+      const uint64_t lo2 = P.rend >= 2 ? P.rend - 2 : 0;
+      const uint64_t a = lo2 > p0 ? lo2 - p0 : 0, z = P.rend - p0 > 16 ? 16 : P.rend - p0;
+      mk |= (uint32_t)((lowbits(z) & ~lowbits(a)) & 0xffffu);
+    }
     if (edge) {
       const uint64_t a = wlo > p0 ? (wlo - p0 > 16 ? 16 : wlo - p0) : 0;
       const uint64_t z = whi > p0 ? (whi - p0 > 16 ? 16 : whi - p0) : 0;
