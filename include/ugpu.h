@@ -198,6 +198,31 @@ int ugpu_find_all(const ugpu_dfa *dfa, const uint8_t *buf, uint64_t len, uint64_
                   ugpu_result **out);
 int ugpu_result_free(ugpu_result *res);
 
+/* Records for a consumer that pops them one at a time (the drop-in matcher's
+   find() loop, lib/matcher.cpp:42-750 returning one match per call), at the
+   rate PCIe moves the input: a host buffer goes H2D in chunks
+   (UGPU_REC_CHUNK, default 64 MiB) on a copy thread, each chunk is scanned
+   from the true chain entry as soon as it (and a 1 MiB halo) is resident, its
+   records are packed to 6 B (8 B when the table has several accept indices)
+   and copied asynchronously into pinned host memory, so input copy, scans and
+   record copy overlap.  ugpu_find_records returns once the last input byte is
+   on the device (a host buffer may then go away); scans and record copies go
+   on behind the consumer on a pipeline thread.  ugpu_records_next pops the
+   records in chain order, waiting for the pipeline where needed (1 = a record,
+   0 = none left, -code on a pipeline error, after which the consumer may go on
+   from the last record's end on the CPU: FIND chains agree there; start, len
+   and cap must not be NULL); ugpu_records_totals waits for the end and equals
+   ugpu_find_all's totals.  A device buffer must stay valid until
+   ugpu_records_free, which waits for the pipeline. */
+typedef struct ugpu_records ugpu_records;
+int ugpu_find_records(const ugpu_dfa *dfa, const uint8_t *buf, uint64_t len, uint64_t start, ugpu_records **out);
+int ugpu_records_next(ugpu_records *r, uint64_t *start, uint32_t *len, uint32_t *cap);
+int ugpu_records_totals(ugpu_records *r, uint64_t *count, uint64_t *digest, uint64_t *dcap);
+/* Pop every remaining record, returning their number and digests (what a
+   native consumer's loop costs; tests and benchmarks). */
+int ugpu_records_drain(ugpu_records *r, uint64_t *n, uint64_t *digest, uint64_t *dcap);
+int ugpu_records_free(ugpu_records *r);
+
 /* Multi-device FIND (the reference has no counterpart: one
    buffer is always scanned by one thread, src/ugrep.cpp:4118-4480).  One
    process drives the devices: [start, len) is cut into `ndev` contiguous

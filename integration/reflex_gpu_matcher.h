@@ -121,6 +121,7 @@ class GpuMatcher : public Matcher {
                    gpu_finds_, cpu_finds(), tab_pat_ == NULL ? "none" : tab_ ? "gpu" : "unsupported",
                    why.empty() ? "-" : why.c_str());
     }
+    src_.clear();
     ugpu_result_free(gres_);
     if (gst_ != NULL)
       on_device();
@@ -180,18 +181,21 @@ class GpuMatcher : public Matcher {
     // same address and size (ugrep re-buffers one std::string per line,
     // src/ugrep.cpp:733-740): any cursor behind the one this class last left
     // means the records may be stale, so scan again
-    if (gres_ == NULL || gbuf_ != buf_ || gend_ != end_ || cur_ < gcur_ || inside_match())
+    if (cpu_buf_ == buf_ && cpu_end_ == end_)
+      return cpu(method, R_ENGINE);  // (the engine failed on this buffer)
+    if (!src_.live() || gbuf_ != buf_ || gend_ != end_ || cur_ < gcur_ || inside_match())
       if (!rescan())
-        return cpu(method, R_ENGINE);
+        return engine_failed(method);
+    // (records that start before the cursor: the caller skipped past them)
+    while (src_.have && src_.start < cur_)
+      src_.pop();
+    if (src_.err)
+      return engine_failed(method);
     ++gpu_finds_;
-    while (gi_ < gres_->count && gres_->start[gi_] < cur_)
-      ++gi_;
-    if (gi_ >= gres_->count)
+    if (!src_.have)
       return exhausted();
-    const size_t start = static_cast<size_t>(gres_->start[gi_]);
-    const size_t len = gres_->len[gi_];
-    const size_t cap = gres_->cap[gi_];
-    ++gi_;
+    const size_t start = static_cast<size_t>(src_.start), len = src_.len, cap = src_.cap;
+    src_.pop();
     return hit(start, len, cap);
   }
 
@@ -341,6 +345,7 @@ class GpuMatcher : public Matcher {
     ugpu_result_free(gres_);
     gres_ = NULL;
     gi_ = 0;
+    src_.clear();
   }
   size_t hit(size_t start, size_t len, size_t cap)
   {
@@ -374,22 +379,42 @@ class GpuMatcher : public Matcher {
     if (chunk_ == 0)
       chunk_ = 1;
   }
-  // cur_ lies strictly inside a match of the current record set
+  // cur_ (at or after the cursor this class left) lies strictly inside a
+  // pending record; the records before it are dropped on the way, the caller
+  // skipped past them
   bool inside_match()
   {
-    size_t i = gi_ > 0 ? gi_ - 1 : 0;
-    while (i < gres_->count && gres_->start[i] + gres_->len[i] <= cur_)
-      ++i;
-    return i < gres_->count && gres_->start[i] < cur_;
+    while (src_.have && src_.start < cur_ && src_.start + src_.len <= cur_)
+      src_.pop();
+    return src_.have && src_.start < cur_;
+  }
+  // the engine failed on this buffer (also midway through its records: the
+  // CPU matcher goes on from the cursor, where the FIND chains agree)
+  size_t engine_failed(Method method)
+  {
+    drop_records();
+    cpu_buf_ = buf_;
+    cpu_end_ = end_;
+    return cpu(method, R_ENGINE);
   }
   bool rescan()
   {
     drop_records();
     on_device();
     const uint8_t* b = reinterpret_cast<const uint8_t*>(buf_);
-    const int rc = devices() > 1 && end_ - cur_ >= multi_min_
-                       ? ugpu_find_all_multi(tables(), b, end_, cur_, UGPU_MODE_OFFSETS, 0, &gres_)
-                       : ugpu_find_all(tables(), b, end_, cur_, UGPU_MODE_OFFSETS, &gres_);
+    int rc;
+    if (devices() > 1 && end_ - cur_ >= multi_min_) {
+      rc = ugpu_find_all_multi(tables(), b, end_, cur_, UGPU_MODE_OFFSETS, 0, &gres_);
+      if (rc == UGPU_OK)
+        src_.set(gres_);
+    } else {
+      // the pipelined host path: records popped from pinned memory as find()
+      // asks for them (ugpu_find_records)
+      ugpu_records* r = NULL;
+      rc = ugpu_find_records(tables(), b, end_, cur_, &r);
+      if (rc == UGPU_OK)
+        src_.set(r);
+    }
     if (rc != UGPU_OK)
       return false;  // (this input stays on the CPU matcher)
     ++scans_;
@@ -536,6 +561,57 @@ class GpuMatcher : public Matcher {
     return true;
   }
 
+  // the records of a whole-buffer scan, popped in chain order: a
+  // ugpu_find_records cursor, or a ugpu_result (multi-device scans)
+  struct Source {
+    ugpu_records* rec = NULL;
+    const ugpu_result* res = NULL;
+    size_t i = 0;
+    bool have = false, err = false;
+    uint64_t start = 0;
+    uint32_t len = 0, cap = 0;
+    bool live() const { return rec != NULL || res != NULL; }
+    void clear()
+    {
+      ugpu_records_free(rec);
+      rec = NULL;
+      res = NULL;  // (owned by gres_)
+      have = err = false;
+    }
+    void set(ugpu_records* r)
+    {
+      clear();
+      rec = r;
+      pop();
+    }
+    void set(const ugpu_result* r)
+    {
+      clear();
+      res = r;
+      i = 0;
+      pop();
+    }
+    void pop()
+    {
+      if (rec != NULL)
+      {
+        const int rc = ugpu_records_next(rec, &start, &len, &cap);
+        have = rc == 1;
+        err = rc < 0;
+      }
+      else if (res != NULL && i < res->count)
+      {
+        start = res->start[i];
+        len = res->len[i];
+        cap = res->cap[i];
+        ++i;
+        have = true;
+      }
+      else
+        have = false;
+    }
+  };
+  Source src_;
   std::shared_ptr<ugpu_dfa> tab_;
   const Pattern* tab_pat_ = NULL;
   bool tab_w_ = false, tab_n_ = false;
@@ -543,6 +619,8 @@ class GpuMatcher : public Matcher {
   bool sparse_ = false;  // the table has a selective prefilter (sparse_kernel)
   ugpu_result* gres_ = NULL;
   const char* gbuf_ = NULL;
+  const char* cpu_buf_ = NULL;  // a buffer the engine failed on (with cpu_end_)
+  size_t cpu_end_ = 0;
   // gcur_: the cursor this class left behind (after the scan or the last hit)
   size_t gend_ = 0, gcur_ = 0, gi_ = 0, scans_ = 0, scans_at_restart_ = 0;
   size_t min_bytes_ = 0, chunk_ = 0, multi_min_ = 0;

@@ -277,7 +277,7 @@ def test_gpu_anchor_starts_streams_and_shards():
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a visible MI355X")
     import ugrep_amd as U
-    data = gen(1, 7, 0, 3 << 20)
+    data = gen(1, 7, 0, 1 << 20)
     data[1000:1004] = np.frombuffer(b"\r\n\n\n", np.uint8)
     picks = [c for c in CASES if c["pattern"] in ("^(?:foo|ba+r)$", "^(?:\\w+)$", "^$", "^\\w+", "\\w+$", "^a|b",
                                                   "^(?:.*)$", "a*", "^ *", " *$")]

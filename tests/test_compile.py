@@ -156,7 +156,7 @@ def test_compiled_tables_on_gpu():
         pytest.fail("GPU tests need a visible MI355X")
     import ugrep_amd as U
     from oracle_lib import OracleDfa, gen
-    host = np.concatenate([gen(4, 7, 0, 1 << 20), gen(3, 7, 0, 1 << 20), gen(1, 7, 0, 1 << 19)])
+    host = np.concatenate([gen(4, 7, 0, 384 << 10), gen(3, 7, 0, 384 << 10), gen(1, 7, 0, 256 << 10)])
     dev = torch.from_numpy(host).to("cuda")
     torch.cuda.synchronize()
     checked = 0

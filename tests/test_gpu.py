@@ -13,7 +13,11 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-UNSUPPORTED = {"anchor_bol", "anchor_eol", "word_boundary", "lookahead"}
+UNSUPPORTED = {"word_boundary", "lookahead"}
+# anchored tables are supported (tests/test_anchor.py); their cases.json
+# results are the reference as ugrep runs it without option N, where its match
+# predictor decides, so the case loops below skip them
+SKIP_CASES = UNSUPPORTED | {"anchor_bol", "anchor_eol"}
 
 
 @pytest.fixture(scope="module")
@@ -65,7 +69,7 @@ def test_golden_small_cases_offsets(U, pats, cases):
     from oracle_lib import case_input
     n = 0
     for c in cases:
-        if c.get("big") or c["pattern"] in UNSUPPORTED:
+        if c.get("big") or c["pattern"] in SKIP_CASES:
             continue
         data = case_input(c["input"])
         r = U.find_all(pats[c["pattern"]], data.tobytes(), offsets=True)
@@ -80,7 +84,7 @@ def test_golden_cases_device_buffers_count_mode(U, pats, cases):
     """Same cases from a device buffer at an unaligned address, COUNT mode."""
     from oracle_lib import case_input
     for c in cases:
-        if c.get("big") or c["pattern"] in UNSUPPORTED or c["input"]["type"] == "hex":
+        if c.get("big") or c["pattern"] in SKIP_CASES or c["input"]["type"] == "hex":
             continue
         data = case_input(c["input"])
         t = torch.zeros(data.size + 32, dtype=torch.uint8, device="cuda")

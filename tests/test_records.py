@@ -1,0 +1,78 @@
+"""GPU: the host records path ugpu_find_records (include/ugpu.h) -- chunked
+H2D on a copy thread, per-chunk scans from the true chain entry, records
+packed to 6/8 B and copied back into pinned memory while the next chunk
+scans.  Record by record it must equal ugpu_find_all (itself pinned to the
+reference's match lists) and the oracle restatement: many chunks (1 MiB),
+nonzero starts, matches across chunk borders, lengths >= 0xFFFF and several
+accept indices (the escape lists), device buffers, option W and anchors."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def U():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd
+    return ugrep_amd
+
+
+@pytest.fixture()
+def small_chunks():
+    os.environ["UGPU_REC_CHUNK"] = str(1 << 20)
+    yield
+    os.environ.pop("UGPU_REC_CHUNK", None)
+
+
+def _check(U, pat, data, start=0, nul=False, word=False):
+    from oracle_lib import OracleDfa
+    o = OracleDfa(pat.opc)
+    want = (o.find_w(data, start=start, want_list=True) if word else
+            o.find(data, start=start, want_list=True, nul=nul))
+    r = U.Records(pat, data, start=start)
+    assert r.totals() == tuple(want[:3])
+    assert r.triples() == want[3]
+    r2 = U.Records(pat, data, start=start)
+    assert r2.drain() == tuple(want[:3])
+
+
+@pytest.mark.parametrize("rx,kind", [("foo|bar|baz", 1), ("[A-Za-z_][A-Za-z0-9_]*", 3), (r"\w+", 4)])
+def test_records_equal_oracle(U, small_chunks, rx, kind):
+    from oracle_lib import gen
+    pat = U.Pattern(U.compile_regex(rx))
+    data = gen(kind, 3, 0, (5 << 20) + 12345)
+    for start in (0, 1, 777777):
+        _check(U, pat, data, start)
+    # a device buffer: no input copy
+    dev = torch.from_numpy(data).cuda()
+    torch.cuda.synchronize()
+    r = U.Records(pat, dev)
+    f = U.find_all(pat, dev, offsets=False)
+    assert r.drain() == (f.count, f.digest, f.dcap)
+
+
+def test_records_escapes_and_borders(U, small_chunks):
+    """Matches longer than 0xFFFF bytes, across chunk borders, and accept
+    indices of several alternatives."""
+    from oracle_lib import gen
+    data = gen(1, 4, 0, 3 << 20).copy()
+    data[1000:1000 + 200000] = ord("a")            # one 200 000-byte match of a+
+    data[(1 << 20) - 5:(1 << 20) + 70000] = ord("a")  # across the first chunk border
+    data[(2 << 20) - 2:(2 << 20) + 2] = np.frombuffer(b"abab", np.uint8)
+    for rx in ("a+|foo|bar", "(ab)+|a+|o"):
+        _check(U, U.Pattern(U.compile_regex(rx)), data)
+
+
+def test_records_word_and_anchors(U, small_chunks):
+    from test_multi import _w_corpus
+    data = _w_corpus(3 << 20)
+    _check(U, U.Pattern(U.compile_regex(r"\w+"), word=True), data, word=True)
+    _check(U, U.Pattern(U.compile_regex(r"de|dei|é"), word=True), data, start=5, word=True)
+    _check(U, U.Pattern(U.compile_regex(r"^\w+"), empty=True), data, nul=True)
+    _check(U, U.Pattern(U.compile_regex(r"^(?:[^\n]*)$"), empty=True), data, nul=True)

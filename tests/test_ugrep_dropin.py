@@ -39,17 +39,25 @@ def _stats(stderr):
     return out
 
 
-def _run_all(exe, env):
+def _run_all(exe, env, workers=8):
+    """Every case, `workers` ugrep processes at a time (each its own GPU
+    context on the GPU run: well under the box's per-card process limit)."""
+    from concurrent.futures import ThreadPoolExecutor
     env = dict(env, **SPEC["env"])
     env.pop("UGREP_COLORS", None)
-    bad, ledger = [], []
-    for c in SPEC["cases"]:
-        r = subprocess.run([exe] + c["args"], cwd=CWD, env=env, capture_output=True, timeout=60,
+
+    def one(c):
+        r = subprocess.run([exe] + c["args"], cwd=CWD, env=env, capture_output=True, timeout=120,
                            input=open(os.path.join(CWD, c["stdin"]), "rb").read() if c["stdin"] else None)
-        h = hashlib.sha256(r.stdout).hexdigest()
-        if h != c["sha256"]:
-            bad.append((c["args"], c["expect"], len(r.stdout), c["size"]))
-        ledger.append(dict(expect=c["expect"], args=c["args"], matchers=_stats(r.stderr)))
+        return c, r
+
+    bad, ledger = [], []
+    with ThreadPoolExecutor(workers) as ex:
+        for c, r in ex.map(one, SPEC["cases"]):
+            h = hashlib.sha256(r.stdout).hexdigest()
+            if h != c["sha256"]:
+                bad.append((c["args"], c["expect"], len(r.stdout), c["size"]))
+            ledger.append(dict(expect=c["expect"], args=c["args"], matchers=_stats(r.stderr)))
     return bad, ledger
 
 

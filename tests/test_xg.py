@@ -68,7 +68,7 @@ def test_ranges_against_oracle(U, gpats, patterns, ginputs, pname):  # noqa: F81
         n = host.size
         t = _dev(host)
         ranges = [(0, n), (0, 1), (1, 2), (0, 65536), (65536, 131072), (1000, 65536 * 3 + 5), (n - 70000, n)]
-        for _ in range(4):
+        for _ in range(2):
             lo = int(rng.integers(0, n))
             hi = int(rng.integers(lo, min(n, lo + int(rng.choice([100, 5000, 200000, 2 << 20]))) + 1))
             ranges.append((lo, hi))

@@ -104,12 +104,14 @@ def test_ranges_against_oracle(U, pats, patterns, inputs, pname):
     rng = np.random.default_rng(sum(pname.encode()))
     opc = patterns[pname]["opc"]
     for name, host in inputs.items():
-        if pname == "dot" and name == "all_ident":
-            host = host[:256 << 10]  # one lane walks it all, at about 1 MB/s
+        if pname == "dot":
+            # (every byte a match: the lane walks are slow, 64 KiB of all_ident
+            # is one lane's walk at about 1 MB/s)
+            host = host[:64 << 10] if name == "all_ident" else host[:512 << 10]
         n = host.size
         t = _dev(host)
         ranges = [(0, n), (0, 1), (1, 2), (0, 65536), (65536, 131072), (1000, 65536 * 3 + 5), (n - 70000, n)]
-        for _ in range(3 if pname == "dot" else 6):
+        for _ in range(2 if pname == "dot" else 4):
             lo = int(rng.integers(0, n))
             hi = int(rng.integers(lo, min(n, lo + int(rng.choice([100, 5000, 200000, 2 << 20]))) + 1))
             ranges.append((lo, hi))

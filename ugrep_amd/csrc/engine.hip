@@ -17,7 +17,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <new>
 #include <string>
@@ -89,6 +92,7 @@ struct ugpu_dfa {
   // costs device allocations and property queries)
   std::mutex pool_mu;
   std::vector<ugpu_scanner*> pool;
+  std::vector<ugpu_scanner*> pool_w;  // scanners that prefer kernels with a record-writing pass (records path)
   // the opcode words and flags it was built from, and its copies on other
   // devices (ugpu_find_all_multi), created on first use
   std::vector<uint32_t> opc;
@@ -106,6 +110,8 @@ struct ugpu_scanner {
   bool xg = false;       // COUNT scans run xg_kernel (gap tables); OFFSETS use the dense kernel
   bool xc = false;       // COUNT and OFFSETS scans run xc_kernel (two-state and, U mode, code-point run tables)
   bool xu_xi = false, xu_xg = false;  // U mode: the kernels a range goes to when it flags UGPU_FLAG_USLOW
+  bool xu = false;       // xc_kernel runs in U mode (code-point run tables)
+  bool pref_write = false;  // created for a records consumer (scanner_acquire)
   bool last_xc = false;  // the last ugpu_scan ran xc_kernel
   bool word = false;     // option W: every pass runs wfind_kernel (wfind.hip) (per scan when wfast)
   bool wfast = false;    // option W on a \w+ table: non-W kernels when the scanned bytes are valid UTF-8
@@ -320,7 +326,7 @@ void geometry_for(ScanParams& P, const ugpu_scanner* s, const uint8_t* dbuf, uin
   if (s->word)
     geometry(P, dbuf, lo, hi, read_end, s->word_rec, wfind_unit(), wfind_waves(), off);
   else if (xi && s->xc)
-    geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xc_unit(dfa_xu(s->dfa)), xc_waves(), off);
+    geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xc_unit(s->xu), xc_waves(), off);
   else if (xi && s->xg)
     geometry(P, dbuf, lo, hi, read_end, s->xi_rec, xg_unit(), xg_waves(), off);
   else if (xi)
@@ -551,6 +557,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
     }
   }
   for (ugpu_scanner* s : d->pool) ugpu_scanner_destroy(s);
+  for (ugpu_scanner* s : d->pool_w) ugpu_scanner_destroy(s);
   if (d->d_trans) (void)hipFree(d->d_trans);
   if (d->d_xtrans) (void)hipFree(d->d_xtrans);
   if (d->d_wtab) (void)hipFree(d->d_wtab);
@@ -734,7 +741,18 @@ int ugpu_tables_equivalent_host(const uint32_t* opc_a, uint32_t nop_a, const uin
   return UGPU_OK;
 }
 
-int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
+namespace {
+int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write);
+}
+
+int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out) { return scanner_create(dfa, out, false); }
+
+namespace {
+
+// prefer_write: code-point run tables take xc_kernel's U mode, which writes
+// its own records, also where xg_kernel (no record pass: OFFSETS rebuilt on
+// dense_kernel) counts a little faster -- the choice of a records consumer
+int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
 {
   if (!dfa || !out) return fail(UGPU_INVAL, "NULL argument");
   *out = nullptr;
@@ -855,11 +873,14 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   }
   // two-state tables: COUNT scans on xc_kernel, ahead of xi/xg (UGPU_XC=0
   // keeps those)
-  if (!s->sparse && (dfa_xc(dfa) || dfa_xu(dfa))) {
+  const char* uenv = std::getenv("UGPU_XU");
+  const bool xu = dfa_xu(dfa) || (prefer_write && dfa->d_xu && (!dfa->d_wtab || dfa->wplus) && !(uenv && uenv[0] == '0'));
+  if (!s->sparse && (dfa_xc(dfa) || xu)) {
     int cpc = 0;
-    HIP_TRY_S(xc_occupancy(dfa_xu(dfa), &cpc));
+    HIP_TRY_S(xc_occupancy(xu, &cpc));
     if (cpc >= 1) {
       s->xc = true;
+      s->xu = xu;
       s->xu_xi = s->xi;
       s->xu_xg = s->xg;
       s->xi = s->xg = false;
@@ -884,6 +905,8 @@ int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out)
   return UGPU_OK;
 #undef HIP_TRY_S
 }
+
+}  // namespace
 
 int ugpu_scanner_destroy(ugpu_scanner* s)
 {
@@ -936,6 +959,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   }
   ScanParams P{};
   fill_tables(P, s->dfa);
+  P.xu_tab = s->xu ? s->dfa->d_xu : nullptr;  // (the scanner's U mode choice)
   P.bol0 = s->bol0;
   if (s->wfast && !s->word) P.wtab = nullptr, P.nwtab = 0;  // the non-W kernels, stitches and forest
   geometry_for(P, s, dbuf, lo, hi, read_end, s->off, s->xi || s->xg || s->xc);
@@ -1287,26 +1311,29 @@ void find_ws_release(FindWs* w)
   g_find_pool.push_back(w);
 }
 
-int scanner_acquire(const ugpu_dfa* dfa, ugpu_scanner** out)
+int scanner_acquire(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write = false)
 {
   ugpu_dfa* d = const_cast<ugpu_dfa*>(dfa);
   {
     std::lock_guard<std::mutex> lk(d->pool_mu);
-    if (!d->pool.empty()) {
-      *out = d->pool.back();
-      d->pool.pop_back();
+    std::vector<ugpu_scanner*>& pool = prefer_write ? d->pool_w : d->pool;
+    if (!pool.empty()) {
+      *out = pool.back();
+      pool.pop_back();
       (*out)->bol0 = 1;  // (a pooled scanner may have served a shard)
       return UGPU_OK;
     }
   }
-  return ugpu_scanner_create(dfa, out);
+  const int rc = scanner_create(dfa, out, prefer_write);
+  if (!rc) (*out)->pref_write = prefer_write;
+  return rc;
 }
 
 void scanner_release(const ugpu_dfa* dfa, ugpu_scanner* s)
 {
   ugpu_dfa* d = const_cast<ugpu_dfa*>(dfa);
   std::lock_guard<std::mutex> lk(d->pool_mu);
-  d->pool.push_back(s);
+  (s->pref_write ? d->pool_w : d->pool).push_back(s);
 }
 
 }  // namespace
@@ -1336,7 +1363,7 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
     return rc;
   }
   ugpu_scanner* s = nullptr;
-  rc = scanner_acquire(dfa, &s);
+  rc = scanner_acquire(dfa, &s, mode == UGPU_MODE_OFFSETS);
   if (rc) {
     std::free(r);
     return rc;
@@ -1387,6 +1414,519 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
     return rc;
   }
   *out = r;
+  return UGPU_OK;
+}
+
+// ---------------------------------------------------------------- records (host path)
+// ugpu_find_records: the FIND records of a host buffer for a consumer that pops
+// them one by one (the drop-in matcher), as fast as PCIe moves the input.  The
+// input goes H2D in chunks on a copy thread; each chunk is scanned from the true
+// chain entry (the previous chunk's exit) as soon as it and the next one are on
+// the device, its records are written, packed to 6 B (u32 start - chunk base,
+// u16 len; + u16 cap when the table has several accept indices) and copied
+// asynchronously into pinned host memory -- H2D, scans and D2H overlap.  The
+// records are decoded when popped.
+struct ugpu_records {
+  struct Piece {
+    uint64_t base = 0, n = 0;
+    uint8_t* host = nullptr;  // pinned: u32 start[n], u16 len[n], (caps) u16 cap[n]
+    size_t host_bytes = 0;
+    std::vector<std::pair<uint64_t, uint64_t>> esc;  // (index, len | cap << 32), sorted
+  };
+  // published by the pipeline thread (under mu; a deque keeps references)
+  std::deque<Piece> pieces;
+  size_t published = 0;
+  bool done = false;
+  bool input_free = false;  // the caller's host buffer is no longer read
+  int rc = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::thread worker;
+  int caps = 0;
+  uint32_t cap1 = 1;
+  uint64_t count = 0, digest = 0, dcap = 0;  // final once done
+  // the consumer's piece: pieces[pi - 1] (pi = 0: none yet)
+  size_t pi = 0;
+  const uint32_t* st = nullptr;
+  const uint16_t* ln = nullptr;
+  const uint16_t* cp = nullptr;
+  const std::pair<uint64_t, uint64_t>* esc = nullptr;
+  uint64_t base = 0, n = 0, ri = 0, ei = 0, ne = 0;
+};
+
+namespace {
+
+// pinned host blocks, pooled (hipHostMalloc pins pages: milliseconds per MiB
+// the first time)
+std::mutex g_pin_mu;
+std::vector<std::pair<uint8_t*, size_t>> g_pin_pool;
+
+uint8_t* pinned_get(size_t need, size_t& got)
+{
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    size_t best = g_pin_pool.size();
+    for (size_t i = 0; i < g_pin_pool.size(); ++i)
+      if (g_pin_pool[i].second >= need && (best == g_pin_pool.size() || g_pin_pool[i].second < g_pin_pool[best].second))
+        best = i;
+    if (best < g_pin_pool.size()) {
+      uint8_t* p = g_pin_pool[best].first;
+      got = g_pin_pool[best].second;
+      g_pin_pool.erase(g_pin_pool.begin() + (long)best);
+      return p;
+    }
+  }
+  size_t c = 64u << 20;
+  while (c < need) c *= 2;
+  void* p = nullptr;
+  // (non-coherent: cached for the host reads that decode the records; every
+  // read follows a stream synchronisation)
+  if (hipHostMalloc(&p, c, hipHostMallocNonCoherent) != hipSuccess) return nullptr;
+  got = c;
+  return static_cast<uint8_t*>(p);
+}
+
+void pinned_put(uint8_t* p, size_t n)
+{
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pin_pool.push_back(std::make_pair(p, n));
+}
+
+// Per-device workspace of the records path, pooled: copy and D2H streams,
+// double-buffered pack / escape buffers and their events.
+struct RecWs {
+  int dev = -1;
+  hipStream_t cst = nullptr, dst = nullptr;
+  uint8_t* d_pack[2] = {nullptr, nullptr};
+  uint64_t pack_cap[2] = {0, 0};
+  uint64_t* d_esc[2] = {nullptr, nullptr};
+  uint64_t esc_cap[2] = {0, 0};
+  uint32_t* d_nesc = nullptr;  // [2]
+  uint32_t* h_nesc = nullptr;  // pinned [2]
+  hipEvent_t packed[2] = {nullptr, nullptr}, copied[2] = {nullptr, nullptr};
+  bool used[2] = {false, false};
+
+  hipError_t init()
+  {
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&cst, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&dst, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipMalloc(&d_nesc, 2 * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipHostMalloc(&h_nesc, 2 * sizeof(uint32_t))) != hipSuccess)
+      return e;
+    for (int i = 0; i < 2; ++i)
+      if ((e = hipEventCreateWithFlags(&packed[i], hipEventDisableTiming)) != hipSuccess ||
+          (e = hipEventCreateWithFlags(&copied[i], hipEventDisableTiming)) != hipSuccess)
+        return e;
+    return hipSuccess;
+  }
+  hipError_t reserve(int b, uint64_t bytes, uint64_t n)
+  {
+    hipError_t e;
+    if (bytes > pack_cap[b]) {
+      (void)hipFree(d_pack[b]);
+      d_pack[b] = nullptr;
+      pack_cap[b] = 0;
+      const uint64_t c = bytes + bytes / 4;
+      if ((e = hipMalloc(&d_pack[b], c)) != hipSuccess) return e;
+      pack_cap[b] = c;
+    }
+    if (n > esc_cap[b]) {
+      (void)hipFree(d_esc[b]);
+      d_esc[b] = nullptr;
+      esc_cap[b] = 0;
+      const uint64_t c = n + n / 4;
+      if ((e = hipMalloc(&d_esc[b], c * 16)) != hipSuccess) return e;
+      esc_cap[b] = c;
+    }
+    return hipSuccess;
+  }
+};
+
+std::mutex g_rec_mu;
+std::vector<RecWs*> g_rec_pool;
+
+RecWs* rec_ws_acquire(int dev)
+{
+  {
+    std::lock_guard<std::mutex> lk(g_rec_mu);
+    for (size_t i = 0; i < g_rec_pool.size(); ++i)
+      if (g_rec_pool[i]->dev == dev) {
+        RecWs* w = g_rec_pool[i];
+        g_rec_pool.erase(g_rec_pool.begin() + (long)i);
+        return w;
+      }
+  }
+  RecWs* w = new (std::nothrow) RecWs;
+  if (!w) return nullptr;
+  w->dev = dev;
+  if (w->init() != hipSuccess) return nullptr;  // (leaks the partial workspace on a broken device)
+  return w;
+}
+
+void rec_ws_release(RecWs* w)
+{
+  std::lock_guard<std::mutex> lk(g_rec_mu);
+  g_rec_pool.push_back(w);
+}
+
+// H2D of a host buffer in chunks on its own thread; waiters block until a
+// prefix is on the device
+struct Uploader {
+  ugpu_records* R = nullptr;  // told when the last byte is on the device
+  const uint8_t* src = nullptr;
+  uint8_t* dst = nullptr;
+  uint64_t len = 0, chunk = 0;
+  hipStream_t st = nullptr;
+  int dev = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t done = 0;
+  int rc = UGPU_OK;
+  std::thread th;
+
+  void run()
+  {
+    (void)hipSetDevice(dev);
+    for (uint64_t o = 0; o < len; o += chunk) {
+      const uint64_t n = len - o < chunk ? len - o : chunk;
+      hipError_t e = hipMemcpyAsync(dst + o, src + o, n, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      std::lock_guard<std::mutex> lk(mu);
+      if (e != hipSuccess) {
+        rc = hip_fail(e, "records input copy");
+        done = len;
+        cv.notify_all();
+        break;
+      }
+      done = o + n;
+      cv.notify_all();
+    }
+    std::lock_guard<std::mutex> lk(R->mu);
+    R->input_free = true;
+    R->cv.notify_all();
+  }
+  // the first `upto` bytes are on the device (or the copy failed)
+  int wait(uint64_t upto)
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done >= upto || rc != UGPU_OK; });
+    return rc;
+  }
+};
+
+}  // namespace
+
+namespace {
+
+// The records pipeline of ugpu_find_records, on its own thread: publishes
+// each chunk's piece as soon as its records are in pinned host memory.
+void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8_t* buf, uint64_t len,
+                      uint64_t start)
+{
+  int rc = UGPU_OK;
+  uint64_t count = 0, digest = 0, dcap = 0;
+  auto publish = [&](ugpu_records::Piece* pc, bool last) {
+    std::lock_guard<std::mutex> lk(R->mu);
+    if (pc) {
+      R->pieces.push_back(std::move(*pc));
+      if (rc == UGPU_OK) R->published = R->pieces.size();
+    }
+    if (last) {
+      R->count = count;
+      R->digest = digest;
+      R->dcap = dcap;
+      R->rc = rc;
+      R->done = true;
+      R->input_free = true;
+    }
+    R->cv.notify_all();
+  };
+  if (hipSetDevice(dev) != hipSuccess) {
+    rc = fail(UGPU_DEVICE, "hipSetDevice");
+    publish(nullptr, true);
+    return;
+  }
+  ugpu_scanner* s = nullptr;
+  if ((rc = scanner_acquire(dfa, &s, true)) != UGPU_OK) {
+    publish(nullptr, true);
+    return;
+  }
+  FindWs* ws = find_ws_acquire(dev);
+  RecWs* rw = ws ? rec_ws_acquire(dev) : nullptr;
+  if (!ws || !rw) {
+    if (ws) find_ws_release(ws);
+    scanner_release(dfa, s);
+    rc = fail(UGPU_NOMEM, "records workspace");
+    publish(nullptr, true);
+    return;
+  }
+  const uint64_t chunk = std::max<uint64_t>(env_u64("UGPU_REC_CHUNK", 64ull << 20), 1ull << 20);
+  const uint64_t halo = 1ull << 20;
+  const bool host = !is_device_ptr(buf);
+  // (the bytes before start are never read but for at_wb / at_bol, 4 back)
+  const uint64_t from = host && start > 4 ? start - 4 : 0;
+  const uint8_t* dbuf = buf;
+  Uploader up;
+  hipError_t e = hipSuccess;
+  if (host) {
+    if ((e = ws->reserve_in(len)) != hipSuccess) {
+      rc = hip_fail(e, "records input");
+    } else {
+      dbuf = ws->d_in;
+      up.src = buf + from;
+      up.dst = ws->d_in + from;
+      up.len = len - from;
+      up.chunk = chunk;
+      up.st = rw->cst;
+      up.dev = dev;
+      up.R = R;
+      up.th = std::thread([&up] { up.run(); });
+    }
+  }
+  auto ready = [&](uint64_t upto) -> int { return host ? up.wait(upto - from) : UGPU_OK; };
+  uint64_t entry = start;
+  int b = 0;
+  s->stage_once = true;  // single-pass OFFSETS for prefiltered tables
+  for (uint64_t lo = start; !rc && lo < len;) {
+    const uint64_t hi = len - lo <= chunk + chunk / 4 ? len : lo + chunk;
+    uint64_t rend = hi + halo < len ? hi + halo : len;
+    ugpu_totals tot{};
+    if (entry < hi) {
+      for (;;) {
+        if ((rc = ready(rend)) != UGPU_OK) break;
+        rc = ugpu_scan(s, dbuf, entry, hi, rend, rend == len, 0, ws->st);
+        if (!rc) rc = ugpu_scan_totals(s, &tot);
+        if (rc == UGPU_HALO && rend < len) {
+          rend = len;
+          continue;
+        }
+        break;
+      }
+      if (rc) break;
+    } else {
+      tot.exit = entry;  // a match of an earlier chunk covers this one
+    }
+    count += tot.count;
+    digest += tot.digest;
+    dcap += tot.dcap;
+    if (tot.count) {
+      ugpu_records::Piece pc;
+      pc.base = lo;
+      pc.n = tot.count;
+      const uint64_t n = pc.n, bytes = n * (R->caps ? 8 : 6);
+      if ((e = ws->reserve_out(n)) != hipSuccess) {
+        rc = hip_fail(e, "records output");
+        break;
+      }
+      if ((rc = ugpu_scan_offsets(s, ws->d_start, ws->d_len, ws->d_cap, n, ws->st)) != UGPU_OK) break;
+      // the pack buffer b was last read by the D2H of two chunks ago
+      if (rw->used[b] && (e = hipStreamWaitEvent(ws->st, rw->copied[b], 0)) != hipSuccess) {
+        rc = hip_fail(e, "records event");
+        break;
+      }
+      if ((e = rw->reserve(b, bytes, n)) != hipSuccess) {
+        rc = hip_fail(e, "records pack buffer");
+        break;
+      }
+      pc.host = pinned_get(bytes, pc.host_bytes);
+      if (!pc.host) {
+        rc = fail(UGPU_NOMEM, "pinned records");
+        break;
+      }
+      if ((e = hipMemsetAsync(rw->d_nesc + b, 0, sizeof(uint32_t), ws->st)) != hipSuccess ||
+          (e = launch_pack_records(ws->d_start, ws->d_len, ws->d_cap, n, lo, rw->d_pack[b], R->caps, rw->d_esc[b],
+                                   rw->d_nesc + b, ws->st)) != hipSuccess ||
+          (e = hipMemcpyAsync(rw->h_nesc + b, rw->d_nesc + b, sizeof(uint32_t), hipMemcpyDeviceToHost, ws->st)) !=
+              hipSuccess ||
+          (e = hipEventRecord(rw->packed[b], ws->st)) != hipSuccess ||
+          (e = hipStreamWaitEvent(rw->dst, rw->packed[b], 0)) != hipSuccess ||
+          (e = hipMemcpyAsync(pc.host, rw->d_pack[b], bytes, hipMemcpyDeviceToHost, rw->dst)) != hipSuccess ||
+          (e = hipEventRecord(rw->copied[b], rw->dst)) != hipSuccess ||
+          (e = hipStreamSynchronize(ws->st)) != hipSuccess) {
+        rc = hip_fail(e, "records pack");
+        publish(&pc, false);  // (not published: handed over so that free() returns its pinned block)
+        break;
+      }
+      rw->used[b] = true;
+      // escapes (lengths or accept indices >= 0xFFFF, rare)
+      const uint32_t ne = rw->h_nesc[b];
+      if (ne) {
+        std::vector<uint64_t> es(2 * (size_t)ne);
+        if ((e = hipMemcpy(es.data(), rw->d_esc[b], 16ull * ne, hipMemcpyDeviceToHost)) != hipSuccess) {
+          rc = hip_fail(e, "records escapes");
+          publish(&pc, false);
+          break;
+        }
+        for (uint32_t k = 0; k < ne; ++k) pc.esc.push_back(std::make_pair(es[2 * k], es[2 * k + 1]));
+        std::sort(pc.esc.begin(), pc.esc.end());
+      }
+      // the piece is the consumer's once its copy has landed
+      if ((e = hipEventSynchronize(rw->copied[b])) != hipSuccess) {
+        rc = hip_fail(e, "records copy");
+        publish(&pc, false);
+        break;
+      }
+      publish(&pc, false);
+      b ^= 1;
+    }
+    entry = tot.exit;
+    lo = hi;
+  }
+  if (host && up.th.joinable()) up.th.join();
+  (void)hipStreamSynchronize(ws->st);
+  (void)hipStreamSynchronize(rw->dst);
+  rw->used[0] = rw->used[1] = false;
+  rec_ws_release(rw);
+  find_ws_release(ws);
+  scanner_release(dfa, s);
+  if (!rc && host) rc = up.rc;
+  publish(nullptr, true);
+}
+
+// the consumer's next piece (blocks until the pipeline publishes it); false
+// at the end or on a pipeline error (*rc)
+bool records_advance(ugpu_records* r, int* rc)
+{
+  std::unique_lock<std::mutex> lk(r->mu);
+  r->cv.wait(lk, [&] { return r->pi < r->published || r->done; });
+  if (r->pi >= r->published) {
+    *rc = r->rc;
+    return false;
+  }
+  const ugpu_records::Piece& p = r->pieces[r->pi++];
+  r->st = reinterpret_cast<const uint32_t*>(p.host);
+  r->ln = reinterpret_cast<const uint16_t*>(p.host + 4 * p.n);
+  r->cp = r->caps ? reinterpret_cast<const uint16_t*>(p.host + 6 * p.n) : nullptr;
+  r->esc = p.esc.data();
+  r->ne = p.esc.size();
+  r->base = p.base;
+  r->n = p.n;
+  r->ri = r->ei = 0;
+  return true;
+}
+
+}  // namespace
+
+int ugpu_find_records(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_t start, ugpu_records** out)
+{
+  if (!dfa || !out || (!buf && len)) return fail(UGPU_INVAL, "NULL argument");
+  *out = nullptr;
+  if (start > len) start = len;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  int rc = dfa_on(dfa, dev, &dfa);
+  if (rc) return rc;
+  ugpu_records* R = new (std::nothrow) ugpu_records();
+  if (!R) return fail(UGPU_NOMEM, "host allocation");
+  R->caps = dfa->t.cap1 == 0 ? 1 : 0;
+  R->cap1 = dfa->t.cap1 ? dfa->t.cap1 : 1;
+  if (len == start) {
+    R->done = R->input_free = true;
+  } else {
+    try {
+      R->worker = std::thread(records_pipeline, R, dfa, dev, buf, len, start);
+    } catch (...) {
+      delete R;
+      return fail(UGPU_NOMEM, "records thread");
+    }
+    // a host buffer may go away once this returns (ugrep unmaps a file when
+    // it stops asking for matches): wait for the last input byte to be on the
+    // device; scans and record copies go on behind the consumer
+    if (!is_device_ptr(buf)) {
+      std::unique_lock<std::mutex> lk(R->mu);
+      R->cv.wait(lk, [&] { return R->input_free; });
+    }
+  }
+  *out = R;
+  return UGPU_OK;
+}
+
+int ugpu_records_next(ugpu_records* r, uint64_t* start, uint32_t* len, uint32_t* cap)
+{
+  if (!r) return -fail(UGPU_INVAL, "NULL argument");
+  while (r->ri >= r->n) {
+    int rc = UGPU_OK;
+    if (!records_advance(r, &rc)) return rc ? -rc : 0;
+  }
+  const uint64_t i = r->ri++;
+  uint32_t l = r->ln[i], c = r->cp ? r->cp[i] : r->cap1;
+  if ((l == 0xFFFFu || c == 0xFFFFu) && r->ei < r->ne && r->esc[r->ei].first == i) {
+    const uint64_t v = r->esc[r->ei++].second;
+    l = (uint32_t)v;
+    if (r->cp) c = (uint32_t)(v >> 32);
+  }
+  *start = r->base + r->st[i];
+  *len = l;
+  *cap = c;
+  return 1;
+}
+
+int ugpu_records_drain(ugpu_records* r, uint64_t* n, uint64_t* digest, uint64_t* dcap)
+{
+  if (!r) return fail(UGPU_INVAL, "NULL argument");
+  // the rest of the current piece through ugpu_records_next, then whole
+  // pieces straight from their arrays as they are published (the loop a
+  // native consumer inlines)
+  uint64_t k = 0, dg = 0, dc = 0, st = 0;
+  uint32_t ln = 0, cp = 0;
+  while (r->ri < r->n && ugpu_records_next(r, &st, &ln, &cp) == 1) {
+    ++k;
+    dg += st * 31 + ln;
+    dc += (st + 1) * cp;
+  }
+  int rc = UGPU_OK;
+  while (records_advance(r, &rc)) {
+    const uint32_t* ps = r->st;
+    const uint16_t* pl = r->ln;
+    const uint16_t* pc = r->cp;
+    const uint64_t pn = r->n, base = r->base;
+    uint64_t sdg = 0, sdc = 0, ssum = 0;
+    for (uint64_t i = 0; i < pn; ++i) {
+      const uint64_t s0 = ps[i];
+      ssum += s0;
+      sdg += s0 * 31 + pl[i];
+      if (pc) sdc += (base + s0 + 1) * pc[i];
+    }
+    // starts are base + s0; caps are cap1 without a cap array
+    dg += sdg + pn * base * 31;
+    dc += pc ? sdc : (ssum + pn * (base + 1)) * r->cap1;
+    for (uint64_t j = 0; j < r->ne; ++j) {
+      // escaped records: replace the 0xFFFF placeholders by the true values
+      const uint64_t i = r->esc[j].first, s0 = base + ps[i];
+      const uint32_t l = (uint32_t)r->esc[j].second, c = pc ? (uint32_t)(r->esc[j].second >> 32) : r->cap1;
+      dg += (uint64_t)l - pl[i];
+      if (pc) dc += (s0 + 1) * ((uint64_t)c - pc[i]);
+    }
+    k += pn;
+    r->ri = r->n;
+  }
+  if (rc) return rc;
+  if (n) *n = k;
+  if (digest) *digest = dg;
+  if (dcap) *dcap = dc;
+  return UGPU_OK;
+}
+
+int ugpu_records_totals(ugpu_records* r, uint64_t* count, uint64_t* digest, uint64_t* dcap)
+{
+  if (!r) return fail(UGPU_INVAL, "NULL argument");
+  std::unique_lock<std::mutex> lk(r->mu);
+  r->cv.wait(lk, [&] { return r->done; });
+  if (r->rc) return r->rc;
+  if (count) *count = r->count;
+  if (digest) *digest = r->digest;
+  if (dcap) *dcap = r->dcap;
+  return UGPU_OK;
+}
+
+int ugpu_records_free(ugpu_records* r)
+{
+  if (!r) return UGPU_OK;
+  if (r->worker.joinable()) r->worker.join();
+  for (auto& p : r->pieces) pinned_put(p.host, p.host_bytes);
+  delete r;
   return UGPU_OK;
 }
 

@@ -168,7 +168,42 @@ __global__ void chain_fix_kernel(ScanParams P, uint64_t old_entry, uint64_t new_
   t->rounds = met ? 1 : 0;
 }
 
+// Host-path record packing (ugpu_find_records): n records (u64 start, u32
+// len, u32 cap) of one chunk into u32 start - base, u16 len and (caps != 0)
+// u16 cap; a len or cap >= 0xFFFF is written as 0xFFFF and its record's
+// (index, len | cap << 32) appended to esc through a counter (rare: the host
+// sorts them).  One record per thread, fully coalesced.
+__global__ void pack_records_kernel(const uint64_t* start, const uint32_t* len, const uint32_t* cap, uint64_t n,
+                                    uint64_t base, uint8_t* out, int caps, uint64_t* esc, uint32_t* nesc)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t* o_start = reinterpret_cast<uint32_t*>(out);
+  uint16_t* o_len = reinterpret_cast<uint16_t*>(out + 4 * n);
+  uint16_t* o_cap = reinterpret_cast<uint16_t*>(out + 6 * n);
+  const uint32_t l = len[i], c = caps ? cap[i] : 0u;
+  o_start[i] = (uint32_t)(start[i] - base);
+  o_len[i] = (uint16_t)(l >= 0xFFFFu ? 0xFFFFu : l);
+  if (caps) o_cap[i] = (uint16_t)(c >= 0xFFFFu ? 0xFFFFu : c);
+  if (l >= 0xFFFFu || c >= 0xFFFFu) {
+    const uint32_t k = atomicAdd(nesc, 1u);
+    esc[2 * k] = i;
+    esc[2 * k + 1] = (uint64_t)l | ((uint64_t)c << 32);
+  }
+}
+
 // ---------------------------------------------------------------- launchers
+hipError_t launch_pack_records(const uint64_t* start, const uint32_t* len, const uint32_t* cap, uint64_t n,
+                               uint64_t base, uint8_t* out, int caps, uint64_t* esc, uint32_t* nesc,
+                               hipStream_t stream)
+{
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(pack_records_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, start, len, cap, n, base,
+                     out, caps, esc, nesc);
+  return hipGetLastError();
+}
+
 hipError_t launch_fix(const ScanParams& P, uint32_t format, hipStream_t stream)
 {
   if (format == 0)

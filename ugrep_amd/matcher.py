@@ -262,6 +262,53 @@ def find_all_multi(pattern, data, ndev=0, start=0, offsets=True):
     return out
 
 
+class Records:
+    """ugpu_find_records: the records of a buffer for a one-at-a-time consumer
+    (pipelined H2D, scans and packed record copy-back; include/ugpu.h)."""
+
+    def __init__(self, pattern, data, start=0):
+        ptr, n, keep = _buffer_ptr(data)
+        h = ctypes.c_void_p()
+        check(lib.ugpu_find_records(pattern.handle, ctypes.c_void_p(ptr), n, start, ctypes.byref(h)))
+        del keep
+        self._h = h
+
+    def next(self):
+        """(start, len, cap) of the next record, or None."""
+        s, ln, c = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32()
+        rc = lib.ugpu_records_next(self._h, ctypes.byref(s), ctypes.byref(ln), ctypes.byref(c))
+        if rc < 0:
+            check(-rc)
+        return (s.value, ln.value, c.value) if rc == 1 else None
+
+    def triples(self):
+        out = []
+        while True:
+            t = self.next()
+            if t is None:
+                return out
+            out.append(list(t))
+
+    def totals(self):
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib.ugpu_records_totals(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def drain(self):
+        """Pop every remaining record natively: (n, digest, dcap)."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib.ugpu_records_drain(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.ugpu_records_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
 class Stream:
     """Streaming FIND over input fed in chunks (ugpu_stream):
     feed() returns the matches that became final, with absolute offsets."""
