@@ -264,7 +264,7 @@ def main():
     torch.cuda.synchronize(dev)
     log("rank %d: shard [%d, %d) read_end %d, pattern %s: %s" % (rank, lo, hi, read_end, rx, info))
 
-    sc = ugrep_amd.Scanner(pat)
+    sc = ugrep_amd.Scanner(pat, records=args.offsets)
     if args.offsets:
         sc.stage(True)  # single-pass OFFSETS (prefiltered tables): the COUNT pass stages the records
     ptr = buf.data_ptr()
@@ -390,9 +390,16 @@ def main():
                           "gathered_to": "all ranks" if world > 1 else "local",
                           "digest_matches_totals": int(st.numel()) == res["count"] and dg == res["digest"]}
     tr = measured_traffic(args.config, hi - lo, KERNELS[info["kernel"]])
+    if tr and tr.get("kernel_ms") and abs(tr["kernel_ms"] - k_avg) > 0.05 * k_avg:
+        # the counters were taken on a run whose kernel time differs from this one's
+        log("traffic.json %s: kernel %.4f ms there, %.4f ms here: not used" % (args.config, tr["kernel_ms"], k_avg))
+        out["roofline"]["traffic_note"] = "profiles/traffic.json entry not used: kernel time %.4f ms there vs %.4f ms" \
+            % (tr["kernel_ms"], k_avg)
+        tr = None
     if tr:
         out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
         out["roofline"]["traffic_source"] = tr["source"]
+        out["roofline"]["traffic_kernel_ms"] = tr.get("kernel_ms")
     if cpu_leg[0] is not None:
         out["cpu_baseline"] = cpu_leg[0]
         if cpu_leg[1] is not None:

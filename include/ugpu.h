@@ -245,6 +245,12 @@ int ugpu_find_all_multi(const ugpu_dfa *dfa, const uint8_t *buf, uint64_t len, u
 
 /* Workspace for scans of device buffers on the current device. */
 int ugpu_scanner_create(const ugpu_dfa *dfa, ugpu_scanner **out);
+/* UGPU_SCANNER_RECORDS: the scans will be followed by ugpu_scan_offsets --
+   prefer kernels with their own record-writing pass (code-point run tables
+   take xc_kernel's U mode instead of xg_kernel, whose OFFSETS are rebuilt on
+   dense_kernel).  Results never depend on it. */
+#define UGPU_SCANNER_RECORDS 1u
+int ugpu_scanner_create_ex(const ugpu_dfa *dfa, uint32_t flags, ugpu_scanner **out);
 int ugpu_scanner_destroy(ugpu_scanner *sc);
 
 /* Enqueue a COUNT scan of dbuf[lo..hi) on `stream` (hipStream_t, NULL = default).

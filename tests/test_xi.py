@@ -116,6 +116,8 @@ def test_ranges_against_oracle(U, pats, patterns, inputs, pname):
             hi = int(rng.integers(lo, min(n, lo + int(rng.choice([100, 5000, 200000, 2 << 20]))) + 1))
             ranges.append((lo, hi))
         for lo, hi in ranges:
+            if not 0 <= lo <= hi <= n:
+                continue  # (the fixed ranges of a shortened input)
             got = _scan(U, pats[pname], t, lo, hi, n)
             want = _oracle_range(opc, host, lo, hi)
             assert got == want, (pname, name, lo, hi, got, want)

@@ -28,13 +28,29 @@ def main(d, match=("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "x
                             "pct": round(pct, 3)})
     scan = [k for k in kernels if any(n in k["name"] for n in match)]
     dom = max(scan, key=lambda k: k["total_us"]) if scan else None
+    # the bench's own scan dispatches only: the persistent grids do not tell a
+    # full-size launch from a smaller one (a PCIe-leg or reference-check
+    # sample), so keep the dispatches within 25 % of the longest one
+    if c and dom:
+        durs = [r[0] / 1e3 for r in c.execute("select duration from kernels where name = ? order by dispatch_id",
+                                              (dom["name"],))]
+        if durs:
+            top = max(durs)
+            main_ = [x for x in durs if x >= 0.75 * top]
+            dom["main_dispatches"] = len(main_)
+            dom["other_dispatches"] = len(durs) - len(main_)
+            dom["main_avg_us"] = round(sum(main_) / len(main_), 3)
     counters = {}
     for sub in ("pmc1", "pmc2", "pmc3"):
         c = db(d, sub)
         if not c or not dom:
             continue
-        last = c.execute("select max(dispatch_id) from counters_collection where kernel_name = ?",
-                         (dom["name"],)).fetchone()[0]
+        rows = c.execute("select dispatch_id, max(duration) from counters_collection where kernel_name = ? "
+                         "group by dispatch_id order by dispatch_id", (dom["name"],)).fetchall()
+        if not rows:
+            continue
+        top = max(r[1] for r in rows)
+        last = [r[0] for r in rows if r[1] >= 0.75 * top][-1]  # the last full-size dispatch
         for name, val in c.execute("select counter_name, sum(value) from counters_collection "
                                    "where kernel_name = ? and dispatch_id = ? group by counter_name",
                                    (dom["name"], last)):
@@ -56,7 +72,12 @@ def main(d, match=("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "x
             res["algorithmic_bytes_per_launch"] = alg
             res["traffic_over_algorithmic"] = round(res["hbm_bytes_per_launch"] / alg, 4)
     if "GRBM_GUI_ACTIVE" in counters and dom:
-        res["effective_clock_ghz"] = round(counters["GRBM_GUI_ACTIVE"] / 8 / (dom["avg_us"] * 1e3), 3)
+        res["effective_clock_ghz"] = round(counters["GRBM_GUI_ACTIVE"] / 8 / (dom.get("main_avg_us", dom["avg_us"]) * 1e3), 3)
+    if dom and "main_avg_us" in dom:
+        res["kernel_ms"] = round(dom["main_avg_us"] / 1e3, 4)
+        if bench and "roofline" in bench:
+            # the trace's average against the bench line's HIP-event time of the same command
+            res["kernel_ms_bench"] = bench["roofline"].get("kernel_ms")
     print(json.dumps(res, indent=1))
 
 

@@ -10,7 +10,9 @@ root=$(pwd)
 out=$root/gpurun_out/prof_$tag
 rm -rf "$out"; mkdir -p "$out"
 export TMPDIR=/tmp
-args=(--config "$cfg" --steps 5 --warmup 1 --no-cpu-baseline "$@")
+# (no PCIe leg, no CPU baseline and its reference-parity sample: the scan
+# kernel's dispatches are then the bench's own warmup + timed steps)
+args=(--config "$cfg" --steps 5 --warmup 1 --no-cpu-baseline --pcie-sample-mib 0 "$@")
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run -- \
     python3 "$root/bench.py" "${args[@]}" > "$out/bench.json" 2> "$out/trace.err"

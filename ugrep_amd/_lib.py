@@ -91,6 +91,7 @@ def _load():
                                                P(P(Result))]),
         "ugpu_result_free": (ctypes.c_int, [P(Result)]),
         "ugpu_scanner_create": (ctypes.c_int, [V, P(V)]),
+        "ugpu_scanner_create_ex": (ctypes.c_int, [V, ctypes.c_uint32, P(V)]),
         "ugpu_scanner_destroy": (ctypes.c_int, [V]),
         "ugpu_scanner_stage": (ctypes.c_int, [V, ctypes.c_int]),
         "ugpu_scan": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,

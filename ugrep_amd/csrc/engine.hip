@@ -127,6 +127,7 @@ struct ugpu_scanner {
   BlockRec* d_recs = nullptr;
   uint64_t* d_entries = nullptr;
   uint64_t* d_obase = nullptr;
+  uint64_t* d_fix = nullptr;  // xc_kernel OFFSETS: per wave, the record whose start an earlier wave wrote
   DevTotals* d_tot = nullptr;
   uint32_t* d_flags = nullptr;
   DevTotals* h_tot = nullptr;  // pinned
@@ -747,6 +748,12 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write);
 
 int ugpu_scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out) { return scanner_create(dfa, out, false); }
 
+int ugpu_scanner_create_ex(const ugpu_dfa* dfa, uint32_t flags, ugpu_scanner** out)
+{
+  if (flags & ~UGPU_SCANNER_RECORDS) return fail(UGPU_INVAL, "unknown scanner flags");
+  return scanner_create(dfa, out, (flags & UGPU_SCANNER_RECORDS) != 0);
+}
+
 namespace {
 
 // prefer_write: code-point run tables take xc_kernel's U mode, which writes
@@ -805,6 +812,7 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
     HIP_TRY_S(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
     HIP_TRY_S(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
     HIP_TRY_S(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
+    HIP_TRY_S(hipMalloc(&s->d_fix, sizeof(uint64_t) * kMaxRec));
     HIP_TRY_S(hipMalloc(&s->d_tot, sizeof(DevTotals)));
     HIP_TRY_S(hipMalloc(&s->d_flags, sizeof(uint32_t)));
     HIP_TRY_S(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
@@ -895,6 +903,7 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   HIP_TRY_S(hipMalloc(&s->d_recs, sizeof(BlockRec) * kMaxRec));
   HIP_TRY_S(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
   HIP_TRY_S(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
+  HIP_TRY_S(hipMalloc(&s->d_fix, sizeof(uint64_t) * kMaxRec));
   HIP_TRY_S(hipMalloc(&s->d_tot, sizeof(DevTotals)));
   HIP_TRY_S(hipMalloc(&s->d_flags, sizeof(uint32_t)));
   HIP_TRY_S(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
@@ -914,6 +923,7 @@ int ugpu_scanner_destroy(ugpu_scanner* s)
   (void)hipFree(s->d_recs);
   (void)hipFree(s->d_entries);
   (void)hipFree(s->d_obase);
+  (void)hipFree(s->d_fix);
   (void)hipFree(s->d_tot);
   (void)hipFree(s->d_flags);
   (void)hipHostFree(s->h_tot);
@@ -1119,6 +1129,7 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
     P.out_len = d_len;
     P.out_cap = d_cap;
     P.out_capacity = capacity;
+    P.out_fix = s->d_fix;
     HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
     HIP_TRY(launch_xc(P, true, st, s->h_tot->count));
     HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));

@@ -118,6 +118,7 @@ struct ScanParams {
   uint32_t* out_len;
   uint32_t* out_cap;
   uint64_t out_capacity;
+  uint64_t* out_fix;         // xc_kernel OFFSETS: per wave, a record whose len holds its raw end (~0: none)
   uint32_t* flags;
   DevTotals* totals;
   uint64_t* entries_out;     // fix_kernel: exact block entries

@@ -407,40 +407,166 @@ struct COut {
   int64_t delta = 0;
   uint32_t cap1 = 0;
   uint32_t over = 0;
+  // the match open at the chunk start (uniform): open = 1 when one is, its
+  // reported start (~0: started by an earlier wave -- its len slot gets the end
+  // position and fix, the index, for xc_fix_kernel)
+  uint32_t open = 0;
+  uint64_t open_start = ~0ull;
+  uint64_t fix = ~0ull;
+  uint16_t* stage = nullptr;  // the wave's LDS staging: kStage start offsets, then kStage end offsets
 };
 
-// Write the chunk's match starts and ends.  Starts get consecutive indices in
-// chain order (the lane's offset is a wave scan of the lanes' start counts);
-// an end at position e (In_{e-1} set, In_e clear or a new start at e) closes
-// the match with the latest index before it, whose len slot temporarily gets
-// the end position (xc_len_kernel subtracts the start afterwards: the start
-// may lie in an earlier lane, chunk or wave).
+// lanes' 16-byte masks: bit 8j of dword d -> bit 4d + j
+__device__ __forceinline__ uint32_t nib16(const uint32_t m[4])
+{
+  uint32_t r = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) r |= ((m[d] * 0x10204080u) >> 28) << (4 * d);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t cscan_add(uint32_t v)
+{
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
+__device__ __forceinline__ void cwave_sync()
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// the staging capacity per wave and kind (starts, ends): 1 KiB of LDS per
+// wave for the pair classifier (16 KiB beside its 128 KiB table); U mode's
+// tables leave less (UGPU_XC_STAGE_U)
+constexpr uint32_t kStage = 256;
+#ifndef UGPU_XC_STAGE_U
+#define UGPU_XC_STAGE_U 256
+#endif
+constexpr uint32_t kStageU = UGPU_XC_STAGE_U;
+
+// Write the chunk's match records.  An end at position e (In_{e-1} set, In_e
+// clear or a new start at e) closes the latest match started before it;
+// starts get consecutive indices in chain order.  The chunk's start and end
+// offsets are staged in the wave's LDS slots (ordered by a wave scan of the
+// lanes' counts), then written by consecutive lanes: start[], cap[] and the
+// lengths (end - start: the start is staged too, or the open match's) leave
+// as coalesced stores.  A match opened by an earlier wave gets its raw end
+// position and is fixed by xc_fix_kernel.  Chunks with more than kStage
+// starts or ends take the per-lane path.
+template <uint32_t kStage>
 __device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], const uint32_t sb[4], uint64_t q, COut& o)
 {
-  const uint32_t ns = __builtin_popcount(sb[0]) + __builtin_popcount(sb[1]) + __builtin_popcount(sb[2]) +
-                      __builtin_popcount(sb[3]);
-  const int lane = threadIdx.x & 63;
-  uint32_t incl = ns;
-#pragma unroll
-  for (int s = 1; s < 64; s <<= 1) {
-    const uint32_t y = __shfl_up(incl, s, 64);
-    if (lane >= s) incl += y;
-  }
-  uint64_t cur = o.cur + (incl - ns);
+  uint32_t enm[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t c = cb[d], st = sb[d];
     const uint32_t in = (L.E[d] | ((L.E[d] >> 1) & c)) & kOnes;  // In_i = G_i | X_i & In_{i-1}
-    const uint32_t en = c & (~in | st);
+    enm[d] = c & (~in | st);
+  }
+  const uint32_t s16 = nib16(sb), e16 = nib16(enm);
+  const uint32_t ns = __builtin_popcount(s16), ne = __builtin_popcount(e16);
+  const uint32_t is = cscan_add(ns), ie = cscan_add(ne);
+  const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)is, 63), E = (uint32_t)__builtin_amdgcn_readlane((int)ie, 63);
+  const int lane = threadIdx.x & 63;
+  const uint64_t q0 = q - 16ull * (uint32_t)lane + (uint64_t)o.delta;  // the chunk's reported base
+  if (R == 0 && E == 0) return;
+  if (R <= kStage && E <= kStage) {
+    uint16_t* S = o.stage;
+    uint16_t* En = o.stage + kStage;
+    const uint32_t lb = 16u * (uint32_t)lane;
+    uint32_t m = s16, k = is - ns;
+    while (m) {
+      S[k++] = (uint16_t)(lb + __builtin_ctz(m));
+      m &= m - 1;
+    }
+    m = e16;
+    k = ie - ne;
+    while (m) {
+      En[k++] = (uint16_t)(lb + __builtin_ctz(m));
+      m &= m - 1;
+    }
+    cwave_sync();
+    for (uint32_t t = (uint32_t)lane; t < R; t += 64) {
+      const uint64_t i = o.cur + t;
+      if (i < o.capacity) {
+        o.start[i] = q0 + S[t];
+        o.cap[i] = o.cap1;
+      } else {
+        o.over = 1;
+      }
+    }
+    for (uint32_t t = (uint32_t)lane; t < E; t += 64) {
+      const uint64_t i = o.cur + t - o.open;  // the match this end closes
+      const uint64_t e = q0 + En[t];
+      if (i < o.capacity) {
+        if (t < o.open) {
+          if (o.open_start == ~0ull) {
+            o.len[i] = (uint32_t)e;  // (raw: xc_fix_kernel subtracts the start)
+            o.fix = i;
+          } else {
+            o.len[i] = (uint32_t)(e - o.open_start);
+          }
+        } else {
+          o.len[i] = (uint32_t)(e - (q0 + S[t - o.open]));
+        }
+      } else {
+        o.over = 1;
+      }
+    }
+    // the match open after the chunk: the last start, when it has no end
+    const uint32_t open = o.open + R - E;
+    if (open && R) o.open_start = q0 + S[R - 1];
+    o.open = open;
+    o.cur += R;
+    cwave_sync();  // (the next chunk's staging overwrites the slots)
+    const uint64_t fl = __ballot(o.fix != ~0ull);  // (only lane 0 can close the open match, t = 0)
+    if (fl) {
+      const int l = __builtin_ctzll(fl);
+      o.fix = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(o.fix >> 32), l) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)o.fix, l);
+    }
+    return;
+  }
+  // the per-lane path: each lane writes its own records; an end closes the
+  // latest start before it -- in the lane, in an earlier lane (a wave max-scan
+  // of the lanes' last start offsets), or the match open at the chunk start
+  const uint32_t top = s16 ? 31u - __builtin_clz(s16) : 0u;
+  uint32_t v = ns ? 16u * (uint32_t)lane + top + 1u : 0u;  // (offset + 1 of the lane's last start)
+#pragma unroll
+  for (int sft = 1; sft < 64; sft <<= 1) {
+    const uint32_t y = __shfl_up(v, sft, 64);
+    if (lane >= sft && y > v) v = y;
+  }
+  uint32_t before = __shfl_up(v, 1, 64);
+  if (lane == 0) before = 0;
+  uint64_t cur = o.cur + (is - ns);
+  uint64_t last = before ? q0 + (before - 1) : o.open_start;  // start of the match open at the lane start
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t en = enm[d], st = sb[d];
     uint32_t mm = en | st;
     while (mm) {
       const uint32_t j = (uint32_t)__builtin_ctz(mm) >> 3, bit = 1u << (8 * j);
       const uint64_t pos = q + 4 * d + j + (uint64_t)o.delta;
       if (en & bit) {
-        if (cur - 1 < o.capacity)
-          o.len[cur - 1] = (uint32_t)pos;
-        else
+        if (cur - 1 < o.capacity) {
+          if (last == ~0ull) {
+            o.len[cur - 1] = (uint32_t)pos;  // (raw: xc_fix_kernel subtracts the start)
+            o.fix = cur - 1;
+          } else {
+            o.len[cur - 1] = (uint32_t)(pos - last);
+          }
+        } else {
           o.over = 1;
+        }
       }
       if (st & bit) {
         if (cur < o.capacity) {
@@ -449,12 +575,27 @@ __device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], con
         } else {
           o.over = 1;
         }
+        last = pos;
         ++cur;
       }
       mm &= ~bit;
     }
   }
-  o.cur += (uint32_t)__shfl((int)incl, 63, 64);
+  // (at most one match per wave has an unknown start: the lane that closed it
+  // holds its index)
+  const uint64_t fl = __ballot(o.fix != ~0ull);
+  if (fl) {
+    const int l = __builtin_ctzll(fl);
+    o.fix = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(o.fix >> 32), l) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)o.fix, l);
+  }
+  const uint32_t open = o.open + R - E;
+  if (open && R) {
+    const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);  // the chunk's last start offset + 1
+    o.open_start = q0 + (vv - 1);
+  }
+  o.open = open;
+  o.cur += R;
 }
 
 // One chunk (16 bytes per lane at q = chunk base + 16 lane); cw = the wave's
@@ -480,7 +621,7 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
   const uint64_t cin = clook(__ballot(gen), __ballot(prop), cw, cw);
   uint32_t sb[4];
   cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb, sb);
-  if constexpr (WR) cwrite(L, cb, sb, q, o);
+  if constexpr (WR) cwrite<U ? kStageU : kStage>(L, cb, sb, q, o);
 }
 
 // U mode, COUNT, a chunk wholly inside [wlo, hi): no byte only continues a
@@ -560,6 +701,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
   __shared__ __attribute__((aligned(16))) uint16_t pcode[(kCPair && !U) ? 65536 : 8];
   __shared__ __attribute__((aligned(16))) uint32_t utab[U ? 65536 / 4 : 1];
   __shared__ __attribute__((aligned(16))) uint32_t ubm3[U ? kXuBm3 : 1];
+  __shared__ __attribute__((aligned(16))) uint16_t wstage[WR ? kCWaves * 2 * (U ? kStageU : kStage) : 2];
   CU u;
   if constexpr (U) {
     // the pair table: entry (x, y) at x << 8 | (y ^ (x << 2 & 0xfc))
@@ -619,6 +761,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     out.capacity = P.out_capacity;
     out.delta = P.delta;
     out.cap1 = P.cap1;
+    out.stage = wstage + (uint32_t)wid * 2u * (U ? kStageU : kStage);
   }
   // option W: the code of the byte before position p (byte 3), 0 at the buffer start
   auto xprev = [&](uint64_t p) -> uint32_t { return W && p > P.bob ? (uint32_t)bcode[P.g[p - 1]] << 24 : 0u; };
@@ -659,6 +802,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     }
   }
   const uint32_t cin0 = cw;
+  if constexpr (WR) out.open = cw;  // a match opened by the previous wave (its start is unknown here)
 
   uint64_t cnt = 0, pos = 0, lbits = 0;  // lane sums (absolute start positions)
   uint64_t exit = whi;
@@ -785,6 +929,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
   }
   if constexpr (WR) {
     if (__ballot(out.over) && lane == 0) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+    if (lane == 0) P.out_fix[gw] = out.fix;  // (~0: none)
     return;  // (the records are the COUNT pass's)
   }
   if constexpr (W) {
@@ -824,12 +969,16 @@ void xu_kernel(ScanParams P)
   xc_body<false, false, true>(P);
 }
 
-// OFFSETS, second step: len[k] held the end position (low 32 bits, reported
-// coordinates); subtract the start
-__global__ __launch_bounds__(256) void xc_len_kernel(uint64_t* start, uint32_t* len, uint64_t n)
+// OFFSETS, second step: the one match per wave whose start an earlier wave
+// wrote (fix[w] = its index, ~0 none) holds its end position (low 32 bits,
+// reported coordinates) in len: subtract the start
+__global__ __launch_bounds__(256) void xc_fix_kernel(const uint64_t* fix, uint32_t nrec, const uint64_t* start,
+                                                     uint32_t* len, uint64_t n)
 {
-  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256)
-    len[k] -= (uint32_t)start[k];
+  const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+  if (w >= nrec) return;
+  const uint64_t k = fix[w];
+  if (k < n) len[k] -= (uint32_t)start[k];
 }
 
 hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64_t count)
@@ -844,10 +993,10 @@ hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t n = count < P.out_capacity ? count : P.out_capacity;
-    if (n) {
-      const uint64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
-      hipLaunchKernelGGL(xc_len_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, P.out_start, P.out_len, n);
-    }
+    const uint32_t nrec = P.grid * (uint32_t)kCWaves;
+    if (n)
+      hipLaunchKernelGGL(xc_fix_kernel, dim3((nrec + 255) / 256), dim3(256), 0, stream, P.out_fix, nrec, P.out_start,
+                         P.out_len, n);
     return hipGetLastError();
   }
   if (P.xu_tab)

@@ -423,10 +423,12 @@ class Matcher:
 class Scanner:
     """Device-resident scans (ugpu_scanner): one per stream/thread."""
 
-    def __init__(self, pattern):
+    def __init__(self, pattern, records=False):
+        """records=True: scans will be followed by offsets() -- prefer kernels
+        with their own record pass (UGPU_SCANNER_RECORDS)."""
         self.pattern = pattern
         h = ctypes.c_void_p()
-        check(lib.ugpu_scanner_create(pattern.handle, ctypes.byref(h)))
+        check(lib.ugpu_scanner_create_ex(pattern.handle, 1 if records else 0, ctypes.byref(h)))
         self._h = h
 
     def scan(self, dptr, lo, hi, read_end=None, at_eof=True, bias=0, stream=0):
