@@ -2,14 +2,20 @@
 // flattened DFA table lookup, the exact FIND walk, match emitters, and the
 // chain step/merge used to stitch speculative pieces.
 #pragma once
+#include <type_traits>
+
 #include "scan_kernels.hpp"
 
 namespace ugpu {
 
 // ---------------------------------------------------------------- tables
+// FMT 0: next[state][byte] (u16 row offsets); 1: cls[byte] + next[state][class]
+// (u16); 2 (wide tables, states x row > 64 Ki): as 1 with u32 row offsets,
+// read from global memory (the exact-walk kernels only: wfind, fix, forest)
 template <int FMT>
 struct Tab {
-  const uint16_t* trans;
+  using E = typename std::conditional<FMT == 2, uint32_t, uint16_t>::type;
+  const E* trans;
   const uint8_t* cls;
   uint32_t start, accb;
   __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t b) const
@@ -20,6 +26,16 @@ struct Tab {
       return trans[s + cls[b]];
   }
 };
+
+// the table of a scan in global memory
+template <int FMT>
+__device__ __forceinline__ Tab<FMT> tab_global(const ScanParams& P)
+{
+  if constexpr (FMT == 2)
+    return Tab<2>{P.trans32, P.cls, P.start, P.accb};
+  else
+    return Tab<FMT>{P.trans, P.cls, P.start, P.accb};
+}
 
 // bytes [base, lend) are staged in LDS; anything else is read from global
 struct Win {

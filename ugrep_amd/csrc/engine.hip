@@ -68,6 +68,7 @@ struct ugpu_dfa {
   int device = 0;
   uint32_t ntrans_pad = 0;
   uint16_t* d_trans = nullptr;
+  uint32_t* d_trans32 = nullptr;  // wide tables (FMT_WIDE)
   uint16_t* d_xtrans = nullptr;  // FIND transducer (restart-local tables on the dense path)
   uint8_t* d_xid = nullptr;      // immediate transducer ids (xi_kernel), COUNT scans
   uint16_t* d_xg = nullptr;      // gap transducer (xg_kernel), COUNT scans
@@ -253,6 +254,7 @@ bool dfa_xu(const ugpu_dfa* d)
 void fill_tables(ScanParams& P, const ugpu_dfa* d)
 {
   P.trans = d->d_trans;
+  P.trans32 = d->d_trans32;
   P.xtrans = d->d_xtrans;
   P.xid = d->d_xid;
   P.xid_rows = d->t.xid_rows;
@@ -471,6 +473,13 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     ugpu_dfa_destroy(d);
     return hip_fail(e, "table upload");
   }
+  if (d->t.format == FMT_WIDE &&
+      ((e = hipMalloc(&d->d_trans32, d->t.trans32.size() * 4)) != hipSuccess ||
+       (e = hipMemcpy(d->d_trans32, d->t.trans32.data(), d->t.trans32.size() * 4, hipMemcpyHostToDevice)) !=
+           hipSuccess)) {
+    ugpu_dfa_destroy(d);
+    return hip_fail(e, "wide table upload");
+  }
   d->nul = (pattern_flags & UGPU_PAT_EMPTY) != 0;
   d->amode = d->t.anchored || (d->nul && d->t.start_acc);
   if (d->amode) {
@@ -560,6 +569,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   for (ugpu_scanner* s : d->pool) ugpu_scanner_destroy(s);
   for (ugpu_scanner* s : d->pool_w) ugpu_scanner_destroy(s);
   if (d->d_trans) (void)hipFree(d->d_trans);
+  if (d->d_trans32) (void)hipFree(d->d_trans32);
   if (d->d_xtrans) (void)hipFree(d->d_xtrans);
   if (d->d_wtab) (void)hipFree(d->d_wtab);
   if (d->d_xid) (void)hipFree(d->d_xid);
@@ -580,13 +590,15 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
   info->classes = d->t.classes;
   info->row = d->t.row;
   info->format = d->t.format;
-  info->table_bytes = (uint32_t)(d->t.trans.size() * 2 + (d->t.format == FMT_CLASS ? 256 : 0));
+  info->table_bytes = (uint32_t)(d->t.trans.size() * 2 + d->t.trans32.size() * 4 + (d->t.format != FMT_BYTE ? 256 : 0));
   info->prefilter_ppm = d->t.filter ? (uint32_t)(d->t.fdensity * 1e6) + 1 : 0;
   info->first_bytes = d->t.first_bytes;
   info->accepting = d->t.accepting;
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
-  info->kernel = d->amode || (d->d_wtab && !d->wplus && !d->xcw && !(d->t.filter && d->t.format == FMT_BYTE)) ? 4u
+  info->kernel = d->amode || d->t.format == FMT_WIDE ||
+                         (d->d_wtab && !d->wplus && !d->xcw && !(d->t.filter && d->t.format == FMT_BYTE))
+                     ? 4u
                  : (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
                  : dfa_xc(d)                                   ? 5u
                  : dfa_xu(d)                                   ? 6u
@@ -609,11 +621,12 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   info->classes = t.classes;
   info->row = t.row;
   info->format = t.format;
-  info->table_bytes = (uint32_t)(t.trans.size() * 2 + (t.format == FMT_CLASS ? 256 : 0));
+  info->table_bytes = (uint32_t)(t.trans.size() * 2 + t.trans32.size() * 4 + (t.format != FMT_BYTE ? 256 : 0));
   info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
   info->kernel = (t.filter && t.format == FMT_BYTE) ? 0u
+                 : t.format == FMT_WIDE              ? 4u
                  : (t.xc && t.cap1 != 0)             ? 5u
                  : (t.xu && t.cap1 != 0)             ? 6u
                  : (t.immediate && t.cap1 != 0)      ? 2u
@@ -622,6 +635,7 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   if (start) *start = t.start;
   if (accb) *accb = t.accb;
   if (trans) {
+    if (t.format == FMT_WIDE) return fail(UGPU_UNSUPPORTED, "wide table (u32 entries): no u16 host form");
     if (trans_cap < t.trans.size()) return fail(UGPU_CAPACITY, "trans capacity");
     std::copy(t.trans.begin(), t.trans.end(), trans);
   }
@@ -787,7 +801,8 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   // option W: prefiltered tables keep sparse_kernel (its candidate walks check
   // the W rules); every other table runs wfind_kernel (tables through the caches)
   // line anchors / option N: every scan runs the context walk on wfind_kernel
-  if (dfa->amode || (dfa->d_wtab && !(dfa->t.filter && dfa->t.format == FMT_BYTE))) {
+  // wide tables: the exact walk on wfind_kernel, transitions from global memory
+  if (dfa->amode || dfa->t.format == FMT_WIDE || (dfa->d_wtab && !(dfa->t.filter && dfa->t.format == FMT_BYTE))) {
     if (wfind_smem_bytes(dfa->ntrans_pad, dfa->t.states, dfa->nwtab, dfa->amode) > 160 * 1024) {
       delete s;
       return fail(UGPU_UNSUPPORTED, "tables do not fit in LDS");

@@ -50,12 +50,17 @@ __device__ __forceinline__ Tab<FMT> fstage_tables(const ScanParams& P, uint8_t* 
 {
   uint16_t* lt = reinterpret_cast<uint16_t*>(smem);
   uint8_t* lc = smem + 2 * (size_t)P.ntrans_pad;
-  const uint4* src = reinterpret_cast<const uint4*>(P.trans);
-  uint4* dst = reinterpret_cast<uint4*>(lt);
-  for (uint32_t i = tid; i < P.ntrans_pad / 8; i += nthr) dst[i] = src[i];
-  if constexpr (FMT == 1)
+  if constexpr (FMT != 2) {
+    const uint4* src = reinterpret_cast<const uint4*>(P.trans);
+    uint4* dst = reinterpret_cast<uint4*>(lt);
+    for (uint32_t i = tid; i < P.ntrans_pad / 8; i += nthr) dst[i] = src[i];
+  }
+  if constexpr (FMT != 0)
     for (int i = tid; i < 256; i += nthr) lc[i] = P.cls[i];
-  return Tab<FMT>{lt, lc, P.start, P.accb};
+  if constexpr (FMT == 2)
+    return Tab<2>{P.trans32, lc, P.start, P.accb};  // (wide: transitions from global memory)
+  else
+    return Tab<FMT>{lt, lc, P.start, P.accb};
 }
 
 __device__ __forceinline__ size_t ftab_bytes(const ScanParams& P) { return ((2 * (size_t)P.ntrans_pad + 256) + 15) & ~size_t(15); }
@@ -404,13 +409,16 @@ hipError_t launch_forest(const ScanParams& P, uint32_t format, const ForestArgs&
                          DevTotals* tot, hipStream_t st)
 {
   if (P.acap)
-    return format == 0 ? forest_fmt<0, kWalkCtx>(P, A, entry, write, tot, st)
-                       : forest_fmt<1, kWalkCtx>(P, A, entry, write, tot, st);
+    return format == 0   ? forest_fmt<0, kWalkCtx>(P, A, entry, write, tot, st)
+           : format == 1 ? forest_fmt<1, kWalkCtx>(P, A, entry, write, tot, st)
+                         : forest_fmt<2, kWalkCtx>(P, A, entry, write, tot, st);
   if (P.wtab)
-    return format == 0 ? forest_fmt<0, kWalkWord>(P, A, entry, write, tot, st)
-                       : forest_fmt<1, kWalkWord>(P, A, entry, write, tot, st);
-  return format == 0 ? forest_fmt<0, kWalkPlain>(P, A, entry, write, tot, st)
-                     : forest_fmt<1, kWalkPlain>(P, A, entry, write, tot, st);
+    return format == 0   ? forest_fmt<0, kWalkWord>(P, A, entry, write, tot, st)
+           : format == 1 ? forest_fmt<1, kWalkWord>(P, A, entry, write, tot, st)
+                         : forest_fmt<2, kWalkWord>(P, A, entry, write, tot, st);
+  return format == 0   ? forest_fmt<0, kWalkPlain>(P, A, entry, write, tot, st)
+         : format == 1 ? forest_fmt<1, kWalkPlain>(P, A, entry, write, tot, st)
+                       : forest_fmt<2, kWalkPlain>(P, A, entry, write, tot, st);
 }
 
 }  // namespace ugpu

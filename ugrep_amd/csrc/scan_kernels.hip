@@ -20,7 +20,7 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
   constexpr int PER = kMaxRec / kFixThreads;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int G = (int)P.nrec;
-  const Tab<FMT> T{P.trans, P.cls, P.start, P.accb};
+  const Tab<FMT> T = tab_global<FMT>(P);
   const Ctx C = P.acap ? Ctx{P.acap, 0u, P.delta} : Ctx{P.caps, P.log_row, P.delta};
   const Win w = win_of(P);
   uint32_t ovf = 0, over = 0;
@@ -147,7 +147,7 @@ template <int FMT>
 __global__ void chain_fix_kernel(ScanParams P, uint64_t old_entry, uint64_t new_entry)
 {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const Tab<FMT> T{P.trans, P.cls, P.start, P.accb};
+  const Tab<FMT> T = tab_global<FMT>(P);
   const Ctx C = P.acap ? Ctx{P.acap, 0u, P.delta} : Ctx{P.caps, P.log_row, P.delta};
   // (option W: at_wb reads the bytes before a walk start; the caller's buffer
   // holds the code point before lo -- shard and stream prefixes, engine.hip)
@@ -208,8 +208,10 @@ hipError_t launch_fix(const ScanParams& P, uint32_t format, hipStream_t stream)
 {
   if (format == 0)
     hipLaunchKernelGGL(fix_kernel<0>, dim3(1), dim3(kFixThreads), 0, stream, P);
-  else
+  else if (format == 1)
     hipLaunchKernelGGL(fix_kernel<1>, dim3(1), dim3(kFixThreads), 0, stream, P);
+  else
+    hipLaunchKernelGGL(fix_kernel<2>, dim3(1), dim3(kFixThreads), 0, stream, P);
   return hipGetLastError();
 }
 
@@ -218,8 +220,10 @@ hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_e
 {
   if (format == 0)
     hipLaunchKernelGGL(chain_fix_kernel<0>, dim3(1), dim3(64), 0, stream, P, old_entry, new_entry);
-  else
+  else if (format == 1)
     hipLaunchKernelGGL(chain_fix_kernel<1>, dim3(1), dim3(64), 0, stream, P, old_entry, new_entry);
+  else
+    hipLaunchKernelGGL(chain_fix_kernel<2>, dim3(1), dim3(64), 0, stream, P, old_entry, new_entry);
   return hipGetLastError();
 }
 

@@ -105,6 +105,7 @@ struct ScanParams {
   uint32_t xg_stride;      // bytes per column
   uint32_t xg_entries;     // u16 entries (multiple of 8)
   const uint8_t* cls;
+  const uint32_t* trans32;  // wide tables (format 2): u32 row offsets, states * row
   const uint32_t* caps;
   uint32_t ntrans_pad;   // u16 entries, multiple of 8
   uint32_t start, accb, log_row;

@@ -575,15 +575,21 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       r <<= 1;
       ++lr;
     }
-    if ((uint64_t)S * r > 65536) {
-      err = "DFA too large for 16-bit device tables";
+    if ((uint64_t)S * r > (1ull << 26)) {
+      err = "DFA too large (more than 2^26 table entries)";
       return 1;
     }
-    t.format = FMT_CLASS;
+    t.format = (uint64_t)S * r > 65536 ? FMT_WIDE : FMT_CLASS;
     t.row = r;
     t.log_row = lr;
   }
   const uint32_t R = t.row;
+  if (t.format == FMT_WIDE) {
+    t.cls = cls;
+    t.trans32.assign((size_t)S * R, 0);
+    for (uint32_t s = 0; s < S; ++s)
+      for (int c = 0; c < 256; ++c) t.trans32[(size_t)s * R + cls[c]] = nxt[(size_t)s * 256 + c] * R;
+  } else {
   t.trans.assign((size_t)S * R, 0);
   if (t.format == FMT_BYTE) {
     for (uint32_t s = 0; s < S; ++s)
@@ -594,6 +600,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
     for (uint32_t s = 0; s < S; ++s)
       for (int c = 0; c < 256; ++c) t.trans[(size_t)s * R + cls[c]] = (uint16_t)(nxt[(size_t)s * 256 + c] * R);
   }
+  }
   t.caps = caps;
   t.acap = acap;
   t.anchored = anchored;
@@ -601,7 +608,8 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   t.start_acc = start_sid >= first_acc;
   // FIND transducer for restart-local tables (tables.hpp); none of the
   // transducer forms below holds for conditional acceptance (anchored tables)
-  if (R >= 4 && !anchored) {
+  const bool wide = t.format == FMT_WIDE;
+  if (R >= 4 && !anchored && !wide) {
     std::vector<int> reps;  // one byte per column class
     {
       std::vector<bool> seen_cls(256, false);
@@ -798,7 +806,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   }
   // two-state tables (tables.hpp XcProg, xc_kernel.hip): start --G--> A,
   // A --X--> A, G a subset of X, both sets inside ASCII
-  if (start_sid < first_acc && !anchored) {
+  if (start_sid < first_acc && !anchored && !wide) {
     uint32_t A = 0;
     bool ok = true;
     for (int c = 0; c < 256 && ok; ++c) {
@@ -829,7 +837,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   }
   t.start = start_sid * R;
   t.accepting = S - first_acc;
-  t.accb = (t.accepting > 0) ? first_acc * R : 0x10000u;
+  t.accb = (t.accepting > 0) ? first_acc * R : (wide ? 0xFFFFFFFFu : 0x10000u);
   for (uint32_t s = first_acc; s < S; ++s) {
     if (s == first_acc)
       t.cap1 = caps[s];
@@ -837,7 +845,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       t.cap1 = 0;
   }
   if (anchored) t.cap1 = 0;  // (conditional accepts: the accept index comes from acap)
-  if (!t.xc && t.cap1 != 0 && start_sid < first_acc) build_xu(nxt, S, first_acc, start_sid, t);
+  if (!t.xc && !wide && t.cap1 != 0 && start_sid < first_acc) build_xu(nxt, S, first_acc, start_sid, t);
   // prefilter (see tables.hpp): per first byte c, the bytes that can follow
   // it (second) and follow those (third); "all" once a prefix accepts
   std::vector<Lead> leads;

@@ -19,7 +19,10 @@
 
 namespace ugpu {
 
-enum TableFormat : uint32_t { FMT_BYTE = 0, FMT_CLASS = 1 };
+// FMT_WIDE: states x row > 64 Ki (e.g. two Unicode classes in a row): u32
+// row offsets in trans32, no transducer forms; served by the exact-walk
+// kernels (wfind_kernel, fix, forest) reading the table from global memory
+enum TableFormat : uint32_t { FMT_BYTE = 0, FMT_CLASS = 1, FMT_WIDE = 2 };
 
 struct DfaTables {
   uint32_t format = FMT_BYTE;
@@ -45,7 +48,8 @@ struct DfaTables {
   uint8_t ft[20] = {};       // T0[8], T1[8], T2[4]
   double fdensity = 1.0;     // estimated candidate fraction on printable ASCII
   uint32_t first_bytes = 0;
-  std::vector<uint16_t> trans;  // states * row
+  std::vector<uint16_t> trans;  // states * row (FMT_BYTE, FMT_CLASS)
+  std::vector<uint32_t> trans32;  // states * row (FMT_WIDE)
   std::vector<uint8_t> cls;     // 256
   std::vector<uint32_t> caps;   // states
   // FIND transducer (dense_kernel.hip lockstep path), valid when the table is

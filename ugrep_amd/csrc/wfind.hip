@@ -56,7 +56,8 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
     uint32_t* wt = cp + ncaps;
     uint8_t* cl = reinterpret_cast<uint8_t*>(wt + 2 * nwt);
     const uint32_t* caps = M == kWalkCtx ? P.acap : P.caps;
-    for (uint32_t i = threadIdx.x; i < P.ntrans_pad; i += blockDim.x) tr[i] = P.trans[i];
+    if constexpr (FMT != 2)  // (wide tables stay in global memory)
+      for (uint32_t i = threadIdx.x; i < P.ntrans_pad; i += blockDim.x) tr[i] = P.trans[i];
     for (uint32_t i = threadIdx.x; i < ncaps; i += blockDim.x) cp[i] = caps[i];
     for (uint32_t i = threadIdx.x; i < 2 * nwt; i += blockDim.x) wt[i] = P.wtab[i];
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) cl[i] = P.cls[i];
@@ -77,7 +78,11 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
   const uint64_t seg = (whi - wlo + 63) / 64;
   const uint64_t slo = wlo + seg * lane < whi ? wlo + seg * lane : whi;
   const uint64_t shi = slo + seg < whi ? slo + seg : whi;
-  const Tab<FMT> T{s_trans, s_cls, P.start, P.accb};
+  Tab<FMT> T;
+  if constexpr (FMT == 2)
+    T = Tab<2>{P.trans32, s_cls, P.start, P.accb};
+  else
+    T = Tab<FMT>{s_trans, s_cls, P.start, P.accb};
   const Ctx C{s_caps, M == kWalkCtx ? 0u : P.log_row, P.delta};
   Win w = win_of(P);
   w.wtab = s_wtab;
@@ -155,7 +160,8 @@ template <int M>
 hipError_t wfind_mode(const ScanParams& P, uint32_t format, bool write, hipStream_t stream)
 {
   if (format == 0) return write ? wfind_one<0, true, M>(P, stream) : wfind_one<0, false, M>(P, stream);
-  return write ? wfind_one<1, true, M>(P, stream) : wfind_one<1, false, M>(P, stream);
+  if (format == 1) return write ? wfind_one<1, true, M>(P, stream) : wfind_one<1, false, M>(P, stream);
+  return write ? wfind_one<2, true, M>(P, stream) : wfind_one<2, false, M>(P, stream);
 }
 
 }  // namespace
@@ -167,10 +173,13 @@ size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, b
   return wfind_smem(ntrans_pad, nstates, nwtab, ctx);
 }
 
-// option W (P.wtab) or line anchors / option N (P.acap)
+// option W (P.wtab), line anchors / option N (P.acap), or neither (wide
+// tables: the plain walk over transitions in global memory)
 hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream)
 {
-  return P.acap ? wfind_mode<kWalkCtx>(P, format, write, stream) : wfind_mode<kWalkWord>(P, format, write, stream);
+  if (P.acap) return wfind_mode<kWalkCtx>(P, format, write, stream);
+  if (P.wtab) return wfind_mode<kWalkWord>(P, format, write, stream);
+  return wfind_mode<kWalkPlain>(P, format, write, stream);
 }
 
 }  // namespace ugpu
