@@ -135,7 +135,7 @@ def gpu_reference_check(pat, buf, sample, want, sptr):
 
 
 KERNELS = {0: "sparse_kernel", 1: "dense_kernel", 2: "xi_kernel", 3: "xg_kernel", 4: "wfind_kernel", 5: "xc_kernel",
-           6: "xc_kernel"}  # (6: its U mode, code-point run tables)
+           6: "xu_kernel"}  # (6: xc_kernel's U mode, code-point run tables)
 
 
 def measured_traffic(cfg, nbytes, kernel):

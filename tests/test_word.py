@@ -110,7 +110,7 @@ def test_gpu_w_word_plus_fast_path():
     bad[(5 << 20) + 2] = ord("a")
     for opc in (ref, U.compile_regex(r"\w+")):
         pat = U.Pattern(opc, word=True)
-        assert pat.info()["kernel"] == 3  # (the non-W kernel: xg_kernel)
+        assert pat.info()["kernel"] == 6  # (the non-W kernel: xc_kernel's U mode)
         for data, fast in ((host, True), (bad, False)):
             dev = torch.from_numpy(data).to("cuda")
             torch.cuda.synchronize()
@@ -129,6 +129,43 @@ def test_gpu_w_word_plus_fast_path():
         for start in (sp, sp + 1, 777):
             res = U.find_all(pat, dev, start=start)
             assert (res.count, res.digest, res.dcap) == OracleDfa(opc).find_w(host, start=start)[:3], start
+
+
+@pytest.mark.gpu
+def test_gpu_w_word_plus_edges():
+    """\\w+ with W runs xc_kernel's U mode (one pass, no isutf8 pass): at a run
+    start after a byte >= 0x80 it evaluates at_wb; where that decodes a word
+    character (a stray continuation byte after one) the range goes to
+    wfind_kernel (no UGPU_TOT_WFAST).  Cut-off leads and non-word code points
+    beside words, and high bytes away from words, keep the fast path.  Every
+    result equals the oracle's W restatement."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd as U
+    ref = next(c["opc"] for c in CASES if c["pattern"] == r"\w+")
+    base = gen(4, 23, 0, 3 << 20)
+    at = 1 << 20
+    base[at - 16:at + 48] = ord(" ")  # (the inserts sit between spaces)
+    cases = [(b"", True), (b" \xff \xc3 \x80\x80 ", True), (b" x\x80a ", False), (b" ab\xc3 ", True),
+             (b" \xe4\xb8ab ", True), (b" word\xe2\x82\xac ", True), (b" \xc3\xa9t\xc3\xa9\xc3 ", True),
+             (b" \xe2\x82\xac\xe2\x82\xac ", True), (b" \xe2\x82\xacab ", True), (b" \xc3\x82\xaca ", False),
+             (b" x\x80\x80\x80a ", False), (b" \xce\xb1\x80\xce\xb2 ", False), (b" _\x80a ", False)]
+    for opc in (ref, U.compile_regex(r"\w+")):
+        pat = U.Pattern(opc, word=True)
+        for ins, fast in cases:
+            data = base.copy()
+            data[at:at + len(ins)] = np.frombuffer(ins, np.uint8)
+            dev = torch.from_numpy(data).to("cuda")
+            torch.cuda.synchronize()
+            want = OracleDfa(opc).find_w(data, want_list=True)
+            sc = U.Scanner(pat)
+            sc.scan(dev.data_ptr(), 0, data.size, data.size, True, 0, torch.cuda.current_stream().cuda_stream)
+            t = sc.totals()
+            assert (t.count, t.digest, t.dcap) == want[:3], ins
+            assert bool(t.flags & 16) == fast, ins
+            res = U.find_all(pat, dev, offsets=True)
+            assert res.triples() == want[3], ins
 
 
 @pytest.mark.gpu

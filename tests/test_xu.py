@@ -136,7 +136,8 @@ def test_four_byte_tokens_hand_off(U, upats, patterns):  # noqa: F811
 
 def test_halo_at_readable_end(U, upats, patterns):  # noqa: F811
     """A run reaching the last 3 bytes before a non-EOF readable end raises
-    UGPU_HALO (their codes depend on bytes not read yet)."""
+    UGPU_HALO (their codes depend on bytes not read yet), unless it ends at an
+    ASCII byte."""
     host = np.frombuffer("ab cd éé".encode() + b" " * 100, np.uint8).copy()
     t = _dev(host)
     sc = U.Scanner(upats["c4_word"])
@@ -146,6 +147,10 @@ def test_halo_at_readable_end(U, upats, patterns):  # noqa: F811
     sc.scan(t.data_ptr(), 0, 7, 9, True, 0, torch.cuda.current_stream().cuda_stream)
     tot = sc.totals()
     assert tot.count == 3
+    # an exit at an ASCII byte is decided: no halo ("cd" ends at the space 5)
+    sc.scan(t.data_ptr(), 0, 4, 6, False, 0, torch.cuda.current_stream().cuda_stream)
+    tot = sc.totals()
+    assert (tot.count, tot.exit) == (2, 5)
 
 
 def test_agrees_with_xg_at_scale(U, patterns):  # noqa: F811

@@ -116,6 +116,9 @@ struct ugpu_scanner {
   bool last_xc = false;  // the last ugpu_scan ran xc_kernel
   bool word = false;     // option W: every pass runs wfind_kernel (wfind.hip) (per scan when wfast)
   bool wfast = false;    // option W on a \w+ table: non-W kernels when the scanned bytes are valid UTF-8
+  bool wu = false;       // ... and those scans run xc_kernel's U mode with the run-edge check (no isutf8 pass)
+  bool wforce = false;   // (the next scan of a wfast scanner runs wfind_kernel)
+  bool xu_exact = false; // U mode: scans run the exact kernel (after a range that flagged UGPU_FLAG_UMIX)
   int word_rec = 0;      // chain records of a wfind scan
   bool wxc = false;      // option W on xc_kernel (dfa->xcw), wfind_kernel when it flags UGPU_FLAG_WSLOW
   uint32_t bol0 = 1;     // dbuf[0] begins a line (ugpu_scanner_context; anchored tables)
@@ -244,11 +247,14 @@ bool dfa_xc(const ugpu_dfa* d)
 // when they have no gap transducer: on C4 (\w+) xg_kernel measured 3.0 ms
 // against U mode's 3.17.  UGPU_XU=1 prefers U mode, UGPU_XU=0
 // never takes it.  Under option W only on \w+ (the W fast path).
+// code-point run tables take xc_kernel's U mode, also when they have a gap
+// transducer (C4 \w+: xu_kernel 2.30 ms, xg_kernel 2.94 ms; UGPU_XU=0 keeps
+// xg_kernel / the table's other kernel)
 bool dfa_xu(const ugpu_dfa* d)
 {
   const char* env = std::getenv("UGPU_XU");
-  const bool force = env && env[0] == '1', off = env && env[0] == '0';
-  return d->d_xu && (!d->d_wtab || d->wplus) && !off && (force || !d->d_xg);
+  const bool off = env && env[0] == '0';
+  return d->d_xu && (!d->d_wtab || d->wplus) && !off;
 }
 
 void fill_tables(ScanParams& P, const ugpu_dfa* d)
@@ -897,13 +903,19 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   // two-state tables: COUNT scans on xc_kernel, ahead of xi/xg (UGPU_XC=0
   // keeps those)
   const char* uenv = std::getenv("UGPU_XU");
-  const bool xu = dfa_xu(dfa) || (prefer_write && dfa->d_xu && (!dfa->d_wtab || dfa->wplus) && !(uenv && uenv[0] == '0'));
+  // option W on \w+ (wfast): U mode checks the run edges itself, one pass
+  // instead of isutf8 + xg_kernel (UGPU_XUW=0 keeps those)
+  const char* wuenv = std::getenv("UGPU_XUW");
+  const bool wu = s->wfast && dfa->d_xu && !(wuenv && wuenv[0] == '0') && !(uenv && uenv[0] == '0');
+  const bool xu = dfa_xu(dfa) || wu ||
+                  (prefer_write && dfa->d_xu && (!dfa->d_wtab || dfa->wplus) && !(uenv && uenv[0] == '0'));
   if (!s->sparse && (dfa_xc(dfa) || xu)) {
     int cpc = 0;
     HIP_TRY_S(xc_occupancy(xu, &cpc));
     if (cpc >= 1) {
       s->xc = true;
       s->xu = xu;
+      s->wu = wu;
       s->xu_xi = s->xi;
       s->xu_xg = s->xg;
       s->xi = s->xg = false;
@@ -965,8 +977,8 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
     // option W on \w+: matches are maximal runs of Word code points, so on valid
     // UTF-8 at_wb/at_we hold at every match edge -- provided the
     // chain enters at the buffer start or after an ASCII non-word byte
-    bool fast = true;
-    if (lo > 0) {
+    bool fast = !s->wforce;
+    if (fast && lo > 0) {
       uint8_t b = 0;
       HIP_TRY(hipMemcpyAsync(&b, dbuf + lo - 1, 1, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
@@ -974,7 +986,7 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
     }
     // isutf8 over [lo, read_end) first (run beside the scan on a second stream
     // it gained nothing: the two kernels slowed each other down)
-    if (fast && read_end > lo) {
+    if (fast && read_end > lo && !s->wu) {
       uint64_t bad = ~0ull;
       const int rc = utf8_scan(dbuf + lo, read_end - lo, false, &bad, stream);
       if (rc) return rc;
@@ -985,6 +997,8 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   ScanParams P{};
   fill_tables(P, s->dfa);
   P.xu_tab = s->xu ? s->dfa->d_xu : nullptr;  // (the scanner's U mode choice)
+  P.xu_w = s->wu && !s->word ? 1u : 0u;
+  P.xu_exact = s->xu_exact ? 1u : 0u;
   P.bol0 = s->bol0;
   if (s->wfast && !s->word) P.wtab = nullptr, P.nwtab = 0;  // the non-W kernels, stitches and forest
   geometry_for(P, s, dbuf, lo, hi, read_end, s->off, s->xi || s->xg || s->xc);
@@ -1065,6 +1079,28 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
   if (!s || !out) return fail(UGPU_INVAL, "NULL argument");
   if (!s->have_scan) return fail(UGPU_INVAL, "no scan issued");
   HIP_TRY(hipStreamSynchronize(s->stream));
+  if (s->last_xc && s->xu && (*s->h_flags & UGPU_FLAG_UMIX)) {
+    // U mode's fast kernel met an XU_MIX or XU_SLOW lead: redo the range with
+    // the exact U kernel (which flags UGPU_FLAG_USLOW for 4-byte tokens)
+    // (and keeps it for the scanner's later scans: inputs with such leads
+    // usually have many)
+    s->xu_exact = true;
+    const int rc = ugpu_scan(s, s->last_buf, s->last_args[0], s->last_args[1], s->last_args[2],
+                             (int)s->last_args[3], s->last_args[4], s->stream);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+  }
+  if (s->wu && !s->word && (*s->h_flags & (UGPU_FLAG_WSLOW | UGPU_FLAG_USLOW))) {
+    // option W on U mode met a stray continuation byte right after a token
+    // byte (at_wb may decode a word character there, xc_kernel.hip umask) or a
+    // 4-byte token: redo the range with wfind_kernel
+    s->wforce = true;
+    const int rc = ugpu_scan(s, s->last_buf, s->last_args[0], s->last_args[1], s->last_args[2],
+                             (int)s->last_args[3], s->last_args[4], s->stream);
+    s->wforce = false;
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+  }
   if (s->wxc && !s->word && (*s->h_flags & UGPU_FLAG_WSLOW)) {
     // option W met bytes >= 0x80 (their at_wb/at_we need the UTF-8 decode):
     // redo the range with wfind_kernel

@@ -78,6 +78,9 @@ struct DevTotals {
 // xc_kernel's U mode met a lead byte of a 4-byte token (tables.hpp XU_SLOW):
 // the host redoes the range with the table's next kernel
 #define UGPU_FLAG_USLOW 128u
+// xc_kernel U mode (fast kernel): a code with bit 3 (an XU_MIX or XU_SLOW lead)
+// was met; the host redoes the range with the exact U kernel (P.xu_exact)
+#define UGPU_FLAG_UMIX 256u
 constexpr uint32_t kStageOver = 0xffffffffu;
 constexpr uint32_t kStageDone = 0xfffffffeu;
 constexpr uint32_t kStagePer = 1024;  // staged records per wave (16 B each: 128 MiB for 8192 waves)
@@ -144,6 +147,8 @@ struct ScanParams {
   uint32_t* st_n;
   uint32_t st_per;
   uint32_t xc_w;          // option W on xc_kernel (X = the ASCII word bytes)
+  uint32_t xu_w;          // option W on xc_kernel's U mode (tables equivalent to \w+): run edges checked
+  uint32_t xu_exact;      // xc_kernel U mode: the exact main loop (XU_MIX / XU_SLOW checked per chunk)
   // code-point run tables (xc_kernel U mode, tables.hpp xu_*) or NULL
   const uint8_t* xu_tab;  // kXuTab bytes (4-byte aligned)
   const uint32_t* xu_bm3; // kXuBm3 dwords

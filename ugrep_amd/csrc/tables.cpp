@@ -252,14 +252,17 @@ void build_xu(const std::vector<uint32_t>& nxt, uint32_t S, uint32_t first_acc, 
     }
   }
   // classes of continuation bytes: refine {all 64} by the third-byte sets of
-  // the 3-byte leads while at most 3 classes result -- General Punctuation
-  // and Currency Symbols (E2 80-82) first, then by code point; the leads whose
-  // set is a union of classes get the class bits, the rest go to xu_bm3
+  // the 3-byte leads while at most 3 classes result -- the blocks most frequent
+  // in text first: General Punctuation (E2 80: quotes, dashes), then E2 82
+  // (the euro sign's block), E2 81, then by code point; the leads whose set is
+  // a union of classes get the class bits, the rest (XU_MIX) go to xu_bm3 and
+  // make the fast U kernel hand the range to the exact one
+  auto rank = [](uint32_t xy) { return xy == 0xe280 ? 0 : xy == 0xe282 ? 1 : xy == 0xe281 ? 2 : 3; };
   std::vector<std::pair<uint32_t, uint64_t> > order = l3;
-  std::stable_sort(order.begin(), order.end(), [](const std::pair<uint32_t, uint64_t>& a,
-                                                  const std::pair<uint32_t, uint64_t>& b) {
-    const bool pa = a.first >= 0xe280 && a.first <= 0xe282, pb = b.first >= 0xe280 && b.first <= 0xe282;
-    return pa != pb ? pa : a.first < b.first;
+  std::stable_sort(order.begin(), order.end(), [&](const std::pair<uint32_t, uint64_t>& a,
+                                                   const std::pair<uint32_t, uint64_t>& b) {
+    const int ra = rank(a.first), rb = rank(b.first);
+    return ra != rb ? ra < rb : a.first < b.first;
   });
   std::vector<uint64_t> parts(1, ~0ull);
   for (const auto& l : order) {

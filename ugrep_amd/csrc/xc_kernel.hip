@@ -197,6 +197,10 @@ struct CU {
   uint32_t nx0 = 0;               // (uniform) the dword after the chunk, filled
   uint32_t cprev = 0;             // (uniform) codes of the 4 bytes before the chunk
   uint32_t slow = 0;              // lane: OR of the codes (bit 3: XU_SLOW, a 4-byte token)
+  // option W (UW: tables equivalent to \w+): the lane's stray continuation
+  // bytes right after a token byte (bit 0 of a byte; see umask)
+  uint32_t risk = 0;
+  uint32_t x8 = 0;  // lane (FAST main loop): OR of the codes, bit 3 = an XU_MIX or XU_SLOW lead
 };
 
 // bytes of the dword at q inside [lo, rend) (0xff per byte)
@@ -282,11 +286,37 @@ __device__ __forceinline__ uint32_t uload_dw(const CU& u, const uint8_t* g, uint
   return (x & uinside(u, q)) | (u.null4 & ~uinside(u, q));
 }
 
+// UW: continuation bytes of w in no token right after a token byte (bit 0 of a
+// byte; m = M of the bytes, mp = M of the bytes before them)
+__device__ __forceinline__ uint32_t ustray(uint32_t w, uint32_t m, uint32_t mp)
+{
+  return (w >> 7) & ~(w >> 6) & ~m & mp;
+}
+
 // One lane's 16 bytes at q: M (bit 0 of each byte: the byte lies inside a
-// token).  FAST (the unmasked COUNT main loop): the 3-byte test runs without
-// the XU_MIX bitmap unless some lane of the wave met a code with bit 3 (an
-// XU_MIX lead or an XU_SLOW 4-byte lead) in this chunk.
-template <bool MASK, bool FAST = false>
+// token).  FAST (the unmasked COUNT main loop of xu_kernel<.., false>): the
+// 3-byte test runs without the XU_MIX bitmap and without the XU_SLOW check;
+// the codes' bit 3 (an XU_MIX or XU_SLOW lead) is collected in u.x8, and the
+// host redoes a range that met one with the exact kernel.  (Deciding that per
+// chunk, by a ballot and a branch, cost 3.19 vs 2.22 ms on C4: the branch
+// splits the chunk bodies, so the loads and LDS lookups of one chunk no longer
+// overlap the VALU of the other.)
+//
+// UW (option W on tables equivalent to \w+): the matches are the
+// runs, and at_wb / at_we (include/reflex/matcher.h:1194-1237) hold at their
+// edges unless at_wb, after a continuation byte, decodes backwards to a word
+// character: the first non-continuation byte j before the run start lies in a
+// token.  The continuation bytes between j and the start are then not all in
+// that token, so one of them is a stray continuation byte (in no token) right
+// after a token byte -- which never occurs in valid UTF-8.  (at_we after a
+// run: the byte is ASCII non-word, a continuation byte (true), or a lead whose
+// restricted decode is a word character only when it starts a token, which
+// would extend the run.)  u.risk collects such bytes; the host redoes a range
+// with any with wfind_kernel.
+// (F: 0 = the exact 3-byte test; 1 = FAST; 2 = the exact test in chunks where
+// some lane of the wave met a code with bit 3, by a ballot: the exact kernel's
+// main loop)
+template <bool MASK, int F = 0, bool UW = false>
 __device__ __forceinline__ void umask(CU& u, const uint4& v, uint64_t q, uint32_t m[4])
 {
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -303,8 +333,9 @@ __device__ __forceinline__ void umask(CU& u, const uint4& v, uint64_t q, uint32_
   for (int d = 0; d < 4; ++d) c[d] = ucode_dw(u, w[d], d < 3 ? w[d + 1] : nx);
   // the code of the byte after the lane (only its first byte is used)
   const uint32_t cn = __builtin_amdgcn_update_dpp(ucode_b0(u, u.nx0), c[0], 0x130, 0xf, 0xf, false);
-  bool exact = !FAST;
-  if constexpr (FAST) exact = __ballot(((c[0] | c[1] | c[2] | c[3]) & 0x08080808u) != 0) != 0;
+  if constexpr (F == 1) u.x8 |= c[0] | c[1] | c[2] | c[3];
+  bool exact = F == 0;
+  if constexpr (F == 2) exact = __ballot(((c[0] | c[1] | c[2] | c[3]) & 0x08080808u) != 0) != 0;
   if (exact) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) u.slow |= c[d] & (c[d] << 3);  // bit 3: XU_SLOW
@@ -323,14 +354,21 @@ __device__ __forceinline__ void umask(CU& u, const uint4& v, uint64_t q, uint32_
     const uint32_t pv = d ? c[d - 1] : cp;
     m[d] = (c[d] | __builtin_amdgcn_alignbit(c[d], pv, 25) | __builtin_amdgcn_alignbit(c[d], pv, 18)) & kOnes;
   }
+  if constexpr (UW) {
+    // M of the byte before the lane's 16 bytes, from the previous lane's codes
+    // (bit k of the code k + 1 bytes back); the fill byte is no continuation
+    const uint32_t m0 = ((cp >> 24) | (cp >> 17) | (cp >> 10)) & 1u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) u.risk |= ustray(w[d], m[d], __builtin_amdgcn_alignbit(m[d], d ? m[d - 1] : m0 << 24, 24));
+  }
 }
 
 // ... as the adder codes e = 0xFF * M (limits as ccodes)
-template <bool MASK>
+template <bool MASK, bool UW = false>
 __device__ __forceinline__ void ucodes(CU& u, const uint4& v, CLane& L, uint64_t q, const CLim& lim)
 {
   uint32_t m[4];
-  umask<MASK>(u, v, q, m);
+  umask<MASK, 0, UW>(u, v, q, m);
 #pragma unroll
   for (int d = 0; d < 4; ++d) L.E[d] = (m[d] << 8) - m[d];  // 0xff per M byte
   if constexpr (MASK) {
@@ -613,7 +651,7 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
 #endif
   CLane L;
   if constexpr (U)
-    ucodes<MASK>(u, v, L, q, lim);
+    ucodes<MASK, W>(u, v, L, q, lim);  // (U mode: W is the UW edge check)
   else
     ccodes<MASK, W>(cc, v, L, q, lim, wc);
   bool prop;
@@ -629,6 +667,7 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
 // counted directly (ls counts In_i here, not In_{i-1}; the caller corrects the
 // difference at the main loop's ends).  mprev (uniform): M of the 4 bytes
 // before the chunk (bit 24: the byte just before).
+template <bool UW, bool FAST>
 __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q, uint32_t& mprev, uint32_t& cs,
                                               uint32_t& ws, uint32_t& ls)
 {
@@ -637,12 +676,15 @@ __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q,
   return;
 #endif
   uint32_t m[4];
-  umask<false, true>(u, v, q, m);
+  umask<false, FAST ? 1 : 2>(u, v, q, m);
   const uint32_t mp = __builtin_amdgcn_update_dpp(mprev, m[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
   mprev = __builtin_amdgcn_readlane(m[3], 63);
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    const uint32_t st = m[d] & ~__builtin_amdgcn_alignbit(m[d], d ? m[d - 1] : mp, 24);
+    const uint32_t pm = __builtin_amdgcn_alignbit(m[d], d ? m[d - 1] : mp, 24);  // M of the byte before
+    const uint32_t st = m[d] & ~pm;
+    if constexpr (UW) u.risk |= ustray(w[d], m[d], pm);
     cs = __builtin_popcount(st) + cs;
     ls = __builtin_popcount(m[d]) + ls;
     const uint32_t wd = (4u * d) | ((4u * d + 1) << 8) | ((4u * d + 2) << 16) | ((4u * d + 3) << 24);
@@ -690,7 +732,7 @@ __device__ __forceinline__ uint32_t ccode(uint32_t cls) { return cls & 0x80u ? 0
 }  // namespace
 
 // (the body of the kernels below)
-template <bool W, bool WR, bool U>
+template <bool W, bool WR, bool U, bool FAST = false>
 __device__ __forceinline__ void xc_body(const ScanParams& P)
 {
   constexpr int kIt = U ? kUIter : kCIter;  // chunks per iteration
@@ -764,7 +806,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     out.stage = wstage + (uint32_t)wid * 2u * (U ? kStageU : kStage);
   }
   // option W: the code of the byte before position p (byte 3), 0 at the buffer start
-  auto xprev = [&](uint64_t p) -> uint32_t { return W && p > P.bob ? (uint32_t)bcode[P.g[p - 1]] << 24 : 0u; };
+  auto xprev = [&](uint64_t p) -> uint32_t { return W && !U && p > P.bob ? (uint32_t)bcode[P.g[p - 1]] << 24 : 0u; };
 
   // ---- the wave's carry-in: the chain enters P.lo fresh; other waves look back
   uint32_t cw = 0;
@@ -840,69 +882,73 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
   // option W: at_wb at the range start decodes the character before it; when
   // lo is chunk aligned no chunk holds that byte, so it is seen here (>= 0x80:
   // the host redoes the range with wfind_kernel)
-  if constexpr (W) {
+  if constexpr (W && !U) {
     if (n && wlo == P.lo && P.lo > P.bob) wc.hi |= (uint32_t)P.g[P.lo - 1];
   }
   if (fte > ftb)
     for (; q0 < ftb * kTile; q0 += kCChunk) masked(q0);
 
-  uint4 cur[kIt], nxt[kIt];
-  // U mode: the first dword of the tile after the current one (the last
-  // chunk's context), loaded one tile ahead; M of the byte before the chunk
-  uint32_t nfc = 0, nfn = 0, mprev = 0;
+  // U mode: M of the byte before the chunk (uniform)
+  uint32_t mprev = 0;
   const uint32_t cw_main = cw;
-  if (fte > ftb) {
-    const uint64_t ts = ftb * kTile;
-    const __amdgpu_buffer_rsrc_t rs = crsrc(P.g + ts, rend16 > ts ? rend16 - ts : 0);
+  {
+    uint4 cur[kIt], nxt[kIt];
+    // U mode: the first dword of the tile after the current one (the last
+    // chunk's context), loaded one tile ahead
+    uint32_t nfc = 0, nfn = 0;
+    if (fte > ftb) {
+      const uint64_t ts = ftb * kTile;
+      const __amdgpu_buffer_rsrc_t rs = crsrc(P.g + ts, rend16 > ts ? rend16 - ts : 0);
 #pragma unroll
-    for (int j = 0; j < kIt; ++j) cur[j] = cload(rs, j * kCChunk + lo16);
-    if constexpr (U) nfc = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)kTile, 0, 0);
-    mprev = cw << 24;
-  }
-  for (uint64_t t = ftb; t < fte; ++t) {
-    const uint64_t ts = t * kTile;
-    {
-      // (U mode reads the next tile also after the last: its first dword is
-      // the last chunk's context)
-      const uint64_t tn = (U || t + 1 < fte) ? ts + kTile : ts;
-      const __amdgpu_buffer_rsrc_t rn = crsrc(P.g + tn, rend16 > tn ? rend16 - tn : 0);
-#pragma unroll
-      for (int j = 0; j < kIt; ++j) nxt[j] = cload(rn, j * kCChunk + lo16);
-      if constexpr (U) nfn = __builtin_amdgcn_raw_buffer_load_b32(rn, (int)kTile, 0, 0);
+      for (int j = 0; j < kIt; ++j) cur[j] = cload(rs, j * kCChunk + lo16);
+      if constexpr (U) nfc = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)kTile, 0, 0);
+      mprev = cw << 24;
     }
-    CIt a;
-    uint32_t cb[4];
-    // (chunk indices are compile-time constants, so cur[] and nxt[] stay in
-    // registers also when the body is too large for the loop unroller)
-    auto chunk = [&](auto jc) __attribute__((always_inline)) {
-      constexpr int j = decltype(jc)::value;
-      if constexpr (U) {
-        if constexpr (j + 1 < kIt) {
-          u.nx0 = __builtin_amdgcn_readlane(cur[j + 1].x, 0);
-        } else {
-          const uint64_t qn = ts + kTile;
-          const uint32_t in = uinside(u, qn);
-          u.nx0 = (__builtin_amdgcn_readfirstlane(nfc) & in) | (u.null4 & ~in);
-        }
+    for (uint64_t t = ftb; t < fte; ++t) {
+      const uint64_t ts = t * kTile;
+      {
+        // (U mode reads the next tile also after the last: its first dword is
+        // the last chunk's context)
+        const uint64_t tn = (U || t + 1 < fte) ? ts + kTile : ts;
+        const __amdgpu_buffer_rsrc_t rn = crsrc(P.g + tn, rend16 > tn ? rend16 - tn : 0);
+#pragma unroll
+        for (int j = 0; j < kIt; ++j) nxt[j] = cload(rn, j * kCChunk + lo16);
+        if constexpr (U) nfn = __builtin_amdgcn_raw_buffer_load_b32(rn, (int)kTile, 0, 0);
       }
-      if constexpr (U && !WR)
-        uchunk_direct(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls);
-      else
-        cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u);
-    };
-    cunroll<0, kIt>(chunk);
-    uint32_t c = 0, cj = 0;
+      CIt a;
+      uint32_t cb[4];
+      // (chunk indices are compile-time constants, so cur[] and nxt[] stay in
+      // registers also when the body is too large for the loop unroller)
+      auto chunk = [&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (U) {
+          // the dword after the chunk (its last lane's context)
+          if constexpr (j + 1 < kIt) {
+            u.nx0 = __builtin_amdgcn_readlane(cur[j + 1].x, 0);
+          } else {
+            const uint32_t in = uinside(u, ts + kTile);
+            u.nx0 = (__builtin_amdgcn_readfirstlane(nfc) & in) | (u.null4 & ~in);
+          }
+        }
+        if constexpr (U && !WR)
+          uchunk_direct<W, FAST>(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls);
+        else
+          cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u);
+      };
+      cunroll<0, kIt>(chunk);
+      uint32_t c = 0, cj = 0;
 #pragma unroll
-    for (int j = 0; j < kIt; ++j) {
-      c += a.cs[j];
-      cj += j * a.cs[j];
+      for (int j = 0; j < kIt; ++j) {
+        c += a.cs[j];
+        cj += j * a.cs[j];
+      }
+      cnt += c;
+      pos += (uint64_t)c * (ts + lo16) + a.ws + kCChunk * cj;
+      lbits += a.ls;
+#pragma unroll
+      for (int j = 0; j < kIt; ++j) cur[j] = nxt[j];
+      nfc = nfn;
     }
-    cnt += c;
-    pos += (uint64_t)c * (ts + lo16) + a.ws + kCChunk * cj;
-    lbits += a.ls;
-#pragma unroll
-    for (int j = 0; j < kIt; ++j) cur[j] = nxt[j];
-    nfc = nfn;
   }
   if (fte > ftb) q0 = fte * kTile;
   if constexpr (U && !WR) {
@@ -921,8 +967,9 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     for (; q0 < whi || (last_wave && !found); q0 += kCChunk) masked(q0);
   if (found) cw = 0;  // past the exit every carry is clear
   // U mode: the codes of the last 3 bytes before a non-EOF readable end
-  // depend on bytes not read yet
-  if (U && last_wave && !P.at_eof && exit + 3 >= P.rend) ovf = 1;
+  // depend on bytes not read yet -- except at an ASCII byte, which lies in no
+  // token that starts before it, so an exit there is decided
+  if (U && last_wave && !P.at_eof && exit + 3 >= P.rend && !(exit < P.rend && P.g[exit] < 0x80)) ovf = 1;
   if (ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
   if constexpr (U) {
     if (__ballot((u.slow & 0x08080808u) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_USLOW);
@@ -932,8 +979,14 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     if (lane == 0) P.out_fix[gw] = out.fix;  // (~0: none)
     return;  // (the records are the COUNT pass's)
   }
-  if constexpr (W) {
+  if constexpr (W && !U) {
     if (__ballot((wc.hi & 0x80808080u) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_WSLOW);
+  }
+  if constexpr (W && U) {
+    if (__ballot((u.risk & kOnes) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_WSLOW);
+  }
+  if constexpr (U && FAST) {
+    if (__ballot((u.x8 & 0x08080808u) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_UMIX);
   }
   const uint64_t c = wave_sum(cnt), s = wave_sum(pos), lb = wave_sum(lbits);
   if (lane == 0) {
@@ -963,10 +1016,11 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
 #ifndef UGPU_XU_WAVES_PER_EU
 #define UGPU_XU_WAVES_PER_EU 8
 #endif
+template <bool UW, bool FAST>
 __global__ __launch_bounds__(kCWaves * 64) __attribute__((amdgpu_waves_per_eu(UGPU_XU_WAVES_PER_EU)))
 void xu_kernel(ScanParams P)
 {
-  xc_body<false, false, true>(P);
+  xc_body<UW, false, true, FAST>(P);
 }
 
 // OFFSETS, second step: the one match per wave whose start an earlier wave
@@ -999,8 +1053,16 @@ hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64
                          P.out_len, n);
     return hipGetLastError();
   }
-  if (P.xu_tab)
-    hipLaunchKernelGGL(xu_kernel, dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  // (U mode: the FAST kernel unless the host redoes a range that met an XU_MIX
+  // or XU_SLOW lead, UGPU_FLAG_UMIX)
+  if (P.xu_tab && P.xu_w && !P.xu_exact)
+    hipLaunchKernelGGL((xu_kernel<true, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  else if (P.xu_tab && P.xu_w)
+    hipLaunchKernelGGL((xu_kernel<true, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  else if (P.xu_tab && !P.xu_exact)
+    hipLaunchKernelGGL((xu_kernel<false, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+  else if (P.xu_tab)
+    hipLaunchKernelGGL((xu_kernel<false, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   else if (P.xc_w)
     hipLaunchKernelGGL((xc_kernel<true, false, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
   else
@@ -1010,7 +1072,7 @@ hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64
 
 hipError_t xc_occupancy(bool u, int* n)
 {
-  if (u) return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xu_kernel, kCWaves * 64, 0);
+  if (u) return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xu_kernel<false, true>, kCWaves * 64, 0);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, xc_kernel<true, true, false>, kCWaves * 64, 0);
 }
 uint32_t xc_unit(bool u) { return u ? kCChunk * kUIter : kCTile; }
