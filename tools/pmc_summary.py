@@ -18,7 +18,7 @@ def db(d, sub):
     return sqlite3.connect(f[0]) if f else None
 
 
-def main(d, match=("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "xc_kernel", "scan_kernel")):
+def main(d, match=("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "xc_kernel", "xu_kernel", "scan_kernel")):
     kernels = []
     c = db(d, "trace")
     if c:
@@ -83,4 +83,4 @@ def main(d, match=("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "x
 
 if __name__ == "__main__":
     # usage: pmc_summary.py DIR [kernel-name-substring ...]
-    main(sys.argv[1], tuple(sys.argv[2:]) or ("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "xc_kernel", "scan_kernel"))
+    main(sys.argv[1], tuple(sys.argv[2:]) or ("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "xc_kernel", "xu_kernel", "scan_kernel"))

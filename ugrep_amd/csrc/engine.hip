@@ -19,6 +19,7 @@
 #include <cstring>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -1493,6 +1494,7 @@ struct ugpu_records {
     uint64_t base = 0, n = 0;
     uint8_t* host = nullptr;  // pinned: u32 start[n], u16 len[n], (caps) u16 cap[n]
     size_t host_bytes = 0;
+    hipEvent_t landed = nullptr;  // the D2H into host has completed (NULL: already waited for)
     std::vector<std::pair<uint64_t, uint64_t>> esc;  // (index, len | cap << 32), sorted
   };
   // published by the pipeline thread (under mu; a deque keeps references)
@@ -1509,6 +1511,9 @@ struct ugpu_records {
   uint64_t count = 0, digest = 0, dcap = 0;  // final once done
   // the consumer's piece: pieces[pi - 1] (pi = 0: none yet)
   size_t pi = 0;
+  bool sync_d2h = false;  // UGPU_REC_SYNC=1: the pipeline waits for each D2H before the next chunk
+  bool trace = false;     // UGPU_REC_TRACE=1: per-chunk timestamps on stderr
+  std::chrono::steady_clock::time_point t0;
   const uint32_t* st = nullptr;
   const uint16_t* ln = nullptr;
   const uint16_t* cp = nullptr;
@@ -1689,6 +1694,12 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
 {
   int rc = UGPU_OK;
   uint64_t count = 0, digest = 0, dcap = 0;
+  auto trace = [&](const char* what, uint64_t lo) {
+    if (R->trace)
+      fprintf(stderr, "[records] %9.3f ms  %-10s chunk at %llu\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - R->t0).count(), what,
+              (unsigned long long)lo);
+  };
   auto publish = [&](ugpu_records::Piece* pc, bool last) {
     std::lock_guard<std::mutex> lk(R->mu);
     if (pc) {
@@ -1758,6 +1769,7 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
     if (entry < hi) {
       for (;;) {
         if ((rc = ready(rend)) != UGPU_OK) break;
+        trace("on device", lo);
         rc = ugpu_scan(s, dbuf, entry, hi, rend, rend == len, 0, ws->st);
         if (!rc) rc = ugpu_scan_totals(s, &tot);
         if (rc == UGPU_HALO && rend < len) {
@@ -1812,6 +1824,7 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
         break;
       }
       rw->used[b] = true;
+      trace("packed", lo);
       // escapes (lengths or accept indices >= 0xFFFF, rare)
       const uint32_t ne = rw->h_nesc[b];
       if (ne) {
@@ -1824,9 +1837,19 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
         for (uint32_t k = 0; k < ne; ++k) pc.esc.push_back(std::make_pair(es[2 * k], es[2 * k + 1]));
         std::sort(pc.esc.begin(), pc.esc.end());
       }
-      // the piece is the consumer's once its copy has landed
-      if ((e = hipEventSynchronize(rw->copied[b])) != hipSuccess) {
-        rc = hip_fail(e, "records copy");
+      // the piece is the consumer's once its copy has landed: the consumer
+      // waits for that (records_advance), so this chunk's D2H overlaps the
+      // next chunk's scans
+      if (R->sync_d2h) {
+        if ((e = hipEventSynchronize(rw->copied[b])) != hipSuccess) {
+          rc = hip_fail(e, "records copy");
+          publish(&pc, false);
+          break;
+        }
+        trace("copied", lo);
+      } else if ((e = hipEventCreateWithFlags(&pc.landed, hipEventDisableTiming)) != hipSuccess ||
+                 (e = hipEventRecord(pc.landed, rw->dst)) != hipSuccess) {
+        rc = hip_fail(e, "records copy event");
         publish(&pc, false);
         break;
       }
@@ -1857,7 +1880,24 @@ bool records_advance(ugpu_records* r, int* rc)
     *rc = r->rc;
     return false;
   }
-  const ugpu_records::Piece& p = r->pieces[r->pi++];
+  ugpu_records::Piece& p = r->pieces[r->pi++];
+  if (p.landed) {
+    // (the pipeline thread only appends to the deque: p stays put)
+    hipEvent_t ev = p.landed;
+    lk.unlock();
+    const hipError_t e = hipEventSynchronize(ev);
+    (void)hipEventDestroy(ev);
+    lk.lock();
+    p.landed = nullptr;
+    if (e != hipSuccess) {
+      *rc = hip_fail(e, "records copy");
+      r->pi = r->published;
+      return false;
+    }
+  }
+  if (r->trace)
+    fprintf(stderr, "[records] %9.3f ms  consumer   piece %zu\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r->t0).count(), r->pi - 1);
   r->st = reinterpret_cast<const uint32_t*>(p.host);
   r->ln = reinterpret_cast<const uint16_t*>(p.host + 4 * p.n);
   r->cp = r->caps ? reinterpret_cast<const uint16_t*>(p.host + 6 * p.n) : nullptr;
@@ -1884,6 +1924,9 @@ int ugpu_find_records(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uin
   if (!R) return fail(UGPU_NOMEM, "host allocation");
   R->caps = dfa->t.cap1 == 0 ? 1 : 0;
   R->cap1 = dfa->t.cap1 ? dfa->t.cap1 : 1;
+  R->sync_d2h = env_u64("UGPU_REC_SYNC", 0) != 0;
+  R->trace = env_u64("UGPU_REC_TRACE", 0) != 0;
+  R->t0 = std::chrono::steady_clock::now();
   if (len == start) {
     R->done = R->input_free = true;
   } else {
@@ -1987,7 +2030,13 @@ int ugpu_records_free(ugpu_records* r)
 {
   if (!r) return UGPU_OK;
   if (r->worker.joinable()) r->worker.join();
-  for (auto& p : r->pieces) pinned_put(p.host, p.host_bytes);
+  for (auto& p : r->pieces) {
+    if (p.landed) {  // (never popped: its copy may still be running)
+      (void)hipEventSynchronize(p.landed);
+      (void)hipEventDestroy(p.landed);
+    }
+    pinned_put(p.host, p.host_bytes);
+  }
   delete r;
   return UGPU_OK;
 }

@@ -232,6 +232,35 @@ __device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t n
   return r;
 }
 
+// token codes of a lane's 16 bytes w (nx: the 4 bytes after them): all 16
+// LDS addresses first, then the 16 lookups two to a VGPR (bytes k and k + 2
+// of a dword in its 16-bit halves: ds_read_u8_d16 / ds_read_u8_d16_hi), so a
+// wave waits on its lookups once instead of once per dword
+__device__ __forceinline__ void ucode_lane(const CU& u, const uint32_t w[4], uint32_t nx, uint32_t c[4])
+{
+  typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
+  uint32_t a[16];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t x = w[d];
+    const uint32_t y = __builtin_amdgcn_alignbit(d < 3 ? w[d + 1] : nx, x, 8);
+    const uint32_t sw = y ^ ((x << 2) & 0xfcfcfcfcu);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[4 * d + k] = __builtin_amdgcn_perm(x, sw, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
+  }
+  v2u16 r[8];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    r[2 * d].x = u.tab[a[4 * d]];
+    r[2 * d].y = u.tab[a[4 * d + 2]];
+    r[2 * d + 1].x = u.tab[a[4 * d + 1]];
+    r[2 * d + 1].y = u.tab[a[4 * d + 3]];
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+    c[d] = __builtin_bit_cast(uint32_t, r[2 * d]) | (__builtin_bit_cast(uint32_t, r[2 * d + 1]) << 8);
+}
+
 // the code of byte 0 of x (byte 1 of x follows it)
 __device__ __forceinline__ uint32_t ucode_b0(const CU& u, uint32_t x)
 {
@@ -329,8 +358,12 @@ __device__ __forceinline__ void umask(CU& u, const uint4& v, uint64_t q, uint32_
   }
   const uint32_t nx = __builtin_amdgcn_update_dpp(u.nx0, w[0], 0x130, 0xf, 0xf, false);  // wave_shl:1
   uint32_t c[4];
+#ifdef UGPU_XU_PERDW
 #pragma unroll
   for (int d = 0; d < 4; ++d) c[d] = ucode_dw(u, w[d], d < 3 ? w[d + 1] : nx);
+#else
+  ucode_lane(u, w, nx, c);
+#endif
   // the code of the byte after the lane (only its first byte is used)
   const uint32_t cn = __builtin_amdgcn_update_dpp(ucode_b0(u, u.nx0), c[0], 0x130, 0xf, 0xf, false);
   if constexpr (F == 1) u.x8 |= c[0] | c[1] | c[2] | c[3];
@@ -912,7 +945,13 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
         const uint64_t tn = (U || t + 1 < fte) ? ts + kTile : ts;
         const __amdgpu_buffer_rsrc_t rn = crsrc(P.g + tn, rend16 > tn ? rend16 - tn : 0);
 #pragma unroll
-        for (int j = 0; j < kIt; ++j) nxt[j] = cload(rn, j * kCChunk + lo16);
+        for (int j = 0; j < kIt; ++j) {
+#if defined(UGPU_XU_ABL) && UGPU_XU_ABL == 4  // compute only: no HBM reads in the main loop (benchmarking; wrong counts)
+          nxt[j] = uint4{cur[j].y, cur[j].z, cur[j].w, cur[j].x ^ (uint32_t)t};
+#else
+          nxt[j] = cload(rn, j * kCChunk + lo16);
+#endif
+        }
         if constexpr (U) nfn = __builtin_amdgcn_raw_buffer_load_b32(rn, (int)kTile, 0, 0);
       }
       CIt a;
