@@ -484,7 +484,7 @@ struct COut {
   uint32_t open = 0;
   uint64_t open_start = ~0ull;
   uint64_t fix = ~0ull;
-  uint16_t* stage = nullptr;  // the wave's LDS staging: kStage start offsets, then kStage end offsets
+  uint16_t* stage = nullptr;  // the wave's LDS staging, two slots: kStage start offsets, then kStage end offsets
 };
 
 // lanes' 16-byte masks: bit 8j of dword d -> bit 4d + j
@@ -514,26 +514,43 @@ __device__ __forceinline__ void cwave_sync()
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// the staging capacity per wave and kind (starts, ends): 1 KiB of LDS per
-// wave for the pair classifier (16 KiB beside its 128 KiB table); U mode's
-// tables leave less (UGPU_XC_STAGE_U)
-constexpr uint32_t kStage = 256;
+// the staging capacity per wave, slot and kind (starts, ends): two slots of
+// 960 B per wave for the pair classifier (30 KiB beside its 128 KiB table);
+// U mode (UGPU_XC_STAGE_U) 2 KiB per wave beside its 72 KiB
+constexpr uint32_t kStage = 240;
 #ifndef UGPU_XC_STAGE_U
 #define UGPU_XC_STAGE_U 256
 #endif
 constexpr uint32_t kStageU = UGPU_XC_STAGE_U;
 
+// A chunk's staged records whose stores wait for the end of the tile (see
+// cflush); all uniform.
+struct CPend {
+  uint64_t q0 = 0, cur = 0, open_start = ~0ull;
+  uint32_t R = 0, E = 0, open = 0;
+};
+
 // Write the chunk's match records.  An end at position e (In_{e-1} set, In_e
 // clear or a new start at e) closes the latest match started before it;
 // starts get consecutive indices in chain order.  The chunk's start and end
-// offsets are staged in the wave's LDS slots (ordered by a wave scan of the
-// lanes' counts), then written by consecutive lanes: start[], cap[] and the
-// lengths (end - start: the start is staged too, or the open match's) leave
-// as coalesced stores.  A match opened by an earlier wave gets its raw end
-// position and is fixed by xc_fix_kernel.  Chunks with more than kStage
-// starts or ends take the per-lane path.
+// offsets are staged in LDS slot `slot` of the wave (ordered by a wave scan of
+// the lanes' counts); cflush then writes them by consecutive lanes: start[],
+// cap[] and the lengths (end - start: the start is staged too, or the open
+// match's) leave as coalesced stores.  A match opened by an earlier wave gets
+// its raw end position and is fixed by xc_fix_kernel.  Chunks with more than
+// kStage starts or ends take the per-lane path (stores at once).
+//
+// The main loop stages a tile's chunks, waits for the next tile's loads (and
+// with them the previous tile's stores: gfx950 counts loads and stores in one
+// in-order vmcnt) and only then issues the tile's stores (cflush), so that no
+// store of a tile is waited for before a whole tile of work.  Measured: the
+// same time as storing right after each chunk (C4 OFFSETS 8.4 ms per step
+// either way); the pass is bound by its own work -- taking the stores out
+// (with their LDS reads) saves 1.9 ms, the staging another 2.0 ms, against
+// 2.1 ms for the scan itself.
 template <uint32_t kStage>
-__device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], const uint32_t sb[4], uint64_t q, COut& o)
+__device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], const uint32_t sb[4], uint64_t q, COut& o,
+                                       CPend& pd, uint16_t* slot)
 {
   uint32_t enm[4];
 #pragma unroll
@@ -548,10 +565,11 @@ __device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], con
   const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)is, 63), E = (uint32_t)__builtin_amdgcn_readlane((int)ie, 63);
   const int lane = threadIdx.x & 63;
   const uint64_t q0 = q - 16ull * (uint32_t)lane + (uint64_t)o.delta;  // the chunk's reported base
+  pd.R = pd.E = 0;
   if (R == 0 && E == 0) return;
   if (R <= kStage && E <= kStage) {
-    uint16_t* S = o.stage;
-    uint16_t* En = o.stage + kStage;
+    uint16_t* S = slot;
+    uint16_t* En = slot + kStage;
     const uint32_t lb = 16u * (uint32_t)lane;
     uint32_t m = s16, k = is - ns;
     while (m) {
@@ -564,46 +582,21 @@ __device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], con
       En[k++] = (uint16_t)(lb + __builtin_ctz(m));
       m &= m - 1;
     }
-    cwave_sync();
-    for (uint32_t t = (uint32_t)lane; t < R; t += 64) {
-      const uint64_t i = o.cur + t;
-      if (i < o.capacity) {
-        o.start[i] = q0 + S[t];
-        o.cap[i] = o.cap1;
-      } else {
-        o.over = 1;
-      }
-    }
-    for (uint32_t t = (uint32_t)lane; t < E; t += 64) {
-      const uint64_t i = o.cur + t - o.open;  // the match this end closes
-      const uint64_t e = q0 + En[t];
-      if (i < o.capacity) {
-        if (t < o.open) {
-          if (o.open_start == ~0ull) {
-            o.len[i] = (uint32_t)e;  // (raw: xc_fix_kernel subtracts the start)
-            o.fix = i;
-          } else {
-            o.len[i] = (uint32_t)(e - o.open_start);
-          }
-        } else {
-          o.len[i] = (uint32_t)(e - (q0 + S[t - o.open]));
-        }
-      } else {
-        o.over = 1;
-      }
-    }
+    pd.q0 = q0;
+    pd.cur = o.cur;
+    pd.open = o.open;
+    pd.open_start = o.open_start;
+    pd.R = R;
+    pd.E = E;
     // the match open after the chunk: the last start, when it has no end
     const uint32_t open = o.open + R - E;
-    if (open && R) o.open_start = q0 + S[R - 1];
+    if (open && R) {
+      const int lh = 63 - __builtin_clzll(__ballot(s16 != 0));
+      const uint32_t last = lb + 31u - (uint32_t)__builtin_clz(s16 | 1u);  // (read in lane lh)
+      o.open_start = q0 + (uint32_t)__builtin_amdgcn_readlane((int)last, lh);
+    }
     o.open = open;
     o.cur += R;
-    cwave_sync();  // (the next chunk's staging overwrites the slots)
-    const uint64_t fl = __ballot(o.fix != ~0ull);  // (only lane 0 can close the open match, t = 0)
-    if (fl) {
-      const int l = __builtin_ctzll(fl);
-      o.fix = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(o.fix >> 32), l) << 32) |
-              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)o.fix, l);
-    }
     return;
   }
   // the per-lane path: each lane writes its own records; an end closes the
@@ -669,12 +662,94 @@ __device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], con
   o.cur += R;
 }
 
+// The stores of a staged chunk (cwrite); the caller has synchronised the
+// wave after staging and does again before the slot is staged anew.
+template <uint32_t kStage>
+__device__ __forceinline__ void cflush(const CPend& p, const uint16_t* slot, COut& o)
+{
+  if (p.R == 0 && p.E == 0) return;
+  const uint16_t* S = slot;
+  const uint16_t* En = slot + kStage;
+  const uint32_t lane = threadIdx.x & 63;
+  if (p.cur + p.R <= o.capacity && p.E <= p.cur + p.R) {
+    // (all in range: wave-uniform bases, 32-bit lane offsets, no checks)
+    uint64_t* const st = o.start + p.cur;
+    uint32_t* const cp = o.cap + p.cur;
+    uint32_t* const ln = o.len + (p.cur - p.open);
+    for (uint32_t t = lane; t < p.R; t += 64) {
+      st[t] = p.q0 + S[t];
+      cp[t] = o.cap1;
+    }
+    uint32_t t = lane;
+    if (p.open && t == 0 && t < p.E) {  // the end of the match open at the chunk start
+      const uint64_t e = p.q0 + En[0];
+      if (p.open_start == ~0ull) {
+        ln[0] = (uint32_t)e;  // (raw: xc_fix_kernel subtracts the start)
+        o.fix = p.cur - 1;
+      } else {
+        ln[0] = (uint32_t)(e - p.open_start);
+      }
+      t += 64;
+    }
+    for (; t < p.E; t += 64) ln[t] = (uint32_t)En[t] - (uint32_t)S[t - p.open];
+  } else {
+    for (uint32_t t = lane; t < p.R; t += 64) {
+      const uint64_t i = p.cur + t;
+      if (i < o.capacity) {
+        o.start[i] = p.q0 + S[t];
+        o.cap[i] = o.cap1;
+      } else {
+        o.over = 1;
+      }
+    }
+    for (uint32_t t = lane; t < p.E; t += 64) {
+      const uint64_t i = p.cur + t - p.open;  // the match this end closes
+      const uint64_t e = p.q0 + En[t];
+      if (i < o.capacity) {
+        if (t < p.open) {
+          if (p.open_start == ~0ull) {
+            o.len[i] = (uint32_t)e;  // (raw: xc_fix_kernel subtracts the start)
+            o.fix = i;
+          } else {
+            o.len[i] = (uint32_t)(e - p.open_start);
+          }
+        } else {
+          o.len[i] = (uint32_t)(e - (p.q0 + S[t - p.open]));
+        }
+      } else {
+        o.over = 1;
+      }
+    }
+  }
+  if (p.open && p.E) {
+    const uint64_t fl = __ballot(o.fix != ~0ull);  // (only lane 0 can close the open match, t = 0)
+    if (fl) {
+      const int l = __builtin_ctzll(fl);
+      o.fix = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(o.fix >> 32), l) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)o.fix, l);
+    }
+  }
+}
+
+// cwrite with its stores at once (the masked chunks), in slot 0
+template <uint32_t kStage>
+__device__ __forceinline__ void cwrite_now(const CLane& L, const uint32_t cb[4], const uint32_t sb[4], uint64_t q,
+                                           COut& o)
+{
+  CPend p;
+  cwrite<kStage>(L, cb, sb, q, o, p, o.stage);
+  if (p.R == 0 && p.E == 0) return;
+  cwave_sync();
+  cflush<kStage>(p, o.stage, o);
+  cwave_sync();
+}
+
 // One chunk (16 bytes per lane at q = chunk base + 16 lane); cw = the wave's
 // carry, updated.  Returns the lane's carry-in bits.
 template <bool MASK, bool W, bool WR = false, bool U = false>
 __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_t q, const CLim& lim, uint32_t& cw,
                                        uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4], CW& wc, COut& o,
-                                       CU& u)
+                                       CU& u, CPend* pd = nullptr, uint16_t* slot = nullptr)
 {
 #if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 1  // loads only (benchmarking; wrong counts)
   if (!MASK) {
@@ -692,7 +767,12 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
   const uint64_t cin = clook(__ballot(gen), __ballot(prop), cw, cw);
   uint32_t sb[4];
   cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb, sb);
-  if constexpr (WR) cwrite<U ? kStageU : kStage>(L, cb, sb, q, o);
+  if constexpr (WR) {
+    if (pd)
+      cwrite<U ? kStageU : kStage>(L, cb, sb, q, o, *pd, slot);  // (stores by the caller's cflush)
+    else
+      cwrite_now<U ? kStageU : kStage>(L, cb, sb, q, o);
+  }
 }
 
 // U mode, COUNT, a chunk wholly inside [wlo, hi): no byte only continues a
@@ -723,6 +803,31 @@ __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q,
     const uint32_t wd = (4u * d) | ((4u * d + 1) << 8) | ((4u * d + 2) << 16) | ((4u * d + 3) << 24);
     ws = __builtin_amdgcn_udot4(st, wd, ws, false);
   }
+}
+
+// U mode, OFFSETS (WRITE), a chunk wholly inside [wlo, hi): In = M here too,
+// so the chunk's records come straight from M -- starts M & !M_prev, ends
+// M_prev & !M -- with no carry chain, in cwrite's form (the adder codes
+// e = 0xFF * M, the carry-in bits M_prev).  FAST as uchunk_direct: the COUNT
+// pass of the same range ran the same test and met no XU_MIX / XU_SLOW lead.
+template <bool FAST>
+__device__ __forceinline__ void uchunk_write(CU& u, const uint4& v, uint64_t q, uint32_t& mprev, COut& o, CPend& pd,
+                                             uint16_t* slot)
+{
+  uint32_t m[4];
+  umask<false, FAST ? 1 : 2>(u, v, q, m);
+  const uint32_t mp = __builtin_amdgcn_update_dpp(mprev, m[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
+  mprev = __builtin_amdgcn_readlane(m[3], 63);
+  CLane L;
+  uint32_t cb[4], sb[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t pm = __builtin_amdgcn_alignbit(m[d], d ? m[d - 1] : mp, 24);  // M of the byte before
+    cb[d] = pm;
+    sb[d] = m[d] & ~pm;
+    L.E[d] = (m[d] << 8) - m[d];
+  }
+  cwrite<kStageU>(L, cb, sb, q, o, pd, slot);
 }
 
 // Exit search after a masked chunk of the wave holding hi: the exit is the
@@ -776,7 +881,8 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
   __shared__ __attribute__((aligned(16))) uint16_t pcode[(kCPair && !U) ? 65536 : 8];
   __shared__ __attribute__((aligned(16))) uint32_t utab[U ? 65536 / 4 : 1];
   __shared__ __attribute__((aligned(16))) uint32_t ubm3[U ? kXuBm3 : 1];
-  __shared__ __attribute__((aligned(16))) uint16_t wstage[WR ? kCWaves * 2 * (U ? kStageU : kStage) : 2];
+  constexpr uint32_t kStg = U ? kStageU : kStage;
+  __shared__ __attribute__((aligned(16))) uint16_t wstage[WR ? kCWaves * 2 * 2 * kStg : 2];
   CU u;
   if constexpr (U) {
     // the pair table: entry (x, y) at x << 8 | (y ^ (x << 2 & 0xfc))
@@ -836,7 +942,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     out.capacity = P.out_capacity;
     out.delta = P.delta;
     out.cap1 = P.cap1;
-    out.stage = wstage + (uint32_t)wid * 2u * (U ? kStageU : kStage);
+    out.stage = wstage + (uint32_t)wid * 4u * kStg;
   }
   // option W: the code of the byte before position p (byte 3), 0 at the buffer start
   auto xprev = [&](uint64_t p) -> uint32_t { return W && !U && p > P.bob ? (uint32_t)bcode[P.g[p - 1]] << 24 : 0u; };
@@ -937,6 +1043,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
       if constexpr (U) nfc = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)kTile, 0, 0);
       mprev = cw << 24;
     }
+    CPend pend[2];  // (WR: the staged chunks of the tile)
     for (uint64_t t = ftb; t < fte; ++t) {
       const uint64_t ts = t * kTile;
       {
@@ -969,10 +1076,28 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
             u.nx0 = (__builtin_amdgcn_readfirstlane(nfc) & in) | (u.null4 & ~in);
           }
         }
+        uint16_t* const slot = out.stage + (uint32_t)(j & 1) * 2u * kStg;
         if constexpr (U && !WR)
           uchunk_direct<W, FAST>(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls);
+        else if constexpr (U && WR)
+          uchunk_write<FAST>(u, cur[j], ts + j * kCChunk + lo16, mprev, out, pend[j & 1], slot);
+        else if constexpr (WR)
+          cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u,
+                                  &pend[j & 1], slot);
         else
           cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u);
+        if constexpr (WR) {
+          // the stores of the staged slots: at the tile end after the next
+          // tile's loads (cwrite: they then overlap the next tile's work),
+          // mid-tile when both slots are full
+          if constexpr ((j & 1) == 1 || j + 1 == kIt) {
+            if constexpr (j + 1 == kIt) __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+            cwave_sync();
+            cflush<kStg>(pend[0], out.stage, out);
+            if constexpr ((j & 1) == 1) cflush<kStg>(pend[1], out.stage + 2u * kStg, out);
+            cwave_sync();
+          }
+        }
       };
       cunroll<0, kIt>(chunk);
       uint32_t c = 0, cj = 0;
@@ -990,6 +1115,9 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     }
   }
   if (fte > ftb) q0 = fte * kTile;
+  if constexpr (U && WR) {
+    if (fte > ftb) cw = (mprev >> 24) & 1u;  // (the match open after the main loop)
+  }
   if constexpr (U && !WR) {
     if (fte > ftb) {
       // the wave carry after the main loop, and ls's In_i -> In_{i-1} form:
@@ -1050,13 +1178,25 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_kernel(ScanParams P)
   xc_body<W, WR, U>(P);
 }
 
+// U mode OFFSETS: FAST unless the COUNT pass needed the exact kernel
+template <bool FAST>
+__global__ __launch_bounds__(kCWaves * 64) void xu_write_kernel(ScanParams P)
+{
+  xc_body<false, true, true, FAST>(P);
+}
+
 // U mode COUNT: LDS-latency bound (its byte lookups), so two workgroups per CU
 // (8 waves per SIMD, at most 64 VGPRs; the tables take 72 KiB per workgroup)
 #ifndef UGPU_XU_WAVES_PER_EU
 #define UGPU_XU_WAVES_PER_EU 8
 #endif
+// (option W: its checks keep more state live; UGPU_XU_W_WAVES_PER_EU)
+#ifndef UGPU_XU_W_WAVES_PER_EU
+#define UGPU_XU_W_WAVES_PER_EU UGPU_XU_WAVES_PER_EU
+#endif
 template <bool UW, bool FAST>
-__global__ __launch_bounds__(kCWaves * 64) __attribute__((amdgpu_waves_per_eu(UGPU_XU_WAVES_PER_EU)))
+__global__ __launch_bounds__(kCWaves * 64) __attribute__((amdgpu_waves_per_eu(UW ? UGPU_XU_W_WAVES_PER_EU
+                                                                                  : UGPU_XU_WAVES_PER_EU)))
 void xu_kernel(ScanParams P)
 {
   xc_body<UW, false, true, FAST>(P);
@@ -1077,8 +1217,10 @@ __global__ __launch_bounds__(256) void xc_fix_kernel(const uint64_t* fix, uint32
 hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64_t count)
 {
   if (write) {
-    if (P.xu_tab)
-      hipLaunchKernelGGL((xc_kernel<false, true, true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    if (P.xu_tab && !P.xu_exact)
+      hipLaunchKernelGGL((xu_write_kernel<true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    else if (P.xu_tab)
+      hipLaunchKernelGGL((xu_write_kernel<false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
     else if (P.xc_w)
       hipLaunchKernelGGL((xc_kernel<true, true, false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
     else
