@@ -1486,15 +1486,18 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
 // input goes H2D in chunks on a copy thread; each chunk is scanned from the true
 // chain entry (the previous chunk's exit) as soon as it and the next one are on
 // the device, its records are written, packed to 6 B (u32 start - chunk base,
-// u16 len; + u16 cap when the table has several accept indices) and copied
-// asynchronously into pinned host memory -- H2D, scans and D2H overlap.  The
-// records are decoded when popped.
+// u16 len; + u16 cap when the table has several accept indices) -- or, for
+// dense chunks of one accept index (a record per < 32 bytes), to 2 B (u8 gap
+// from the previous record's end, u8 len) -- and copied asynchronously into
+// pinned host memory -- H2D, scans and D2H overlap.  The records are decoded
+// when popped.
 struct ugpu_records {
   struct Piece {
     uint64_t base = 0, n = 0;
     uint8_t* host = nullptr;  // pinned: u32 start[n], u16 len[n], (caps) u16 cap[n]
     size_t host_bytes = 0;
     hipEvent_t landed = nullptr;  // the D2H into host has completed (NULL: already waited for)
+    bool dense = false;           // host: u8 gap[n], u8 len[n] (pack_records_kernel dense)
     std::vector<std::pair<uint64_t, uint64_t>> esc;  // (index, len | cap << 32), sorted
   };
   // published by the pipeline thread (under mu; a deque keeps references)
@@ -1517,6 +1520,9 @@ struct ugpu_records {
   const uint32_t* st = nullptr;
   const uint16_t* ln = nullptr;
   const uint16_t* cp = nullptr;
+  const uint8_t* dg = nullptr;  // dense piece: gaps (ln, cp unused)
+  const uint8_t* dl = nullptr;  // dense piece: lengths
+  uint64_t last = 0;            // dense piece: the end of the last popped record (offset from base)
   const std::pair<uint64_t, uint64_t>* esc = nullptr;
   uint64_t base = 0, n = 0, ri = 0, ei = 0, ne = 0;
 };
@@ -1789,7 +1795,8 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
       ugpu_records::Piece pc;
       pc.base = lo;
       pc.n = tot.count;
-      const uint64_t n = pc.n, bytes = n * (R->caps ? 8 : 6);
+      pc.dense = !R->caps && pc.n * 32 >= hi - lo && env_u64("UGPU_REC_DENSE", 0) != 0;
+      const uint64_t n = pc.n, bytes = n * (pc.dense ? 2 : R->caps ? 8 : 6);
       if ((e = ws->reserve_out(n)) != hipSuccess) {
         rc = hip_fail(e, "records output");
         break;
@@ -1810,8 +1817,8 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
         break;
       }
       if ((e = hipMemsetAsync(rw->d_nesc + b, 0, sizeof(uint32_t), ws->st)) != hipSuccess ||
-          (e = launch_pack_records(ws->d_start, ws->d_len, ws->d_cap, n, lo, rw->d_pack[b], R->caps, rw->d_esc[b],
-                                   rw->d_nesc + b, ws->st)) != hipSuccess ||
+          (e = launch_pack_records(ws->d_start, ws->d_len, ws->d_cap, n, lo, rw->d_pack[b], R->caps, pc.dense ? 1 : 0,
+                                   rw->d_esc[b], rw->d_nesc + b, ws->st)) != hipSuccess ||
           (e = hipMemcpyAsync(rw->h_nesc + b, rw->d_nesc + b, sizeof(uint32_t), hipMemcpyDeviceToHost, ws->st)) !=
               hipSuccess ||
           (e = hipEventRecord(rw->packed[b], ws->st)) != hipSuccess ||
@@ -1898,9 +1905,19 @@ bool records_advance(ugpu_records* r, int* rc)
   if (r->trace)
     fprintf(stderr, "[records] %9.3f ms  consumer   piece %zu\n",
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r->t0).count(), r->pi - 1);
-  r->st = reinterpret_cast<const uint32_t*>(p.host);
-  r->ln = reinterpret_cast<const uint16_t*>(p.host + 4 * p.n);
-  r->cp = r->caps ? reinterpret_cast<const uint16_t*>(p.host + 6 * p.n) : nullptr;
+  if (p.dense) {
+    r->st = nullptr;
+    r->ln = nullptr;
+    r->cp = nullptr;
+    r->dg = p.host;
+    r->dl = p.host + p.n;
+    r->last = 0;
+  } else {
+    r->dg = r->dl = nullptr;
+    r->st = reinterpret_cast<const uint32_t*>(p.host);
+    r->ln = reinterpret_cast<const uint16_t*>(p.host + 4 * p.n);
+    r->cp = r->caps ? reinterpret_cast<const uint16_t*>(p.host + 6 * p.n) : nullptr;
+  }
   r->esc = p.esc.data();
   r->ne = p.esc.size();
   r->base = p.base;
@@ -1956,6 +1973,22 @@ int ugpu_records_next(ugpu_records* r, uint64_t* start, uint32_t* len, uint32_t*
     if (!records_advance(r, &rc)) return rc ? -rc : 0;
   }
   const uint64_t i = r->ri++;
+  if (r->dg) {
+    uint64_t so;
+    uint32_t l = r->dl[i];
+    if ((l == 0xFFu || r->dg[i] == 0xFFu) && r->ei < r->ne && r->esc[r->ei].first == i) {
+      const uint64_t v = r->esc[r->ei++].second;
+      so = (uint32_t)v;
+      l = (uint32_t)(v >> 32);
+    } else {
+      so = r->last + r->dg[i];
+    }
+    r->last = so + l;
+    *start = r->base + so;
+    *len = l;
+    *cap = r->cap1;
+    return 1;
+  }
   uint32_t l = r->ln[i], c = r->cp ? r->cp[i] : r->cap1;
   if ((l == 0xFFFFu || c == 0xFFFFu) && r->ei < r->ne && r->esc[r->ei].first == i) {
     const uint64_t v = r->esc[r->ei++].second;
@@ -1983,6 +2016,31 @@ int ugpu_records_drain(ugpu_records* r, uint64_t* n, uint64_t* digest, uint64_t*
   }
   int rc = UGPU_OK;
   while (records_advance(r, &rc)) {
+    if (r->dg) {
+      // a dense piece: starts are sums of gaps and lengths, escapes in order
+      const uint8_t* g = r->dg;
+      const uint8_t* l = r->dl;
+      const uint64_t pn = r->n, base = r->base;
+      uint64_t so = 0, sdg = 0, ssum = 0, ei = 0;
+      for (uint64_t i = 0; i < pn; ++i) {
+        uint64_t li = l[i];
+        if ((li == 0xFFu || g[i] == 0xFFu) && ei < r->ne && r->esc[ei].first == i) {
+          const uint64_t v = r->esc[ei++].second;
+          so = (uint32_t)v;
+          li = v >> 32;
+        } else {
+          so += g[i];
+        }
+        ssum += so;
+        sdg += so * 31 + li;
+        so += li;
+      }
+      dg += sdg + pn * base * 31;
+      dc += (ssum + pn * (base + 1)) * r->cap1;
+      k += pn;
+      r->ri = r->n;
+      continue;
+    }
     const uint32_t* ps = r->st;
     const uint16_t* pl = r->ln;
     const uint16_t* pc = r->cp;

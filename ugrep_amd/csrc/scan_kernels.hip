@@ -173,11 +173,31 @@ __global__ void chain_fix_kernel(ScanParams P, uint64_t old_entry, uint64_t new_
 // u16 cap; a len or cap >= 0xFFFF is written as 0xFFFF and its record's
 // (index, len | cap << 32) appended to esc through a counter (rare: the host
 // sorts them).  One record per thread, fully coalesced.
+//
+// dense (one accept index, many records per byte -- identifiers, words): u8
+// gap from the previous record's end (the chunk base for the first) and u8
+// len, 2 B per record; a gap or len >= 0xFF is written as 0xFF and the
+// record's (index, start - base | len << 32) escapes.
 __global__ void pack_records_kernel(const uint64_t* start, const uint32_t* len, const uint32_t* cap, uint64_t n,
-                                    uint64_t base, uint8_t* out, int caps, uint64_t* esc, uint32_t* nesc)
+                                    uint64_t base, uint8_t* out, int caps, int dense, uint64_t* esc, uint32_t* nesc)
 {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (dense) {
+    const uint64_t s = start[i] - base;
+    const uint32_t l = len[i];
+    const uint64_t pe = i ? start[i - 1] - base + len[i - 1] : 0;  // (FIND matches do not overlap: s >= pe)
+    const uint64_t g = s - pe;
+    const bool ok = g < 0xFFu && l < 0xFFu;
+    out[i] = (uint8_t)(ok ? g : 0xFFu);
+    out[n + i] = (uint8_t)(ok ? l : 0xFFu);
+    if (!ok) {
+      const uint32_t k = atomicAdd(nesc, 1u);
+      esc[2 * k] = i;
+      esc[2 * k + 1] = (s & 0xffffffffull) | ((uint64_t)l << 32);
+    }
+    return;
+  }
   uint32_t* o_start = reinterpret_cast<uint32_t*>(out);
   uint16_t* o_len = reinterpret_cast<uint16_t*>(out + 4 * n);
   uint16_t* o_cap = reinterpret_cast<uint16_t*>(out + 6 * n);
@@ -194,13 +214,13 @@ __global__ void pack_records_kernel(const uint64_t* start, const uint32_t* len, 
 
 // ---------------------------------------------------------------- launchers
 hipError_t launch_pack_records(const uint64_t* start, const uint32_t* len, const uint32_t* cap, uint64_t n,
-                               uint64_t base, uint8_t* out, int caps, uint64_t* esc, uint32_t* nesc,
+                               uint64_t base, uint8_t* out, int caps, int dense, uint64_t* esc, uint32_t* nesc,
                                hipStream_t stream)
 {
   if (n == 0) return hipSuccess;
   const uint64_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL(pack_records_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, start, len, cap, n, base,
-                     out, caps, esc, nesc);
+                     out, caps, dense, esc, nesc);
   return hipGetLastError();
 }
 

@@ -182,7 +182,7 @@ uint64_t forest_block();
 // launchers (scan_kernels.hip, gen.hip)
 hipError_t launch_fix(const ScanParams& P, uint32_t format, hipStream_t stream);
 hipError_t launch_pack_records(const uint64_t* start, const uint32_t* len, const uint32_t* cap, uint64_t n,
-                               uint64_t base, uint8_t* out, int caps, uint64_t* esc, uint32_t* nesc,
+                               uint64_t base, uint8_t* out, int caps, int dense, uint64_t* esc, uint32_t* nesc,
                                hipStream_t stream);
 hipError_t launch_chain_fix(const ScanParams& P, uint32_t format, uint64_t old_entry, uint64_t new_entry,
                             hipStream_t stream);
