@@ -231,7 +231,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     xdev = dev if backend == "nccl" else torch.device("cpu")
-    if world > 1:
+    # UGPU_BENCH_PG=1: the process group and the stitch / gather collectives
+    # also for one rank (rehearses the RCCL path on a one-GPU box)
+    pg = world > 1 or os.environ.get("UGPU_BENCH_PG") == "1"
+    if pg:
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
@@ -286,7 +289,7 @@ def main():
         sc.offsets(recs_dev["start"].data_ptr(), recs_dev["len"].data_ptr(), recs_dev["acc"].data_ptr(), count,
                    sptr)
         st, ln, ac = recs_dev["start"][:count], recs_dev["len"][:count], recs_dev["acc"][:count]
-        if world > 1:
+        if pg:
             st, ln, ac = gather_offsets(st.to(xdev), ln.to(xdev), ac.to(xdev))
         return st, ln, ac
 
@@ -295,11 +298,11 @@ def main():
         t = sc.totals()
         kms.append(sc.kernel_ms())
         rec = dict(entry=t.entry + lo, exit=t.exit + lo, count=t.count, digest=t.digest, dcap=t.dcap)
-        if world > 1:
+        if pg:
             rec = stitch(rec, fix_fn, device=xdev)
         if args.offsets:
             count = t.count
-            if world > 1 and rec["entries"][rank] != lo:  # chain re-entered this shard: re-scan from there
+            if pg and rec["entries"][rank] != lo:  # chain re-entered this shard: re-scan from there
                 # (an entry at or past hi: the previous shard's last match covers this whole shard)
                 ent = min(rec["entries"][rank], hi)
                 sc.scan(ptr, ent - lo, hi - lo, n_read, eof, lo, sptr)
@@ -310,17 +313,17 @@ def main():
     for _ in range(args.warmup):
         res = step()
     kms.clear()
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if pg:
         e = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -344,10 +347,10 @@ def main():
         del buf
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
-        if world > 1:
+        if pg:
             dist.barrier()  # every shard buffer is released before rank 0 allocates the whole stream
         verified = verify_whole(args, kind, total, pat, res, rank, dev, sptr) if rank == 0 else None
-        if world > 1:
+        if pg:
             dist.barrier()
 
     k_avg = float(np.mean(kms)) if kms else float("nan")
@@ -387,7 +390,7 @@ def main():
         m64 = (1 << 64) - 1
         dg = int((st * 31 + ln.to(torch.int64)).sum().item()) & m64  # int64 sums wrap like the u64 digest
         out["offsets"] = {"records": int(st.numel()), "bytes_per_record": 16,
-                          "gathered_to": "all ranks" if world > 1 else "local",
+                          "gathered_to": "all ranks" if pg else "local",
                           "digest_matches_totals": int(st.numel()) == res["count"] and dg == res["digest"]}
     tr = measured_traffic(args.config, hi - lo, KERNELS[info["kernel"]])
     if tr and tr.get("kernel_ms") and abs(tr["kernel_ms"] - k_avg) > 0.05 * k_avg:
@@ -406,7 +409,7 @@ def main():
             out["parity_vs_reference"] = cpu_leg[1]
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 
