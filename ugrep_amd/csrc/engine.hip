@@ -2017,25 +2017,49 @@ int ugpu_records_drain(ugpu_records* r, uint64_t* n, uint64_t* digest, uint64_t*
   int rc = UGPU_OK;
   while (records_advance(r, &rc)) {
     if (r->dg) {
-      // a dense piece: starts are sums of gaps and lengths, escapes in order
+      // a dense piece: start_i = so + sum of gaps up to i + lengths before i,
+      // so between escapes the sums of starts are weighted sums of the gaps
+      // and lengths (no serial chain; the loop vectorises); an escaped record
+      // carries its own start and restarts the sum after it
       const uint8_t* g = r->dg;
       const uint8_t* l = r->dl;
       const uint64_t pn = r->n, base = r->base;
-      uint64_t so = 0, sdg = 0, ssum = 0, ei = 0;
-      for (uint64_t i = 0; i < pn; ++i) {
-        uint64_t li = l[i];
-        if ((li == 0xFFu || g[i] == 0xFFu) && ei < r->ne && r->esc[ei].first == i) {
-          const uint64_t v = r->esc[ei++].second;
-          so = (uint32_t)v;
-          li = v >> 32;
-        } else {
-          so += g[i];
+      uint64_t so = 0, ssum = 0, slen = 0, a = 0;
+      auto seg = [&](uint64_t b) {
+        // (blocks of 256: the in-block weights j * byte fit 16 bits, so the
+        // inner loop vectorises with 16-bit multiplies)
+        uint64_t sg = 0, skg = 0, sl = 0, skl = 0;
+        for (uint64_t kb = a; kb < b; kb += 256) {
+          const uint32_t m = b - kb < 256 ? (uint32_t)(b - kb) : 256u;
+          const uint8_t* gp = g + kb;
+          const uint8_t* lp = l + kb;
+          uint32_t bg = 0, bjg = 0, bl = 0, bjl = 0;
+          for (uint32_t j = 0; j < m; ++j) {
+            bg += gp[j];
+            bjg += (uint16_t)((uint16_t)j * gp[j]);
+            bl += lp[j];
+            bjl += (uint16_t)((uint16_t)j * lp[j]);
+          }
+          sg += bg;
+          sl += bl;
+          skg += kb * bg + bjg;
+          skl += kb * bl + bjl;
         }
+        ssum += (b - a) * so + (b * sg - skg) + (b ? (b - 1) * sl - skl : 0);
+        slen += sl;
+        so += sg + sl;
+      };
+      for (uint64_t j = 0; j < r->ne; ++j) {
+        const uint64_t e = r->esc[j].first, v = r->esc[j].second;
+        seg(e);
+        so = (uint32_t)v;
         ssum += so;
-        sdg += so * 31 + li;
-        so += li;
+        slen += v >> 32;
+        so += v >> 32;
+        a = e + 1;
       }
-      dg += sdg + pn * base * 31;
+      seg(pn);
+      dg += 31 * (ssum + pn * base) + slen;
       dc += (ssum + pn * (base + 1)) * r->cap1;
       k += pn;
       r->ri = r->n;
