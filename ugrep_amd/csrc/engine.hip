@@ -132,6 +132,10 @@ struct ugpu_scanner {
   BlockRec* d_recs = nullptr;
   uint64_t* d_entries = nullptr;
   uint64_t* d_obase = nullptr;
+  // xc_kernel COUNT passes of record scanners also write the In bits
+  // (ScanParams::inbits) when UGPU_XC_BITMAP is on; OFFSETS then expands them
+  uint16_t* d_inbits = nullptr;
+  uint64_t inbits_cap = 0;  // bytes
   uint64_t* d_fix = nullptr;  // xc_kernel OFFSETS: per wave, the record whose start an earlier wave wrote
   DevTotals* d_tot = nullptr;
   uint32_t* d_flags = nullptr;
@@ -793,6 +797,7 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   }
   ugpu_scanner* s = new (std::nothrow) ugpu_scanner();
   if (!s) return fail(UGPU_NOMEM, "host allocation");
+  s->pref_write = prefer_write;
   s->dfa = dfa;
   // every failure below releases what was allocated so far
 #define HIP_TRY_S(expr)                      \
@@ -951,6 +956,7 @@ int ugpu_scanner_destroy(ugpu_scanner* s)
   (void)hipFree(s->d_recs);
   (void)hipFree(s->d_entries);
   (void)hipFree(s->d_obase);
+  (void)hipFree(s->d_inbits);
   (void)hipFree(s->d_fix);
   (void)hipFree(s->d_tot);
   (void)hipFree(s->d_flags);
@@ -1043,6 +1049,22 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
     s->staged_last = true;
   }
   s->stage_once = false;
+  P.inbits = nullptr;
+  if (s->pref_write && s->xc && !s->word && !P.xc_w && !P.xu_w && env_u64("UGPU_XC_BITMAP", 0) != 0) {
+    // one bit per byte up to the chunk after the readable end (the last wave
+    // searches for the exit up to there)
+    const uint64_t need = ((((P.rend + 15) & ~uint64_t(15)) + 2048) >> 3) + 64;
+    if (need > s->inbits_cap) {
+      (void)hipFree(s->d_inbits);
+      s->d_inbits = nullptr;
+      s->inbits_cap = 0;
+      if (hipMalloc(&s->d_inbits, need + need / 8) == hipSuccess)
+        s->inbits_cap = need + need / 8;
+      else
+        (void)hipGetLastError();  // (no bitmap: OFFSETS runs the WRITE pass)
+    }
+    if (s->d_inbits) P.inbits = s->d_inbits;
+  }
   UGPU_TRACE("scan lo %llu hi %llu rend %llu eof %d grid %u xi %d xg %d sparse %d word %d\n", (unsigned long long)P.lo,
              (unsigned long long)P.hi, (unsigned long long)P.rend, at_eof, P.grid, (int)s->xi, (int)s->xg,
              (int)s->sparse, (int)s->word);
@@ -1183,7 +1205,10 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
     P.out_capacity = capacity;
     P.out_fix = s->d_fix;
     HIP_TRY(hipMemsetAsync(s->d_flags, 0, sizeof(uint32_t), st));
-    HIP_TRY(launch_xc(P, true, st, s->h_tot->count));
+    if (P.inbits)
+      HIP_TRY(launch_xc_expand(P, st, s->h_tot->count));  // (the COUNT pass wrote the In bits)
+    else
+      HIP_TRY(launch_xc(P, true, st, s->h_tot->count));
     HIP_TRY(hipMemcpyAsync(s->h_flags, s->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (*s->h_flags & UGPU_FLAG_CAPACITY) return fail(UGPU_CAPACITY, "output capacity exceeded");

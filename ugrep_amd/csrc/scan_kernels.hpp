@@ -153,6 +153,11 @@ struct ScanParams {
   const uint8_t* xu_tab;  // kXuTab bytes (4-byte aligned)
   const uint32_t* xu_bm3; // kXuBm3 dwords
   uint32_t xu_null;       // the fill byte
+  // xc_kernel COUNT (U mode or carry chain, no option W): also write the In
+  // bit of every byte (bit p % 16 of inbits[p / 16], base coordinates), which
+  // xc_expand_kernel turns into the match records (OFFSETS without a second
+  // walk); NULL: not written
+  uint16_t* inbits;
   // line anchors / option N (tables.hpp acap): per-context accept indices
   // (sid * 4 + bol * 2 + eol) or NULL; bol0: the position bob starts a line
   // (the byte before the buffer is '\n', or the buffer begins the input);
@@ -254,6 +259,10 @@ uint32_t xg_waves();
 hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64_t count = 0);
 hipError_t xc_occupancy(bool u, int* blocks_per_cu);  // u: the U-mode COUNT kernel
 uint32_t xc_unit(bool u);  // wave-tile bytes (u: U mode)
+// OFFSETS from the In bits of an xc_kernel COUNT pass (P.inbits): one
+// workgroup per COUNT wave record writes that wave's records; then the fix of
+// the one record per wave whose start an earlier wave wrote
+hipError_t launch_xc_expand(const ScanParams& P, hipStream_t stream, uint64_t count);
 uint32_t xc_waves();
 // dense wave-persistent kernel, dense_kernel.hip
 hipError_t launch_dense(const ScanParams& P, uint32_t format, bool write, size_t smem, hipStream_t stream);

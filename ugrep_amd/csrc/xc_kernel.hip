@@ -746,10 +746,10 @@ __device__ __forceinline__ void cwrite_now(const CLane& L, const uint32_t cb[4],
 
 // One chunk (16 bytes per lane at q = chunk base + 16 lane); cw = the wave's
 // carry, updated.  Returns the lane's carry-in bits.
-template <bool MASK, bool W, bool WR = false, bool U = false>
+template <bool MASK, bool W, bool WR = false, bool U = false, bool BM = false>
 __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_t q, const CLim& lim, uint32_t& cw,
                                        uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4], CW& wc, COut& o,
-                                       CU& u, CPend* pd = nullptr, uint16_t* slot = nullptr)
+                                       CU& u, CPend* pd = nullptr, uint16_t* slot = nullptr, uint16_t* ib = nullptr)
 {
 #if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 1  // loads only (benchmarking; wrong counts)
   if (!MASK) {
@@ -767,6 +767,12 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
   const uint64_t cin = clook(__ballot(gen), __ballot(prop), cw, cw);
   uint32_t sb[4];
   cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb, sb);
+  if constexpr (BM) {
+    uint32_t in[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) in[d] = (L.E[d] | ((L.E[d] >> 1) & cb[d])) & kOnes;  // In_i = G_i | X_i & In_{i-1}
+    ib[q >> 4] = (uint16_t)nib16(in);
+  }
   if constexpr (WR) {
     if (pd)
       cwrite<U ? kStageU : kStage>(L, cb, sb, q, o, *pd, slot);  // (stores by the caller's cflush)
@@ -780,9 +786,9 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
 // counted directly (ls counts In_i here, not In_{i-1}; the caller corrects the
 // difference at the main loop's ends).  mprev (uniform): M of the 4 bytes
 // before the chunk (bit 24: the byte just before).
-template <bool UW, bool FAST>
+template <bool UW, bool FAST, bool BM = false>
 __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q, uint32_t& mprev, uint32_t& cs,
-                                              uint32_t& ws, uint32_t& ls)
+                                              uint32_t& ws, uint32_t& ls, uint16_t* ib = nullptr)
 {
 #if defined(UGPU_XU_ABL) && UGPU_XU_ABL == 3  // loads only (benchmarking; wrong counts)
   cs += v.x ^ v.y ^ v.z ^ v.w;
@@ -803,6 +809,7 @@ __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q,
     const uint32_t wd = (4u * d) | ((4u * d + 1) << 8) | ((4u * d + 2) << 16) | ((4u * d + 3) << 24);
     ws = __builtin_amdgcn_udot4(st, wd, ws, false);
   }
+  if constexpr (BM) ib[q >> 4] = (uint16_t)nib16(m);  // (In = M here)
 }
 
 // U mode, OFFSETS (WRITE), a chunk wholly inside [wlo, hi): In = M here too,
@@ -870,7 +877,7 @@ __device__ __forceinline__ uint32_t ccode(uint32_t cls) { return cls & 0x80u ? 0
 }  // namespace
 
 // (the body of the kernels below)
-template <bool W, bool WR, bool U, bool FAST = false>
+template <bool W, bool WR, bool U, bool FAST = false, bool BM = false>
 __device__ __forceinline__ void xc_body(const ScanParams& P)
 {
   constexpr int kIt = U ? kUIter : kCIter;  // chunks per iteration
@@ -1002,7 +1009,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     const uint4 v = cload(crsrc(P.g + q0, rend16 > q0 ? rend16 - q0 : 0), lo16);
     uint32_t cs = 0, ws = 0, ls = 0, cb[4];
     if constexpr (U) u.nx0 = uload_dw(u, P.g, q0 + kCChunk);
-    cchunk<true, W, WR, U>(cc, v, q0 + lo16, lim, cw, cs, ws, ls, cb, wc, out, u);
+    cchunk<true, W, WR, U, BM>(cc, v, q0 + lo16, lim, cw, cs, ws, ls, cb, wc, out, u, nullptr, nullptr, P.inbits);
     cnt += cs;
     pos += (uint64_t)cs * (q0 + lo16) + ws;
     lbits += ls;
@@ -1078,14 +1085,15 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
         }
         uint16_t* const slot = out.stage + (uint32_t)(j & 1) * 2u * kStg;
         if constexpr (U && !WR)
-          uchunk_direct<W, FAST>(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls);
+          uchunk_direct<W, FAST, BM>(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls, P.inbits);
         else if constexpr (U && WR)
           uchunk_write<FAST>(u, cur[j], ts + j * kCChunk + lo16, mprev, out, pend[j & 1], slot);
         else if constexpr (WR)
           cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u,
                                   &pend[j & 1], slot);
         else
-          cchunk<false, W, WR, U>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out, u);
+          cchunk<false, W, WR, U, BM>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out,
+                                      u, nullptr, nullptr, P.inbits);
         if constexpr (WR) {
           // the stores of the staged slots: at the tile end after the next
           // tile's loads (cwrite: they then overlap the next tile's work),
@@ -1202,6 +1210,173 @@ void xu_kernel(ScanParams P)
   xc_body<UW, false, true, FAST>(P);
 }
 
+// COUNT passes that also write the In bits (P.inbits; no option W)
+template <bool FAST>
+__global__ __launch_bounds__(kCWaves * 64) __attribute__((amdgpu_waves_per_eu(UGPU_XU_WAVES_PER_EU)))
+void xu_bm_kernel(ScanParams P)
+{
+  xc_body<false, false, true, FAST, true>(P);
+}
+__global__ __launch_bounds__(kCWaves * 64) void xc_bm_kernel(ScanParams P)
+{
+  xc_body<false, false, false, false, true>(P);
+}
+
+// OFFSETS from the In bits of the COUNT pass.  In is the FIND chain's
+// "inside a match" bit per byte, so the matches are its runs: a start where
+// In rises, an end where it falls, and the k-th end of the chain closes the
+// k-th start.  Block b writes the records of COUNT wave b: the starts in its
+// range [wlo, whi) (the last wave's ends run on to the chain exit) at indices
+// from that wave's output base, and the ends in the range, which close the
+// match open at wlo first (index base - 1; its start was written by an
+// earlier block: the raw end goes into len and out_fix names the index for
+// xc_fix_kernel, as in the WRITE pass).  64-bit words of In bits, 256 a round;
+// the round's starts and lengths are ordered by block scans and staged in LDS,
+// then stored by consecutive threads.  No table, no walk: the pass reads 1/8
+// of the input's bytes and writes the records.
+constexpr int kXeThreads = 256;
+constexpr uint32_t kXeCap = 64 * kXeThreads / 2;  // records a round can hold (a start needs a 0 before it)
+
+// The range is cut into 4 quarters of whole words, one per wave.  A first
+// pass counts each quarter's starts and ends and finds its last start; after
+// one block barrier every wave knows its output bases and writes its quarter
+// alone: per round 64 words, one per lane, ordered by DPP scans, the starts
+// staged in the wave's LDS slice for coalesced stores.
+constexpr uint32_t kXeWaveCap = 64 * 32;  // starts a wave-round can hold
+
+template <bool U>
+__global__ __launch_bounds__(kXeThreads) void xc_expand_kernel(ScanParams P)
+{
+  __shared__ uint32_t st_off[4][kXeWaveCap];  // a round's start positions, from the round's first position
+  __shared__ uint32_t qs[4], qe[4];
+  __shared__ int64_t ql[4];
+  __shared__ uint64_t fix_s;
+  constexpr uint64_t kTile = (uint64_t)kCChunk * (U ? kUIter : kCIter);
+  const uint64_t gw = blockIdx.x;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t tb = P.t0 + gw * P.tpb;
+  const uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
+  if (tb > te) tb = te;
+  if (threadIdx.x == 0) fix_s = ~0ull;
+  const uint64_t wlo = clampu(tb * kTile, P.lo, P.hi), whi = clampu(te * kTile, P.lo, P.hi);
+  const bool any = te > tb;
+  const bool last = any && whi == P.hi;
+  const uint64_t end = !any ? wlo : last ? P.totals->exit + 1 : whi;  // event positions [wlo, end)
+  const uint64_t* words = reinterpret_cast<const uint64_t*>(P.inbits);
+  // the events of word wi (positions [wlo, end) only)
+  auto events = [&](uint64_t wi, uint64_t& st, uint64_t& en) __attribute__((always_inline)) {
+    const uint64_t pos = wi * 64;
+    st = en = 0;
+    if (pos >= end || pos + 64 <= wlo) return;
+    const uint64_t w = words[wi];
+    const uint64_t prev = (w << 1) | (pos > P.lo ? words[wi - 1] >> 63 : 0ull);
+    const uint64_t a = wlo > pos ? wlo - pos : 0, z = end - pos;
+    const uint64_t lim = (~0ull << a) & (z >= 64 ? ~0ull : ((1ull << z) - 1ull));
+    st = w & ~prev & lim;
+    en = prev & ~w & lim;
+  };
+  const uint64_t wb = wlo >> 6, we = end > wlo ? (end + 63) >> 6 : wb;  // words [wb, we)
+  const uint64_t nq = (we - wb + 3) / 4;
+  const uint64_t qb = wb + wv * nq, qend = qb + nq < we ? qb + nq : we;  // this wave's words
+  // pass 1: the quarter's counts and last start
+  {
+    uint32_t ns = 0, ne = 0;
+    int64_t ls = -1;
+    for (uint64_t wi = qb + lane; wi < qend; wi += 64) {
+      uint64_t st, en;
+      events(wi, st, en);
+      ns += (uint32_t)__builtin_popcountll(st);
+      ne += (uint32_t)__builtin_popcountll(en);
+      if (st) ls = (int64_t)(wi * 64 + 63 - __builtin_clzll(st));
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      ns += __shfl_xor(ns, d, 64);
+      ne += __shfl_xor(ne, d, 64);
+      const int64_t o = __shfl_xor(ls, d, 64);
+      ls = o > ls ? o : ls;
+    }
+    if (lane == 0) {
+      qs[wv] = ns;
+      qe[wv] = ne;
+      ql[wv] = ls;
+    }
+  }
+  __syncthreads();
+  if (any) {
+    const uint64_t base = P.out_base[gw];
+    const uint32_t open0 = wlo > P.lo ? (uint32_t)((words[(wlo - 1) >> 6] >> ((wlo - 1) & 63)) & 1ull) : 0u;
+    uint64_t s_before = 0, e_before = 0;
+    int64_t last_start = -1;
+    for (uint32_t w = 0; w < wv; ++w) {
+      s_before += qs[w];
+      e_before += qe[w];
+      if (ql[w] >= 0) last_start = ql[w];
+    }
+    uint32_t* so = st_off[wv];
+    for (uint64_t w0 = qb; w0 < qend; w0 += 64) {
+      const uint64_t wi = w0 + lane, pos = wi * 64;
+      uint64_t st = 0, en = 0;
+      if (wi < qend) events(wi, st, en);
+      const uint32_t ns = (uint32_t)__builtin_popcountll(st), ne = (uint32_t)__builtin_popcountll(en);
+      const uint32_t is = cscan_add(ns), ie = cscan_add(ne);
+      const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)is, 63);
+      const uint32_t E = (uint32_t)__builtin_amdgcn_readlane((int)ie, 63);
+      // the last start before this lane's word: in the nearest lower lane with
+      // starts, else before the round
+      const uint64_t hs = __ballot(st != 0);
+      const uint64_t lower = hs & ((1ull << lane) - 1ull);
+      const int64_t myls = st ? (int64_t)(pos + 63 - __builtin_clzll(st)) : -1;
+      const int src = lower ? 63 - __builtin_clzll(lower) : 0;
+      const int64_t nb = __shfl(myls, src, 64);
+      const int64_t ls = lower ? nb : last_start;
+      const uint64_t pb = w0 * 64;
+      uint64_t m = st;
+      for (uint32_t k = is - ns; m; ++k) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        so[k] = (uint32_t)(pos + j - pb);
+      }
+      // the lengths, written by their lanes (end indices are consecutive)
+      m = en;
+      for (uint64_t i = base - open0 + e_before + (ie - ne); m; ++i) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint64_t e = pos + j;
+        const uint64_t sb = st & ((1ull << j) - 1ull);  // starts of the word before the end
+        const int64_t s = sb ? (int64_t)(pos + 63 - __builtin_clzll(sb)) : ls;
+        if (i < P.out_capacity) {
+          if (s >= 0) {
+            P.out_len[i] = (uint32_t)(e - (uint64_t)s);
+          } else {
+            P.out_len[i] = (uint32_t)(e + (uint64_t)P.delta);  // raw (reported): the match open at wlo
+            fix_s = i;
+          }
+        } else {
+          atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+        }
+      }
+      cwave_sync();
+      for (uint32_t t = lane; t < R; t += 64) {
+        const uint64_t i = base + s_before + t;
+        if (i < P.out_capacity) {
+          P.out_start[i] = pb + so[t] + (uint64_t)P.delta;
+          P.out_cap[i] = P.cap1;
+        } else {
+          atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+        }
+      }
+      s_before += R;
+      e_before += E;
+      const int64_t rl = __shfl(myls, hs ? 63 - __builtin_clzll(hs) : 0, 64);
+      if (hs) last_start = rl;
+      cwave_sync();  // (the next round stages anew)
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) P.out_fix[gw] = fix_s;
+}
+
 // OFFSETS, second step: the one match per wave whose start an earlier wave
 // wrote (fix[w] = its index, ~0 none) holds its end position (low 32 bits,
 // reported coordinates) in len: subtract the start
@@ -1234,6 +1409,15 @@ hipError_t launch_xc(const ScanParams& P, bool write, hipStream_t stream, uint64
                          P.out_len, n);
     return hipGetLastError();
   }
+  if (P.inbits && !P.xc_w && !P.xu_w) {
+    if (P.xu_tab && !P.xu_exact)
+      hipLaunchKernelGGL((xu_bm_kernel<true>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    else if (P.xu_tab)
+      hipLaunchKernelGGL((xu_bm_kernel<false>), dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    else
+      hipLaunchKernelGGL(xc_bm_kernel, dim3(P.grid), dim3(kCWaves * 64), 0, stream, P);
+    return hipGetLastError();
+  }
   // (U mode: the FAST kernel unless the host redoes a range that met an XU_MIX
   // or XU_SLOW lead, UGPU_FLAG_UMIX)
   if (P.xu_tab && P.xu_w && !P.xu_exact)
@@ -1258,5 +1442,21 @@ hipError_t xc_occupancy(bool u, int* n)
 }
 uint32_t xc_unit(bool u) { return u ? kCChunk * kUIter : kCTile; }
 uint32_t xc_waves() { return kCWaves; }
+
+hipError_t launch_xc_expand(const ScanParams& P, hipStream_t stream, uint64_t count)
+{
+  const uint32_t nrec = P.grid * (uint32_t)kCWaves;
+  if (P.xu_tab)
+    hipLaunchKernelGGL((xc_expand_kernel<true>), dim3(nrec), dim3(kXeThreads), 0, stream, P);
+  else
+    hipLaunchKernelGGL((xc_expand_kernel<false>), dim3(nrec), dim3(kXeThreads), 0, stream, P);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint64_t n = count < P.out_capacity ? count : P.out_capacity;
+  if (n)
+    hipLaunchKernelGGL(xc_fix_kernel, dim3((nrec + 255) / 256), dim3(256), 0, stream, P.out_fix, nrec, P.out_start,
+                       P.out_len, n);
+  return hipGetLastError();
+}
 
 }  // namespace ugpu
