@@ -93,6 +93,16 @@ class OracleDfa:
             lst = arr[:3 * cnt].reshape(-1, 3).tolist()
         return cnt, dg.value, dc.value, lst
 
+    def find_arrays(self, data, start=0):
+        """FIND over data[start:] as numpy arrays (start, len, cap) of uint64,
+        for match lists too long for Python lists."""
+        buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+        cnt = L.orc_find(self.h, buf.ctypes.data, buf.size, start, 0, None, None, None, 0)
+        arr = np.zeros(3 * max(cnt, 1), np.uint64)
+        L.orc_find(self.h, buf.ctypes.data, buf.size, start, 0, None, None, arr.ctypes.data, cnt)
+        a = arr[:3 * cnt].reshape(-1, 3)
+        return a[:, 0], a[:, 1], a[:, 2]
+
     def find_w(self, data, start=0, want_list=False):
         """FIND with option W (ugrep -w, orc_find_w): (count, digest, dcap, list|None)."""
         buf = _u8(data)

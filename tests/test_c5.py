@@ -153,6 +153,29 @@ def test_dense_shards_arbitrary_cuts(U, patterns, streams, name):
     assert out["fixes"] >= 1
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c4_128m", "c3_256m"])
+def test_offsets_record_by_record(U, patterns, streams, name):
+    """The records of the table's own OFFSETS pass (C4: xc_kernel's U mode,
+    xu_kernel + xu_write_kernel; C3: xc_kernel) over the whole stream, record
+    by record against the oracle's match list (which is pinned to the
+    reference's totals)."""
+    from oracle_lib import OracleDfa, gen
+    s = streams[name]
+    n = s["bytes"]
+    opc = patterns[s["pattern"]]["opc"]
+    host = gen(s["kind"], 1, 0, n)
+    o = OracleDfa(opc)
+    ws, wl, wc = o.find_arrays(host)
+    assert ws.size == s["count"]
+    whole = _whole(U, s["kind"], n)
+    res = U.find_all(U.Pattern(opc), whole[:n], offsets=True)
+    assert (res.count, res.digest, res.dcap) == (s["count"], s["digest"], s["dcap"])
+    assert np.array_equal(np.asarray(res.start, np.uint64), ws)
+    assert np.array_equal(np.asarray(res.length, np.uint64), wl)
+    assert np.array_equal(np.asarray(res.cap, np.uint64), wc)
+
+
 def _free_port():
     so = socket.socket()
     so.bind(("127.0.0.1", 0))
