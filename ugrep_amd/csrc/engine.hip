@@ -1540,6 +1540,7 @@ struct ugpu_records {
   // the consumer's piece: pieces[pi - 1] (pi = 0: none yet)
   size_t pi = 0;
   bool sync_d2h = false;  // UGPU_REC_SYNC=1: the pipeline waits for each D2H before the next chunk
+  bool zero_copy = false; // UGPU_REC_ZC=1: the pack kernel stores straight into the pinned block
   bool trace = false;     // UGPU_REC_TRACE=1: per-chunk timestamps on stderr
   std::chrono::steady_clock::time_point t0;
   const uint32_t* st = nullptr;
@@ -1841,6 +1842,42 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
         rc = fail(UGPU_NOMEM, "pinned records");
         break;
       }
+      void* hdev = nullptr;
+      if (R->zero_copy && hipHostGetDevicePointer(&hdev, pc.host, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        hdev = nullptr;
+      }
+      if (hdev) {
+        // zero copy: the pack kernel's stores cross PCIe into the pinned block
+        // (no device pack buffer, no D2H copy); the block is the consumer's
+        // once the kernel has finished
+        if ((e = hipMemsetAsync(rw->d_nesc + b, 0, sizeof(uint32_t), ws->st)) != hipSuccess ||
+            (e = launch_pack_records(ws->d_start, ws->d_len, ws->d_cap, n, lo, static_cast<uint8_t*>(hdev), R->caps,
+                                     pc.dense ? 1 : 0, rw->d_esc[b], rw->d_nesc + b, ws->st)) != hipSuccess ||
+            (e = hipMemcpyAsync(rw->h_nesc + b, rw->d_nesc + b, sizeof(uint32_t), hipMemcpyDeviceToHost, ws->st)) !=
+                hipSuccess ||
+            (e = hipStreamSynchronize(ws->st)) != hipSuccess) {
+          rc = hip_fail(e, "records pack");
+          publish(&pc, false);
+          break;
+        }
+        trace("packed", lo);
+        const uint32_t ne = rw->h_nesc[b];
+        if (ne) {
+          std::vector<uint64_t> es(2 * (size_t)ne);
+          if ((e = hipMemcpy(es.data(), rw->d_esc[b], 16ull * ne, hipMemcpyDeviceToHost)) != hipSuccess) {
+            rc = hip_fail(e, "records escapes");
+            publish(&pc, false);
+            break;
+          }
+          for (uint32_t k = 0; k < ne; ++k) pc.esc.push_back(std::make_pair(es[2 * k], es[2 * k + 1]));
+          std::sort(pc.esc.begin(), pc.esc.end());
+        }
+        publish(&pc, false);
+        entry = tot.exit;
+        lo = hi;
+        continue;
+      }
       if ((e = hipMemsetAsync(rw->d_nesc + b, 0, sizeof(uint32_t), ws->st)) != hipSuccess ||
           (e = launch_pack_records(ws->d_start, ws->d_len, ws->d_cap, n, lo, rw->d_pack[b], R->caps, pc.dense ? 1 : 0,
                                    rw->d_esc[b], rw->d_nesc + b, ws->st)) != hipSuccess ||
@@ -1967,6 +2004,7 @@ int ugpu_find_records(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uin
   R->caps = dfa->t.cap1 == 0 ? 1 : 0;
   R->cap1 = dfa->t.cap1 ? dfa->t.cap1 : 1;
   R->sync_d2h = env_u64("UGPU_REC_SYNC", 0) != 0;
+  R->zero_copy = env_u64("UGPU_REC_ZC", 0) != 0;
   R->trace = env_u64("UGPU_REC_TRACE", 0) != 0;
   R->t0 = std::chrono::steady_clock::now();
   if (len == start) {
