@@ -26,7 +26,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import ugrep_amd  # noqa: E402
-from ugrep_amd.dist import gather_offsets, shard_bounds, stitch  # noqa: E402
+from ugrep_amd.dist import gather_offsets, scan_shard, shard_bounds, stitch  # noqa: E402
 
 METRIC = "GB/s scanned + matches/s, 16 GiB synthetic buffer, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
@@ -256,20 +256,29 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    buf = torch.empty(n_read + 16, dtype=torch.uint8, device=dev)
-    if kind == 0:
-        data = open(os.path.join(REPO, "tests", "golden", "lorem.utf8.txt"), "rb").read()
-        tile = np.frombuffer(data, np.uint8)
-        idx = (np.arange(lo, read_end, dtype=np.int64) % tile.size)
-        buf[:n_read].copy_(torch.from_numpy(tile[idx]))
-    else:
-        ugrep_amd.gen(kind, 1, lo, buf.data_ptr(), n_read, sptr)
-    torch.cuda.synchronize(dev)
-    log("rank %d: shard [%d, %d) read_end %d, pattern %s: %s" % (rank, lo, hi, read_end, rx, info))
+
+    def fetch(a, z):
+        """The synthetic stream's bytes [a, z) in a fresh device buffer."""
+        t = torch.empty(z - a + 16, dtype=torch.uint8, device=dev)
+        if kind == 0:
+            data = open(os.path.join(REPO, "tests", "golden", "lorem.utf8.txt"), "rb").read()
+            tile = np.frombuffer(data, np.uint8)
+            idx = (np.arange(a, z, dtype=np.int64) % tile.size)
+            t[:z - a].copy_(torch.from_numpy(tile[idx]))
+        else:
+            ugrep_amd.gen(kind, 1, a, t.data_ptr(), z - a, sptr)
+        torch.cuda.synchronize(dev)
+        return t
 
     sc = ugrep_amd.Scanner(pat, records=args.offsets)
     if args.offsets:
         sc.stage(True)  # single-pass OFFSETS (prefiltered tables): the COUNT pass stages the records
+    # one scan before the timed steps: a match longer than the halo grows it
+    # (dist.scan_shard), so the steps run on a shard that holds its matches
+    _, buf, read_end = scan_shard(sc, fetch, lo, hi, total, args.halo, stream=sptr)
+    eof = read_end == total
+    n_read = read_end - lo
+    log("rank %d: shard [%d, %d) read_end %d, pattern %s: %s" % (rank, lo, hi, read_end, rx, info))
     ptr = buf.data_ptr()
     kms = []
 

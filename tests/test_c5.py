@@ -153,6 +153,32 @@ def test_dense_shards_arbitrary_cuts(U, patterns, streams, name):
     assert out["fixes"] >= 1
 
 
+def test_scan_shard_grows_the_halo(U):
+    """A match longer than the halo (a 3 MiB run of 'a' across the end of a
+    4 MiB shard, halo 64 KiB): dist.scan_shard grows the halo until the match
+    ends inside it, and the shard's record equals the whole-stream scan's."""
+    from ugrep_amd.dist import scan_shard
+    n = 8 << 20
+    host = np.frombuffer(b"xy " * (n // 3 + 1), np.uint8)[:n].copy()
+    host[3 << 20:6 << 20] = ord("a")
+    whole = torch.from_numpy(host).to("cuda")
+    pat = U.Pattern(U.compile_regex("a+"))
+
+    def fetch(a, z):
+        t = torch.zeros(z - a + 16, dtype=torch.uint8, device="cuda")
+        t[:z - a].copy_(whole[a:z])
+        torch.cuda.synchronize()
+        return t
+
+    sc = U.Scanner(pat)
+    rec, buf, rend = scan_shard(sc, fetch, 0, 4 << 20, n, halo=64 << 10, stream=_stream())
+    assert rend > 6 << 20  # (grown from 64 KiB past the end of the run; the exit must lie before it)
+    want = U.find_all(pat, whole, offsets=True)
+    assert want.count == 1 and int(want.start[0]) == 3 << 20 and int(want.length[0]) == 3 << 20
+    assert (rec["count"], rec["digest"], rec["dcap"]) == (want.count, want.digest, want.dcap)
+    assert rec["exit"] == 6 << 20
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["c4_128m", "c3_256m"])
 def test_offsets_record_by_record(U, patterns, streams, name):

@@ -108,6 +108,36 @@ def stitch(rec, fix_fn, device="cpu", group=None):
     return resolve(recs, fix)
 
 
+def scan_shard(scanner, fetch, lo, hi, total, halo=1 << 20, entry=None, stream=0):
+    """Scan shard [lo, hi) of a total-byte stream from `entry` (default lo),
+    growing the readable halo when a match runs past it.
+
+    fetch(lo, read_end) -> a uint8 CUDA tensor holding the stream's bytes
+    [lo, read_end) (with the 16 bytes of padding the engine may read past
+    them).  A match longer than the halo makes the scan fail with UGPU_HALO
+    (DESIGN §5): the halo is then doubled and the shard fetched and scanned
+    again, up to the stream end (where no match can run past).  Returns
+    (record, buffer, read_end): the record in stitch()'s form with global
+    positions, and the buffer and readable end the record was scanned on
+    (fix_fn and the OFFSETS pass must use the same)."""
+    from ._lib import UGPU_HALO, UgpuError
+    h = max(int(halo), 1)
+    while True:
+        read_end = min(total, hi + h)
+        buf = fetch(lo, read_end)
+        e = lo if entry is None else min(max(entry, lo), hi)
+        try:
+            scanner.scan(buf.data_ptr(), e - lo, hi - lo, read_end - lo, read_end == total, lo, stream)
+            t = scanner.totals()
+        except UgpuError as err:
+            if err.code != UGPU_HALO or read_end == total:
+                raise
+            h *= 2
+            continue
+        rec = dict(entry=t.entry + lo, exit=t.exit + lo, count=t.count, digest=t.digest, dcap=t.dcap)
+        return rec, buf, read_end
+
+
 def shard_bounds(total, world, rank, halo):
     """[lo, hi) of rank's shard, its readable end, and whether that is the stream end."""
     per = total // world
