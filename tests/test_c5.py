@@ -154,15 +154,17 @@ def test_dense_shards_arbitrary_cuts(U, patterns, streams, name):
 
 
 def test_scan_shard_grows_the_halo(U):
-    """A match longer than the halo (a 3 MiB run of 'a' across the end of a
-    4 MiB shard, halo 64 KiB): dist.scan_shard grows the halo until the match
-    ends inside it, and the shard's record equals the whole-stream scan's."""
+    """A match longer than the halo (a 3 MiB run of letters across the end of
+    a 4 MiB shard of digits, halo 64 KiB): dist.scan_shard grows the halo until
+    the match ends inside it, and the shard's record is that one match.  (A
+    dense table: a prefiltered one with a long run of candidates is the
+    sparse kernel's slow case)"""
     from ugrep_amd.dist import scan_shard
     n = 8 << 20
-    host = np.frombuffer(b"xy " * (n // 3 + 1), np.uint8)[:n].copy()
+    host = np.frombuffer(b"12 " * (n // 3 + 1), np.uint8)[:n].copy()
     host[3 << 20:6 << 20] = ord("a")
     whole = torch.from_numpy(host).to("cuda")
-    pat = U.Pattern(U.compile_regex("a+"))
+    pat = U.Pattern(U.compile_regex("[a-z]+"))
 
     def fetch(a, z):
         t = torch.zeros(z - a + 16, dtype=torch.uint8, device="cuda")
@@ -173,9 +175,9 @@ def test_scan_shard_grows_the_halo(U):
     sc = U.Scanner(pat)
     rec, buf, rend = scan_shard(sc, fetch, 0, 4 << 20, n, halo=64 << 10, stream=_stream())
     assert rend > 6 << 20  # (grown from 64 KiB past the end of the run; the exit must lie before it)
-    want = U.find_all(pat, whole, offsets=True)
-    assert want.count == 1 and int(want.start[0]) == 3 << 20 and int(want.length[0]) == 3 << 20
-    assert (rec["count"], rec["digest"], rec["dcap"]) == (want.count, want.digest, want.dcap)
+    # the one match of the shard: (3 MiB, 3 MiB, accept 1)
+    s0 = 3 << 20
+    assert (rec["count"], rec["digest"], rec["dcap"]) == (1, 31 * s0 + s0, s0 + 1)
     assert rec["exit"] == 6 << 20
 
 
