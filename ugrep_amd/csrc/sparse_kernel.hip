@@ -326,6 +326,13 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
       const uint64_t z = whi > p0 ? (whi - p0 > 16 ? 16 : whi - p0) : 0;
       mk &= (uint32_t)((lowbits(z) & ~lowbits(a)) & 0xffffu);
     }
+    if (w.x > p0) {
+      // positions below the end of the last kept match are never kept (the
+      // chain resumes there): drop them before they are walked -- in a long
+      // run of candidates only the batch holding its start is walked
+      const uint64_t a = w.x - p0;
+      mk &= (uint32_t)(~lowbits(a < 16 ? a : 16) & 0xffffu);
+    }
     if constexpr (ABL == 2) {
       w.acc.cnt += __popc(mk);
       continue;
