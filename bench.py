@@ -25,8 +25,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-import ugrep_amd  # noqa: E402
-from ugrep_amd.dist import gather_offsets, scan_shard, shard_bounds, stitch  # noqa: E402
+# the engine (libugrep_amd.so) is loaded by main() after the launcher decision,
+# so that a parent that only starts the rank processes never loads HIP code
+ugrep_amd = gather_offsets = scan_shard = shard_bounds = stitch = None
 
 METRIC = "GB/s scanned + matches/s, 16 GiB synthetic buffer, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
@@ -194,6 +195,48 @@ def pcie_inclusive(pat, buf, nbytes, dev, reps=3):
             "equals_device_resident": ok}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE): start N
+    rank processes with torch.distributed.run (one per GPU, rendezvous on
+    127.0.0.1) and exit with its status.  This process never touches the GPU
+    (only `import torch`, which initialises nothing), and it starts the ranks
+    as children -- it does not exec."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    log("launching %d ranks: %s" % (n, " ".join(cmd[1:])))
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(backend):
+    """--launch-check: the rank bring-up alone (process group, one all_gather of
+    every rank's identity, barrier), no GPU work; rank 0 prints one JSON line.
+    The CPU test of the launcher runs this with UGPU_BENCH_BACKEND=gloo."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    mine = torch.tensor([rank, local, os.getpid()], dtype=torch.int64)
+    allr = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "backend": backend,
+                          "ranks": [dict(rank=int(t[0]), local_rank=int(t[1]), pid=int(t[2])) for t in allr]}),
+              flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -216,16 +259,30 @@ def main():
                          "dumped opcode words")
     ap.add_argument("--word", action="store_true",
                     help="Matcher option W (ugrep -w) on the same pattern: wfind_kernel (not a BASELINE config)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="bring the ranks up (process group, all_gather, barrier) and report them; no GPU work")
     args = ap.parse_args()
+
+    # rehearsal knobs for a one-GPU box: UGPU_BENCH_BACKEND=gloo puts every rank
+    # on UGPU_BENCH_DEVICE (default 0) and stitches over gloo on the host
+    backend = os.environ.get("UGPU_BENCH_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no external launcher: start one rank per GPU ourselves (before any GPU call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.launch_check:
+        launch_check(backend)
+        return
+    global ugrep_amd, gather_offsets, scan_shard, shard_bounds, stitch
+    import ugrep_amd as _u
+    from ugrep_amd import dist as _d
+    ugrep_amd, gather_offsets, scan_shard, shard_bounds, stitch = (_u, _d.gather_offsets, _d.scan_shard,
+                                                                  _d.shard_bounds, _d.stitch)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
-    # rehearsal knobs for a one-GPU box: UGPU_BENCH_BACKEND=gloo puts every rank
-    # on UGPU_BENCH_DEVICE (default 0) and stitches over gloo on the host
-    backend = os.environ.get("UGPU_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local = int(os.environ.get("UGPU_BENCH_DEVICE", "0"))
     torch.cuda.set_device(local)
@@ -363,6 +420,12 @@ def main():
             dist.barrier()
 
     k_avg = float(np.mean(kms)) if kms else float("nan")
+    rank_kms = [k_avg]
+    if pg:  # every rank's own scan-kernel time (HIP events), reported by rank 0
+        mine = torch.tensor([k_avg], dtype=torch.float64, device=xdev)
+        allk = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allk, mine)
+        rank_kms = [round(float(t.item()), 4) for t in allk]
     achieved = (hi - lo) / (k_avg * 1e-3) / 1e9
     value = total * args.steps / elapsed / 1e9
     matches_per_s = res["count"] * args.steps / elapsed
@@ -389,6 +452,7 @@ def main():
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel_ms": round(k_avg, 4), "algorithmic_bytes_per_launch": hi - lo},
+        "rank_kernel_ms": rank_kms,
     }
     if pcie is not None:
         out["pcie_inclusive"] = pcie
