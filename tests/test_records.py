@@ -76,3 +76,29 @@ def test_records_word_and_anchors(U, small_chunks):
     _check(U, U.Pattern(U.compile_regex(r"de|dei|é"), word=True), data, start=5, word=True)
     _check(U, U.Pattern(U.compile_regex(r"^\w+"), empty=True), data, nul=True)
     _check(U, U.Pattern(U.compile_regex(r"^(?:[^\n]*)$"), empty=True), data, nul=True)
+
+
+@pytest.mark.gpu
+def test_records_early_free_and_bounded_pieces(U, patterns, monkeypatch):
+    """An early stop (ugrep -m1 / -l / -q): free() after a few pops cancels the
+    pipeline instead of scanning and pinning the rest (the pipeline runs at
+    most UGPU_REC_AHEAD pieces ahead of the consumer); totals() before any pop
+    lifts that limit instead of waiting for pops (no deadlock); a later
+    Records on the same table is exact."""
+    import time
+    from oracle_lib import OracleDfa, gen
+    monkeypatch.setenv("UGPU_REC_CHUNK", str(1 << 20))
+    monkeypatch.setenv("UGPU_REC_AHEAD", "2")
+    opc = patterns["c3_ident"]["opc"]
+    pat = U.Pattern(opc)
+    host = gen(3, 9, 0, 64 << 20)
+    r = U.Records(pat, host)
+    first = [r.next() for _ in range(10)]
+    t0 = time.perf_counter()
+    r.close()
+    assert time.perf_counter() - t0 < 5.0
+    want = OracleDfa(opc).find(host[:1 << 20], want_list=True)[3][:10]
+    assert [list(x) for x in first] == [list(x) for x in want]
+    r2 = U.Records(pat, host)
+    assert r2.totals() == tuple(OracleDfa(opc).find(host)[:3])
+    r2.close()

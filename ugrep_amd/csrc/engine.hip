@@ -137,6 +137,9 @@ struct ugpu_scanner {
   uint16_t* d_inbits = nullptr;
   uint64_t inbits_cap = 0;  // bytes
   uint64_t* d_fix = nullptr;  // xc_kernel OFFSETS: per wave, the record whose start an earlier wave wrote
+  OpenRec* d_open = nullptr;  // sparse_kernel: per wave, its open walk (walk truncation)
+  uint32_t* d_susp = nullptr;  // sparse_kernel: per wave, suspended at a long walk (resume launch)
+  SuspRec* d_srec = nullptr;   // ... and its suspended state
   DevTotals* d_tot = nullptr;
   uint32_t* d_flags = nullptr;
   DevTotals* h_tot = nullptr;  // pinned
@@ -937,6 +940,11 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   HIP_TRY_S(hipMalloc(&s->d_entries, sizeof(uint64_t) * kMaxRec));
   HIP_TRY_S(hipMalloc(&s->d_obase, sizeof(uint64_t) * kMaxRec));
   HIP_TRY_S(hipMalloc(&s->d_fix, sizeof(uint64_t) * kMaxRec));
+  if (s->sparse) {
+    HIP_TRY_S(hipMalloc(&s->d_open, sizeof(OpenRec) * kMaxRec));
+    HIP_TRY_S(hipMalloc(&s->d_susp, sizeof(uint32_t) * kMaxRec));
+    HIP_TRY_S(hipMalloc(&s->d_srec, sizeof(SuspRec) * kMaxRec));
+  }
   HIP_TRY_S(hipMalloc(&s->d_tot, sizeof(DevTotals)));
   HIP_TRY_S(hipMalloc(&s->d_flags, sizeof(uint32_t)));
   HIP_TRY_S(hipHostMalloc(&s->h_tot, sizeof(DevTotals)));
@@ -958,6 +966,9 @@ int ugpu_scanner_destroy(ugpu_scanner* s)
   (void)hipFree(s->d_obase);
   (void)hipFree(s->d_inbits);
   (void)hipFree(s->d_fix);
+  (void)hipFree(s->d_open);
+  (void)hipFree(s->d_susp);
+  (void)hipFree(s->d_srec);
   (void)hipFree(s->d_tot);
   (void)hipFree(s->d_flags);
   (void)hipHostFree(s->h_tot);
@@ -1017,6 +1028,15 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   P.totals = s->d_tot;
   P.entries_out = s->d_entries;
   P.out_base_out = s->d_obase;
+  // sparse_kernel walks stop at their wave's range end (open walks, resolved
+  // by fix_kernel): a long match costs each wave its own bytes only
+  // (UGPU_TRUNC=0: walks run to the readable end)
+  static const bool trunc = env_u64("UGPU_TRUNC", 1) != 0;
+  P.open = s->sparse && !P.wtab && trunc ? s->d_open : nullptr;
+  // walks longer than their window: the wave suspends, a resume launch of
+  // the kernel completes it (coop_walk); option W keeps its per-lane walks
+  P.susp = s->sparse && !P.wtab ? s->d_susp : nullptr;
+  P.srec = P.susp ? s->d_srec : nullptr;
   s->staged_last = false;
   if (s->sparse && (s->stage || s->stage_once)) {
     if (!s->d_st_n) {
@@ -1164,7 +1184,7 @@ int ugpu_scan_totals(ugpu_scanner* s, ugpu_totals* out)
   out->dcap = t.dcap;
   out->entry = t.entry - s->off;
   out->exit = t.exit - s->off;
-  out->flags = (*s->h_flags & ~UGPU_FLAG_WSLOW) | (s->forest ? UGPU_TOT_FOREST : 0u) |
+  out->flags = (*s->h_flags & ~(UGPU_FLAG_WSLOW | UGPU_FLAG_OPEN)) | (s->forest ? UGPU_TOT_FOREST : 0u) |
                ((s->wfast || s->wxc) && !s->word ? UGPU_TOT_WFAST : 0u);
   out->fix_rounds = t.rounds;
   if (out->flags & UGPU_FLAG_HALO) return fail(UGPU_HALO, "a match walked past the readable end of the shard");
@@ -1409,6 +1429,7 @@ int scanner_acquire(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write =
       *out = pool.back();
       pool.pop_back();
       (*out)->bol0 = 1;  // (a pooled scanner may have served a shard)
+      (*out)->xu_exact = false;  // (nor keep the exact U kernel an earlier input needed)
       return UGPU_OK;
     }
   }
@@ -1530,6 +1551,9 @@ struct ugpu_records {
   size_t published = 0;
   bool done = false;
   bool input_free = false;  // the caller's host buffer is no longer read
+  bool cancel = false;      // ugpu_records_free before the end: the pipeline stops at its next chunk
+  bool unbounded = false;   // ugpu_records_totals waits for the end: no limit on pieces ahead
+  size_t ahead = 4;         // pieces the pipeline may publish ahead of the consumer (UGPU_REC_AHEAD)
   int rc = 0;
   std::mutex mu;
   std::condition_variable cv;
@@ -1559,6 +1583,9 @@ namespace {
 // the first time)
 std::mutex g_pin_mu;
 std::vector<std::pair<uint8_t*, size_t>> g_pin_pool;
+// (the pool keeps at most kPinKeep bytes; blocks beyond that are unpinned)
+constexpr size_t kPinKeep = 1ull << 30;
+size_t g_pin_kept = 0;
 
 uint8_t* pinned_get(size_t need, size_t& got)
 {
@@ -1572,6 +1599,7 @@ uint8_t* pinned_get(size_t need, size_t& got)
       uint8_t* p = g_pin_pool[best].first;
       got = g_pin_pool[best].second;
       g_pin_pool.erase(g_pin_pool.begin() + (long)best);
+      g_pin_kept -= got;
       return p;
     }
   }
@@ -1585,11 +1613,19 @@ uint8_t* pinned_get(size_t need, size_t& got)
   return static_cast<uint8_t*>(p);
 }
 
+
 void pinned_put(uint8_t* p, size_t n)
 {
   if (!p) return;
-  std::lock_guard<std::mutex> lk(g_pin_mu);
-  g_pin_pool.push_back(std::make_pair(p, n));
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (g_pin_kept + n <= kPinKeep) {
+      g_pin_pool.push_back(std::make_pair(p, n));
+      g_pin_kept += n;
+      return;
+    }
+  }
+  (void)hipHostFree(p);
 }
 
 // Per-device workspace of the records path, pooled: copy and D2H streams,
@@ -1795,6 +1831,13 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
   int b = 0;
   s->stage_once = true;  // single-pass OFFSETS for prefiltered tables
   for (uint64_t lo = start; !rc && lo < len;) {
+    {
+      // at most R->ahead pieces past the consumer's (their pinned blocks go
+      // back to the pool as the consumer moves on); a free() stops the scan
+      std::unique_lock<std::mutex> lk(R->mu);
+      R->cv.wait(lk, [&] { return R->cancel || R->unbounded || R->pieces.size() < R->pi + R->ahead; });
+      if (R->cancel) break;
+    }
     const uint64_t hi = len - lo <= chunk + chunk / 4 ? len : lo + chunk;
     uint64_t rend = hi + halo < len ? hi + halo : len;
     ugpu_totals tot{};
@@ -1944,6 +1987,20 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
 bool records_advance(ugpu_records* r, int* rc)
 {
   std::unique_lock<std::mutex> lk(r->mu);
+  if (r->pi > 0) {
+    // the consumer is done with its piece (ugpu_records_next returns copies):
+    // its pinned block goes back to the pool, and the pipeline may run ahead
+    ugpu_records::Piece& prev = r->pieces[r->pi - 1];
+    if (prev.host && !prev.landed) {
+      pinned_put(prev.host, prev.host_bytes);
+      prev.host = nullptr;
+    }
+    r->dg = r->dl = nullptr;
+    r->st = nullptr;
+    r->ln = r->cp = nullptr;
+    r->n = r->ri = 0;
+    r->cv.notify_all();
+  }
   r->cv.wait(lk, [&] { return r->pi < r->published || r->done; });
   if (r->pi >= r->published) {
     *rc = r->rc;
@@ -2006,6 +2063,7 @@ int ugpu_find_records(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uin
   R->sync_d2h = env_u64("UGPU_REC_SYNC", 0) != 0;
   R->zero_copy = env_u64("UGPU_REC_ZC", 0) != 0;
   R->trace = env_u64("UGPU_REC_TRACE", 0) != 0;
+  R->ahead = (size_t)std::max<uint64_t>(env_u64("UGPU_REC_AHEAD", 4), 1);
   R->t0 = std::chrono::steady_clock::now();
   if (len == start) {
     R->done = R->input_free = true;
@@ -2163,6 +2221,8 @@ int ugpu_records_totals(ugpu_records* r, uint64_t* count, uint64_t* digest, uint
 {
   if (!r) return fail(UGPU_INVAL, "NULL argument");
   std::unique_lock<std::mutex> lk(r->mu);
+  r->unbounded = true;  // (the pipeline must not wait for pops that come after this)
+  r->cv.notify_all();
   r->cv.wait(lk, [&] { return r->done; });
   if (r->rc) return r->rc;
   if (count) *count = r->count;
@@ -2174,6 +2234,13 @@ int ugpu_records_totals(ugpu_records* r, uint64_t* count, uint64_t* digest, uint
 int ugpu_records_free(ugpu_records* r)
 {
   if (!r) return UGPU_OK;
+  {
+    // an early stop (ugrep -m1, -l, -q): the pipeline stops at its next chunk
+    // instead of scanning (and pinning records for) the rest of the input
+    std::lock_guard<std::mutex> lk(r->mu);
+    r->cancel = true;
+    r->cv.notify_all();
+  }
   if (r->worker.joinable()) r->worker.join();
   for (auto& p : r->pieces) {
     if (p.landed) {  // (never popped: its copy may still be running)
@@ -2279,7 +2346,7 @@ void shard_scan(Shard& sh, const uint8_t* buf, uint64_t len, bool host, int src_
 
 // the shard's records into r at its base (a shard whose chain entry moved
 // is scanned again from the true entry first)
-void shard_records(Shard& sh, uint64_t len, ugpu_result* r)
+void shard_records(Shard& sh, const uint8_t* src_buf, bool src_host, int src_dev, uint64_t len, ugpu_result* r)
 {
   if ((sh.rc = hipSetDevice(sh.dev)) != hipSuccess) {
     sh.rc = hip_fail((hipError_t)sh.rc, "hipSetDevice");
@@ -2289,9 +2356,16 @@ void shard_records(Shard& sh, uint64_t len, ugpu_result* r)
   if (n == 0) return;
   if (sh.entry != sh.lo) {
     ugpu_totals t{};
-    sh.rc = ugpu_scan(sh.sc, sh.dbuf, sh.entry - sh.org, sh.hi - sh.org, sh.rend - sh.org, sh.rend == len, sh.org,
-                      sh.ws->st);
-    if (!sh.rc) sh.rc = ugpu_scan_totals(sh.sc, &t);
+    for (;;) {
+      sh.rc = ugpu_scan(sh.sc, sh.dbuf, sh.entry - sh.org, sh.hi - sh.org, sh.rend - sh.org, sh.rend == len, sh.org,
+                        sh.ws->st);
+      if (!sh.rc) sh.rc = ugpu_scan_totals(sh.sc, &t);
+      // the chain from the true entry may walk farther than the one from lo:
+      // again with the rest of the buffer readable
+      if (sh.rc != UGPU_HALO || sh.rend == len) break;
+      sh.rend = len;
+      if ((sh.rc = shard_load(sh, src_buf, src_host, src_dev)) != UGPU_OK) return;
+    }
     if (sh.rc) return;
     if (t.count != n) {
       sh.rc = fail(UGPU_DEVICE, "shard re-scan disagrees with the stitched count");
@@ -2394,8 +2468,15 @@ int ugpu_find_all_multi(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, u
     ugpu_totals d{};
     const hipError_t he = hipSetDevice(sh.dev);
     if (he != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
-    rc = ugpu_chain_fix(sh.sc, sh.dbuf, sh.lo - sh.org, sh.hi - sh.org, sh.rend - sh.org, sh.rend == len, sh.org,
-                        sh.entry - sh.org, e - sh.org, &d, sh.ws->st);
+    for (;;) {
+      rc = ugpu_chain_fix(sh.sc, sh.dbuf, sh.lo - sh.org, sh.hi - sh.org, sh.rend - sh.org, sh.rend == len, sh.org,
+                          sh.entry - sh.org, e - sh.org, &d, sh.ws->st);
+      // the chain from the true entry may walk past the halo the speculative
+      // scan needed: again with the rest of the buffer readable
+      if (rc != UGPU_HALO || sh.rend == len) break;
+      sh.rend = len;
+      if ((rc = shard_load(sh, buf, host, src_dev)) != UGPU_OK) break;
+    }
     if (rc) return finish(rc);
     sh.tot.count += d.count;
     sh.tot.digest += d.digest;
@@ -2420,7 +2501,7 @@ int ugpu_find_all_multi(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, u
       ugpu_result_free(r);
       return finish(fail(UGPU_NOMEM, "match list allocation"));
     }
-    each_shard(shards, [&](Shard& sh) { shard_records(sh, len, r); });
+    each_shard(shards, [&](Shard& sh) { shard_records(sh, buf, host, src_dev, len, r); });
     for (Shard& sh : shards)
       if (sh.rc) {
         ugpu_result_free(r);

@@ -95,7 +95,13 @@ __device__ __forceinline__ void forest_n(const Tab<FMT>& T, const Win& w, uint64
     uint32_t le, ovf = 0;
     const uint64_t len = walk<FMT, W>(T, w, bs + r, le, ovf);
     uint64_t nx = (uint64_t)r + (len ? len : 1);
-    if (nx > kFNMask) nx = kFNMask;  // (a match longer than 512 MiB)
+    if (nx > kFNMask) {
+      // a match longer than 512 MiB does not fit the entry: fail loudly (the
+      // HALO flag: the caller gets UGPU_HALO and, in the drop-in adapter, the
+      // CPU matcher) instead of a wrong length
+      nx = kFNMask;
+      ovf = 1;
+    }
     const bool empty = W == kWalkCtx && !len && le && w.nul;  // option N: the empty match at p
     N[r] = (uint32_t)nx | (len || empty ? kFMatch : 0u) | (empty ? kFEmpty : 0u) | (ovf ? kFOvf : 0u);
     if constexpr (LE) le_out[r] = le;

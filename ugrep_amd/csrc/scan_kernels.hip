@@ -7,16 +7,264 @@ namespace ugpu {
 
 
 // ---------------------------------------------------------------- fix kernel
+// Open walks (sparse_kernel walk truncation, OpenRec): a wave whose chain
+// ended in a walk still alive at its range end `lim` counted no match for it.
+// The walk W is resolved from the records of the waves after it:
+//   R1 (one thread per open wave k): walk W on from lim, and from the first
+//      match start c1 of wave k+1 on, the walk V of c1 beside it; when both
+//      are alive in the same state at the same position they are the same
+//      walk from there on (kOpenConv), so W's accepts after that point are
+//      V's: V's end e1 (a closed first match) or, when V is wave k+1's own
+//      open walk, that walk's resolved end.  W may die first (kOpenDead).
+//      A walk that neither dies nor converges within kOpenConvBudget bytes
+//      gives up (kOpenUnres: UGPU_FLAG_BUDGET, the forest FIND).
+//   R2 (wave 0, open waves in descending order, 64 at a time): the ends, each
+//      from the next one's (a run of candidate bytes across many waves is one
+//      chain of converged open walks).
+//   R3 (one thread per open wave): the match [c, e) joins the wave's counts
+//      and its exit becomes e; an end before lim re-walks the rest of the
+//      wave's chain from there (the COUNT pass had dropped those candidates).
+// Afterwards every record is what an untruncated walk would have given, and
+// the stitch below runs as for any kernel.
+// fix_kernel applies each block's corrections to its record in place (count,
+// digest, dcap; the owner thread only): the stitch loop keeps no per-block
+// arrays in registers, and the records' entries and pads (the sparse
+// kernel's first-match shortcut, its open walks) stay as the scan wrote them.
+__device__ __forceinline__ void rec_add(const ScanParams& P, uint64_t b, uint64_t dcnt, uint64_t ddg, uint64_t ddc)
+{
+  uint64_t* r = reinterpret_cast<uint64_t*>(P.recs + b);
+  r[2] += dcnt;
+  r[3] += ddg;
+  r[4] += ddc;
+}
+
+template <int FMT>
+__device__ __forceinline__ void resolve_open(const ScanParams& P, const Tab<FMT>& T, const Ctx& C, const Win& w, int G,
+                                             int tid, uint64_t* exi, const uint32_t* openm, uint32_t& ovf, uint32_t& over)
+{
+  constexpr int PER = kMaxRec / kFixThreads;
+  const int lane = tid & 63, wid = tid >> 6;
+  // R1
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int b = j * kFixThreads + tid;
+    if (b >= G || !((openm[b >> 5] >> (b & 31)) & 1u)) continue;
+    OpenRec* o = P.open + b;
+    uint32_t s = o->s, v = 0, lew = 0, type = kOpenUnres;
+    uint64_t q = o->lim, lastw = 0;
+    uint64_t c1 = ~0ull;
+    if (b + 1 < G) {
+      const BlockRec nr = P.recs[b + 1];
+      if ((nr.pad2 & kRecFirst) && nr.pad1 != 0) c1 = nr.pad0;
+    }
+    const uint64_t qmax = q + kOpenConvBudget;
+    if (c1 != ~0ull && c1 < q) {
+      // (W stands kOpenSlack past the range end: bring V there first)
+      v = T.start;
+      for (uint64_t p = c1; p < q && v; ++p) v = T.step(v, w.g[p]);
+    }
+    for (;;) {
+      if (q == c1) v = T.start;
+      if (v != 0 && v == s) {
+        type = kOpenConv;
+        break;
+      }
+      if (q >= w.rend) {  // the end of the readable bytes: the walk ends here
+        if (!w.eof) ovf = 1;
+        type = kOpenDead;
+        break;
+      }
+      if (q >= qmax) break;
+      const uint32_t byte = w.g[q];
+      s = T.step(s, byte);
+      if (v) v = T.step(v, byte);
+      if (s == 0) {
+        type = kOpenDead;
+        break;
+      }
+      ++q;
+      if (s >= T.accb) {
+        lastw = q;
+        lew = s;
+      }
+    }
+    o->q = q;
+    o->lastw = lastw;
+    o->lew = lew;
+    o->type = type;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // R2
+  if (wid == 0) {
+    uint64_t carry = 0;
+    uint32_t carry_le = 0;
+    for (int base = (G - 1) & ~63; base >= 0; base -= 64) {
+      const int b = base + lane;
+      const bool op = b < G && ((openm[b >> 5] >> (b & 31)) & 1u);
+      const uint64_t om = __ballot(op);
+      if (!om) continue;
+      uint64_t oc = 0, olast = 0, oq = 0, olastw = 0, ne1 = 0;
+      uint32_t ole = 0, olew = 0, otype = 0, nle1 = 0;
+      if (op) {
+        const OpenRec o = P.open[b];
+        oc = o.c;
+        olast = o.last;
+        ole = o.le;
+        oq = o.q;
+        olastw = o.lastw;
+        olew = o.lew;
+        otype = o.type;
+        if (b + 1 < G) {
+          const BlockRec nr = P.recs[b + 1];
+          ne1 = nr.pad1;
+          nle1 = (uint32_t)nr.pad2;
+        }
+      }
+      uint64_t mye = 0;
+      uint32_t myle = 0;
+      for (uint64_t m = om; m;) {
+        const int k = 63 - __builtin_clzll(m);
+        m &= ~(1ull << k);
+        auto rl64 = [k](uint64_t x) {
+          return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), k) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((uint32_t)x, k);
+        };
+        const uint32_t ty = (uint32_t)__builtin_amdgcn_readlane(otype, k);
+        const uint64_t lw = rl64(olastw);
+        // W's own last accept: after lim, else before it (== c: none)
+        uint64_t e = lw ? lw : rl64(olast);
+        uint32_t le = lw ? (uint32_t)__builtin_amdgcn_readlane(olew, k) : (uint32_t)__builtin_amdgcn_readlane(ole, k);
+        if (ty == kOpenConv) {
+          // after the convergence point W accepts where V does
+          const uint64_t n1 = rl64(ne1);
+          const uint64_t ve = n1 == kOpenEnd ? carry : n1;  // (wave b+1 was resolved just before)
+          const uint32_t vle = n1 == kOpenEnd ? carry_le : (uint32_t)__builtin_amdgcn_readlane(nle1, k);
+          if (ve > rl64(oq)) {
+            e = ve;
+            le = vle;
+          }
+        } else if (ty == kOpenUnres) {
+          over = 1;
+        }
+        (void)oc;
+        carry = e;
+        carry_le = le;
+        if (lane == k) {
+          mye = e;
+          myle = le;
+        }
+      }
+      if (op) {
+        P.open[b].e = mye;
+        P.open[b].le_e = myle;
+      }
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  // R3
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int b = j * kFixThreads + tid;
+    if (b >= G || !((openm[b >> 5] >> (b & 31)) & 1u)) continue;
+    const OpenRec o = P.open[b];
+    uint64_t tb = P.t0 + (uint64_t)b * P.tpb;
+    uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
+    if (tb > te) tb = te;
+    const uint64_t bhi = clampu(te * P.unit, P.lo, P.hi);
+    CountEm d;
+    uint64_t p = o.c + 1;
+    if (o.e > o.c) {
+      d.put(C, o.c, o.e - o.c, o.le_e, +1);
+      p = o.e;
+    }
+    // an end before the range end: the chain goes on from there (those
+    // candidates were dropped by the COUNT pass)
+    const uint64_t lim = p + P.merge_budget;
+    while (p < bhi) {
+      if (p > lim) {
+        over = 1;
+        break;
+      }
+      p = chain_step<FMT, CountEm>(T, w, C, p, d, +1, ovf);
+    }
+    exi[b] = p;
+    rec_add(P, (uint64_t)b, d.cnt, d.dg, d.dc);
+  }
+  __threadfence_block();
+  __syncthreads();
+}
+
+// Block b re-entered at nx instead of its entry `ent` (one fix_kernel round):
+// its record's counts corrected in place; returns whether its exit is
+// unchanged, else sets `exit`.
+template <int FMT>
+__device__ __forceinline__ bool fix_block(const ScanParams& P, const Tab<FMT>& T, const Ctx& C, const Win& w, uint64_t b,
+                                          uint64_t ent, uint64_t nx, uint64_t bhi, uint64_t& exit, uint32_t& ovf,
+                                          uint32_t& over)
+{
+  uint64_t* r = reinterpret_cast<uint64_t*>(P.recs + b);  // entry, exit, cnt, dg, dc, pad0, pad1, pad2
+  if (nx >= bhi) {
+    // the true chain enters at or past the block's end (a long match covers
+    // it): no chain position in the block, no matches
+    if (ent < bhi) r[2] = r[3] = r[4] = 0;
+    exit = nx;
+    return false;
+  }
+  CountEm d;
+  uint64_t ne = 0, po = ent;
+  bool met = false, done = false;
+  if constexpr (FMT == 0) {
+    const uint64_t pad2 = r[7];
+    if (po == r[0] && (pad2 & kRecFirst)) {
+      // the speculative chain from the record's entry visits every position
+      // up to its first kept match c1 and then its end e1: a true entry there
+      // meets it
+      uint64_t c1 = r[5], e1 = r[6];
+      uint32_t le1 = (uint32_t)pad2;
+      if (e1 == kOpenEnd) {
+        const OpenRec o = P.open[b];
+        e1 = o.e > o.c ? o.e : 0;  // (no match: the chain went on at c1 + 1)
+        le1 = o.le_e;
+        if (e1 == 0) c1 = 0;  // (no shortcut past c1)
+      }
+      if (r[6] == 0 || nx <= c1) {
+        met = done = true;
+      } else if (e1 != 0) {
+        d.put(C, c1, e1 - c1, le1, -1);  // the first match is not on the true chain
+        if (nx == e1)
+          met = done = true;
+        else
+          po = e1;
+      }
+    }
+  }
+  if (!done)
+    met = P.acap   ? merge<FMT, kWalkCtx>(T, w, C, po, nx, bhi, d, ne, ovf, P.merge_budget, &over)
+          : P.wtab ? merge<FMT, kWalkWord>(T, w, C, po, nx, bhi, d, ne, ovf, P.merge_budget, &over)
+                   : merge<FMT>(T, w, C, po, nx, bhi, d, ne, ovf, P.merge_budget, &over);
+  r[2] += d.cnt;
+  r[3] += d.dg;
+  r[4] += d.dc;
+  exit = ne;
+  return met;
+}
+
 // One workgroup re-enters every block whose speculative entry differs from its
 // predecessor's exit (merge over the block's byte range, bytes from global),
 // repeating until no exit changes; then reduces the totals and produces the
-// exact block entries and output bases for the OFFSETS pass.
+// exact block entries and output bases for the OFFSETS pass.  A block the
+// true chain enters at or past its end is skipped in one step (a long match
+// covers it); a sparse_kernel record whose first kept match the true entry
+// reaches or ends at is corrected without a walk (BlockRec pads).
 template <int FMT>
 __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
 {
   __shared__ uint64_t ent[kMaxRec], exi[kMaxRec];
   __shared__ uint64_t wred[3][kFixThreads / 64];
   __shared__ uint64_t wscan[kFixThreads / 64];
+  __shared__ uint32_t openm[kMaxRec / 32];
   constexpr int PER = kMaxRec / kFixThreads;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int G = (int)P.nrec;
@@ -26,73 +274,76 @@ __global__ __launch_bounds__(kFixThreads) void fix_kernel(ScanParams P)
   uint32_t ovf = 0, over = 0;
   // the scan kernel already gave up on these chains (UGPU_FLAG_BUDGET): the host
   // resolves the range with the forest FIND, nothing to stitch
-  if (__hip_atomic_load(P.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & UGPU_FLAG_BUDGET) return;
-
-  uint64_t cnt[PER], dg[PER], dc[PER];
+  const uint32_t fl = __hip_atomic_load(P.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (fl & UGPU_FLAG_BUDGET) return;
+  const bool any_open = FMT == 0 && P.open && (fl & UGPU_FLAG_OPEN);
+  if (any_open)
+    for (int i = tid; i < kMaxRec / 32; i += kFixThreads) openm[i] = 0;
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int b = j * kFixThreads + tid;
     if (b < G) {
-      BlockRec r = P.recs[b];
-      ent[b] = r.entry;
-      exi[b] = r.exit;
-      cnt[j] = r.cnt;
-      dg[j] = r.dg;
-      dc[j] = r.dc;
-    } else {
-      cnt[j] = dg[j] = dc[j] = 0;
+      const uint64_t* r = reinterpret_cast<const uint64_t*>(P.recs + b);
+      ent[b] = r[0];
+      exi[b] = r[1];
+      if (any_open && (r[7] & kRecOpen)) atomicOr(&openm[b >> 5], 1u << (b & 31));
     }
+  }
+  if (any_open) {
+    __syncthreads();
+    resolve_open<FMT>(P, T, C, w, G, tid, exi, openm, ovf, over);
+    over = __syncthreads_or(over) ? 1u : 0u;
   }
   uint32_t rounds = 0;
   for (;;) {
     __syncthreads();
-    uint64_t nx[PER];
-    bool ch[PER], any = false;
+    uint32_t chm = 0;  // bit j: block j * kFixThreads + tid changed
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int b = j * kFixThreads + tid;
-      ch[j] = false;
-      if (b > 0 && b < G) {
-        nx[j] = exi[b - 1];
-        ch[j] = nx[j] != ent[b];
-        any |= ch[j];
-      }
+      if (b > 0 && b < G && exi[b - 1] != ent[b]) chm |= 1u << j;
     }
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      if (!ch[j]) continue;
+    // (a block's new entry is its predecessor's exit as read here: one that a
+    // merge of this round already moved only brings the fixpoint closer)
+    for (uint32_t m = chm; m;) {
+      const int j = __builtin_ctz(m);
+      m &= m - 1;
       const uint64_t b = (uint64_t)j * kFixThreads + tid;
+      const uint64_t nx = exi[b - 1];
+      if (nx == ent[b]) continue;
       uint64_t tb = P.t0 + b * P.tpb;
       uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
       if (tb > te) tb = te;
       const uint64_t bhi = clampu(te * P.unit, P.lo, P.hi);
-      CountEm d;
-      uint64_t ne;
-      const bool met =
-          P.acap   ? merge<FMT, kWalkCtx>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over)
-          : P.wtab ? merge<FMT, kWalkWord>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over)
-                   : merge<FMT>(T, w, C, ent[b], nx[j], bhi, d, ne, ovf, P.merge_budget, &over);
-      if (!met) exi[b] = ne;
-      ent[b] = nx[j];
-      cnt[j] += d.cnt;
-      dg[j] += d.dg;
-      dc[j] += d.dc;
+      uint64_t ne = 0;
+      if (!fix_block<FMT>(P, T, C, w, b, ent[b], nx, bhi, ne, ovf, over)) exi[b] = ne;
+      ent[b] = nx;
     }
-    if (!__syncthreads_or(any)) break;
+    if (!__syncthreads_or(chm != 0)) break;
     if (__syncthreads_or(over) || ++rounds >= P.max_rounds) {  // chains that do not resynchronise
       over = 1;
       break;
     }
   }
-  // totals + exclusive scan of block counts (block order b = j * kFixThreads + tid:
-  // one workgroup scan per j, carried across j)
+  __threadfence_block();
+  __syncthreads();
+  uint64_t cnt[PER];
   uint64_t md = 0, mdc = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    md += dg[j];
-    mdc += dc[j];
+    const int b = j * kFixThreads + tid;
+    cnt[j] = 0;
+    if (b < G) {
+      const uint64_t* r = reinterpret_cast<const uint64_t*>(P.recs + b);
+      cnt[j] = r[2];
+      md += r[3];
+      mdc += r[4];
+    }
   }
+  // totals + exclusive scan of block counts (block order b = j * kFixThreads + tid:
+  // one workgroup scan per j, carried across j)
   const uint64_t sd = wave_sum(md), sdc = wave_sum(mdc);
   if (lane == 0) {
     wred[1][wid] = sd;

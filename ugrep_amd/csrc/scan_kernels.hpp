@@ -57,6 +57,50 @@ constexpr uint64_t kMaxRecBytes = 1ull << 30;  // bytes per chain record (32-bit
 struct BlockRec {
   uint64_t entry, exit, cnt, dg, dc, pad0, pad1, pad2;
 };
+// sparse_kernel COUNT records also describe the first match their speculative
+// chain keeps, for fix_kernel's shortcuts (pad0 = its start c1, pad1 = its end
+// e1: 0 = the chain keeps no match, kOpenEnd = the open walk below; pad2 =
+// accept entry | kRecOpen | kRecFirst)
+constexpr uint64_t kOpenEnd = ~0ull;
+constexpr uint64_t kRecOpen = 1ull << 32;   // the wave ends in an open walk (OpenRec)
+constexpr uint64_t kRecFirst = 1ull << 33;  // pad0 / pad1 are valid
+
+// Open walk of a sparse_kernel wave (walk truncation, P.open): the walk of a
+// kept candidate was still alive at the wave's walk limit `lim` (its range
+// end).  The wave counts no match for it and keeps nothing after it
+// (optimistically: the walk's match covers the rest of its range).  fix_kernel
+// resolves it from the next waves' records (convergence with their first
+// walks) and stores the walk's true end; the WRITE pass reads that back.
+struct OpenRec {
+  uint64_t c;      // walk start
+  uint64_t last;   // last accept position before lim (== c: none)
+  uint64_t lim;    // where the walk stands: kOpenSlack past the wave's range end (or less at rend)
+  uint32_t s, le;  // DFA entry at lim, entry of the last accepting state
+  // fix_kernel resolution
+  uint64_t q;      // R1: position where the walk converged with / died
+  uint64_t lastw;  // R1: last accept of the walk at or after lim (0: none)
+  uint32_t lew;    // R1: its accepting entry
+  uint32_t type;   // R1: kOpenDead / kOpenConv / kOpenUnres
+  uint64_t e;      // R2: the walk's last accept overall (== c: it never accepts)
+  uint32_t le_e;   // R2: its accepting entry
+  uint32_t pad;
+};
+constexpr uint32_t kOpenDead = 1, kOpenConv = 2, kOpenUnres = 3;
+
+// A sparse_kernel wave suspended at a walk longer than its 32-byte window: its
+// chain state and the walked batch, for the resume launch (sparse_kernel.hip)
+struct PendSlot {
+  uint64_t c;
+  uint32_t s, le, packed;  // qr | lr << 8 | st << 16 | todo << 24
+  uint32_t pad;
+};
+struct SuspRec {
+  uint64_t x, widx, cnt, dg, dc, c1, e1, rs, sgn;
+  uint32_t wover, ovf, first, open, le1, sgover, tile, dn;
+  PendSlot lanes[64];
+};
+constexpr uint64_t kOpenConvBudget = 4096;  // bytes R1 may walk looking for convergence
+constexpr uint64_t kOpenSlack = 256;        // bytes a walk goes on past its wave's range end before it is open
 
 struct DevTotals {
   uint64_t count, digest, dcap, entry, exit;
@@ -81,6 +125,8 @@ struct DevTotals {
 // xc_kernel U mode (fast kernel): a code with bit 3 (an XU_MIX or XU_SLOW lead)
 // was met; the host redoes the range with the exact U kernel (P.xu_exact)
 #define UGPU_FLAG_UMIX 256u
+// sparse_kernel: a wave's walk was truncated at its range end (OpenRec); fix_kernel resolves it
+#define UGPU_FLAG_OPEN 512u
 constexpr uint32_t kStageOver = 0xffffffffu;
 constexpr uint32_t kStageDone = 0xfffffffeu;
 constexpr uint32_t kStagePer = 1024;  // staged records per wave (16 B each: 128 MiB for 8192 waves)
@@ -165,6 +211,13 @@ struct ScanParams {
   const uint32_t* acap;
   uint32_t bol0;
   uint32_t nul;
+  // sparse_kernel walk truncation: per wave, the open walk (COUNT pass writes,
+  // fix_kernel resolves, the WRITE pass reads); NULL: walks run to rend
+  OpenRec* open;
+  // sparse_kernel long walks: per wave, suspended (1) or not (0), and the
+  // suspended state; NULL: walks complete in their lanes (option W)
+  uint32_t* susp;
+  SuspRec* srec;
 };
 
 // Forest FIND (forest.hip): exact for every table, no resynchronisation

@@ -129,11 +129,6 @@ constexpr int kDefer = 64;                          // deferred candidates per w
 constexpr int kAux = 2048;                          // per-wave aux LDS bytes
 static_assert(kDefer * 8 <= kAux && 64 * 32 <= kAux, "aux region too small");
 
-// Greedy FIND rule over up to 64 walked candidates held one per lane in
-// position order: keep the match at c iff c >= x, the end of the last kept
-// match (Appendix A: a non-candidate position only steps p+1).  With the
-// exclusive prefix-max of match ends (relative to x) the rule is exact unless
-// two candidate matches overlap; those batches take a 64-step in-wave pass.
 // Records staged by a COUNT pass for the OFFSETS pass (single-pass OFFSETS):
 // the wave's slice of the staging arrays, filled in chain order from index 0.
 struct Stage {
@@ -144,11 +139,44 @@ struct Stage {
   uint32_t over = 0;    // the slice was too small
 };
 
+// State of one wave's FIND chain over its tile range.
+struct WaveChain {
+  uint64_t x;      // end of the last kept match (wave-uniform): the chain resumes there
+  uint32_t dn;     // deferred candidates in the list
+  uint64_t widx;   // next output slot (WRITE)
+  uint32_t wover;  // output capacity exceeded
+  uint32_t ovf;    // a walk ran past the read window
+  CountEm acc;
+  Stage sg;        // COUNT pass with staging: the wave's staged records
+  // COUNT pass: the first match the chain keeps (fix_kernel shortcuts) and
+  // whether the chain ended in an open walk (OpenRec)
+  uint32_t first, open;
+  uint64_t c1, e1;
+  uint32_t le1;
+  // a batch left pending by flush_deferred (a walk outgrew its window), and
+  // the position the tile loop resumes from (earlier candidates are consumed)
+  uint32_t pend;
+  uint64_t rs, ptile;  // (ptile: start of the tile the wave suspended in)
+};
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);  // (readlane is int: no sign extension)
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Greedy FIND rule over up to 64 walked candidates held one per lane in
+// position order: keep the match at c iff c >= x, the end of the last kept
+// match (Appendix A: a non-candidate position only steps p+1).  With the
+// exclusive prefix-max of match ends (relative to x) the rule is exact unless
+// two candidate matches overlap; those batches take a 64-step in-wave pass.
+// COUNT: also stages the kept records (STAGE) and notes the first kept match.
 template <bool WRITE, bool STAGE = false>
 __device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, uint32_t le, int lane, const Ctx& C,
-                                        const ScanParams& P, uint64_t& x, CountEm& acc, uint64_t& widx,
-                                        uint32_t& wover, Stage& sg)
+                                        const ScanParams& P, WaveChain& w)
 {
+  const uint64_t x = w.x;
   const bool vm = valid && len != 0 && c >= x;
   const uint64_t endr = vm ? c + len - x : 0;  // > 0 for vm lanes
   const bool wide = __ballot(endr > 0xffffffffull) != 0;
@@ -159,6 +187,7 @@ __device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, ui
     uint64_t xx = x;
     kept = false;
     const uint64_t e = vm ? c + len : 0ull;
+#pragma unroll 1
     for (int i = 0; i < 64; ++i) {
       const uint64_t ci = __shfl(c, i, 64), ei = __shfl(e, i, 64);
       if (ei != 0 && ci >= xx) {
@@ -170,34 +199,256 @@ __device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, ui
   const uint64_t kb = __ballot(kept);
   if (!kb) return;
   if constexpr (WRITE) {
-    WriteEm we{widx + lanes_below(kb), P.out_capacity, P.out_start, P.out_len, P.out_cap};
+    WriteEm we{w.widx + lanes_below(kb), P.out_capacity, P.out_start, P.out_len, P.out_cap};
     if (kept) we.put(C, c, len, le, +1);
-    wover |= we.overflow;
-    widx += __popcll(kb);
+    w.wover |= we.overflow;
+    w.widx += __popcll(kb);
   } else {
-    if (kept) acc.put(C, c, len, le, +1);
+    if (kept) w.acc.put(C, c, len, le, +1);
     if constexpr (STAGE) {
-      WriteEm se{sg.n + lanes_below(kb), P.st_per, sg.start, sg.len, sg.cap};
+      WriteEm se{w.sg.n + lanes_below(kb), P.st_per, w.sg.start, w.sg.len, w.sg.cap};
       if (kept) se.put(C, c, len, le, +1);
-      sg.over |= se.overflow;
-      sg.n += __popcll(kb);
+      w.sg.over |= se.overflow;
+      w.sg.n += __popcll(kb);
+    }
+    if (!w.first) {
+      const int f = __builtin_ctzll(kb);
+      w.first = 1;
+      w.c1 = readlane64(c, f);
+      w.e1 = w.c1 + readlane64(len, f);
+      w.le1 = (uint32_t)__builtin_amdgcn_readlane(le, f);
     }
   }
   // kept matches are disjoint and ordered: the last one ends last
-  const int ll = 63 - __builtin_clzll(kb);
-  const uint64_t e = c + len;
-  const uint32_t ehi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(e >> 32), ll);
-  const uint32_t elo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)e, ll);  // readlane is int: no sign extension
-  x = ((uint64_t)ehi << 32) | elo;
+  w.x = readlane64(c + len, 63 - __builtin_clzll(kb));
+}
+
+// A walk continued by the whole wave (wave-uniform in and out).
+struct CoopWalk {
+  uint64_t last;  // last accept position (unchanged: none since the entry)
+  uint32_t s;     // DFA entry at `lim` when the walk is still alive there
+  uint32_t le;    // entry of the last accepting state
+  uint32_t done;  // the walk ended: it died, or reached the end of the stream
+  uint32_t ovf;   // it reached a readable end that is not the end of the stream
+};
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+
+// Continue one walk -- DFA entry s before byte q, last accept `last` / `le` --
+// with all 64 lanes, up to `lim` (<= rend).  A walk that outgrows its 32-byte
+// window (a long match, e.g. `a+` over a run of `a`) would otherwise read one
+// byte per dependent global load.  Each round stages the 1 KiB from q & ~15 in
+// the wave's LDS scratch, 16 bytes per lane; every lane walks its 16 bytes
+// from a guessed entry -- the walk's state run over the 4 bytes before them,
+// which is exact whenever the state depends on the last few bytes only (a run
+// of one byte, a `.*`-like loop) -- and the guesses are checked in lane order
+// against the previous lane's exit (DPP).  The walk advances to the first lane
+// whose guess was wrong, or dies in the first dying lane before it: at least
+// the rest of lane 0's 16 bytes per round, up to 1 KiB.
+// (noinline: called from the rare long-walk path, it keeps its registers out
+// of the main loop's budget)
+__device__ __forceinline__ CoopWalk coop_walk(const lds_u16* trans, uint32_t accb, const uint8_t* g,
+                                                       uint64_t rend, uint32_t eof, lds_u8* scr, uint32_t s,
+                                                       uint64_t q, uint64_t last, uint32_t le, uint64_t lim)
+{
+  const int lane = threadIdx.x & 63;
+  const uint64_t last16 = (rend - 1) & ~uint64_t(15);
+  CoopWalk r{last, s, le, 0u, 0u};
+  while (q < lim) {
+    const uint64_t base = q & ~uint64_t(15);
+    const uint64_t sa = base + 16u * (uint32_t)lane;
+    uint4 v{0u, 0u, 0u, 0u};
+    if (sa <= last16) v = *reinterpret_cast<const uint4*>(g + sa);
+    wave_lds_sync();  // the previous round's reads are done
+    {
+      typedef __attribute__((address_space(3))) uint32_t lds_u32;
+      lds_u32* d = reinterpret_cast<lds_u32*>(scr + 16 * lane);
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+    wave_lds_sync();
+    const uint64_t a = sa > q ? sa : q;
+    const uint64_t z = sa + 16 < lim ? sa + 16 : lim;
+    uint32_t spec = r.s;
+    if (lane != 0) {
+      uint32_t t = r.s;
+#pragma unroll
+      for (int k = 4; k > 0; --k) t = t ? (uint32_t)trans[t | scr[16 * lane - k]] : 0u;
+      spec = t ? t : r.s;
+    }
+    uint32_t cur = spec, lel = 0;
+    uint64_t lastl = 0;  // (an accept position follows a consumed byte: never 0)
+    bool died = false;
+    for (uint64_t i = a; i < z; ++i) {
+      const uint32_t e = trans[cur | scr[i - base]];
+      if (e == 0) {
+        died = true;
+        break;
+      }
+      cur = e;
+      if (e >= accb) {
+        lastl = i + 1;
+        lel = e;
+      }
+    }
+    const uint32_t prev = dpp_prev_lane(cur);
+    const bool seg = a < z;
+    const uint64_t live = __ballot(seg);  // a prefix of the lanes (lane 0 owns q)
+    const int nl = __popcll(live);
+    const uint64_t bad = __ballot(seg && lane != 0 && spec != prev);
+    const uint64_t dead = __ballot(seg && died);
+    const uint64_t accm = __ballot(lastl != 0);
+    const int j = bad ? __builtin_ctzll(bad) : nl;  // lanes [0, j) walked from their true entry
+    const int d = dead ? __builtin_ctzll(dead) : 64;
+    if (d < j) {  // the walk dies in lane d
+      const uint64_t m = accm & lowbits((uint64_t)d + 1);
+      if (m) {
+        const int k = 63 - __builtin_clzll(m);
+        r.last = readlane64(lastl, k);
+        r.le = (uint32_t)__builtin_amdgcn_readlane(lel, k);
+      }
+      r.done = 1;
+      return r;
+    }
+    const uint64_t m = accm & lowbits((uint64_t)j);
+    if (m) {
+      const int k = 63 - __builtin_clzll(m);
+      r.last = readlane64(lastl, k);
+      r.le = (uint32_t)__builtin_amdgcn_readlane(lel, k);
+    }
+    r.s = (uint32_t)__builtin_amdgcn_readlane(cur, j - 1);
+    const uint64_t qn = base + 16u * (uint32_t)j;
+    q = (j < nl || qn < lim) ? qn : lim;
+  }
+  if (lim >= rend) {  // alive at the end of the readable bytes: the walk ends there
+    r.done = 1;
+    r.ovf = eof ? 0u : 1u;
+  }
+  return r;
+}
+
+// Per-lane state of a walked batch (window-relative 32-bit offsets): st 0 =
+// the walk ended, match [c, c + lr); 1 = alive at the window end, DFA entry s
+// before byte c + qr, last accept c + lr; 2 = alive at the walk limit.
+struct BatchLane {
+  uint64_t c;
+  uint32_t s, qr, lr, le, st;
+  bool todo;  // not resolved yet
+};
+
+// Resolve a walked batch in position order up to the first lane whose walk
+// outgrew its window and that the chain can still keep.  Returns that lane, or
+// 64 when the whole batch is resolved.
+template <bool WRITE, bool STAGE>
+__device__ __forceinline__ int batch_resolve(BatchLane& L, int lane, const Ctx& C, const ScanParams& P, WaveChain& w)
+{
+  for (;;) {
+    const uint64_t pend = __ballot(L.todo && L.st != 0);
+    const int i = pend ? __builtin_ctzll(pend) : 64;
+    // the candidates before lane i have their walks: resolve them
+    resolve<WRITE, STAGE>(L.todo && lane < i, L.c, L.st == 0 ? (uint64_t)L.lr : 0ull, L.le, lane, C, P, w);
+    if (!pend) return 64;
+    L.todo = L.todo && lane > i;
+    if (readlane64(L.c, i) >= w.x) return i;  // (else inside a kept match: never kept, its walk is not needed)
+  }
+}
+
+// Lane i's walk outgrew its window: complete it with the whole wave
+// (coop_walk) and resolve it.  A walk still alive at the walk limit: the COUNT
+// pass records it as the wave's open walk (no match counted, nothing kept
+// after it: fix_kernel finds its end from the next waves' records); the WRITE
+// pass takes the end fix_kernel resolved when it is that walk, else walks on.
+template <bool WRITE, bool STAGE>
+__device__ __forceinline__ void long_lane(int i, const BatchLane& L, int lane, uint8_t* scr, const Tab<0>& T,
+                                          const Ctx& C, const ScanParams& P, WaveChain& w, uint64_t lim, uint64_t gw)
+{
+  const uint64_t ci = readlane64(L.c, i);
+  CoopWalk r{ci + (uint32_t)__builtin_amdgcn_readlane(L.lr, i), (uint32_t)__builtin_amdgcn_readlane(L.s, i),
+             (uint32_t)__builtin_amdgcn_readlane(L.le, i), 0u, 0u};
+  if (__builtin_amdgcn_readlane(L.st, i) == 1)
+    r = coop_walk((const lds_u16*)T.trans, T.accb, P.g, P.rend, P.at_eof, (lds_u8*)scr, r.s,
+                  ci + (uint32_t)__builtin_amdgcn_readlane(L.qr, i), r.last, r.le, lim);
+  // a walk alive at the range end usually ends a few bytes later (a needle
+  // across the cut): walk on up to kOpenSlack bytes before calling it open
+  uint64_t lim2 = lim;
+  if (!r.done) {
+    lim2 = lim + kOpenSlack < P.rend ? lim + kOpenSlack : P.rend;
+    r = coop_walk((const lds_u16*)T.trans, T.accb, P.g, P.rend, P.at_eof, (lds_u8*)scr, r.s, lim, r.last, r.le, lim2);
+  }
+  w.ovf |= r.ovf;
+  if (!r.done) {  // alive at lim2 (< rend), past the wave's range end
+    if constexpr (!WRITE) {
+      if (lane == 0) {
+        OpenRec o{};
+        o.c = ci;
+        o.last = r.last;
+        o.lim = lim2;
+        o.s = r.s;
+        o.le = r.le;
+        P.open[gw] = o;
+      }
+      w.open = 1;
+      if (!w.first) {
+        w.first = 1;
+        w.c1 = ci;
+        w.e1 = kOpenEnd;
+        w.le1 = 0;
+      }
+      w.x = kOpenEnd;
+      return;
+    } else {
+      bool got = false;
+      if (P.open && (P.recs[gw].pad2 & kRecOpen)) {
+        const OpenRec o = P.open[gw];
+        if (o.c == ci) {
+          r.last = o.e;
+          r.le = o.le_e;
+          got = true;
+        }
+      }
+      if (!got) {
+        r = coop_walk((const lds_u16*)T.trans, T.accb, P.g, P.rend, P.at_eof, (lds_u8*)scr, r.s, lim2, r.last, r.le,
+                      P.rend);
+        w.ovf |= r.ovf;
+      }
+    }
+  }
+  resolve<WRITE, STAGE>(lane == i, L.c, r.last - ci, r.le, lane, C, P, w);
+}
+
+// Resolve a walked batch completely: in position order, each lane whose walk
+// outgrew its window and that the chain can still keep is completed by the
+// whole wave (long_lane), up to an open walk (nothing after it is kept).
+template <bool WRITE, bool STAGE>
+__device__ __forceinline__ void batch_finish(BatchLane& L, int lane, uint8_t* scr, const Tab<0>& T, const Ctx& C,
+                                             const ScanParams& P, WaveChain& w, uint64_t lim, uint64_t gw)
+{
+  for (;;) {
+    const int i = batch_resolve<WRITE, STAGE>(L, lane, C, P, w);
+    if (i == 64) break;
+    long_lane<WRITE, STAGE>(i, L, lane, scr, T, C, P, w, lim, gw);
+    if (w.x == kOpenEnd) break;
+  }
+  wave_lds_sync();  // the aux region is reused
 }
 
 // Walk the deferred candidates (one per lane) and resolve them.  Each lane
 // copies the 32 bytes from c & ~15 into its LDS window (the tiles are gone
-// from registers); longer walks continue from global memory.
-template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
+// from registers) and walks its candidate there.  A walk still alive at the
+// window end (a long match, e.g. `a+` over a run of `a`) needs the whole wave
+// (coop_walk): the main kernel then suspends the wave (w.pend: its state goes
+// to P.srec) and the RESUME instantiation of the kernel, launched right
+// after, completes the batch and the rest of the wave's tiles -- so the long
+// path's registers never count against the main kernel's occupancy.  `lim`
+// bounds every walk: the wave's range end when walks are truncated (P.open),
+// else the readable end.  Option W keeps its per-lane walks (walk<0, true>).
+template <bool WRITE, int ABL, bool W = false, bool STAGE = false, bool RESUME = false>
 __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr, uint32_t dn, int lane, const Tab<0>& T,
-                                            const Ctx& C, const ScanParams& P, uint64_t& x, CountEm& acc,
-                                            uint64_t& widx, uint32_t& wover, uint32_t& ovf, Stage& sg)
+                                            const Ctx& C, const ScanParams& P, WaveChain& w, uint64_t lim,
+                                            uint64_t gw)
 {
   wave_lds_sync();
   const bool valid = (uint32_t)lane < dn;
@@ -209,37 +460,71 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
   *reinterpret_cast<uint4*>(scr + 32 * lane) = v0;
   *reinterpret_cast<uint4*>(scr + 32 * lane + 16) = v1;
   wave_lds_sync();
-  uint64_t len = 0;
-  uint32_t le = 0;
-  if (valid && ABL != 3) {
-    Win w;
-    w.lds = scr + 32 * lane;
-    w.base = a;
-    w.lend = a + 32;
-    w.g = P.g;
-    w.rend = P.rend;
-    w.eof = P.at_eof;
-    w.wtab = P.wtab;
-    w.nwtab = P.nwtab;
-    w.bob = P.bob;
-    // option W: the walk checks at_wb/at_we (device_common.hpp); candidates
-    // stay a superset (W only removes matches), so the prefilter is unchanged
-    len = walk<0, W>(T, w, c, le, ovf);
+  if constexpr (W) {
+    uint64_t len = 0;
+    uint32_t le = 0;
+    if (valid && ABL != 3) {
+      Win win;
+      win.lds = scr + 32 * lane;
+      win.base = a;
+      win.lend = a + 32;
+      win.g = P.g;
+      win.rend = P.rend;
+      win.eof = P.at_eof;
+      win.wtab = P.wtab;
+      win.nwtab = P.nwtab;
+      win.bob = P.bob;
+      // option W: the walk checks at_wb/at_we (device_common.hpp); candidates
+      // stay a superset (W only removes matches), so the prefilter is unchanged
+      len = walk<0, W>(T, win, c, le, w.ovf);
+    }
+    resolve<WRITE, STAGE>(valid, c, len, le, lane, C, P, w);
+    wave_lds_sync();  // the aux region is reused
+    return;
   }
-  resolve<WRITE, STAGE>(valid, c, len, le, lane, C, P, x, acc, widx, wover, sg);
-  wave_lds_sync();  // the aux region is reused
+  BatchLane L{c, T.start, 0u, 0u, 0u, 0u, valid};
+  if (valid && ABL != 3) {
+    const uint64_t wl = a + 32 < lim ? a + 32 : lim;
+    const uint32_t wr = (uint32_t)(wl - c);
+    for (;;) {
+      if (L.qr >= wr) {
+        if (c + L.qr >= P.rend) {
+          if (!P.at_eof) w.ovf = 1;  // a live walk ran into the end of this shard's readable bytes
+        } else {
+          L.st = c + L.qr >= lim ? 2u : 1u;
+        }
+        break;
+      }
+      const uint32_t e = T.step(L.s, scr[32 * lane + (uint32_t)(c - a) + L.qr]);
+      if (e == 0) break;
+      L.s = e;
+      ++L.qr;
+      if (e >= T.accb) {
+        L.lr = L.qr;
+        L.le = e;
+      }
+    }
+  }
+  if (!__ballot(L.st != 0)) {  // (the common case: every walk ended in its window)
+    resolve<WRITE, STAGE>(valid, c, L.lr, L.le, lane, C, P, w);
+    wave_lds_sync();  // the aux region is reused
+    return;
+  }
+  wave_lds_sync();  // (the windows are dead from here)
+  if constexpr (RESUME) {
+    batch_finish<WRITE, STAGE>(L, lane, scr, T, C, P, w, lim, gw);
+  } else {
+    PendSlot ps;
+    ps.c = L.c;
+    ps.s = L.s;
+    ps.le = L.le;
+    ps.packed = L.qr | L.lr << 8 | L.st << 16 | (uint32_t)L.todo << 24;
+    ps.pad = 0;
+    P.srec[gw].lanes[lane] = ps;
+    w.pend = 1;
+    w.rs = readlane64(c, (int)dn - 1) + 1;  // the batch's candidates are consumed
+  }
 }
-
-// State of one wave's FIND chain over its tile range.
-struct WaveChain {
-  uint64_t x;      // end of the last kept match (wave-uniform): the chain resumes there
-  uint32_t dn;     // deferred candidates in the list
-  uint64_t widx;   // next output slot (WRITE)
-  uint32_t wover;  // output capacity exceeded
-  uint32_t ovf;    // a walk ran past the read window
-  CountEm acc;
-  Stage sg;        // COUNT pass with staging: the wave's staged records
-};
 
 // Prefilter one 4 KiB wave-tile held in registers (v_k = chunk k: bytes
 // [ts + 1024k + 16*lane, +16)) and append its candidates, in position order
@@ -248,16 +533,17 @@ struct WaveChain {
 // by the wave's range [wlo, whi).
 // ABL (benchmarking only; results are not matches): 1 loads alone, 2 loads +
 // prefilter, 3 everything but the walks.
-template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
+template <bool WRITE, int ABL, bool W = false, bool STAGE = false, bool RESUME = false>
 __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3,
                                           uint64_t ts, bool edge, uint64_t wlo, uint64_t whi, int lane,
                                           const FTab& F, const Tab<0>& T, const Ctx& C, const ScanParams& P,
-                                          uint64_t* dl, uint8_t* scr, WaveChain& w)
+                                          uint64_t* dl, uint8_t* scr, WaveChain& w, uint64_t lim, uint64_t gw)
 {
   if constexpr (ABL == 1) {
     w.acc.cnt += (v0.x ^ v1.y ^ v2.z ^ v3.w) & 1;
     return;
   }
+  if (!RESUME && w.pend) return;  // suspended: the rest of the range is the resume launch's
   // the 4 bytes after chunk k of a lane are the next lane's first dword
   // (DPP wave_shl:1), or lane 0's of chunk k+1 for lane 63; past the tile
   // they are unknown and pass
@@ -326,11 +612,15 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
       const uint64_t z = whi > p0 ? (whi - p0 > 16 ? 16 : whi - p0) : 0;
       mk &= (uint32_t)((lowbits(z) & ~lowbits(a)) & 0xffffu);
     }
-    if (w.x > p0) {
+    const uint64_t xr = w.x > w.rs ? w.x : w.rs;
+    if (xr > p0) {
       // positions below the end of the last kept match are never kept (the
       // chain resumes there): drop them before they are walked -- in a long
-      // run of candidates only the batch holding its start is walked
-      const uint64_t a = w.x - p0;
+      // run of candidates only the batch holding its start is walked.  (w.x
+      // comes from the batches flushed so far, so it can lag behind the
+      // queued candidates: resolve drops those.)  Below w.rs: candidates a
+      // pending batch already consumed, when the tile is processed again.
+      const uint64_t a = xr - p0;
       mk &= (uint32_t)(~lowbits(a < 16 ? a : 16) & 0xffffu);
     }
     if constexpr (ABL == 2) {
@@ -344,8 +634,12 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
     const uint32_t rank = incl - cnt;
     for (uint32_t done = 0; done < tot;) {
       if (w.dn == (uint32_t)kDefer) {
-        flush_deferred<WRITE, ABL, W, STAGE>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf, w.sg);
+        flush_deferred<WRITE, ABL, W, STAGE, RESUME>(dl, scr, w.dn, lane, T, C, P, w, lim, gw);
         w.dn = 0;
+        if (!RESUME && w.pend) {  // the wave suspends (the resume launch repeats this tile)
+          w.ptile = ts;
+          return;
+        }
       }
       const uint32_t take = tot - done < kDefer - w.dn ? tot - done : kDefer - w.dn;
       uint32_t m = mk, r = rank;
@@ -375,14 +669,22 @@ __device__ __forceinline__ TileLoad wave_tile(const uint8_t* wbase, uint32_t i, 
 
 }  // namespace
 
-template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
-__global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
+template <bool WRITE, int ABL, bool W = false, bool STAGE = false, bool RESUME = false>
+__global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar control flow
+  const uint64_t gw = (uint64_t)blockIdx.x * kSpWaves + wid;
+  // RESUME: only the waves the main launch suspended (the others return)
+  bool mine = true;
+  if constexpr (RESUME) {
+    mine = P.susp[gw] != 0;
+    if (!__syncthreads_or(mine)) return;
+  }
   // per-wave aux region, time-multiplexed: the deferred candidate list (u64)
-  // and, while it is walked, the walk windows (32 B per lane)
+  // and, while it is walked, the walk windows (32 B per lane) / coop_walk's
+  // staging
   uint8_t* aux = smem + wid * kAux;
   uint64_t* dl = reinterpret_cast<uint64_t*>(aux);
   uint8_t* scr = aux;
@@ -395,11 +697,11 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
     for (uint32_t i = tid; i < P.nstates; i += kSpWaves * 64) lcaps[i] = P.caps[i];
   }
   __syncthreads();  // the only workgroup barrier: tables staged
+  if (!mine) return;
   const Tab<0> T{ltrans, nullptr, P.start, P.accb};
   const Ctx C{lcaps, P.log_row, P.delta};
   const FTab F{P.ft[0], P.ft[1], P.ft[2], P.ft[3], P.ft[4]};
 
-  const uint64_t gw = (uint64_t)blockIdx.x * kSpWaves + wid;
   uint64_t tb = P.t0 + gw * P.tpb;
   uint64_t te = tb + P.tpb < P.t1 ? tb + P.tpb : P.t1;
   if (tb > te) tb = te;
@@ -411,8 +713,20 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
   w.widx = WRITE ? P.out_base[gw] : 0;
   w.wover = 0;
   w.ovf = 0;
-  if constexpr (WRITE) {  // single-pass OFFSETS: this wave's records were staged and copied already
-    if (P.st_n && P.st_n[gw] == kStageDone) return;
+  w.first = w.open = 0;
+  w.c1 = w.e1 = 0;
+  w.le1 = 0;
+  w.pend = 0;
+  w.rs = w.ptile = 0;
+  // walk limit: with truncation (P.open) a walk still alive at the range end
+  // of any wave but the last becomes the wave's open walk (fix_kernel); the
+  // last wave's walks run to the readable end, as the range's exit needs
+  const uint64_t lim = (!W && P.open && whi < P.hi) ? whi : P.rend;
+  if constexpr (WRITE && !RESUME) {  // single-pass OFFSETS: this wave's records were staged and copied already
+    if (P.st_n && P.st_n[gw] == kStageDone) {
+      if (P.susp && lane == 0) P.susp[gw] = 0;
+      return;
+    }
   }
   if constexpr (STAGE) {
     w.sg.start = P.st_start + gw * P.st_per;
@@ -432,26 +746,51 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
   const uint32_t rel = (uint32_t)(relw < (uint64_t)n * kWaveTile ? relw : (uint64_t)n * kWaveTile);
   const bool clip_lo = wlo != wb, clip_hi = whi != te * kWaveTile;
   const uint32_t lo16 = 16u * lane;
+  uint32_t i = 0;
+  if constexpr (RESUME) {
+    // the suspended state: the chain so far, then the pending batch
+    const SuspRec& sr = P.srec[gw];
+    w.x = sr.x;
+    w.widx = sr.widx;
+    w.wover = sr.wover;
+    w.ovf = sr.ovf;
+    w.acc.cnt = lane == 0 ? sr.cnt : 0;
+    w.acc.dg = lane == 0 ? sr.dg : 0;
+    w.acc.dc = lane == 0 ? sr.dc : 0;
+    w.sg.n = sr.sgn;
+    w.sg.over = sr.sgover;
+    w.first = sr.first;
+    w.open = sr.open;
+    w.c1 = sr.c1;
+    w.e1 = sr.e1;
+    w.le1 = sr.le1;
+    w.rs = sr.rs;
+    i = sr.tile;
+    const PendSlot ps = sr.lanes[lane];
+    BatchLane L{ps.c, ps.s, ps.packed & 0xffu, (ps.packed >> 8) & 0xffu, ps.le, (ps.packed >> 16) & 0xffu,
+                (ps.packed >> 24) != 0};
+    batch_finish<WRITE, STAGE>(L, lane, scr, T, C, P, w, lim, gw);
+  }
   uint4 a0, a1, a2, a3, b0, b1, b2, b3;
   {
-    const TileLoad La = wave_tile(wbase, 0, rel);
+    const TileLoad La = wave_tile(wbase, i, rel);
     a0 = stream16(La, lo16);
     a1 = stream16(La, lo16 + 1024);
     a2 = stream16(La, lo16 + 2048);
     a3 = stream16(La, lo16 + 3072);
-    const TileLoad Lb = wave_tile(wbase, 1, rel);
+    const TileLoad Lb = wave_tile(wbase, i + 1, rel);
     b0 = stream16(Lb, lo16);
     b1 = stream16(Lb, lo16 + 1024);
     b2 = stream16(Lb, lo16 + 2048);
     b3 = stream16(Lb, lo16 + 3072);
   }
   // one exit at the bottom (a mid-loop break let hipcc rotate the loop so that
-  // its header waited on the loads just issued); an odd last tile follows
-  uint32_t i = 0;
-  if (n >= 2) {
+  // its header waited on the loads just issued; a suspended wave streams the
+  // rest of its range without processing it); an odd last tile follows
+  if (n >= i + 2) {
     do {
-      tile_pass<WRITE, ABL, W, STAGE>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, i == 0 && clip_lo, wlo, whi, lane, F, T, C,
-                            P, dl, scr, w);
+      tile_pass<WRITE, ABL, W, STAGE, RESUME>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, i == 0 && clip_lo, wlo, whi,
+                                              lane, F, T, C, P, dl, scr, w, lim, gw);
       {
         const TileLoad L = wave_tile(wbase, i + 2, rel);
         a0 = stream16(L, lo16);
@@ -459,8 +798,8 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
         a2 = stream16(L, lo16 + 2048);
         a3 = stream16(L, lo16 + 3072);
       }
-      tile_pass<WRITE, ABL, W, STAGE>(b0, b1, b2, b3, wb + (uint64_t)(i + 1) * kWaveTile, i + 2 == n && clip_hi, wlo, whi,
-                            lane, F, T, C, P, dl, scr, w);
+      tile_pass<WRITE, ABL, W, STAGE, RESUME>(b0, b1, b2, b3, wb + (uint64_t)(i + 1) * kWaveTile, i + 2 == n && clip_hi,
+                                              wlo, whi, lane, F, T, C, P, dl, scr, w, lim, gw);
       {
         const TileLoad L = wave_tile(wbase, i + 3, rel);
         b0 = stream16(L, lo16);
@@ -472,13 +811,49 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
     } while (i + 1 < n);
   }
   if (i < n)  // a* holds tile i = n - 1
-    tile_pass<WRITE, ABL, W, STAGE>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, (i == 0 && clip_lo) || clip_hi, wlo, whi,
-                          lane, F, T, C, P, dl, scr, w);
-  if (w.dn) flush_deferred<WRITE, ABL, W, STAGE>(dl, scr, w.dn, lane, T, C, P, w.x, w.acc, w.widx, w.wover, w.ovf, w.sg);
+    tile_pass<WRITE, ABL, W, STAGE, RESUME>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile,
+                                            (i == 0 && clip_lo) || clip_hi, wlo, whi, lane, F, T, C, P, dl, scr, w,
+                                            lim, gw);
+  if (!w.pend && w.dn) {
+    flush_deferred<WRITE, ABL, W, STAGE, RESUME>(dl, scr, w.dn, lane, T, C, P, w, lim, gw);
+    w.ptile = te * kWaveTile;  // (no tile left to repeat)
+  }
+  if constexpr (!RESUME) {
+    if (P.susp) {
+      if (w.pend) {  // suspend: the resume launch continues from here
+        const uint64_t c = wave_sum(w.acc.cnt), d = wave_sum(w.acc.dg), dc = wave_sum(w.acc.dc);
+        if (lane == 0) {
+          SuspRec* sr = P.srec + gw;
+          sr->x = w.x;
+          sr->widx = w.widx;
+          sr->cnt = c;
+          sr->dg = d;
+          sr->dc = dc;
+          sr->c1 = w.c1;
+          sr->e1 = w.e1;
+          sr->rs = w.rs;
+          sr->sgn = w.sg.n;
+          sr->wover = w.wover;
+          sr->ovf = w.ovf;
+          sr->first = w.first;
+          sr->open = w.open;
+          sr->le1 = w.le1;
+          sr->sgover = w.sg.over;
+          sr->tile = (uint32_t)((w.ptile - wb) / kWaveTile);
+          sr->dn = 0;
+          P.susp[gw] = 1;
+        }
+        return;
+      }
+      if (lane == 0) P.susp[gw] = 0;
+    }
+  }
   uint64_t x = w.x > whi ? w.x : whi;  // chain exit: the last kept match end or the range end
   if (tb == te) x = wlo;
+  if (w.open) x = lim;  // (placeholder: fix_kernel resolves the open walk)
 
   if (w.ovf) atomicOr(P.flags, UGPU_FLAG_HALO);
+  if (!WRITE && w.open && lane == 0) atomicOr(P.flags, UGPU_FLAG_OPEN);
   if (w.wover) atomicOr(P.flags, UGPU_FLAG_CAPACITY);
   if constexpr (!WRITE) {
     const uint64_t c = wave_sum(w.acc.cnt), d = wave_sum(w.acc.dg), dc = wave_sum(w.acc.dc);
@@ -491,6 +866,11 @@ __global__ __launch_bounds__(kSpWaves * 64) void sparse_kernel(ScanParams P)
       rec.dg = d;
       rec.dc = dc;
       rec.pad0 = rec.pad1 = rec.pad2 = 0;
+      if (!W) {  // the first kept match (fix_kernel shortcuts), the open walk
+        rec.pad0 = w.c1;
+        rec.pad1 = w.first ? w.e1 : 0;
+        rec.pad2 = (uint64_t)w.le1 | (w.open ? kRecOpen : 0) | kRecFirst;
+      }
       P.recs[gw] = rec;
     }
   }
@@ -505,18 +885,31 @@ size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates)
 
 namespace {
 
-template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
-hipError_t sparse_one(const ScanParams& P, size_t smem, hipStream_t stream)
+template <bool WRITE, int ABL, bool W = false, bool STAGE = false, bool RESUME = false>
+hipError_t sparse_launch(const ScanParams& P, size_t smem, hipStream_t stream)
 {
   static size_t attr_smem = 65536;
   if (smem > attr_smem) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE, ABL, W, STAGE>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE, ABL, W, STAGE, RESUME>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_smem = smem;
   }
-  hipLaunchKernelGGL((sparse_kernel<WRITE, ABL, W, STAGE>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream, P);
+  hipLaunchKernelGGL((sparse_kernel<WRITE, ABL, W, STAGE, RESUME>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream,
+                     P);
   return hipGetLastError();
+}
+
+// The main launch, then (plain walks) the resume launch for the waves it
+// suspended at long walks.
+template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
+hipError_t sparse_one(const ScanParams& P, size_t smem, hipStream_t stream)
+{
+  hipError_t e = sparse_launch<WRITE, ABL, W, STAGE>(P, smem, stream);
+  if constexpr (!W && ABL == 0) {
+    if (e == hipSuccess && P.susp) e = sparse_launch<WRITE, 0, false, STAGE, true>(P, smem, stream);
+  }
+  return e;
 }
 
 // Single-pass OFFSETS, second half: one workgroup per staged wave record
