@@ -89,8 +89,8 @@ def cpu_baseline(cfg, sample, threads):
             out = dict(value=round(j["bytes"] / j["seconds"] / 1e9, 3), unit="GB/s", cores=threads, kind="reference",
                        build="AVX2 (-DHAVE_AVX2)",
                        sample="%d MiB of the same corpus (seed 1, bytes [0, %d)), reference libreflex Matcher::find() "
-                              "loop, newline-split across %d threads sharing one Pattern, best of 3; %d matches"
-                              % (sample >> 20, sample, threads, j["count"]),
+                              "loop, newline-split across %d threads (one GPU's share of the node's cores) sharing "
+                              "one Pattern, best of 3; %d matches" % (sample >> 20, sample, threads, j["count"]),
                        one_core={"value": round(j1["bytes"] / j1["seconds"] / 1e9, 3), "unit": "GB/s",
                                  "sample_bytes": one_sample, "best_of": 2},
                        host_cpus_visible=len(os.sched_getaffinity(0)))
@@ -398,11 +398,26 @@ def main():
         pcie = pcie_inclusive(pat, buf, min(args.pcie_sample_mib << 20, hi - lo), dev)
     cpu_leg = (None, None)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # the box's CPU share for one GPU is 16 cores (os.sched_getaffinity shows the whole machine)
-        threads = min(16, len(os.sched_getaffinity(0)))
+        # value: the reference on one GPU's share of the node's cores (the
+        # visible CPUs / 8 GPUs of an MI355X node, at least 16); also reported:
+        # the same on every visible core (os.sched_getaffinity shows the whole
+        # machine; capped at 256 threads)
+        visible = len(os.sched_getaffinity(0))
+        threads = int(os.environ.get("UGPU_BENCH_CPU_THREADS", "0")) or max(16, visible // 8)
+        threads = min(threads, visible)
         sample = min(args.cpu_sample_mib << 20, per_gpu)
-        log("cpu baseline: %d MiB, %d threads" % (sample >> 20, threads))
+        log("cpu baseline: %d MiB, %d threads (per-GPU share of %d visible CPUs)" % (sample >> 20, threads, visible))
         base, ref = cpu_baseline(args.config, sample, threads)
+        allc = min(visible, 256)
+        if base is not None and base.get("kind") == "reference" and allc > threads:
+            try:
+                pkey_, mode_, rx_, kind_, _, _ = CONFIGS[args.config]
+                ja = _harness(os.path.join(REPO, "oracle", "_ref", "ref_harness_avx2"), mode_, rx_,
+                              _spec(kind_, sample), allc, 2)
+                base["all_cores"] = {"value": round(ja["bytes"] / ja["seconds"] / 1e9, 3), "unit": "GB/s",
+                                     "cores": allc, "best_of": 2}
+            except Exception as e:  # pragma: no cover - diagnostic path
+                log("all-cores reference leg failed: %s" % e)
         chk = None
         if ref is not None and not args.word:  # the same bytes on the GPU, compared with the reference
             chk = gpu_reference_check(pat, buf, sample, ref, sptr)

@@ -129,6 +129,13 @@ int ugpu_dfa_create(const uint32_t *opc, uint32_t nop, uint32_t pattern_flags, u
 int ugpu_dfa_destroy(ugpu_dfa *dfa);
 int ugpu_dfa_info_get(const ugpu_dfa *dfa, ugpu_dfa_info *info);
 
+/* Host-only: what ugpu_dfa_create(opc, nop, pattern_flags) would return
+   (UGPU_OK, UGPU_UNSUPPORTED, UGPU_INVAL) and, on UGPU_OK, the info it would
+   report (the kernel a COUNT scan runs) -- without touching a device, so a
+   caller can decide whether a device is worth initialising (the drop-in
+   matcher decides CPU or GPU per input before any HIP call). */
+int ugpu_dfa_plan_host(const uint32_t *opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa_info *info);
+
 /* Host-only: build the dense tables without touching a device (inspection and
    CPU tests).  trans gets states*row u16 entries (entry = target_state*row,
    0 = dead), cls 256 bytes, caps `states` accept indices; *start is the start
@@ -400,6 +407,12 @@ const char *ugpu_version(void);
    the devices this way. */
 int ugpu_device_count(int *n);
 int ugpu_select_device(int dev);
+/* Initialise device dev for this process ahead of its first scan: the HIP
+   context, a scan and a records workspace (streams), a pinned block, the
+   kernels' code object -- the ~0.2-0.4 s a fresh process pays at its first
+   GPU call (tools/probe/startup_probe.cpp).  The drop-in matcher runs it on a
+   thread of its own while the CPU matcher serves the first inputs. */
+int ugpu_warmup(int dev);
 
 #ifdef __cplusplus
 }

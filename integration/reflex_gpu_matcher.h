@@ -44,11 +44,13 @@
 //     tables, 64 KiB for dense ones; a stream counts when it ends before its
 //     first feed) stay on the CPU matcher: a device round trip costs more than
 //     the reference's scan of a small buffer;
-//   * patterns with a selective prefilter (sparse_kernel, e.g. foo|bar|baz) use
-//     the GPU only while at most UGPU_ADAPTER_SPARSE_MAX (default 4) GpuMatchers
-//     per device exist: host buffers cross PCIe at ~55 GB/s per device link,
-//     which a few reference AVX2 cores match on such patterns (11 GB/s each),
-//     while dense patterns (C3/C4 class, ~0.2-2 GB/s per core) always gain;
+//   * patterns with a selective prefilter (sparse_kernel, e.g. foo|bar|baz) go
+//     through a per-device queue of UGPU_ADAPTER_SPARSE_MAX (default 2) slots:
+//     host buffers cross PCIe at ~55 GB/s per device link, which a few
+//     reference AVX2 cores match on such patterns (11 GB/s each), so an input
+//     that finds every slot taken is scanned by the CPU matcher meanwhile (with
+//     ugrep's workers the GPU and the cores scan at once); dense patterns
+//     (C3/C4 class, ~0.2-2 GB/s per core) always take the GPU;
 //   * devices: matchers are dealt round-robin over the visible devices
 //     (ugpu_select_device before every engine call), and a buffer of at least
 //     UGPU_ADAPTER_MULTI_MIN bytes (default 64 MiB) is cut over all of them
@@ -62,18 +64,26 @@
 // anchored tables stay on the CPU: there the reference's match predictor
 // (lib/pattern.cpp:4342-4430) can skip positions its DFA matches at -- ugrep -c
 // 'a$|ab' prints 0 on "xa\nb\nzzzz\n", and '^\w+' without N finds nothing --
-// and the GPU walks the DFA (tests/test_anchor.py records both).  Everything
-// else -- SCAN/SPLIT/MATCH, option A, tables the engine rejects (\b,
-// lookahead, W with anchors or N: UGPU_UNSUPPORTED) -- stays on the CPU matcher.
+// and the GPU walks the DFA (tests/test_anchor.py records both).
+//
+// SCAN and MATCH (scan(), matches()) on whole buffers come from the same FIND
+// records: the longest match at the cursor is the FIND record that starts
+// there, if any (MATCH's empty match goes to the CPU matcher).  Everything
+// else -- SPLIT, option A, streamed SCAN/MATCH, tables the engine rejects
+// (lookahead, W with anchors or N: UGPU_UNSUPPORTED) -- stays on the CPU
+// matcher.
 #ifndef REFLEX_GPU_MATCHER_H
 #define REFLEX_GPU_MATCHER_H
 
 #include <atomic>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include <poll.h>
 
@@ -92,17 +102,16 @@ class GpuMatcher : public Matcher {
       : Matcher(pattern, input, opt)
   {
     init_policy();
-    dev_ = next_device();
     ++live();
   }
   /// Clones (ugrep's worker threads, src/ugrep.cpp:4146, :9006) share the
   /// device tables; per-input state starts empty.
   GpuMatcher(const GpuMatcher& m)
       : Matcher(m), tab_(m.tab_), tab_pat_(m.tab_pat_), tab_w_(m.tab_w_), tab_n_(m.tab_n_),
-        tab_anchor_(m.tab_anchor_), sparse_(m.sparse_),
-        min_bytes_(m.min_bytes_), chunk_(m.chunk_), multi_min_(m.multi_min_), sparse_max_(m.sparse_max_)
+        tab_anchor_(m.tab_anchor_), tab_ok_(m.tab_ok_), sparse_(m.sparse_),
+        min_bytes_(m.min_bytes_), chunk_(m.chunk_), multi_min_(m.multi_min_), sparse_max_(m.sparse_max_),
+        warm_async_(m.warm_async_)
   {
-    dev_ = next_device();
     ++live();
   }
   virtual GpuMatcher* clone() { return new GpuMatcher(*this); }
@@ -118,7 +127,7 @@ class GpuMatcher : public Matcher {
         if (cpu_why_[r] != 0)
           why += std::string(why.empty() ? "" : ",") + reason_name(r) + ":" + std::to_string(cpu_why_[r]);
       std::fprintf(stderr, "[ugpu-adapter] scans=%zu gpu_finds=%zu cpu_finds=%zu table=%s cpu_why=%s\n", scans_,
-                   gpu_finds_, cpu_finds(), tab_pat_ == NULL ? "none" : tab_ ? "gpu" : "unsupported",
+                   gpu_finds_, cpu_finds(), tab_pat_ == NULL ? "none" : tab_ok_ ? "gpu" : "unsupported",
                    why.empty() ? "-" : why.c_str());
     }
     src_.clear();
@@ -126,6 +135,7 @@ class GpuMatcher : public Matcher {
     if (gst_ != NULL)
       on_device();
     ugpu_stream_destroy(gst_);
+    release_slot();
     --live();
   }
   /// New input (input() calls this, absmatcher.h:533-540) or options.
@@ -133,11 +143,14 @@ class GpuMatcher : public Matcher {
   {
     Matcher::reset(opt);
     drop_records();
+    release_slot();
     if (gst_ != NULL)
       on_device();
     ugpu_stream_destroy(gst_);
     gst_ = NULL;
     cpu_stream_ = false;
+    sopen_ = false;
+    sfit_ = false;
   }
 
   /// GPU scans (whole-buffer scans and stream feeds) issued so far (tests).
@@ -151,30 +164,46 @@ class GpuMatcher : public Matcher {
       n += cpu_why_[r];
     return n;
   }
-  /// Whether the engine supports this pattern (builds the tables if needed).
+  /// Whether the engine supports this pattern (builds the device tables if
+  /// needed).
   bool gpu_ready() { return tables() != NULL; }
   /// Smallest input sent to the GPU (0: every input).
   void gpu_min_bytes(size_t n) { min_bytes_ = n; }
-  /// Prefiltered (sparse) patterns use the GPU while at most n GpuMatchers exist.
+  /// Prefiltered (sparse) patterns: at most n GPU scans per device at once (the
+  /// device queue; an input that finds every slot taken is scanned on the CPU).
   void gpu_sparse_max(int n) { sparse_max_ = n; }
 
  protected:
   virtual size_t match(Method method)
   {
-    if (method != Const::FIND)
+    // FIND, and SCAN / MATCH on whole buffers, come from the engine's FIND
+    // records; SPLIT stays on the CPU matcher
+    if (method == Const::SPLIT)
       return cpu(method, R_METHOD);
     if (opt_.A)
       return cpu(method, R_OPT_A);
-    if (tables() == NULL)
+    // (decided on the host: a device is initialised at the first input the
+    // policy sends to the GPU, never for runs the CPU matcher serves)
+    if (!eligible())
       return cpu(method, tab_anchor_ ? R_ANCHOR : R_TABLE);
-    if (sparse_ && live() > sparse_max_ * devices())
-      return cpu(method, R_SPARSE);
     if (own_)
+    {
+      if (method != Const::FIND)
+        return cpu(method, R_METHOD);
+      if (sfit_ && !device_ready())
+        return cpu(method, warm_reason());
+      if (sparse_ && sfit_ && !device_slot())
+        return cpu(method, R_SPARSE);
       return stream_match();
+    }
     if (!eof_)
       return cpu(method, R_PARTIAL);
     if (end_ < min_bytes())
       return cpu(method, R_SMALL);
+    if (!device_ready())
+      return cpu(method, warm_reason());
+    if (sparse_ && !device_slot())
+      return cpu(method, R_SPARSE);
     reset_text();
     // buffer() is non-virtual and rewinds cur_ without telling this class
     // (absmatcher.h:542-591), and the caller may hand over new bytes at the
@@ -191,7 +220,31 @@ class GpuMatcher : public Matcher {
       src_.pop();
     if (src_.err)
       return engine_failed(method);
-    ++gpu_finds_;
+    if (method != Const::FIND)
+    {
+      // SCAN and MATCH try the longest match at the cursor only
+      // (lib/matcher.cpp:125-546 without adv_, nul = MATCH).  The cursor is a
+      // position of the records' FIND chain (it is not inside a record), and
+      // a FIND record starting there is the longest non-empty match there;
+      // none means there is no non-empty match at the cursor
+      const bool here = src_.have && src_.start == cur_ && src_.len > 0;
+      if (!here && method == Const::MATCH)
+        return cpu(method, R_METHOD);  // (the empty match MATCH accepts: the table's start state decides)
+      ++gpu_finds_;
+      if (!here)
+      {
+        // no match: the scan stops at the cursor (:673-679, :694-724)
+        set_current(cur_);
+        txt_ = buf_ + cur_;
+        len_ = 0;
+        gcur_ = cur_;
+        return cap_ = 0;
+      }
+    }
+    else
+    {
+      ++gpu_finds_;
+    }
     if (!src_.have)
       return exhausted();
     const size_t start = static_cast<size_t>(src_.start), len = src_.len, cap = src_.cap;
@@ -201,11 +254,11 @@ class GpuMatcher : public Matcher {
 
  private:
   // why the CPU matcher answered a call (adapter statistics)
-  enum Reason { R_METHOD, R_OPT_A, R_ANCHOR, R_TABLE, R_SPARSE, R_PARTIAL, R_SMALL, R_ENGINE, kReasons };
+  enum Reason { R_METHOD, R_OPT_A, R_ANCHOR, R_TABLE, R_SPARSE, R_PARTIAL, R_SMALL, R_ENGINE, R_WARMUP, R_COLD, kReasons };
   static const char* reason_name(int r)
   {
-    static const char* const n[kReasons] = {"method",  "option_A", "anchor_predictor", "table",
-                                            "sparse_limit", "partial",  "small",            "engine"};
+    static const char* const n[kReasons] = {"method",  "option_A", "anchor_predictor", "table", "sparse_limit",
+                                            "partial", "small",    "engine",           "warmup", "cold"};
     return n[r];
   }
   size_t cpu(Method method, int why)
@@ -213,10 +266,21 @@ class GpuMatcher : public Matcher {
     ++cpu_why_[why];
     return Matcher::match(method);
   }
-  // device tables of (pattern, option W, option N), shared with clones; NULL
-  // when the engine does not support the pattern or its anchors are left to the
-  // reference's predictor (tab_anchor_)
-  const ugpu_dfa* tables()
+  // The engine's tables of (pattern, option W, option N), shared with clones:
+  // the opcode words and flags, and the device tables uploaded at the first
+  // GPU scan (failed: the upload failed, the inputs stay on the CPU matcher)
+  struct Tables {
+    std::vector<uint32_t> opc;
+    uint32_t flags = 0;
+    std::mutex mu;
+    ugpu_dfa* d = NULL;
+    bool failed = false;
+    ~Tables() { ugpu_dfa_destroy(d); }
+  };
+  // whether the engine takes the table (false: unsupported, or anchors left to
+  // the reference's predictor, tab_anchor_), and whether it is prefiltered --
+  // all on the host (ugpu_dfa_plan_host), no HIP call
+  bool eligible()
   {
     if (!tab_pat_ || tab_pat_ != pat_ || tab_w_ != opt_.W || tab_n_ != opt_.N)
     {
@@ -225,41 +289,134 @@ class GpuMatcher : public Matcher {
       tab_w_ = opt_.W;
       tab_n_ = opt_.N;
       tab_anchor_ = false;
+      tab_ok_ = false;
+      sparse_ = false;
       if (pat_ != NULL)
       {
         const std::string rx = (*pat_)[0];
         uint32_t* opc = NULL;
         uint32_t nop = 0;
-        ugpu_dfa* d = NULL;
         if (ugpu_compile(rx.data(), rx.size(), UGPU_RX_REFLEX, &opc, &nop) == UGPU_OK)
         {
           int anchored = 0;
+          const uint32_t flags = (opt_.W ? UGPU_PAT_WORD : 0u) | (opt_.N ? UGPU_PAT_EMPTY : 0u);
+          ugpu_dfa_info info;
           if (ugpu_tables_context_host(opc, nop, NULL, 0, &anchored, NULL) == UGPU_OK && anchored &&
               !(opt_.N && anchors_outer(rx)))
+          {
             tab_anchor_ = true;
-          else if (ugpu_dfa_create(opc, nop, (opt_.W ? UGPU_PAT_WORD : 0u) | (opt_.N ? UGPU_PAT_EMPTY : 0u), &d) !=
-                   UGPU_OK)
-            d = NULL;
+          }
+          else if (ugpu_dfa_plan_host(opc, nop, flags, &info) == UGPU_OK)
+          {
+            tab_ok_ = true;
+            sparse_ = info.kernel == 0;
+            tab_ = std::make_shared<Tables>();
+            tab_->opc.assign(opc, opc + nop);
+            tab_->flags = flags;
+          }
           ugpu_opc_free(opc);
         }
         if (tab_anchor_)
           tab_err_ = "line anchors without option N or inside the regex (the reference's predictor decides there)";
-        else if (d == NULL)
+        else if (!tab_ok_)
           tab_err_ = ugpu_last_error();
         const char* dump = std::getenv("UGPU_ADAPTER_DUMP");
         if (dump != NULL && *dump == '1')
-          std::fprintf(stderr, "[ugpu-adapter] regex=%s tables=%s%s\n", rx.c_str(), d ? "gpu" : "unsupported: ",
-                       d ? "" : tab_err_.c_str());
-        if (d != NULL)
-        {
-          tab_.reset(d, ugpu_dfa_destroy);
-          ugpu_dfa_info info;
-          sparse_ = ugpu_dfa_info_get(d, &info) == UGPU_OK && info.kernel == 0;
-
-        }
+          std::fprintf(stderr, "[ugpu-adapter] regex=%s tables=%s%s\n", rx.c_str(), tab_ok_ ? "gpu" : "unsupported: ",
+                       tab_ok_ ? "" : tab_err_.c_str());
       }
     }
-    return tab_.get();
+    return tab_ok_;
+  }
+  // Device warm-up, once per process.  A fresh process pays ~0.2-0.4 s at its
+  // first GPU call (HIP context, queues, pinned memory, code object:
+  // ugpu_warmup, tools/probe/startup_probe.cpp); the first input the policy
+  // sends to the GPU starts it on a thread of its own and the CPU matcher
+  // answers (reason "warmup") until the devices are ready -- inputs then move
+  // to the GPU at their cursor, as after a device queue slot frees up.
+  // UGPU_ADAPTER_WARM=0: warm up on the calling thread (the first GPU input
+  // waits; tests that count GPU answers use it).  The thread is joined at exit.
+  // Prefiltered tables do not start an asynchronous warm-up (reason "cold"):
+  // on host buffers their GPU scans are PCIe-bound, ugrep's workers scan them
+  // faster on their cores (tools/bench_ugrep.py: C2 at ~100 GB/s on 16
+  // workers), and a run that ends before the warm-up would wait for it at
+  // exit; they take the GPU once a dense table has warmed it.
+  struct Warm {
+    std::mutex mu;
+    std::thread th;
+    std::atomic<int> state{0};  // 0 not started, 1 warming, 2 ready, 3 failed
+    ~Warm()
+    {
+      if (th.joinable())
+        th.join();
+    }
+  };
+  static Warm& warm()
+  {
+    static Warm w;
+    return w;
+  }
+  static void run_warm(Warm* w)
+  {
+    bool ok = true;
+    for (int d = 0; d < devices(); ++d)
+      ok = ugpu_warmup(d) == UGPU_OK && ok;
+    w->state.store(ok ? 2 : 3, std::memory_order_release);
+  }
+  bool device_ready()
+  {
+    Warm& w = warm();
+    int st = w.state.load(std::memory_order_acquire);
+    if (st == 0 && !(sparse_ && warm_async_))
+    {
+      std::lock_guard<std::mutex> lk(w.mu);
+      if (w.state.load(std::memory_order_acquire) == 0)
+      {
+        w.state.store(1, std::memory_order_release);
+        bool async = warm_async_;
+        if (async)
+        {
+          try
+          {
+            w.th = std::thread(run_warm, &w);
+          }
+          catch (...)
+          {
+            async = false;
+          }
+        }
+        if (!async)
+          run_warm(&w);
+      }
+      st = w.state.load(std::memory_order_acquire);
+    }
+    return st == 2;
+  }
+  static int warm_reason()
+  {
+    const int st = warm().state.load(std::memory_order_acquire);
+    return st == 3 ? R_ENGINE : st == 0 ? R_COLD : R_WARMUP;
+  }
+  // the device tables (uploaded on this matcher's device at the first call;
+  // the engine copies them to other devices itself); NULL: not eligible, or
+  // the upload failed
+  const ugpu_dfa* tables()
+  {
+    if (!eligible())
+      return NULL;
+    std::lock_guard<std::mutex> lk(tab_->mu);
+    if (tab_->d == NULL && !tab_->failed)
+    {
+      on_device();
+      if (ugpu_dfa_create(tab_->opc.data(), static_cast<uint32_t>(tab_->opc.size()), tab_->flags, &tab_->d) !=
+          UGPU_OK)
+      {
+        tab_->d = NULL;
+        tab_->failed = true;
+        tab_err_ = ugpu_last_error();
+      }
+    }
+    return tab_->d;
   }
   // the regex's line anchors are at most a leading ^ (after the (?m...) prefix
   // ugrep puts first, src/ugrep.cpp:8586-8604) and a trailing $: ^ and $ in
@@ -323,6 +480,55 @@ class GpuMatcher : public Matcher {
     static std::atomic<int> n(0);
     return n;
   }
+  // The device queue for prefiltered tables.  Their GPU scans of host buffers
+  // are bound by the PCIe link (~55 GB/s per device), which a few reference
+  // AVX2 cores match, so each device runs at most sparse_max_ of them at once
+  // and an input that finds no free slot is scanned by the CPU matcher: with
+  // ugrep's 16 workers on one device, 2 workers feed the GPU and the others
+  // scan on their cores, all at once.  A slot is held from the scan of an
+  // input to its last record (or a reset / new input).  Dense tables gain
+  // 100-200x per matcher and always take the GPU.
+  struct DevQueue {
+    std::mutex mu;
+    int busy = 0;
+  };
+  static DevQueue& queue(int dev)
+  {
+    static DevQueue q[64];
+    return q[dev & 63];
+  }
+  bool device_slot()
+  {
+    if (slot_)
+      return true;
+    // the decision holds for the rest of the input (a cursor that moves back
+    // means new bytes: decide again)
+    if (!own_ && slot_buf_ == buf_ && slot_end_ == end_ && cur_ >= slot_cur_)
+    {
+      slot_cur_ = cur_;
+      return false;
+    }
+    slot_buf_ = buf_;
+    slot_end_ = end_;
+    slot_cur_ = cur_;
+    DevQueue& q = queue(dev());
+    std::lock_guard<std::mutex> lk(q.mu);
+    if (q.busy >= sparse_max_)
+      return false;
+    ++q.busy;
+    slot_ = true;
+    return true;
+  }
+  void release_slot()
+  {
+    if (!slot_)
+      return;
+    DevQueue& q = queue(dev());
+    std::lock_guard<std::mutex> lk(q.mu);
+    --q.busy;
+    slot_ = false;
+    slot_buf_ = NULL;
+  }
   // visible devices (at least 1), and the next matcher's device
   static int devices()
   {
@@ -337,9 +543,17 @@ class GpuMatcher : public Matcher {
     static std::atomic<int> k(0);
     return k++ % devices();
   }
+  // this matcher's device, assigned round-robin at its first GPU input (the
+  // first HIP call of the process is there)
+  int dev()
+  {
+    if (dev_ < 0)
+      dev_ = next_device();
+    return dev_;
+  }
   // this matcher's device current on the calling thread (ugrep calls a matcher
   // from the worker thread that owns it, but clones are made elsewhere)
-  void on_device() const { (void)ugpu_select_device(dev_); }
+  void on_device() { (void)ugpu_select_device(dev()); }
   void drop_records()
   {
     ugpu_result_free(gres_);
@@ -360,6 +574,7 @@ class GpuMatcher : public Matcher {
   }
   size_t exhausted()
   {
+    release_slot();  // (the input's records are all popped)
     set_current(end_);
     txt_ = buf_ + end_;
     len_ = 0;
@@ -371,9 +586,11 @@ class GpuMatcher : public Matcher {
     const char* e = std::getenv("UGPU_ADAPTER_MIN_BYTES");
     min_bytes_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : ~static_cast<size_t>(0);  // ~0: per table
     e = std::getenv("UGPU_ADAPTER_SPARSE_MAX");
-    sparse_max_ = e && *e ? std::atoi(e) : 4;
+    sparse_max_ = e && *e ? std::atoi(e) : 2;  // device queue slots for prefiltered tables
     e = std::getenv("UGPU_ADAPTER_MULTI_MIN");
     multi_min_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (64u << 20);
+    e = std::getenv("UGPU_ADAPTER_WARM");
+    warm_async_ = !(e && *e == '0');
     e = std::getenv("UGPU_ADAPTER_CHUNK");
     chunk_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (8u << 20);
     if (chunk_ == 0)
@@ -401,17 +618,20 @@ class GpuMatcher : public Matcher {
   {
     drop_records();
     on_device();
+    const ugpu_dfa* t = tables();
+    if (t == NULL)
+      return false;
     const uint8_t* b = reinterpret_cast<const uint8_t*>(buf_);
     int rc;
     if (devices() > 1 && end_ - cur_ >= multi_min_) {
-      rc = ugpu_find_all_multi(tables(), b, end_, cur_, UGPU_MODE_OFFSETS, 0, &gres_);
+      rc = ugpu_find_all_multi(t, b, end_, cur_, UGPU_MODE_OFFSETS, 0, &gres_);
       if (rc == UGPU_OK)
         src_.set(gres_);
     } else {
       // the pipelined host path: records popped from pinned memory as find()
       // asks for them (ugpu_find_records)
       ugpu_records* r = NULL;
-      rc = ugpu_find_records(tables(), b, end_, cur_, &r);
+      rc = ugpu_find_records(t, b, end_, cur_, &r);
       if (rc == UGPU_OK)
         src_.set(r);
     }
@@ -434,9 +654,8 @@ class GpuMatcher : public Matcher {
     reset_text();
     txt_ = buf_ + cur_;  // bytes before the cursor may be shifted out (as lib/matcher.cpp:51)
     const uint64_t at = static_cast<uint64_t>(num_ + cur_);
-    if (gst_ == NULL || at < gcur_abs_ || at > sfed_ || stream_inside(at))
-      if (!stream_restart(at))
-        return cpu(Const::FIND, cpu_stream_why_);
+    if (!sopen_ || at < gcur_abs_ || at > sfed_ || stream_inside(at))
+      stream_restart(at);
     ++gpu_finds_;
     for (;;)
     {
@@ -489,10 +708,40 @@ class GpuMatcher : public Matcher {
         // a small input, all of it read before any feed: the CPU matcher is faster
         cpu_stream_ = true;
         cpu_stream_why_ = R_SMALL;
+        if (gst_ != NULL)
+          on_device();
         ugpu_stream_destroy(gst_);
         gst_ = NULL;
         --gpu_finds_;
         return cpu(Const::FIND, R_SMALL);
+      }
+      if (gst_ == NULL)
+      {
+        // the first feed of this stream: a prefiltered table takes a device
+        // queue slot first (none free: the CPU matcher goes on from the
+        // cursor, and the stream restarts there once a slot frees up), then
+        // the device tables and the stream
+        sfit_ = true;
+        if (!device_ready())
+        {
+          --gpu_finds_;
+          return cpu(Const::FIND, warm_reason());
+        }
+        if (sparse_ && !device_slot())
+        {
+          --gpu_finds_;
+          return cpu(Const::FIND, R_SPARSE);
+        }
+        on_device();
+        const ugpu_dfa* t = tables();
+        if (t == NULL || ugpu_stream_create(t, 0, &gst_) != UGPU_OK)
+        {
+          gst_ = NULL;
+          cpu_stream_ = true;
+          cpu_stream_why_ = R_ENGINE;
+          --gpu_finds_;
+          return cpu(Const::FIND, R_ENGINE);
+        }
       }
       const size_t from = static_cast<size_t>(sfed_ - num_);
       drop_records();
@@ -541,24 +790,20 @@ class GpuMatcher : public Matcher {
     }
     return false;
   }
-  bool stream_restart(uint64_t at)
+  // a new stream from absolute offset at (created at its first feed)
+  void stream_restart(uint64_t at)
   {
     drop_records();
+    if (gst_ != NULL)
+      on_device();
     ugpu_stream_destroy(gst_);
     gst_ = NULL;
-    on_device();
-    if (ugpu_stream_create(tables(), 0, &gst_) != UGPU_OK)
-    {
-      cpu_stream_ = true;
-      cpu_stream_why_ = R_ENGINE;
-      return false;
-    }
+    sopen_ = true;
     sbase_ = at;
     sfed_ = at;
     sdone_ = false;
     gcur_abs_ = at;
     scans_at_restart_ = scans_;
-    return true;
   }
 
   // the records of a whole-buffer scan, popped in chain order: a
@@ -612,10 +857,11 @@ class GpuMatcher : public Matcher {
     }
   };
   Source src_;
-  std::shared_ptr<ugpu_dfa> tab_;
+  std::shared_ptr<Tables> tab_;
   const Pattern* tab_pat_ = NULL;
   bool tab_w_ = false, tab_n_ = false;
   bool tab_anchor_ = false;  // anchored table left to the CPU matcher (see anchors_outer)
+  bool tab_ok_ = false;      // the engine takes the table (eligible())
   bool sparse_ = false;  // the table has a selective prefilter (sparse_kernel)
   ugpu_result* gres_ = NULL;
   const char* gbuf_ = NULL;
@@ -624,12 +870,18 @@ class GpuMatcher : public Matcher {
   // gcur_: the cursor this class left behind (after the scan or the last hit)
   size_t gend_ = 0, gcur_ = 0, gi_ = 0, scans_ = 0, scans_at_restart_ = 0;
   size_t min_bytes_ = 0, chunk_ = 0, multi_min_ = 0;
-  int dev_ = 0;  // this matcher's device
+  int dev_ = -1;  // this matcher's device (dev(): assigned at the first GPU input)
   int sparse_max_ = 4;
+  bool warm_async_ = true;  // device warm-up on its own thread (UGPU_ADAPTER_WARM)
   ugpu_stream* gst_ = NULL;
   uint64_t sbase_ = 0, sfed_ = 0, gcur_abs_ = 0;
   bool sdone_ = false, cpu_stream_ = false;
+  bool sopen_ = false;  // a stream was started for this input (its ugpu_stream at the first feed)
+  bool sfit_ = false;   // this input passed the small-input test (device queue decisions from here)
   int cpu_stream_why_ = R_ENGINE;
+  bool slot_ = false;  // this matcher holds a device queue slot (prefiltered tables)
+  const char* slot_buf_ = NULL;  // the input the last slot decision was for
+  size_t slot_end_ = 0, slot_cur_ = 0;
   std::string tab_err_;  // why the engine rejected the table (ugpu_last_error)
   size_t gpu_finds_ = 0;
   size_t cpu_why_[kReasons] = {};

@@ -112,11 +112,40 @@ struct Hit {
 // loop kind: 0 plain, 1 skip('\n') after each hit, 2 skip(' ') after every other
 // hit, 3 plain loop, then new bytes at the same address and size handed over
 // with buffer() and a second plain loop (ugrep re-buffers one reused std::string
-// per line, src/ugrep.cpp:733-740; buffer() is non-virtual, absmatcher.h:542)
+// per line, src/ugrep.cpp:733-740; buffer() is non-virtual, absmatcher.h:542);
+// 4, 5: kinds 0, 1 on a stream; 6: a tokenizer loop, scan() until it fails,
+// then input() past one byte (the position of each failure recorded as a hit
+// of size 0, accept 0); 7: matches() of the whole buffer
+static bool buffer_kind(int kind) { return kind < 4 || kind >= 6; }
+
 template <class M>
 static std::vector<Hit> run(M& m, std::vector<char>& buf, int kind, bool& at_end)
 {
   std::vector<Hit> out;
+  if (kind == 6)
+  {
+    m.buffer(buf.data(), buf.size());
+    for (;;)
+    {
+      while (m.scan())
+        out.push_back(Hit{m.first(), m.size(), m.accept(), m.lineno(), m.columno()});
+      if (m.at_end())
+        break;
+      out.push_back(Hit{m.first(), 0, 0, m.lineno(), m.columno()});
+      if (m.input() == EOF)
+        break;
+    }
+    at_end = m.at_end();
+    return out;
+  }
+  if (kind == 7)
+  {
+    m.buffer(buf.data(), buf.size());
+    const size_t r = m.matches();
+    out.push_back(Hit{r, r ? m.size() : 0, m.accept(), 0, 0});
+    at_end = m.at_end();
+    return out;
+  }
   for (int pass = 0; pass < (kind == 3 ? 2 : 1); ++pass)
   {
     if (kind < 4)
@@ -190,6 +219,7 @@ int main(int argc, char** argv)
     return 2;
   }
   setenv("UGPU_ADAPTER_CHUNK", "100000", 0);  // many stream feeds per input
+  setenv("UGPU_ADAPTER_WARM", "0", 0);         // the first GPU input waits for the device (no CPU answers meanwhile)
   std::ifstream spec(argv[1]);
   std::string line;
   int bad = 0, n = 0;
@@ -208,11 +238,11 @@ int main(int argc, char** argv)
     reflex::Pattern pat(build_regex(mode, rx), "r");
     std::vector<char> a = load_input(in), b = a;
     const std::string text(a.data(), a.size() - 1);  // (stream input: no NUL)
-    for (int kind = 0; kind < 6; ++kind)
+    for (int kind = 0; kind < 8; ++kind)
     {
       std::istringstream sa(text), sb(text);
-      reflex::Matcher cpu(pat, kind < 4 ? reflex::Input() : reflex::Input(sa), opt);
-      reflex::GpuMatcher gpu(pat, kind < 4 ? reflex::Input() : reflex::Input(sb), opt);
+      reflex::Matcher cpu(pat, buffer_kind(kind) ? reflex::Input() : reflex::Input(sa), opt);
+      reflex::GpuMatcher gpu(pat, buffer_kind(kind) ? reflex::Input() : reflex::Input(sb), opt);
       gpu.gpu_min_bytes(0);  // parity on every size and pattern (the dispatch policy is measured separately)
       gpu.gpu_sparse_max(1 << 30);
       const bool ready = gpu.gpu_ready();
@@ -235,7 +265,7 @@ int main(int argc, char** argv)
       }
       // the GPU path must actually have served supported tables (option W on
       // streams stays on the CPU by design)
-      if (ready && gpu.gpu_scans() == 0 && !ra.empty() && !(word && kind >= 4))
+      if (ready && gpu.gpu_scans() == 0 && !ra.empty() && !(word && kind >= 4 && kind <= 5))
       {
         printf("FAIL gpu matcher fell back to the CPU for /%s/ kind=%d\n", rx.c_str(), kind);
         ++bad;

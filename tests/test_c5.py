@@ -154,17 +154,16 @@ def test_dense_shards_arbitrary_cuts(U, patterns, streams, name):
 
 
 def test_scan_shard_grows_the_halo(U):
-    """A match longer than the halo (a 3 MiB run of letters across the end of
-    a 4 MiB shard of digits, halo 64 KiB): dist.scan_shard grows the halo until
-    the match ends inside it, and the shard's record is that one match.  (A
-    dense table: a prefiltered one with a long run of candidates is the
-    sparse kernel's slow case)"""
+    """A match longer than the halo (a 3 MiB run of `a` across the end of a
+    4 MiB shard of digits, halo 64 KiB): dist.scan_shard grows the halo until
+    the match ends inside it, and the shard's record is that one match.  Both
+    a prefiltered table (`a+`: sparse_kernel, its long walk continued by the
+    whole wave) and a dense one (`[a-z]+`: xc_kernel)."""
     from ugrep_amd.dist import scan_shard
     n = 8 << 20
     host = np.frombuffer(b"12 " * (n // 3 + 1), np.uint8)[:n].copy()
     host[3 << 20:6 << 20] = ord("a")
     whole = torch.from_numpy(host).to("cuda")
-    pat = U.Pattern(U.compile_regex("[a-z]+"))
 
     def fetch(a, z):
         t = torch.zeros(z - a + 16, dtype=torch.uint8, device="cuda")
@@ -172,13 +171,16 @@ def test_scan_shard_grows_the_halo(U):
         torch.cuda.synchronize()
         return t
 
-    sc = U.Scanner(pat)
-    rec, buf, rend = scan_shard(sc, fetch, 0, 4 << 20, n, halo=64 << 10, stream=_stream())
-    assert rend > 6 << 20  # (grown from 64 KiB past the end of the run; the exit must lie before it)
-    # the one match of the shard: (3 MiB, 3 MiB, accept 1)
-    s0 = 3 << 20
-    assert (rec["count"], rec["digest"], rec["dcap"]) == (1, 31 * s0 + s0, s0 + 1)
-    assert rec["exit"] == 6 << 20
+    for rx, kernel in (("a+", 0), ("[a-z]+", 5)):
+        pat = U.Pattern(U.compile_regex(rx))
+        assert pat.info()["kernel"] == kernel, rx
+        sc = U.Scanner(pat)
+        rec, buf, rend = scan_shard(sc, fetch, 0, 4 << 20, n, halo=64 << 10, stream=_stream())
+        assert rend > 6 << 20  # (grown from 64 KiB past the end of the run; the exit must lie before it)
+        # the one match of the shard: (3 MiB, 3 MiB, accept 1)
+        s0 = 3 << 20
+        assert (rec["count"], rec["digest"], rec["dcap"]) == (1, 31 * s0 + s0, s0 + 1), rx
+        assert rec["exit"] == 6 << 20, rx
 
 
 @pytest.mark.gpu

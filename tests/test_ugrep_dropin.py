@@ -10,9 +10,9 @@ reference's own golden file tests/out/*.out (tests/golden/verify_cases.json,
 tools/gen_verify_golden.py; inputs copied to tests/golden/verify/).
 
 CPU test: the reference build oracle/_ref/ugrep reproduces every golden (pins
-the harness).  GPU test: ugrep_gpu with UGPU_ADAPTER_MIN_BYTES=0 and no sparse
-limit (every input on the GPU, the suite's files are tiny) reproduces them too, and the engine
-really served the FIND calls (adapter statistics on stderr)."""
+the harness).  GPU test: ugrep_gpu with UGPU_ADAPTER_MIN_BYTES=0 (every input on the GPU,
+the suite's files are tiny) and the default device queue reproduces them too,
+and the engine really served the FIND calls (adapter statistics on stderr)."""
 import hashlib
 import json
 import os
@@ -63,8 +63,12 @@ def _run_all(exe, env, workers=8):
 
 # CPU answers that are by design: line anchors the reference's match predictor
 # decides (anchored tables without option N or with anchors inside the regex:
-# tests/test_anchor.py)
-BY_DESIGN = {"anchor_predictor"}
+# tests/test_anchor.py), and inputs of prefiltered tables that found the
+# device queue's slots taken, or that came while the devices warmed up (the
+# CPU matcher scans them meanwhile; both are timing, so these reasons are left
+# out of the ledger)
+BY_DESIGN = {"anchor_predictor", "sparse_limit", "warmup", "cold"}
+TIMING = {"sparse_limit", "warmup", "cold"}
 LEDGER = os.path.join(ROOT, "tests", "golden", "dropin_fallbacks.json")
 
 
@@ -86,11 +90,34 @@ def test_fallback_ledger_is_consistent():
     if not os.path.exists(LEDGER):
         pytest.skip("no ledger yet")
     led = json.load(open(LEDGER))
-    known = {"method", "option_A", "anchor_predictor", "table", "sparse_limit", "partial", "small", "engine"}
+    known = {"method", "option_A", "anchor_predictor", "table", "sparse_limit", "partial", "small", "engine", "warmup", "cold"}
     expects = {c["expect"] for c in SPEC["cases"]}
     for e, why in led["cpu_cases"].items():
         assert e in expects, e
         assert why and set(why) <= known, (e, why)
+
+
+def test_dropin_default_policy_never_touches_a_device():
+    """ugrep_gpu with the adapter's default policy on the suite's small inputs:
+    the CPU matcher answers (reason "small"), decided on the host -- the
+    tables are planned by ugpu_dfa_plan_host, no HIP call is made, so this runs
+    in a container without a GPU and no FIND call falls back for "engine"."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")
+    if not os.path.exists(exe):
+        pytest.skip("ugrep_gpu not built (make -C oracle ref, build container)")
+    env = dict(os.environ, UGPU_ADAPTER_STATS="1")
+    for k in ("UGPU_ADAPTER_MIN_BYTES", "UGPU_ADAPTER_SPARSE_MAX"):
+        env.pop(k, None)
+    bad, ledger = _run_all(exe, env)
+    assert not bad, bad[:5]
+    why = {}
+    for c in ledger:
+        for m in c["matchers"]:
+            assert m["scans"] == 0, (c["expect"], m)
+            for k in m["why"]:
+                why[k] = why.get(k, 0) + 1
+    assert "engine" not in why, why
+    assert why.get("small", 0) > 100, why
 
 
 @pytest.mark.gpu
@@ -98,7 +125,12 @@ def test_dropin_ugrep_reproduces_goldens():
     exe = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")
     if not os.path.exists(exe):
         pytest.skip("ugrep_gpu not built (make -C oracle ref, build container)")
-    env = dict(os.environ, UGPU_ADAPTER_MIN_BYTES="0", UGPU_ADAPTER_SPARSE_MAX="1000000", UGPU_ADAPTER_STATS="1")
+    # every input on the GPU (the suite's files are tiny), the device queue
+    # at its default size; the first GPU input waits for the device warm-up
+    # (by default the CPU matcher answers meanwhile, and these inputs would be
+    # done before the device is)
+    env = dict(os.environ, UGPU_ADAPTER_MIN_BYTES="0", UGPU_ADAPTER_STATS="1", UGPU_ADAPTER_WARM="0")
+    env.pop("UGPU_ADAPTER_SPARSE_MAX", None)
     bad, ledger = _run_all(exe, env)
     assert not bad, bad[:5]
     # attribution: per case, which FIND calls the GPU answered and why the CPU
@@ -108,7 +140,8 @@ def test_dropin_ugrep_reproduces_goldens():
         why = {}
         for m in c["matchers"]:
             for k, v in m["why"].items():
-                why[k] = why.get(k, 0) + v
+                if k not in TIMING:
+                    why[k] = why.get(k, 0) + v
             # a table the engine accepted: every FIND call not excluded by design ran on the GPU
             if m["table"] == "gpu" and set(m["why"]) - BY_DESIGN:
                 leaks.append((c["expect"], m))

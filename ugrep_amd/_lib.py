@@ -70,6 +70,7 @@ def _load():
         "ugpu_dfa_create": (ctypes.c_int, [c_u32p, ctypes.c_uint32, ctypes.c_uint32, P(V)]),
         "ugpu_dfa_destroy": (ctypes.c_int, [V]),
         "ugpu_dfa_info_get": (ctypes.c_int, [V, P(DfaInfo)]),
+        "ugpu_dfa_plan_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, ctypes.c_uint32, P(DfaInfo)]),
         "ugpu_tables_build_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, P(DfaInfo), c_u16p, ctypes.c_uint32,
                                                   c_u8p, c_u32p, ctypes.c_uint32, c_u32p, c_u32p]),
         "ugpu_tables_prefilter_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, c_u8p, P(ctypes.c_int)]),
@@ -127,6 +128,7 @@ def _load():
         "ugpu_records_drain": (ctypes.c_int, [V, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                               ctypes.POINTER(ctypes.c_uint64)]),
         "ugpu_select_device": (ctypes.c_int, [ctypes.c_int]),
+        "ugpu_warmup": (ctypes.c_int, [ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -425,6 +425,67 @@ int forest_run(ugpu_scanner* s, ScanParams P, uint64_t entry, bool write, hipStr
   return UGPU_OK;
 }
 
+// What ugpu_dfa_create uploads for a table under pattern flags, and so which
+// kernels its scans run: decided on the host alone (ugpu_dfa_plan_host answers
+// it without touching a device)
+struct DfaPlan {
+  bool ok = true;  // false: option W with line anchors or empty matches (UGPU_UNSUPPORTED)
+  bool nul = false, amode = false;
+  bool wtab = false, wplus = false, xcw = false;
+  bool xtrans = false, xid = false, xu = false, xg = false;
+};
+
+DfaPlan dfa_plan(const DfaTables& t, uint32_t flags)
+{
+  DfaPlan p;
+  p.nul = (flags & UGPU_PAT_EMPTY) != 0;
+  p.amode = t.anchored || (p.nul && t.start_acc);
+  if (p.amode) {
+    p.ok = !(flags & UGPU_PAT_WORD);
+    return p;
+  }
+  if (flags & UGPU_PAT_WORD) {
+    p.wtab = true;
+    const bool wf = !(std::getenv("UGPU_WFAST") && std::getenv("UGPU_WFAST")[0] == '0');
+    p.wplus = wf && t.gap && !t.filter && t.cap1 != 0 && is_word_plus(t);
+    p.xcw = wf && t.xc && t.xc_w && !t.filter && t.cap1 != 0;
+    if (!p.wplus && !p.xcw) return p;  // option W runs wfind_kernel only: no transducer tables
+  }
+  const bool tx = !t.filter && t.cap1 != 0;
+  p.xtrans = t.restart_local && tx;
+  p.xid = t.immediate && tx;
+  p.xu = t.xu && tx;
+  p.xg = t.gap && tx;
+  return p;
+}
+
+void dfa_info_fill(const DfaTables& t, const DfaPlan& p, ugpu_dfa_info* info)
+{
+  info->states = t.states;
+  info->classes = t.classes;
+  info->row = t.row;
+  info->format = t.format;
+  info->table_bytes = (uint32_t)(t.trans.size() * 2 + t.trans32.size() * 4 + (t.format != FMT_BYTE ? 256 : 0));
+  info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
+  info->first_bytes = t.first_bytes;
+  info->accepting = t.accepting;
+  const char* xenv = std::getenv("UGPU_XI");
+  const char* genv = std::getenv("UGPU_XG");
+  const char* cenv = std::getenv("UGPU_XC");
+  const char* uenv = std::getenv("UGPU_XU");
+  const bool byte_filter = t.filter && t.format == FMT_BYTE;
+  // (dfa_xc and dfa_xu, from the plan instead of the uploaded tables)
+  const bool xc = t.xc && !t.filter && t.cap1 != 0 && (!p.wtab || p.xcw) && !(cenv && cenv[0] == '0');
+  const bool xu = p.xu && (!p.wtab || p.wplus) && !(uenv && uenv[0] == '0');
+  info->kernel = p.amode || t.format == FMT_WIDE || (p.wtab && !p.wplus && !p.xcw && !byte_filter) ? 4u
+                 : byte_filter                                                                  ? 0u
+                 : xc                                                                           ? 5u
+                 : xu                                                                           ? 6u
+                 : (p.xid && !(xenv && xenv[0] == '0'))                                          ? 2u
+                 : (p.xg && !(genv && genv[0] == '0'))                                           ? 3u
+                                                                                                  : 1u;
+}
+
 int dfa_on(const ugpu_dfa* d, int dev, const ugpu_dfa** out);
 
 }  // namespace
@@ -465,6 +526,11 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     delete d;
     return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
   }
+  const DfaPlan pl = dfa_plan(d->t, pattern_flags);
+  if (!pl.ok) {
+    delete d;
+    return fail(UGPU_UNSUPPORTED, "option W with line anchors or empty matches");
+  }
   hipError_t e = hipGetDevice(&d->device);
   if (e != hipSuccess) {
     delete d;
@@ -472,6 +538,10 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
   }
   d->opc.assign(opc, opc + nop);
   d->pflags = pattern_flags;
+  d->nul = pl.nul;
+  d->amode = pl.amode;
+  d->wplus = pl.wplus;
+  d->xcw = pl.xcw;
   const size_t n = d->t.trans.size();
   d->ntrans_pad = (uint32_t)((n + 7) & ~size_t(7));
   std::vector<uint16_t> tr(d->ntrans_pad, 0);
@@ -494,23 +564,14 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     ugpu_dfa_destroy(d);
     return hip_fail(e, "wide table upload");
   }
-  d->nul = (pattern_flags & UGPU_PAT_EMPTY) != 0;
-  d->amode = d->t.anchored || (d->nul && d->t.start_acc);
-  if (d->amode) {
-    if (pattern_flags & UGPU_PAT_WORD) {
-      ugpu_dfa_destroy(d);
-      return fail(UGPU_UNSUPPORTED, "option W with line anchors or empty matches");
-    }
+  if (d->amode &&
+      ((e = hipMalloc(&d->d_acap, d->t.acap.size() * 4)) != hipSuccess ||
+       (e = hipMemcpy(d->d_acap, d->t.acap.data(), d->t.acap.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)) {
     // the per-context accepts; every scan runs the context walk (no transducers)
-    if ((e = hipMalloc(&d->d_acap, d->t.acap.size() * 4)) != hipSuccess ||
-        (e = hipMemcpy(d->d_acap, d->t.acap.data(), d->t.acap.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
-      ugpu_dfa_destroy(d);
-      return hip_fail(e, "context accept upload");
-    }
-    *out = d;
-    return UGPU_OK;
+    ugpu_dfa_destroy(d);
+    return hip_fail(e, "context accept upload");
   }
-  if (pattern_flags & UGPU_PAT_WORD) {
+  if (pl.wtab) {
     std::vector<uint32_t> wt;
     ugpu_word_ranges(wt);
     d->nwtab = (uint32_t)(wt.size() / 2);
@@ -519,15 +580,8 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       ugpu_dfa_destroy(d);
       return hip_fail(e, "word table upload");
     }
-    const bool wf = !(std::getenv("UGPU_WFAST") && std::getenv("UGPU_WFAST")[0] == '0');
-    d->wplus = wf && d->t.gap && !d->t.filter && d->t.cap1 != 0 && is_word_plus(d->t);
-    d->xcw = wf && d->t.xc && d->t.xc_w && !d->t.filter && d->t.cap1 != 0;
-    if (!d->wplus && !d->xcw) {
-      *out = d;  // option W runs wfind_kernel only: no transducer tables
-      return UGPU_OK;
-    }
   }
-  if (d->t.restart_local && !d->t.filter && d->t.cap1 != 0) {
+  if (pl.xtrans) {
     std::vector<uint16_t> xt(d->ntrans_pad, 0);
     std::copy(d->t.xtrans.begin(), d->t.xtrans.end(), xt.begin());
     if ((e = hipMalloc(&d->d_xtrans, xt.size() * 2)) != hipSuccess ||
@@ -536,14 +590,14 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       return hip_fail(e, "transducer table upload");
     }
   }
-  if (d->t.immediate && !d->t.filter && d->t.cap1 != 0) {
+  if (pl.xid) {
     if ((e = hipMalloc(&d->d_xid, d->t.xid.size())) != hipSuccess ||
         (e = hipMemcpy(d->d_xid, d->t.xid.data(), d->t.xid.size(), hipMemcpyHostToDevice)) != hipSuccess) {
       ugpu_dfa_destroy(d);
       return hip_fail(e, "immediate transducer upload");
     }
   }
-  if (d->t.xu && !d->t.filter && d->t.cap1 != 0) {
+  if (pl.xu) {
     if ((e = hipMalloc(&d->d_xu, kXuTab + 4 * kXuBm3)) != hipSuccess ||
         (e = hipMemcpy(d->d_xu, d->t.xu_tab.data(), kXuTab, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(d->d_xu + kXuTab, d->t.xu_bm3.data(), 4 * kXuBm3, hipMemcpyHostToDevice)) != hipSuccess) {
@@ -551,7 +605,7 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       return hip_fail(e, "code-point run table upload");
     }
   }
-  if (d->t.gap && !d->t.filter && d->t.cap1 != 0) {
+  if (pl.xg) {
     // device form: the class-major product table (tables.hpp xg2), padded to 8 entries
     std::vector<uint16_t> xg((d->t.xg2.size() + 7) & ~size_t(7), 0);
     std::copy(d->t.xg2.begin(), d->t.xg2.end(), xg.begin());
@@ -565,6 +619,20 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     }
   }
   *out = d;
+  return UGPU_OK;
+}
+
+int ugpu_dfa_plan_host(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa_info* info)
+{
+  if (!info) return fail(UGPU_INVAL, "info is NULL");
+  if (pattern_flags & ~(UGPU_PAT_WORD | UGPU_PAT_EMPTY)) return fail(UGPU_INVAL, "unknown pattern flags");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  const DfaPlan pl = dfa_plan(t, pattern_flags);
+  if (!pl.ok) return fail(UGPU_UNSUPPORTED, "option W with line anchors or empty matches");
+  dfa_info_fill(t, pl, info);
   return UGPU_OK;
 }
 
@@ -600,25 +668,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
 int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
 {
   if (!d || !info) return fail(UGPU_INVAL, "NULL argument");
-  info->states = d->t.states;
-  info->classes = d->t.classes;
-  info->row = d->t.row;
-  info->format = d->t.format;
-  info->table_bytes = (uint32_t)(d->t.trans.size() * 2 + d->t.trans32.size() * 4 + (d->t.format != FMT_BYTE ? 256 : 0));
-  info->prefilter_ppm = d->t.filter ? (uint32_t)(d->t.fdensity * 1e6) + 1 : 0;
-  info->first_bytes = d->t.first_bytes;
-  info->accepting = d->t.accepting;
-  const char* xenv = std::getenv("UGPU_XI");
-  const char* genv = std::getenv("UGPU_XG");
-  info->kernel = d->amode || d->t.format == FMT_WIDE ||
-                         (d->d_wtab && !d->wplus && !d->xcw && !(d->t.filter && d->t.format == FMT_BYTE))
-                     ? 4u
-                 : (d->t.filter && d->t.format == FMT_BYTE)    ? 0u
-                 : dfa_xc(d)                                   ? 5u
-                 : dfa_xu(d)                                   ? 6u
-                 : (d->d_xid && !(xenv && xenv[0] == '0')) ? 2u
-                 : (d->d_xg && !(genv && genv[0] == '0'))  ? 3u
-                                                           : 1u;
+  dfa_info_fill(d->t, dfa_plan(d->t, d->pflags), info);
   return UGPU_OK;
 }
 
@@ -2046,6 +2096,41 @@ bool records_advance(ugpu_records* r, int* rc)
 }
 
 }  // namespace
+
+int ugpu_warmup(int dev)
+{
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (dev < 0 || dev >= n) return fail(UGPU_INVAL, "no such device");
+  HIP_TRY(hipSetDevice(dev));
+  // the device context, one scan workspace and one records workspace (their
+  // streams: a queue each), a pinned block, and one kernel launch (the
+  // library's code object is loaded at the first launch)
+  FindWs* w = find_ws_acquire(dev);
+  if (!w) return fail(UGPU_DEVICE, "scan workspace");
+  RecWs* r = rec_ws_acquire(dev);
+  if (!r) {
+    find_ws_release(w);
+    return fail(UGPU_DEVICE, "records workspace");
+  }
+  int rc = UGPU_OK;
+  uint8_t* d = nullptr;
+  hipError_t e = hipMalloc(&d, 64);
+  if (e == hipSuccess) e = hipMemsetAsync(d, '\n', 64, w->st);
+  if (e == hipSuccess) e = hipStreamSynchronize(w->st);
+  if (e != hipSuccess) {
+    rc = hip_fail(e, "warm-up");
+  } else {
+    uint64_t pos = 0;
+    rc = ugpu_find_nul(d, 64, &pos, w->st);
+  }
+  if (d) (void)hipFree(d);
+  size_t got = 0;
+  if (uint8_t* p = pinned_get(1u << 20, got)) pinned_put(p, got);
+  rec_ws_release(r);
+  find_ws_release(w);
+  return rc;
+}
 
 int ugpu_find_records(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_t start, ugpu_records** out)
 {

@@ -95,6 +95,17 @@ def host_prefilter(opc):
     return bool(en.value), ft
 
 
+def host_plan(opc, word=False, empty=False):
+    """The info dict Pattern(opc, word, empty).info() would report (kernel
+    choice included), decided on the host without a device
+    (ugpu_dfa_plan_host); raises like Pattern() for unsupported tables."""
+    a, p = _as_u32(compile_regex(opc) if isinstance(opc, (str, bytes)) else opc)
+    info = _lib.DfaInfo()
+    check(lib.ugpu_dfa_plan_host(p, len(a), (PAT_WORD if word else 0) | (PAT_EMPTY if empty else 0),
+                                 ctypes.byref(info)))
+    return {f: getattr(info, f) for f, _ in _lib.DfaInfo._fields_}
+
+
 def host_transducer(opc):
     """FIND transducer table (u16 numpy array, tables.hpp) or None when the DFA
     is not restart-local."""
