@@ -68,7 +68,15 @@ typedef struct ugpu_dfa_info
                            4 wfind (option W, UGPU_PAT_WORD), 5 xc (two-state carry chain; UGPU_XC=0),
                            6 xc U mode (code-point runs without a gap transducer; UGPU_XU=1 prefers it,
                            UGPU_XU=0 never) */
+  uint32_t contexts;    /* accept contexts per state of the per-context accepts (ugpu_tables_context_host):
+                           1 = none (no meta edges), 4 = line anchors (bol * 2 + eol), 64 = word boundaries
+                           (ugrep_amd/csrc/ctx_bits.hpp) */
+  uint32_t shape;       /* UGPU_SHAPE_* bits (the drop-in matcher's test of where the reference's
+                           match predictor is exact for word-boundary patterns) */
 } ugpu_dfa_info;
+
+#define UGPU_SHAPE_FINITE 1u     /* the language is finite (no cycle in the DFA) */
+#define UGPU_SHAPE_WORD_COND 2u  /* a state whose accept depends on a word boundary also has byte edges */
 
 /* Totals of one scan.  digest = sum(start*31 + len), dcap = sum((start+1)*cap),
    both mod 2^64, start = byte offset + bias. */

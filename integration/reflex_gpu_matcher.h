@@ -298,15 +298,14 @@ class GpuMatcher : public Matcher {
         uint32_t nop = 0;
         if (ugpu_compile(rx.data(), rx.size(), UGPU_RX_REFLEX, &opc, &nop) == UGPU_OK)
         {
-          int anchored = 0;
           const uint32_t flags = (opt_.W ? UGPU_PAT_WORD : 0u) | (opt_.N ? UGPU_PAT_EMPTY : 0u);
           ugpu_dfa_info info;
-          if (ugpu_tables_context_host(opc, nop, NULL, 0, &anchored, NULL) == UGPU_OK && anchored &&
-              !(opt_.N && anchors_outer(rx)))
+          const bool planned = ugpu_dfa_plan_host(opc, nop, flags, &info) == UGPU_OK;
+          if (planned && !predictor_exact(rx, info))
           {
             tab_anchor_ = true;
           }
-          else if (ugpu_dfa_plan_host(opc, nop, flags, &info) == UGPU_OK)
+          else if (planned)
           {
             tab_ok_ = true;
             sparse_ = info.kernel == 0;
@@ -317,7 +316,8 @@ class GpuMatcher : public Matcher {
           ugpu_opc_free(opc);
         }
         if (tab_anchor_)
-          tab_err_ = "line anchors without option N or inside the regex (the reference's predictor decides there)";
+          tab_err_ = "meta edges where the reference's match predictor decides (line anchors without option N or "
+                     "inside the regex, word boundaries after loops or before more bytes)";
         else if (!tab_ok_)
           tab_err_ = ugpu_last_error();
         const char* dump = std::getenv("UGPU_ADAPTER_DUMP");
@@ -417,6 +417,66 @@ class GpuMatcher : public Matcher {
       }
     }
     return tab_->d;
+  }
+  // Tables with meta edges (line anchors, word boundaries) whose FIND results
+  // the reference's match predictor shares: ugrep runs FIND between candidate
+  // positions its Pattern predicts (lib/matcher.cpp:52-86, :797-954), and for
+  // meta edges the prediction can reject positions the DFA matches at -- the
+  // engine implements the DFA (the reference with its predictor off).
+  //  - line anchors: option N on and only a leading ^ / trailing $
+  //    (tests/test_anchor.py: "a$|ab", "^\w+" without N differ);
+  //  - word boundaries: a finite language whose boundary-dependent accepts
+  //    end the walk (\bfoo\b, \<(foo|bar)\>, \b\w\w\b); loops before the
+  //    assertion ("\w+\b" prints nothing in the reference CLI) and accepts
+  //    that go on with bytes ("x\b|xy") stay on the CPU matcher
+  //    (tests/test_wordb.py, a fuzz over tools/fuzz_wordb.py agrees).
+  bool predictor_exact(const std::string& rx, const ugpu_dfa_info& info) const
+  {
+    if (info.contexts == 1)
+      return true;
+    if (has_line_anchor(rx) && !(opt_.N && anchors_outer(rx)))
+      return false;
+    if (info.contexts == 64 && !((info.shape & UGPU_SHAPE_FINITE) && !(info.shape & UGPU_SHAPE_WORD_COND)))
+      return false;
+    return true;
+  }
+  // a ^ or $ that is a line anchor (not in a bracket expression, escaped or
+  // inside \Q...\E)
+  static bool has_line_anchor(const std::string& rx)
+  {
+    size_t i = 0;
+    const size_t n = rx.size();
+    while (i < n)
+    {
+      const char c = rx[i];
+      if (c == '\\')
+      {
+        if (i + 1 < n && rx[i + 1] == 'Q')
+        {
+          const size_t e = rx.find("\\E", i + 2);
+          i = e == std::string::npos ? n : e + 2;
+        }
+        else
+          i += 2;
+        continue;
+      }
+      if (c == '[')
+      {
+        size_t j = i + 1;
+        if (j < n && rx[j] == '^')
+          ++j;
+        if (j < n && rx[j] == ']')
+          ++j;
+        while (j < n && rx[j] != ']')
+          j += rx[j] == '\\' ? 2 : 1;
+        i = j + 1;
+        continue;
+      }
+      if (c == '^' || c == '$')
+        return true;
+      ++i;
+    }
+    return false;
   }
   // the regex's line anchors are at most a leading ^ (after the (?m...) prefix
   // ugrep puts first, src/ugrep.cpp:8586-8604) and a trailing $: ^ and $ in

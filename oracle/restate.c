@@ -16,9 +16,10 @@
  *     include/reflex/pattern.h:1155-1247 (GOTO lo<<24|hi<<16|idx, HALT
  *     0x00FFFFFF, LONG idx 0xFFFE + next word, TAKE 0xFE..).  TAKE at the head
  *     of a block (lib/pattern.cpp:2945-2952) makes the state accepting.
- *     REDO/TAIL/HEAD and meta edges other than META_BOL / META_EOL are
- *     rejected (ORC_UNSUPPORTED); BOL/EOL edges are kept per state in block
- *     order (orc_find_a).
+ *     REDO/TAIL/HEAD and meta edges other than META_BOL / META_EOL and the
+ *     word boundaries META_WBB .. META_EWE (pattern.h:933-943) are rejected
+ *     (ORC_UNSUPPORTED); meta edges are kept per state in block order
+ *     (orc_find_a).
  *   orc_find -- the FIND driver of Matcher::match (lib/matcher.cpp:42-750) for
  *     tables without meta/lookahead, options A/N/W off: from p walk the DFA,
  *     remember the last TAKE (:139-150, :207-217), stop on HALT/EOF (:448-459,
@@ -118,8 +119,8 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
     }
     /* block header: [REDO|TAKE]? TAIL* HEAD*, then meta edges (not goto
        words: the interpreter tests them in block order before the byte edges,
-       lib/matcher.cpp:193-450); only META_BOL (0x109) and META_EOL (0x10a),
-       include/reflex/pattern.h:942-943 */
+       lib/matcher.cpp:193-450); META_BOL (0x109), META_EOL (0x10a) and the
+       word boundaries 0x101-0x108, include/reflex/pattern.h:933-943 */
     {
       uint32_t nm = 0;
       while (g < nop && !is_goto(opc[g]))
@@ -127,7 +128,7 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
         uint32_t w = opc[g], op = w >> 24;
         if (op == 0xfe)
           d->accept[s] = w & 0xffffff;
-        else if (is_meta(w) && (op == 0x09 || op == 0x0a) && nm < ORC_MAXMETA)
+        else if (is_meta(w) && op >= 0x01 && op <= 0x0a && nm < ORC_MAXMETA)
         {
           uint32_t idx = w & 0xffff, tgt = idx == 0xfffe ? (g + 1 < nop ? opc[g + 1] & 0xffffff : nop) : idx;
           if (idx == 0xffff || tgt >= nop)
@@ -458,10 +459,101 @@ uint64_t orc_find_w(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t s
  * (the backtrack point, :405-440).  Empty matches (:682-728): without option N
  * the search moves to p+1; with N the empty match is reported and the search
  * moves to p+1, except at the end of the input. */
-static uint32_t orc_accept_at(const orc_dfa *d, uint32_t s, int bol, const uint8_t *buf, uint64_t n, uint64_t q)
+/* Word boundaries (lib/matcher.cpp:317-404, include/reflex/matcher.h:1238-1319,
+ * WITH_SPAN forms), tested after the interpreter fetched ch = buf[q] (pos_ =
+ * q + 1; at EOF ch = EOF and pos_ = q).  Of the match begin p (txt_, len_ = 0
+ * during FIND): at_wb() as for option W, at_bw() = a word character at p.  Of
+ * the position: at_ew(ch) = a word character before q (k = pos_ + (ch == EOF)
+ * = q + 1, byte buf[k - 2], got_ = BOB when q == 0), at_we(ch, pos_) = no word
+ * character at q, where a lead byte's code point is read from buf[pos_] --
+ * one byte past it. */
+static int orc_at_bw(const uint8_t *buf, uint64_t n, uint64_t p)
+{
+  uint32_t c = orc_rd(buf, n, p);
+  if (c == '_')
+    return 1;
+  if ((c & 0xC0) == 0xC0)
+    return orc_iswword(orc_utf8(buf, n, p));
+  return orc_isalnum(c);
+}
+
+static int orc_at_ew(const uint8_t *buf, uint64_t n, uint64_t q)
+{
+  uint64_t k = q + 1;
+  uint32_t c;
+  (void)n;
+  if (k <= 1)
+    return 0; /* got_ = BOB */
+  c = buf[k - 2];
+  if (c == '\n')
+    return 0;
+  if (c == '_')
+    return 1;
+  if ((c & 0xC0) == 0x80 && k > 2)
+  {
+    k -= 3;
+    if ((buf[k] & 0xC0) == 0x80)
+      if (k > 0 && (buf[--k] & 0xC0) == 0x80)
+        if (k > 0)
+          --k;
+    return orc_iswword(orc_utf8(buf, n, k));
+  }
+  return orc_isalnum(c);
+}
+
+static int orc_at_we_meta(const uint8_t *buf, uint64_t n, uint64_t q)
+{
+  uint32_t c;
+  if (q >= n)
+    return 1; /* EOF */
+  c = buf[q];
+  if (c == '_')
+    return 0;
+  if ((c & 0xC0) == 0xC0)
+    return !orc_iswword(orc_utf8(buf, n, q + 1));
+  return !orc_isalnum(c);
+}
+
+/* at_wb() as the meta edges call it during a walk from p: got_ = buf[p - 1],
+ * but a continuation byte there is decoded back from cur_ - 1 (matcher.h:
+ * 1202-1210), and cur_ is the end of the walk's last accept so far (TAKE sets
+ * it, lib/matcher.cpp:207-217), p before any */
+static int orc_at_wb_cur(const uint8_t *buf, uint64_t n, uint64_t p, uint64_t cur)
+{
+  uint32_t c;
+  if (p == 0)
+    return 1; /* got_ = '\n' at the buffer begin (set_current, absmatcher.h:1571-1580) */
+  c = buf[p - 1];
+  if (c == '\n')
+    return 1;
+  if (c == '_')
+    return 0;
+  if ((c & 0xC0) == 0x80 && cur > 0)
+  {
+    uint64_t k = cur - 1;
+    if (k > 0 && (buf[--k] & 0xC0) == 0x80)
+      if (k > 0 && (buf[--k] & 0xC0) == 0x80)
+        if (k > 0)
+          --k;
+    return !orc_iswword(orc_utf8(buf, n, k));
+  }
+  return !orc_isalnum(c);
+}
+
+/* walk context of a walk from p whose last accept ended at cur (p before
+   any): bit 0 bol, bit 1 at_wb, bit 2 at_bw */
+static int orc_walk_ctx(const uint8_t *buf, uint64_t n, uint64_t p, uint64_t cur)
+{
+  int bol = p == 0 || buf[p - 1] == '\n';
+  return bol | orc_at_wb_cur(buf, n, p, cur) << 1 | orc_at_bw(buf, n, p) << 2;
+}
+
+static uint32_t orc_accept_at(const orc_dfa *d, uint32_t s, int wctx, const uint8_t *buf, uint64_t n, uint64_t q)
 {
   uint32_t cap = d->accept[s];
+  int bol = wctx & 1, wb = (wctx >> 1) & 1, bw = (wctx >> 2) & 1;
   int eol = q >= n || buf[q] == '\n' || (buf[q] == '\r' && q + 1 < n && buf[q + 1] == '\n');
+  int ew = orc_at_ew(buf, n, q), we = orc_at_we_meta(buf, n, q);
   int jumps;
   for (jumps = 0; jumps < 5; ++jumps)
   {
@@ -469,9 +561,23 @@ static uint32_t orc_accept_at(const orc_dfa *d, uint32_t s, int bol, const uint8
     for (k = 0; k < ORC_MAXMETA; ++k)
     {
       uint32_t e = d->meta[(size_t)s * ORC_MAXMETA + k], m = e >> 24;
+      int holds;
       if (e == 0)
         break;
-      if ((m == 0x09 && bol) || (m == 0x0a && eol))
+      switch (m)
+      {
+        case 0x01: holds = bw == wb; break;   /* META_WBB at_wbb() */
+        case 0x02: holds = we == ew; break;   /* META_WBE at_wbe(ch) */
+        case 0x03: holds = bw != wb; break;   /* META_NWB at_nwb() */
+        case 0x04: holds = we != ew; break;   /* META_NWE at_nwe(ch) */
+        case 0x05: holds = bw && wb; break;   /* META_BWB at_bwb() */
+        case 0x06: holds = !bw && !wb; break; /* META_EWB at_ewb() */
+        case 0x07: holds = !we && !ew; break; /* META_BWE at_bwe(ch) */
+        case 0x08: holds = we && ew; break;   /* META_EWE at_ewe(ch) */
+        case 0x09: holds = bol; break;
+        default: holds = eol; break;
+      }
+      if (holds)
       {
         t = e & 0xffffff;
         break;
@@ -496,11 +602,10 @@ uint64_t orc_find_a(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t s
   uint64_t p = start, cnt = 0, dg = 0, dc = 0;
   while (p < n)
   {
-    int bol = p == 0 || buf[p - 1] == '\n';
     uint32_t s = d->start, a = 0, c;
     uint64_t q = p, last = p;
     int hit = 0;
-    if ((c = orc_accept_at(d, s, bol, buf, n, q)) != 0)
+    if ((c = orc_accept_at(d, s, orc_walk_ctx(buf, n, p, p), buf, n, q)) != 0)
     {
       hit = 1;
       a = c;
@@ -512,7 +617,7 @@ uint64_t orc_find_a(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t s
         break;
       s = t;
       ++q;
-      if ((c = orc_accept_at(d, s, bol, buf, n, q)) != 0)
+      if ((c = orc_accept_at(d, s, orc_walk_ctx(buf, n, p, last), buf, n, q)) != 0)
       {
         hit = 1;
         last = q;

@@ -8,13 +8,12 @@ anchored context walk, W with anchors rejected).  GPU: the plan equals
 Pattern(...).info() of the uploaded tables over patterns x options W, N."""
 import pytest
 
-import ugrep_amd as U
-
 PATS = ["foo|bar|baz", "[A-Za-z_][A-Za-z0-9_]*", r"\w+", "a+", "^foo", "foo$", "x[a-z]*y", r"\d+\.\d+",
         "(ab)+", "[a-z]+ing", r"\S+", "[[:alpha:]]+", "é+", "a|b", ".", r"[0-9]{3}-[0-9]{4}", "a*"]
 
 
 def test_plan_known_tables():
+    import ugrep_amd as U
     assert U.host_plan("foo|bar|baz")["kernel"] == 0
     assert U.host_plan("[A-Za-z_][A-Za-z0-9_]*")["kernel"] == 5
     assert U.host_plan(r"\w+")["kernel"] == 6
@@ -27,6 +26,7 @@ def test_plan_known_tables():
 
 
 def test_plan_matches_host_tables():
+    import ugrep_amd as U
     for rx in PATS:
         try:
             t = U.host_tables(U.compile_regex(rx))["info"]
@@ -42,6 +42,7 @@ def test_plan_equals_uploaded_info():
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd as U
     for rx in PATS:
         for word in (False, True):
             for empty in (False, True):

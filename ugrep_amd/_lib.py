@@ -35,7 +35,7 @@ c_u64p = ctypes.POINTER(ctypes.c_uint64)
 class DfaInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in
                 ("states", "classes", "row", "format", "table_bytes", "prefilter_ppm", "first_bytes", "accepting",
-                 "kernel")]
+                 "kernel", "contexts", "shape")]
 
 
 class Totals(ctypes.Structure):
@@ -59,7 +59,23 @@ class Unsupported(UgpuError):
     pass
 
 
+def _torch_runtime_first():
+    """One HIP runtime per process.  The engine library links libamdhip64 by
+    soname; when PyTorch-ROCm is importable, load it first so that the engine
+    binds to the runtime torch uses (device buffers and streams are shared with
+    torch tensors).  Loading the engine first would bring in /opt/rocm's runtime
+    and torch's own beside it, and the first of them to initialise can leave
+    the other without a device ("no ROCm-capable device is detected")."""
+    if os.environ.get("UGPU_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load():
+    _torch_runtime_first()
     if not os.path.exists(LIB_PATH):
         raise ImportError("libugrep_amd.so not built (%s); run __graft_entry__.build() or make -C ugrep_amd"
                           % LIB_PATH)

@@ -4,6 +4,7 @@
 #pragma once
 #include <type_traits>
 
+#include "ctx_bits.hpp"
 #include "scan_kernels.hpp"
 
 namespace ugpu {
@@ -55,6 +56,8 @@ struct Win {
   uint32_t log_row = 0;
   uint32_t bol0 = 1;
   uint32_t nul = 0;
+  uint32_t cword = 0;  // word-boundary meta edges: 64 contexts (ctx_bits.hpp), Word ranges in wtab
+  const uint32_t* amap = nullptr;  // cword: each state's row of acap (tables.hpp acap_map)
 };
 
 // Walk modes (template argument W of walk / chain_step / merge)
@@ -77,6 +80,8 @@ __device__ __forceinline__ Win win_of(const ScanParams& P)
   w.log_row = P.log_row;
   w.bol0 = P.bol0;
   w.nul = P.nul;
+  w.cword = P.ctx_word;
+  w.amap = P.amap;
   return w;
 }
 
@@ -184,11 +189,96 @@ __device__ __forceinline__ uint32_t at_eol(const Win& w, uint64_t q, uint32_t& o
   return w.g[q + 1] == '\n' ? 1u : 0u;
 }
 
-// accept at q in the state of entry e: the acap index (0 = none; index 0..3
-// is the dead state, which never accepts)
-__device__ __forceinline__ uint32_t ctx_accept(const Win& w, uint32_t e, uint32_t bol, uint64_t q, uint32_t& ovf)
+// Word-boundary meta edges (META_WBB .. META_EWE, include/reflex/pattern.h:
+// 933-940), tested by the interpreter after it fetched the byte at the
+// current position q (lib/matcher.cpp:317-404) through
+// include/reflex/matcher.h:1194-1319: at_wb / at_bw of the match begin p
+// (txt_, len_ = 0 during FIND; fixed for the walk like bol) and at_ew / at_we
+// of q.
+// at_bw(): a word character at the match begin p (matcher.h:1239-1254)
+__device__ __forceinline__ bool at_bw(const Win& w, uint64_t p, uint32_t& ovf)
 {
-  const uint32_t b = ((e >> w.log_row) << 2) | (bol << 1);
+  if (p >= w.rend && !w.eof) ovf = 1;
+  const uint32_t c = wrd(w, p);
+  if (c == '_') return true;
+  if ((c & 0xC0) == 0xC0) {
+    const uint64_t need = c >= 0xF0 ? 4u : c >= 0xE0 ? 3u : 2u;
+    if (p + need > w.rend && !w.eof) ovf = 1;
+    return wisword(w, wutf8(w, p));
+  }
+  return walnum(c);
+}
+
+// at_ew(): a word character before q (matcher.h:1256-1279; before the buffer
+// begin: got_ = BOB, no word)
+__device__ __forceinline__ bool at_ew(const Win& w, uint64_t q)
+{
+  if (q <= w.bob) return false;
+  const uint32_t c = w.g[q - 1];
+  if (c == '\n') return false;
+  if (c == '_') return true;
+  if ((c & 0xC0) == 0x80 && q - w.bob >= 2) {
+    // back over at most two more continuation bytes to the lead byte
+    uint64_t k = q - 2;
+    if ((w.g[k] & 0xC0) == 0x80)
+      if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
+        if (k > w.bob) --k;
+    return wisword(w, wutf8(w, k));
+  }
+  return walnum(c);
+}
+
+// at_we() as the meta edges call it: at_we(c, pos_) with pos_ one past the
+// byte c at q (matcher.h:1281-1313), so a lead byte's code point is decoded
+// from the byte after it (a continuation byte in valid UTF-8: no word
+// character, the boundary holds); at EOF true
+__device__ __forceinline__ bool at_we_meta(const Win& w, uint64_t q, uint32_t& ovf)
+{
+  if (q >= w.rend) {
+    if (!w.eof) ovf = 1;
+    return true;
+  }
+  const uint32_t c = w.g[q];
+  if (c == '_') return false;
+  if ((c & 0xC0) == 0xC0) {
+    if (q + 5 > w.rend && !w.eof) ovf = 1;
+    return !wisword(w, wutf8(w, q + 1));
+  }
+  return !walnum(c);
+}
+
+// at_wb() as the meta edges call it during a walk from p whose last accept
+// ended at cur (p before any): got_ is the byte before p, but a continuation
+// byte there is decoded back from cur_ - 1 (matcher.h:1202-1210), and TAKE
+// moves cur_ (lib/matcher.cpp:207-217).  Only reached for p > bob.
+__device__ __forceinline__ bool at_wb_cur(const Win& w, uint64_t cur)
+{
+  uint64_t k = cur - 1;
+  if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
+    if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
+      if (k > w.bob) --k;
+  return !wisword(w, wutf8(w, k));
+}
+
+// the walk bits of a walk starting at p (shifted into the acap index):
+// line contexts bol << 1; word contexts CTX_BOL | CTX_WB | CTX_BW
+__device__ __forceinline__ uint32_t ctx_walk_bits(const Win& w, uint64_t p, uint32_t& ovf)
+{
+  const uint32_t bol = p <= w.bob ? w.bol0 : (w.g[p - 1] == '\n' ? 1u : 0u);
+  if (!w.cword) return bol << 1;
+  return (bol ? CTX_BOL : 0u) | (at_wb(w, p) ? CTX_WB : 0u) | (at_bw(w, p, ovf) ? CTX_BW : 0u);
+}
+
+// accept at q in the state of entry e: the acap index (0 = none; the dead
+// state's indices never accept).  wb: ctx_walk_bits of the walk.
+__device__ __forceinline__ uint32_t ctx_accept(const Win& w, uint32_t e, uint32_t wb, uint64_t q, uint32_t& ovf)
+{
+  if (w.cword) {
+    const uint32_t b = (w.amap[e >> w.log_row] << 6) | wb;
+    const uint32_t k = b | at_eol(w, q, ovf) | (at_ew(w, q) ? CTX_EW : 0u) | (at_we_meta(w, q, ovf) ? CTX_WE : 0u);
+    return w.acap[k] ? k : 0u;
+  }
+  const uint32_t b = ((e >> w.log_row) << 2) | wb;
   const uint32_t a0 = w.acap[b], a1 = w.acap[b + 1];
   if (a0 == a1) return a0 ? b : 0u;
   const uint32_t k = b + at_eol(w, q, ovf);
@@ -207,7 +297,9 @@ __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64
   uint64_t q = p, last = p;
   le = 0;
   if constexpr (W == kWalkCtx) {
-    const uint32_t bol = p <= w.bob ? w.bol0 : (w.g[p - 1] == '\n' ? 1u : 0u);
+    uint32_t bol = ctx_walk_bits(w, p, ovf);
+    // (a continuation byte before p: at_wb follows the last accept, at_wb_cur)
+    const bool wbc = w.cword && p > w.bob && (w.g[p - 1] & 0xC0) == 0x80;
     le = ctx_accept(w, s, bol, q, ovf);
     while (q < w.rend) {
       const uint32_t e = T.step(s, w.g[q]);
@@ -215,6 +307,7 @@ __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64
       s = e;
       ++q;
       if (e >= T.accb) {
+        if (wbc && last != p) bol = (bol & ~CTX_WB) | (at_wb_cur(w, last) ? CTX_WB : 0u);
         const uint32_t a = ctx_accept(w, e, bol, q, ovf);
         if (a) {
           last = q;

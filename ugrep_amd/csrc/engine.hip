@@ -89,7 +89,7 @@ struct ugpu_dfa {
   // or matches the empty string under N; its scans run the context walk
   // (wfind_kernel, device_common.hpp kWalkCtx) on the per-context accepts
   bool nul = false, amode = false;
-  uint32_t* d_acap = nullptr;
+  uint32_t* d_acap = nullptr;  // acap, or (word boundaries) acap_rows then acap_map
   // idle scanners of ugpu_find_all calls on this table (reused: creating one
   // costs device allocations and property queries)
   std::mutex pool_mu;
@@ -293,6 +293,9 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.xu_bm3 = d->d_xu ? reinterpret_cast<const uint32_t*>(d->d_xu + kXuTab) : nullptr;
   P.xu_null = d->t.xu_null;
   P.acap = d->amode ? d->d_acap : nullptr;
+  P.ctx_word = d->amode && d->t.ctx_word ? 1u : 0u;
+  P.acap_n = (uint32_t)(P.ctx_word ? d->t.acap_rows.size() : d->t.acap.size());
+  P.amap = P.ctx_word ? d->d_acap + d->t.acap_rows.size() : nullptr;
   P.nul = d->nul ? 1u : 0u;
   P.bol0 = 1;
   // chain bytes one stitch merge may cross before the chains count as not
@@ -469,6 +472,8 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, ugpu_dfa_info* info)
   info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
+  info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;
+  info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u);
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
   const char* cenv = std::getenv("UGPU_XC");
@@ -565,13 +570,20 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     return hip_fail(e, "wide table upload");
   }
   if (d->amode &&
-      ((e = hipMalloc(&d->d_acap, d->t.acap.size() * 4)) != hipSuccess ||
-       (e = hipMemcpy(d->d_acap, d->t.acap.data(), d->t.acap.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)) {
+      ((e = hipMalloc(&d->d_acap, d->t.ctx_word ? (d->t.acap_rows.size() + d->t.acap_map.size()) * 4
+                                                : d->t.acap.size() * 4)) != hipSuccess ||
+       (e = d->t.ctx_word
+                ? hipMemcpy(d->d_acap, d->t.acap_rows.data(), d->t.acap_rows.size() * 4, hipMemcpyHostToDevice)
+                : hipMemcpy(d->d_acap, d->t.acap.data(), d->t.acap.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+       (d->t.ctx_word &&
+        (e = hipMemcpy(d->d_acap + d->t.acap_rows.size(), d->t.acap_map.data(), d->t.acap_map.size() * 4,
+                       hipMemcpyHostToDevice)) != hipSuccess))) {
     // the per-context accepts; every scan runs the context walk (no transducers)
     ugpu_dfa_destroy(d);
     return hip_fail(e, "context accept upload");
   }
-  if (pl.wtab) {
+  if (pl.wtab || (d->amode && d->t.ctx_word)) {
+    // (option W, and word-boundary meta edges: both test Unicode word characters)
     std::vector<uint32_t> wt;
     ugpu_word_ranges(wt);
     d->nwtab = (uint32_t)(wt.size() / 2);
@@ -689,6 +701,8 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
+  info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;
+  info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u);
   info->kernel = (t.filter && t.format == FMT_BYTE) ? 0u
                  : t.format == FMT_WIDE              ? 4u
                  : (t.xc && t.cap1 != 0)             ? 5u
@@ -868,7 +882,10 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   // line anchors / option N: every scan runs the context walk on wfind_kernel
   // wide tables: the exact walk on wfind_kernel, transitions from global memory
   if (dfa->amode || dfa->t.format == FMT_WIDE || (dfa->d_wtab && !(dfa->t.filter && dfa->t.format == FMT_BYTE))) {
-    if (wfind_smem_bytes(dfa->ntrans_pad, dfa->t.states, dfa->nwtab, dfa->amode) > 160 * 1024) {
+    const uint32_t nacap = !dfa->amode ? dfa->t.states
+                           : dfa->t.ctx_word ? (uint32_t)dfa->t.acap_rows.size() : (uint32_t)dfa->t.acap.size();
+    const uint32_t nmap = dfa->amode && dfa->t.ctx_word ? dfa->t.states : 0u;
+    if (wfind_smem_bytes(dfa->ntrans_pad, dfa->t.states, dfa->nwtab, nacap, nmap) > 160 * 1024) {
       delete s;
       return fail(UGPU_UNSUPPORTED, "tables do not fit in LDS");
     }

@@ -27,6 +27,11 @@
 // they become per-context accepts encoded as META_BOL / META_EOL edges to
 // accept-only states (include/reflex/pattern.h:942-943), the shape the
 // reference's Pattern gives them (^ moved to the accept side).
+// Word boundaries \b \B \< \> before the first atom of a top-level
+// alternative (the begin-of-match forms META_WBB/NWB/BWB/EWB, which RE/flex
+// also tests on the accept side, lib/pattern.cpp:2527-2538 k->anchor()) or
+// after its last (META_WBE/NWE/BWE/EWE): per-context accepts over 64 contexts
+// (ctx_bits.hpp), encoded as exhaustive meta-edge splits (encode()).
 // Returns UGPU_UNSUPPORTED for what the GPU tables cannot express or this
 // compiler does not cover (other anchors, word boundaries, lazy quantifiers,
 // lookaround, backreferences, other \p names, \p{Lu} under -i): the caller keeps
@@ -44,6 +49,14 @@
 #include <vector>
 
 #include "ugpu.h"
+#include "ctx_bits.hpp"
+
+using ugpu::CTX_BOL;
+using ugpu::CTX_BW;
+using ugpu::CTX_EOL;
+using ugpu::CTX_EW;
+using ugpu::CTX_WB;
+using ugpu::CTX_WE;
 
 namespace {
 
@@ -415,8 +428,10 @@ class Parser
     for (;;)
     {
       bol_ = eol_ = false;
+      wmask_ = 0x3F;
       alts.push_back(parse_concat(true));
       anchors.push_back((bol_ ? 1 : 0) | (eol_ ? 2 : 0));
+      wmasks.push_back(wmask_);
       if (p_ >= s_.size() || s_[p_] != '|')
         break;
       ++p_;
@@ -428,6 +443,10 @@ class Parser
 
   // per top-level alternative: 1 = starts with ^, 2 = ends with $
   std::vector<int> anchors;
+  // per top-level alternative: the word-boundary classes its accept allows,
+  // bits 0-2 of the match begin (A: at_bw && at_wb, B: neither, N: one of
+  // them) and bits 3-5 of the match end (A: at_we && at_ew, B: neither, N)
+  std::vector<int> wmasks;
 
  private:
   const std::string &s_;
@@ -438,6 +457,24 @@ class Parser
   bool dotall_ = false;  // REFLEX mode (?s): '.' matches '\n'
   bool multiline_ = false;  // REFLEX mode (?m): ^ and $ are line anchors
   bool bol_ = false, eol_ = false;  // anchors of the top-level alternative being parsed
+  int wmask_ = 0x3F;                // word-boundary classes of the alternative being parsed
+
+  // a word-boundary assertion at p_ (\b \B \< \>): its class mask (for the
+  // begin of the match, bits 0-2; as the reference's META_WBB/NWB/BWB/EWB and
+  // META_WBE/NWE/BWE/EWE hold: include/reflex/matcher.h:1281-1319), or 0
+  int word_assertion(size_t q) const
+  {
+    if (q + 1 >= s_.size() || s_[q] != '\\')
+      return 0;
+    switch (s_[q + 1])
+    {
+      case 'b': return 1 | 2;  // \b: A or B
+      case 'B': return 4;      // \B: N
+      case '<': return 1;      // \< : begin of a word
+      case '>': return 2;      // \> : end of a word
+      default: return 0;
+    }
+  }
 
   bool icase() const { return ic_; }
   bool reflex() const { return (flags_ & UGPU_RX_REFLEX) != 0; }
@@ -489,6 +526,38 @@ class Parser
           ++p_;
           continue;
         }
+      }
+      // word boundaries of a top-level alternative: before its first atom, or
+      // followed only by other assertions and $ up to the alternative's end
+      if (top && word_assertion(p_))
+      {
+        size_t q = p_;
+        while (q < s_.size())
+        {
+          if (word_assertion(q))
+            q += 2;
+          else if (s_[q] == '$' && (multiline_ || !reflex()))
+            ++q;
+          else
+            break;
+        }
+        const bool last = q == s_.size() || s_[q] == '|';
+        if (!atoms || last)
+        {
+          if (p_ + 2 < s_.size() && strchr("*+?{", s_[p_ + 2]) != NULL)
+            fail(UGPU_UNSUPPORTED, "repeated word boundary");
+          const int m = word_assertion(p_);
+          // an assertion with atoms after it tests the match begin, one with
+          // none (also an alternative of assertions only: "\\b" compiles to
+          // META_WBE) the end.  \< at the end of a match is a begin of a word
+          // there (B of the end pair: no word before, a word after), \> an end (A)
+          const bool at_end = last;
+          const int cls = !at_end ? m : (m == 1 ? 2 : m == 2 ? 1 : m);
+          wmask_ &= !at_end ? (cls | 0x38) : (cls << 3 | 0x07);
+          p_ += 2;
+          continue;
+        }
+        fail(UGPU_UNSUPPORTED, "word boundary between consumed characters");
       }
       // REFLEX mode: a (?imsx) modifier after atoms of its branch opens a group
       // that runs to the end of the enclosing group, later alternatives
@@ -1241,6 +1310,7 @@ struct Glushkov
   std::vector<std::vector<int>> follow;  // position -> follow positions
   std::vector<int> accept;               // position -> accept index (end markers), 0 otherwise
   std::vector<int> anchor;               // end marker -> 1: needs a walk begun at a line begin, 2: needs a line end next
+  std::vector<int> wmask;                // end marker -> word-boundary classes allowed (Parser::wmasks)
 
   struct Info
   {
@@ -1269,6 +1339,7 @@ struct Glushkov
     follow.emplace_back();
     accept.push_back(acc);
     anchor.push_back(0);
+    wmask.push_back(0x3F);
     return static_cast<int>(bytes.size() - 1);
   }
 
@@ -1332,12 +1403,36 @@ struct Glushkov
 // accept index per line context (bit 0: the walk began at a line begin, bit 1:
 // a line end follows), the lowest satisfied top-level alternative, 0 = none
 typedef std::array<uint32_t, 4> Ctx4;
+// per context: 4 line contexts as Ctx4, or (word boundaries) 64 contexts in
+// the tables' layout (ctx_bits.hpp)
+typedef std::vector<uint32_t> CtxN;
+
+// the word-boundary classes of a 64-context index: of the match begin (A:
+// at_bw && at_wb, B: neither, N: one) and of the position (A: at_we && at_ew)
+inline int bcls_of(uint32_t ctx)
+{
+  const bool bw = ctx & CTX_BW, wb = ctx & CTX_WB;
+  return bw && wb ? 0 : (!bw && !wb) ? 1 : 2;
+}
+inline int ecls_of(uint32_t ctx)
+{
+  const bool we = ctx & CTX_WE, ew = ctx & CTX_EW;
+  return we && ew ? 0 : (!we && !ew) ? 1 : 2;
+}
+// a context of classes (bc, ec) and line bits
+inline uint32_t ctx_of(int bc, int ec, bool bol, bool eol)
+{
+  uint32_t c = bc == 0 ? (CTX_BW | CTX_WB) : bc == 1 ? 0u : CTX_BW;
+  c |= ec == 0 ? (CTX_WE | CTX_EW) : ec == 1 ? 0u : CTX_WE;
+  return c | (bol ? CTX_BOL : 0u) | (eol ? CTX_EOL : 0u);
+}
 
 struct Dfa
 {
   std::vector<std::vector<uint32_t>> next;  // state -> 256 targets (0 = dead state)
-  std::vector<uint32_t> acc;                // accept index without line context (cx[s][0]), 0 = none
-  std::vector<Ctx4> cx;                     // accept index per line context
+  std::vector<uint32_t> acc;                // accept index without context (cx[s][0]), 0 = none
+  std::vector<CtxN> cx;                     // accept index per context
+  uint32_t nctx = 4;                        // 4 (line anchors) or 64 (word boundaries)
   bool anchored = false;                    // some accept depends on the context
 };
 
@@ -1377,17 +1472,31 @@ Dfa subsets(Glushkov &g, const std::vector<int> &start)
   for (int b = 0; b < 256; ++b)
     if (rep[cls[b]] < 0)
       rep[cls[b]] = b;
+  for (int m : g.wmask)
+    if (m != 0x3F)
+      d.nctx = 64;
   for (size_t k = 0; k < sets.size(); ++k)
   {
     std::vector<int> cur = sets[k];  // copy: sets grows
-    Ctx4 cx = {0, 0, 0, 0};
-    for (int ctx = 0; ctx < 4; ++ctx)
+    CtxN cx(d.nctx, 0);
+    for (uint32_t ctx = 0; ctx < d.nctx; ++ctx)
       for (int p : cur)
-        if (g.accept[p] && (g.anchor[p] & ~ctx) == 0 && (cx[ctx] == 0 || static_cast<uint32_t>(g.accept[p]) < cx[ctx]))
+      {
+        if (!g.accept[p])
+          continue;
+        bool ok;
+        if (d.nctx == 4)
+          ok = (g.anchor[p] & ~static_cast<int>(ctx)) == 0;
+        else
+          ok = (!(g.anchor[p] & 1) || (ctx & CTX_BOL)) && (!(g.anchor[p] & 2) || (ctx & CTX_EOL)) &&
+               ((g.wmask[p] >> bcls_of(ctx)) & 1) && ((g.wmask[p] >> (3 + ecls_of(ctx))) & 1);
+        if (ok && (cx[ctx] == 0 || static_cast<uint32_t>(g.accept[p]) < cx[ctx]))
           cx[ctx] = g.accept[p];
+      }
     d.acc.push_back(cx[0]);
+    for (uint32_t ctx = 1; ctx < d.nctx; ++ctx)
+      d.anchored = d.anchored || cx[ctx] != cx[0];
     d.cx.push_back(cx);
-    d.anchored = d.anchored || cx[1] != cx[0] || cx[2] != cx[0] || cx[3] != cx[0];
     std::vector<uint32_t> row(256, 0);
     std::vector<uint32_t> by_cls(ncls, 0);
     for (int c = 0; c < ncls; ++c)
@@ -1412,7 +1521,7 @@ Dfa minimize(const Dfa &d, uint32_t start)
   size_t n = d.acc.size();
   std::vector<uint32_t> part(n);
   {
-    std::map<Ctx4, uint32_t> m;
+    std::map<CtxN, uint32_t> m;
     for (size_t s = 0; s < n; ++s)
       part[s] = m.emplace(d.cx[s], static_cast<uint32_t>(m.size())).first->second;
   }
@@ -1443,9 +1552,10 @@ Dfa minimize(const Dfa &d, uint32_t start)
     rep[part[s]] = static_cast<uint32_t>(s);
   Dfa out;
   out.anchored = d.anchored;
+  out.nctx = d.nctx;
   newid[dead] = 0;
   out.acc.push_back(0);
-  out.cx.push_back(Ctx4{0, 0, 0, 0});
+  out.cx.push_back(CtxN(d.nctx, 0));
   out.next.push_back(std::vector<uint32_t>(256, 0));
   std::vector<uint32_t> order{part[start]};
   if (part[start] != dead)
@@ -1600,9 +1710,106 @@ std::vector<uint32_t> encode(const Dfa &d)
   // reference evaluates it (lib/matcher.cpp:193-450): its TAKE f[0], then the
   // first meta edge that holds -- BOL to Q(f[1], f[3]) (whose EOL edge gives
   // f[3]), else EOL to P(f[2])
-  for (size_t s = 1; s < n; ++s)
+  // the line encoding of f (bit 0 bol, bit 1 eol) into block k
+  auto line_encode = [&](size_t bi, const Ctx4 &f) {
+    blocks[bi].take = f[0];
+    const bool by_bol = f[1] != f[0] || f[3] != f[2];
+    const bool by_eol = f[2] != f[0] || f[3] != f[1];
+    if (by_bol && by_eol)
+    {
+      const uint32_t q = accept_only(f[1], f[3]);
+      blocks[bi].metas.push_back(std::make_pair(kBol, q));
+      if (f[2] != f[0])
+      {
+        const uint32_t pe = accept_only(f[2], f[2]);
+        blocks[bi].metas.push_back(std::make_pair(kEol, pe));
+      }
+    }
+    else if (by_bol)
+    {
+      const uint32_t pb = accept_only(f[1], f[1]);  // (before indexing: blocks may grow)
+      blocks[bi].metas.push_back(std::make_pair(kBol, pb));
+    }
+    else if (by_eol)
+    {
+      const uint32_t pe = accept_only(f[2], f[2]);
+      blocks[bi].metas.push_back(std::make_pair(kEol, pe));
+    }
+  };
+  if (d.nctx == 64)
   {
-    const Ctx4 &f = d.cx[s];
+    // word boundaries: per state, an exhaustive split over the match begin's
+    // class (META_BWB A, META_EWB B, META_NWB N: exactly one holds), each
+    // target an exhaustive split over the position's class (META_EWE A,
+    // META_BWE B, META_NWE N), each of those the line encoding -- at most 4
+    // meta jumps (the interpreter follows 5, lib/matcher.cpp:194-195).  A
+    // block with splits carries no TAKE (a later TAKE cannot cancel one).
+    const uint32_t kBWB = 0x05, kEWB = 0x06, kNWB = 0x03, kEWE = 0x08, kBWE = 0x07, kNWE = 0x04;
+    std::map<Ctx4, uint32_t> line_blocks;
+    auto line_block = [&](const Ctx4 &f) -> uint32_t {
+      auto it = line_blocks.find(f);
+      if (it != line_blocks.end())
+        return it->second;
+      Block k;
+      k.runs.push_back(Run{0, 255, 0});
+      blocks.push_back(k);
+      const uint32_t id = static_cast<uint32_t>(blocks.size());
+      line_encode(id - 1, f);
+      return line_blocks.emplace(f, id).first->second;
+    };
+    auto line_of = [](const CtxN &f, int bc, int ec) {
+      Ctx4 r;
+      for (int i = 0; i < 4; ++i)
+        r[i] = f[ctx_of(bc, ec, i & 1, (i >> 1) & 1)];
+      return r;
+    };
+    // the position-class level for begin class bc into block bi
+    auto e_encode = [&](size_t bi, const CtxN &f, int bc) {
+      const Ctx4 a = line_of(f, bc, 0), b = line_of(f, bc, 1), c = line_of(f, bc, 2);
+      if (a == b && b == c)
+      {
+        line_encode(bi, a);
+        return;
+      }
+      const uint32_t ta = line_block(a), tb = line_block(b), tc = line_block(c);
+      blocks[bi].metas.push_back(std::make_pair(kEWE, ta));
+      blocks[bi].metas.push_back(std::make_pair(kBWE, tb));
+      blocks[bi].metas.push_back(std::make_pair(kNWE, tc));
+    };
+    std::map<std::array<Ctx4, 3>, uint32_t> e_blocks;
+    auto e_block = [&](const CtxN &f, int bc) -> uint32_t {
+      const std::array<Ctx4, 3> key{line_of(f, bc, 0), line_of(f, bc, 1), line_of(f, bc, 2)};
+      auto it = e_blocks.find(key);
+      if (it != e_blocks.end())
+        return it->second;
+      Block k;
+      k.runs.push_back(Run{0, 255, 0});
+      blocks.push_back(k);
+      const uint32_t id = static_cast<uint32_t>(blocks.size());
+      e_encode(id - 1, f, bc);
+      return e_blocks.emplace(key, id).first->second;
+    };
+    for (size_t s = 1; s < n; ++s)
+    {
+      const CtxN f = d.cx[s];  // (copy: blocks grows)
+      bool by_b = false;
+      for (uint32_t ctx = 0; ctx < 64 && !by_b; ++ctx)
+        by_b = f[ctx] != f[ctx_of(0, ecls_of(ctx), ctx & CTX_BOL, ctx & CTX_EOL)];
+      if (by_b)
+      {
+        const uint32_t xa = e_block(f, 0), xb = e_block(f, 1), xn = e_block(f, 2);
+        blocks[s - 1].metas.push_back(std::make_pair(kBWB, xa));
+        blocks[s - 1].metas.push_back(std::make_pair(kEWB, xb));
+        blocks[s - 1].metas.push_back(std::make_pair(kNWB, xn));
+      }
+      else
+        e_encode(s - 1, f, 0);
+    }
+  }
+  for (size_t s = 1; s < n && d.nctx == 4; ++s)
+  {
+    Ctx4 f;
+    std::copy(d.cx[s].begin(), d.cx[s].end(), f.begin());
     Block &k = blocks[s - 1];
     k.take = f[0];
     const bool by_bol = f[1] != f[0] || f[3] != f[2];
@@ -1718,6 +1925,7 @@ int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, 
       Glushkov::Info info = g.walk(alts[k]);
       int end = g.new_pos(ByteSet(), static_cast<int>(k + 1));
       g.anchor[end] = k < parser.anchors.size() ? parser.anchors[k] : 0;
+      g.wmask[end] = k < parser.wmasks.size() ? parser.wmasks[k] : 0x3F;
       g.link(info.last, std::vector<int>{end});
       Glushkov::merge(start, info.first);
       if (info.nullable)

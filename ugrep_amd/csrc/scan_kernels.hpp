@@ -205,12 +205,18 @@ struct ScanParams {
   // walk); NULL: not written
   uint16_t* inbits;
   // line anchors / option N (tables.hpp acap): per-context accept indices
-  // (sid * 4 + bol * 2 + eol) or NULL; bol0: the position bob starts a line
-  // (the byte before the buffer is '\n', or the buffer begins the input);
-  // nul: option N, empty matches are reported
+  // (sid * 4 + bol * 2 + eol; ctx_word: sid * 64 + CTX_* bits, with wtab
+  // set) or NULL; bol0: the position bob starts a line (the byte before the
+  // buffer is '\n', or the buffer begins the input); nul: option N, empty
+  // matches are reported
   const uint32_t* acap;
   uint32_t bol0;
   uint32_t nul;
+  uint32_t ctx_word;
+  // the number of acap entries (4 * states, or ctx_word: 64 * distinct rows)
+  // and, ctx_word, each state's row (tables.hpp acap_rows / acap_map)
+  uint32_t acap_n;
+  const uint32_t* amap;
   // sparse_kernel walk truncation: per wave, the open walk (COUNT pass writes,
   // fix_kernel resolves, the WRITE pass reads); NULL: walks run to rend
   OpenRec* open;
@@ -295,7 +301,7 @@ uint32_t utf8_tile();
 hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream);
 uint32_t wfind_unit();
 uint32_t wfind_waves();
-size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, bool ctx);  // ctx: anchors / N
+size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, uint32_t nacap, uint32_t nmap);
 // immediate-transducer kernel, xi_kernel.hip (COUNT mode only)
 hipError_t launch_xi(const ScanParams& P, size_t smem, hipStream_t stream);
 hipError_t xi_occupancy(size_t smem, int* blocks_per_cu);

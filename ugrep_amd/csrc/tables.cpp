@@ -36,6 +36,31 @@ struct RawState {
 };
 
 constexpr uint32_t kMetaBol = 0x09, kMetaEol = 0x0a;  // META_BOL / META_EOL - META_MIN (pattern.h:942-943)
+// word boundaries (pattern.h:933-940): WBB WBE NWB NWE BWB EWB BWE EWE
+constexpr uint32_t kMetaWordMin = 0x01, kMetaWordMax = 0x08;
+
+// Whether meta edge `op` holds in context ctx (tables.hpp CTX_*), as the
+// interpreter tests it after fetching the byte at the current position
+// (lib/matcher.cpp:294-404; include/reflex/matcher.h:1281-1319 at_ewe ..
+// at_wbb over at_wb/at_bw of the match begin and at_ew/at_we of the position).
+bool meta_holds(uint32_t op, uint32_t ctx, bool word)
+{
+  if (!word) return op == kMetaBol ? (ctx & 2) != 0 : (ctx & 1) != 0;  // (line contexts: bit 1 bol, bit 0 eol)
+  const bool eol = ctx & CTX_EOL, ew = ctx & CTX_EW, we = ctx & CTX_WE, bol = ctx & CTX_BOL, wb = ctx & CTX_WB,
+             bw = ctx & CTX_BW;
+  switch (op) {
+    case 0x01: return bw == wb;    // META_WBB \b at begin: at_bw() == at_wb()
+    case 0x02: return we == ew;    // META_WBE \b at end:   at_we() == at_ew()
+    case 0x03: return bw != wb;    // META_NWB \B at begin
+    case 0x04: return we != ew;    // META_NWE \B at end
+    case 0x05: return bw && wb;    // META_BWB \< at begin
+    case 0x06: return !bw && !wb;  // META_EWB \> at begin
+    case 0x07: return !we && !ew;  // META_BWE \< at end
+    case 0x08: return we && ew;    // META_EWE \> at end
+    case kMetaBol: return bol;
+    default: return eol;           // kMetaEol
+  }
+}
 
 // Bucket approximation used by the GPU prefilter: the bytes whose 3-bit
 // fields (lo3, mid3, hi2) each occur among the members' fields.
@@ -338,7 +363,8 @@ void build_xu(const std::vector<uint32_t>& nxt, uint32_t S, uint32_t first_acc, 
 bool tables_equivalent(const DfaTables& a, const DfaTables& b)
 {
   auto step = [](const DfaTables& t, uint32_t s, int c) {
-    return (uint32_t)t.trans[(size_t)s * t.row + (t.format == FMT_BYTE ? (uint32_t)c : t.cls[c])] / t.row;
+    const size_t i = (size_t)s * t.row + (t.format == FMT_BYTE ? (uint32_t)c : t.cls[c]);
+    return t.format == FMT_WIDE ? t.trans32[i] / t.row : (uint32_t)t.trans[i] / t.row;  // (wide: u32 entries)
   };
   auto live = [&](const DfaTables& t) {  // co-reachable states
     std::vector<std::vector<uint32_t> > rev(t.states);
@@ -365,6 +391,12 @@ bool tables_equivalent(const DfaTables& a, const DfaTables& b)
     }
     return ok;
   };
+  // the accept of state s in a 64-context (ctx_bits.hpp) of either layout
+  auto acc = [](const DfaTables& t, uint32_t s, uint32_t ctx) -> uint32_t {
+    if (t.ctx_word) return t.acap[(size_t)s * 64 + ctx];
+    if (t.anchored) return t.acap[(size_t)s * 4 + ((ctx & CTX_BOL) ? 2 : 0) + ((ctx & CTX_EOL) ? 1 : 0)];
+    return t.caps[s];
+  };
   const std::vector<bool> la = live(a), lb = live(b);
   const uint32_t sa = a.start / a.row, sb = b.start / b.row;
   std::set<std::pair<uint32_t, uint32_t> > seen;
@@ -379,6 +411,9 @@ bool tables_equivalent(const DfaTables& a, const DfaTables& b)
     if ((p.first == 0) != (p.second == 0)) return false;
     if (p.first == 0) continue;
     if (a.caps[p.first] != b.caps[p.second]) return false;
+    if (a.anchored || b.anchored)
+      for (uint32_t ctx = 0; ctx < 64; ++ctx)
+        if (acc(a, p.first, ctx) != acc(b, p.second, ctx)) return false;
     for (int c = 0; c < 256; ++c) {
       const std::pair<uint32_t, uint32_t> q(norm(la, step(a, p.first, c)), norm(lb, step(b, p.second, c)));
       if (seen.insert(q).second) work.push_back(q);
@@ -410,8 +445,8 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
         cap = w & 0xffffff;
       } else if (word_is_meta(w)) {
         const uint32_t idx = w & 0xffff;
-        if (op != kMetaBol && op != kMetaEol) {
-          err = "opcode table uses meta edges other than ^ and $ (word boundaries, \\A, \\Z, indent)";
+        if (op != kMetaBol && op != kMetaEol && !(op >= kMetaWordMin && op <= kMetaWordMax)) {
+          err = "opcode table uses meta edges other than ^, $ and word boundaries (\\A, \\Z, indent)";
           return 1;
         }
         uint64_t t = idx;
@@ -497,18 +532,22 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   // that holds, that target's TAKE, its first meta edge that holds, ... (at
   // most 5 meta jumps); a meta target that goes on with byte edges is not
   // supported (the reference would continue that walk from the same byte)
+  // (word boundaries: 64 contexts, tables.hpp CTX_*; line anchors only: 4)
   const uint32_t n = (uint32_t)raw.size();
-  bool anchored = false;
-  std::vector<uint32_t> acc4((size_t)n * 4, 0);
+  bool anchored = false, word = false;
   for (uint32_t i = 0; i < n; ++i) {
     anchored = anchored || !raw[i].metas.empty();
-    for (uint32_t ctx = 0; ctx < 4; ++ctx) {
-      const bool bol = ctx & 2, eol = ctx & 1;
+    for (const auto& m : raw[i].metas) word = word || (m.first >= kMetaWordMin && m.first <= kMetaWordMax);
+  }
+  const uint32_t nctx = word ? 64u : 4u;
+  std::vector<uint32_t> acc4((size_t)n * nctx, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    for (uint32_t ctx = 0; ctx < nctx; ++ctx) {
       uint32_t cap = raw[i].cap, cur = i;
       for (int jumps = 0; jumps < 5; ++jumps) {
         uint32_t to = ~0u;
         for (const auto& m : raw[cur].metas)
-          if ((m.first == kMetaBol && bol) || (m.first == kMetaEol && eol)) {
+          if (meta_holds(m.first, ctx, word)) {
             to = index_of_pc[m.second];
             break;
           }
@@ -521,11 +560,13 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
         if (raw[to].cap) cap = raw[to].cap;
         cur = to;
       }
-      acc4[(size_t)i * 4 + ctx] = cap;
+      acc4[(size_t)i * nctx + ctx] = cap;
     }
   }
   auto accepts = [&](uint32_t i) {
-    return acc4[(size_t)i * 4] | acc4[(size_t)i * 4 + 1] | acc4[(size_t)i * 4 + 2] | acc4[(size_t)i * 4 + 3];
+    uint32_t a = 0;
+    for (uint32_t ctx = 0; ctx < nctx; ++ctx) a |= acc4[(size_t)i * nctx + ctx];
+    return a;
   };
   // renumber: dead = 0, non-accepting states, then accepting states (for an
   // anchored table: accepting in some context)
@@ -540,12 +581,12 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
 
   // dense next[sid][byte] in new ids
   std::vector<uint32_t> nxt((size_t)S * 256, 0);
-  std::vector<uint32_t> caps(S, 0), acap((size_t)S * 4, 0);
+  std::vector<uint32_t> caps(S, 0), acap((size_t)S * nctx, 0);
   for (uint32_t i = 0; i < n; ++i) {
     caps[sid[i]] = raw[i].cap;
-    for (uint32_t ctx = 0; ctx < 4; ++ctx) acap[(size_t)sid[i] * 4 + ctx] = acc4[(size_t)i * 4 + ctx];
+    for (uint32_t ctx = 0; ctx < nctx; ++ctx) acap[(size_t)sid[i] * nctx + ctx] = acc4[(size_t)i * nctx + ctx];
     if (anchored && !raw[i].cap) {  // (caps: the state's accept in some context, for the prefilter's superset)
-      for (uint32_t ctx = 0; ctx < 4 && !caps[sid[i]]; ++ctx) caps[sid[i]] = acc4[(size_t)i * 4 + ctx];
+      for (uint32_t ctx = 0; ctx < nctx && !caps[sid[i]]; ++ctx) caps[sid[i]] = acc4[(size_t)i * nctx + ctx];
     }
     for (int c = 0; c < 256; ++c) {
       int64_t t = raw[i].target_pc[c];
@@ -607,6 +648,55 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   t.caps = caps;
   t.acap = acap;
   t.anchored = anchored;
+  t.ctx_word = word;
+  if (word) {
+    std::map<std::vector<uint32_t>, uint32_t> rows;
+    rows.emplace(std::vector<uint32_t>(64, 0), 0u);
+    t.acap_rows.assign(64, 0);
+    t.acap_map.assign(S, 0);
+    for (uint32_t s = 0; s < S; ++s) {
+      std::vector<uint32_t> r(acap.begin() + (size_t)s * 64, acap.begin() + (size_t)(s + 1) * 64);
+      auto it = rows.find(r);
+      if (it == rows.end()) {
+        it = rows.emplace(r, (uint32_t)rows.size()).first;
+        t.acap_rows.insert(t.acap_rows.end(), r.begin(), r.end());
+      }
+      t.acap_map[s] = it->second;
+    }
+  }
+  // shape (ugpu_dfa_info.shape): a finite language (no cycle reachable from
+  // the start), and word-context accepts in states that also go on with bytes
+  {
+    std::vector<uint8_t> color(S, 0);  // 0 new, 1 on the path, 2 done
+    std::vector<std::pair<uint32_t, int>> stack;
+    bool cycle = false;
+    stack.emplace_back(sid[0], 0);
+    color[sid[0]] = 1;
+    while (!stack.empty() && !cycle) {
+      auto& top = stack.back();
+      if (top.second == 256) {
+        color[top.first] = 2;
+        stack.pop_back();
+        continue;
+      }
+      const uint32_t v = nxt[(size_t)top.first * 256 + top.second++];
+      if (v == 0) continue;
+      if (color[v] == 1) cycle = true;
+      else if (color[v] == 0) {
+        color[v] = 1;
+        stack.emplace_back(v, 0);
+      }
+    }
+    t.finite = !cycle;
+    t.word_cond_edges = false;
+    if (word)
+      for (uint32_t s = 1; s < S && !t.word_cond_edges; ++s) {
+        bool uniform = true, edges = false;
+        for (uint32_t ctx = 1; ctx < nctx; ++ctx) uniform = uniform && acap[(size_t)s * nctx + ctx] == acap[(size_t)s * nctx];
+        for (int c = 0; c < 256 && !edges; ++c) edges = nxt[(size_t)s * 256 + c] != 0;
+        t.word_cond_edges = !uniform && edges;
+      }
+  }
   const uint32_t start_sid = sid[0];
   t.start_acc = start_sid >= first_acc;
   // FIND transducer for restart-local tables (tables.hpp); none of the

@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <string>
 #include <vector>
+#include "ctx_bits.hpp"
 
 namespace ugpu {
 
@@ -129,9 +130,23 @@ struct DfaTables {
   // anchored: the table has meta edges, so its acceptance is conditional and
   // only the context walk (device_common.hpp walk mode 2) may scan it.
   // start_acc: the start state accepts in some context (empty matches).
-  bool anchored = false, start_acc = false;
-  std::vector<uint32_t> acap;  // states * 4
+  // Word boundaries (META_WBB .. META_EWE, pattern.h:933-940; ctx_word): the
+  // context grows to 64 (CTX_* below) -- acap[sid * 64 + ctx] -- with the
+  // match begin's at_wb / at_bw (fixed at the walk start like bol) and the
+  // position's at_ew / at_we (include/reflex/matcher.h:1194-1319).  Meta
+  // targets must be accept-only states (a meta edge into byte edges makes the
+  // interpreter backtrack, lib/matcher.cpp:405-460: UGPU_UNSUPPORTED).
+  bool anchored = false, start_acc = false, ctx_word = false;
+  // ctx_word: the distinct 64-context rows of acap (row 0 all zero) and each
+  // state's row -- the device form (tables fit LDS: most states share a row)
+  std::vector<uint32_t> acap_rows, acap_map;
+  // shape: the language is finite (acyclic DFA); a state whose accept depends
+  // on the word context also has byte edges
+  bool finite = false, word_cond_edges = false;
+  std::vector<uint32_t> acap;  // states * 4, or states * 64 (ctx_word)
 };
+
+// (context bits CTX_*: ctx_bits.hpp)
 
 // xu codes.  Bits 0-3: a thermometer of the token's bytes (bit k: the token
 // covers byte x + k; 0x0F = a 4-byte token may start here, XU_SLOW: the kernel

@@ -34,11 +34,11 @@ constexpr uint32_t kWUnit = 4096;   // bytes per tile (records hold whole tiles)
 constexpr int kWWaves = UGPU_WF_WAVES;  // waves (records) per workgroup: one staged table copy
 
 // LDS image: transitions (u16, ntrans_pad), accept indices (u32 per state;
-// mode kWalkCtx: 4 per state, tables.hpp acap), Word ranges (2 x u32 each),
-// class bytes (256)
-__host__ __device__ inline size_t wfind_smem(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, bool ctx)
+// mode kWalkCtx: acap, P.acap_n entries), the per-state acap rows of word
+// boundary tables (u32, nmap), Word ranges (2 x u32 each), class bytes (256)
+__host__ __device__ inline size_t wfind_smem(uint32_t ntrans_pad, uint32_t nwtab, uint32_t nacap, uint32_t nmap)
 {
-  return 2 * (size_t)ntrans_pad + 4 * (size_t)nstates * (ctx ? 4 : 1) + 8 * (size_t)nwtab + 256;
+  return 2 * (size_t)ntrans_pad + 4 * ((size_t)nacap + nmap) + 8 * (size_t)nwtab + 256;
 }
 
 // M: kWalkWord (option W) or kWalkCtx (line anchors / option N): the same
@@ -47,25 +47,27 @@ template <int FMT, bool WRITE, int M>
 __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
-  const uint32_t ncaps = M == kWalkCtx ? 4 * P.nstates : P.nstates;
-  const uint32_t nwt = M == kWalkCtx ? 0u : P.nwtab;
+  const uint32_t ncaps = M == kWalkCtx ? P.acap_n : P.nstates;
+  const uint32_t nmap = M == kWalkCtx && P.ctx_word ? P.nstates : 0u;
+  const uint32_t nwt = M == kWalkCtx && !P.ctx_word ? 0u : P.nwtab;
   {
     // stage the tables once per workgroup (the walks look them up per byte)
     uint16_t* tr = reinterpret_cast<uint16_t*>(wsm);
     uint32_t* cp = reinterpret_cast<uint32_t*>(wsm + 2 * (size_t)P.ntrans_pad);
-    uint32_t* wt = cp + ncaps;
+    uint32_t* wt = cp + ncaps + nmap;
     uint8_t* cl = reinterpret_cast<uint8_t*>(wt + 2 * nwt);
     const uint32_t* caps = M == kWalkCtx ? P.acap : P.caps;
     if constexpr (FMT != 2)  // (wide tables stay in global memory)
       for (uint32_t i = threadIdx.x; i < P.ntrans_pad; i += blockDim.x) tr[i] = P.trans[i];
     for (uint32_t i = threadIdx.x; i < ncaps; i += blockDim.x) cp[i] = caps[i];
+    for (uint32_t i = threadIdx.x; i < nmap; i += blockDim.x) cp[ncaps + i] = P.amap[i];
     for (uint32_t i = threadIdx.x; i < 2 * nwt; i += blockDim.x) wt[i] = P.wtab[i];
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) cl[i] = P.cls[i];
     __syncthreads();
   }
   const uint16_t* s_trans = reinterpret_cast<const uint16_t*>(wsm);
   const uint32_t* s_caps = reinterpret_cast<const uint32_t*>(wsm + 2 * (size_t)P.ntrans_pad);
-  const uint32_t* s_wtab = s_caps + ncaps;
+  const uint32_t* s_wtab = s_caps + ncaps + nmap;
   const uint8_t* s_cls = reinterpret_cast<const uint8_t*>(s_wtab + 2 * nwt);
   const int lane = threadIdx.x & 63;
   const uint64_t r = (uint64_t)blockIdx.x * kWWaves + (threadIdx.x >> 6);
@@ -87,6 +89,7 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
   Win w = win_of(P);
   w.wtab = s_wtab;
   w.acap = s_caps;
+  w.amap = s_caps + ncaps;
   uint32_t ovf = 0;
 
   // speculative lane chains (lane 0 enters at the record's entry)
@@ -144,7 +147,8 @@ __global__ __launch_bounds__(kWWaves * 64) void wfind_kernel(ScanParams P)
 template <int FMT, bool WRITE, int M>
 hipError_t wfind_one(const ScanParams& P, hipStream_t stream)
 {
-  const size_t smem = wfind_smem(P.ntrans_pad, P.nstates, P.nwtab, M == kWalkCtx);
+  const size_t smem = wfind_smem(P.ntrans_pad, P.nwtab, M == kWalkCtx ? P.acap_n : P.nstates,
+                                 M == kWalkCtx && P.ctx_word ? P.nstates : 0u);
   static size_t attr_smem = 65536;
   if (smem > attr_smem) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wfind_kernel<FMT, WRITE, M>),
@@ -168,9 +172,10 @@ hipError_t wfind_mode(const ScanParams& P, uint32_t format, bool write, hipStrea
 
 uint32_t wfind_unit() { return kWUnit; }
 uint32_t wfind_waves() { return kWWaves; }
-size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, bool ctx)
+size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, uint32_t nacap, uint32_t nmap)
 {
-  return wfind_smem(ntrans_pad, nstates, nwtab, ctx);
+  (void)nstates;
+  return wfind_smem(ntrans_pad, nwtab, nacap, nmap);
 }
 
 // option W (P.wtab), line anchors / option N (P.acap), or neither (wide

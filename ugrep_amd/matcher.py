@@ -79,7 +79,7 @@ def host_context(opc):
     a, p = _as_u32(opc)
     info = _lib.DfaInfo()
     check(lib.ugpu_tables_build_host(p, len(a), ctypes.byref(info), None, 0, None, None, 0, None, None))
-    acap = np.zeros(info.states * 4, np.uint32)
+    acap = np.zeros(info.states * max(info.contexts, 4), np.uint32)
     an, sa = ctypes.c_int(), ctypes.c_int()
     check(lib.ugpu_tables_context_host(p, len(a), acap.ctypes.data_as(_lib.c_u32p), len(acap), ctypes.byref(an),
                                        ctypes.byref(sa)))
