@@ -346,17 +346,23 @@ def main():
 
     recs_dev = {}  # --offsets: device record arrays, grown outside the timed steps when possible
 
+    # 12-byte records (start, len) when every match has the same accept index
+    # (C3, C4); 16 bytes with the accept index otherwise (C2: 3)
+    one_accept = bool(info["shape"] & ugrep_amd._lib.SHAPE_ONE_ACCEPT)
+
     def records(count):
         if recs_dev.get("cap", -1) < count:
             cap = count + count // 8 + 1024
             recs_dev.update(cap=cap, start=torch.empty(cap, dtype=torch.int64, device=dev),
                             len=torch.empty(cap, dtype=torch.int32, device=dev),
-                            acc=torch.empty(cap, dtype=torch.int32, device=dev))
-        sc.offsets(recs_dev["start"].data_ptr(), recs_dev["len"].data_ptr(), recs_dev["acc"].data_ptr(), count,
-                   sptr)
-        st, ln, ac = recs_dev["start"][:count], recs_dev["len"][:count], recs_dev["acc"][:count]
+                            acc=None if one_accept else torch.empty(cap, dtype=torch.int32, device=dev))
+        acc = recs_dev["acc"]
+        sc.offsets(recs_dev["start"].data_ptr(), recs_dev["len"].data_ptr(), 0 if acc is None else acc.data_ptr(),
+                   count, sptr)
+        st, ln = recs_dev["start"][:count], recs_dev["len"][:count]
+        ac = None if acc is None else acc[:count]
         if pg:
-            st, ln, ac = gather_offsets(st.to(xdev), ln.to(xdev), ac.to(xdev))
+            st, ln, ac = gather_offsets(st.to(xdev), ln.to(xdev), None if ac is None else ac.to(xdev))
         return st, ln, ac
 
     def step():
@@ -477,7 +483,7 @@ def main():
         st, ln, _ = res["records"]
         m64 = (1 << 64) - 1
         dg = int((st * 31 + ln.to(torch.int64)).sum().item()) & m64  # int64 sums wrap like the u64 digest
-        out["offsets"] = {"records": int(st.numel()), "bytes_per_record": 16,
+        out["offsets"] = {"records": int(st.numel()), "bytes_per_record": 12 if one_accept else 16,
                           "gathered_to": "all ranks" if pg else "local",
                           "digest_matches_totals": int(st.numel()) == res["count"] and dg == res["digest"]}
     tr = measured_traffic(args.config, hi - lo, KERNELS[info["kernel"]])

@@ -77,6 +77,7 @@ typedef struct ugpu_dfa_info
 
 #define UGPU_SHAPE_FINITE 1u     /* the language is finite (no cycle in the DFA) */
 #define UGPU_SHAPE_WORD_COND 2u  /* a state whose accept depends on a word boundary also has byte edges */
+#define UGPU_SHAPE_ONE_ACCEPT 4u /* every match has the same accept index: 12-byte records (ugpu_scan_offsets d_cap NULL) */
 
 /* Totals of one scan.  digest = sum(start*31 + len), dcap = sum((start+1)*cap),
    both mod 2^64, start = byte offset + bias. */
@@ -283,7 +284,10 @@ int ugpu_scanner_context(ugpu_scanner *sc, int bol0);
 /* Synchronize the scanner's stream and return the totals of the last scan. */
 int ugpu_scan_totals(ugpu_scanner *sc, ugpu_totals *out);
 /* After ugpu_scan + ugpu_scan_totals: write the match records of the last scan
-   into device arrays (capacity entries each) on `stream`. */
+   into device arrays (capacity entries each) on `stream`.  d_cap may be NULL
+   for a table with one accept index (ugpu_dfa_info.accepting states all take
+   the same index; the records are then 12 bytes: start, len) -- the accept
+   index of every record is that index; UGPU_INVAL for other tables. */
 int ugpu_scan_offsets(ugpu_scanner *sc, uint64_t *d_start, uint32_t *d_len, uint32_t *d_cap, uint64_t capacity,
                       void *stream);
 /* Shard-boundary stitch: the scan of [lo,hi) assumed the chain entered at

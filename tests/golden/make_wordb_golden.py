@@ -51,6 +51,11 @@ PATTERNS = [
     r"^foo\b", r"\bfoo$", r"^\<\w\w\>$",
     # assertions alone
     r"\b", r"\B", r"\<", r"\>",
+    # alternatives ending at the same byte under different assertions: the
+    # accept is the first meta edge that holds in descending META code, not
+    # the lowest satisfied index (^ab|ab$ with both: 2)
+    r"\bé|é\b|\Bx\B", r"\bab|ab\b", r"ab\>|ab|\bab", r"\bab\b|ab\b", r"^ab|ab$", r"^ab$|ab$", r"\bfoo\b|foo",
+    r"\<the|the\>|\Bthe",
 ]
 MODES = ["re", "reN", "reU"]
 

@@ -92,7 +92,7 @@ def test_stitch_nonsynchronising(patterns):
     assert out["fixes"] == 1
 
 
-def _gather_worker(rank, world, port, recs, dst, q):
+def _gather_worker(rank, world, port, recs, dst, q, no_cap=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -101,15 +101,16 @@ def _gather_worker(rank, world, port, recs, dst, q):
         from ugrep_amd.dist import gather_offsets
         mine = np.asarray(recs[rank], dtype=np.int64).reshape(-1, 3)
         out = gather_offsets(torch.from_numpy(mine[:, 0].copy()), torch.from_numpy(mine[:, 1].astype(np.int32)),
-                             torch.from_numpy(mine[:, 2].astype(np.int32)), dst=dst)
-        q.put((rank, None if out is None else [t.tolist() for t in out]))
+                             None if no_cap else torch.from_numpy(mine[:, 2].astype(np.int32)), dst=dst)
+        q.put((rank, None if out is None else [None if t is None else t.tolist() for t in out]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,dst", [(2, None), (3, None), (3, 1)])
-def test_gather_offsets(patterns, world, dst):
-    """Per-shard records of the true chain, exchanged, equal one sequential scan's list."""
+@pytest.mark.parametrize("world,dst,no_cap", [(2, None, False), (3, None, False), (3, 1, False), (3, None, True)])
+def test_gather_offsets(patterns, world, dst, no_cap):
+    """Per-shard records of the true chain, exchanged, equal one sequential scan's
+    list (no_cap: 12-byte records, one accept index)."""
     from oracle_lib import OracleDfa, gen
     from ugrep_amd.dist import shard_bounds
     data = gen(3, 5, 0, 50021)
@@ -124,7 +125,7 @@ def test_gather_offsets(patterns, world, dst):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, recs, dst, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, recs, dst, q, no_cap)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
@@ -136,4 +137,8 @@ def test_gather_offsets(patterns, world, dst):
             assert res[r] is None
             continue
         s, ln, cp = res[r]
-        assert [list(t) for t in zip(s, ln, cp)] == [list(m) for m in want]
+        if no_cap:
+            assert cp is None
+            assert [list(t) for t in zip(s, ln)] == [m[:2] for m in want]
+        else:
+            assert [list(t) for t in zip(s, ln, cp)] == [list(m) for m in want]

@@ -89,7 +89,7 @@ struct AbsWriteEm {
     if (idx < capacity) {
       start[idx] = base + p;
       len[idx] = l;
-      cap[idx] = caps[le >> log_row];
+      if (cap) cap[idx] = caps[le >> log_row];  // (NULL: 12-byte records, one accept index)
     } else {
       overflow = 1;
     }

@@ -395,7 +395,7 @@ struct WriteEm {
     if (idx < capacity) {
       start[idx] = pos + (uint64_t)c.delta;
       len[idx] = (uint32_t)l;
-      cap[idx] = c.caps[le >> c.log_row];
+      if (cap) cap[idx] = c.caps[le >> c.log_row];  // (NULL: 12-byte records, one accept index)
     } else {
       overflow = 1;
     }

@@ -133,7 +133,7 @@ struct ugpu_scanner {
   uint64_t* d_entries = nullptr;
   uint64_t* d_obase = nullptr;
   // xc_kernel COUNT passes of record scanners also write the In bits
-  // (ScanParams::inbits) when UGPU_XC_BITMAP is on; OFFSETS then expands them
+  // (ScanParams::inbits) unless UGPU_XC_BITMAP=0; OFFSETS then expands them
   uint16_t* d_inbits = nullptr;
   uint64_t inbits_cap = 0;  // bytes
   uint64_t* d_fix = nullptr;  // xc_kernel OFFSETS: per wave, the record whose start an earlier wave wrote
@@ -473,7 +473,8 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, ugpu_dfa_info* info)
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
   info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;
-  info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u);
+  info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u) |
+                (t.cap1 != 0 && !t.anchored ? UGPU_SHAPE_ONE_ACCEPT : 0u);
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
   const char* cenv = std::getenv("UGPU_XC");
@@ -702,7 +703,8 @@ int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* inf
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
   info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;
-  info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u);
+  info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u) |
+                (t.cap1 != 0 && !t.anchored ? UGPU_SHAPE_ONE_ACCEPT : 0u);
   info->kernel = (t.filter && t.format == FMT_BYTE) ? 0u
                  : t.format == FMT_WIDE              ? 4u
                  : (t.xc && t.cap1 != 0)             ? 5u
@@ -1137,7 +1139,10 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   }
   s->stage_once = false;
   P.inbits = nullptr;
-  if (s->pref_write && s->xc && !s->word && !P.xc_w && !P.xu_w && env_u64("UGPU_XC_BITMAP", 0) != 0) {
+  // (default on, round 4: with the expansion's coalesced length stores and
+  // 12-byte records, C4 OFFSETS 6.4 ms against 8.1 ms for the WRITE pass, C3
+  // 9.8 against 11.7 ms, profiles/r04_offsets_ab.txt; UGPU_XC_BITMAP=0 restores it)
+  if (s->pref_write && s->xc && !s->word && !P.xc_w && !P.xu_w && env_u64("UGPU_XC_BITMAP", 1) != 0) {
     // one bit per byte up to the chunk after the readable end (the last wave
     // searches for the exit up to there)
     const uint64_t need = ((((P.rend + 15) & ~uint64_t(15)) + 2048) >> 3) + 64;
@@ -1278,6 +1283,8 @@ int ugpu_scan_offsets(ugpu_scanner* s, uint64_t* d_start, uint32_t* d_len, uint3
                       void* stream)
 {
   if (!s || !s->have_scan) return fail(UGPU_INVAL, "no scan issued");
+  if (!d_cap && (s->dfa->t.cap1 == 0 || s->dfa->t.anchored))
+    return fail(UGPU_INVAL, "the table has several accept indices: d_cap is needed");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(hipStreamSynchronize(s->stream));
   ScanParams P = s->last;

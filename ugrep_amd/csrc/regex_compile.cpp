@@ -427,11 +427,16 @@ class Parser
       fail(UGPU_INVAL, "empty first alternative");  // the reference rejects "|a" (but not "a|")
     for (;;)
     {
-      bol_ = eol_ = false;
-      wmask_ = 0x3F;
+      eol_ = false;
+      begin_.clear();
+      end_.clear();
       alts.push_back(parse_concat(true));
-      anchors.push_back((bol_ ? 1 : 0) | (eol_ ? 2 : 0));
-      wmasks.push_back(wmask_);
+      // the alternative's meta edges in the order RE/flex chains them after
+      // its last byte: the end assertions as written, then the begin ones
+      // (^ \< ... moved to the accept side), e.g. ^\<ab\>$ -> EWE EOL BOL BWB
+      std::vector<uint8_t> seq(end_);
+      seq.insert(seq.end(), begin_.begin(), begin_.end());
+      metaseqs.push_back(seq);
       if (p_ >= s_.size() || s_[p_] != '|')
         break;
       ++p_;
@@ -441,12 +446,9 @@ class Parser
     return alts;
   }
 
-  // per top-level alternative: 1 = starts with ^, 2 = ends with $
-  std::vector<int> anchors;
-  // per top-level alternative: the word-boundary classes its accept allows,
-  // bits 0-2 of the match begin (A: at_bw && at_wb, B: neither, N: one of
-  // them) and bits 3-5 of the match end (A: at_we && at_ew, B: neither, N)
-  std::vector<int> wmasks;
+  // per top-level alternative: the meta edges (META - META_MIN) its accept
+  // passes through, in chain order
+  std::vector<std::vector<uint8_t>> metaseqs;
 
  private:
   const std::string &s_;
@@ -456,8 +458,8 @@ class Parser
   bool ic_;             // case-insensitive (flag, or RE/flex (?i) in REFLEX mode)
   bool dotall_ = false;  // REFLEX mode (?s): '.' matches '\n'
   bool multiline_ = false;  // REFLEX mode (?m): ^ and $ are line anchors
-  bool bol_ = false, eol_ = false;  // anchors of the top-level alternative being parsed
-  int wmask_ = 0x3F;                // word-boundary classes of the alternative being parsed
+  bool eol_ = false;  // the top-level alternative being parsed ended with $
+  std::vector<uint8_t> begin_, end_;  // its begin / end assertions (META - META_MIN), as written
 
   // a word-boundary assertion at p_ (\b \B \< \>): its class mask (for the
   // begin of the match, bits 0-2; as the reference's META_WBB/NWB/BWB/EWB and
@@ -522,7 +524,13 @@ class Parser
         {
           if (p_ + 1 < s_.size() && strchr("*+?{", s_[p_ + 1]) != NULL)
             fail(UGPU_UNSUPPORTED, "repeated anchor");
-          (first ? bol_ : eol_) = true;
+          if (first)
+            begin_.push_back(0x09);  // META_BOL
+          else
+          {
+            end_.push_back(0x0a);  // META_EOL
+            eol_ = true;
+          }
           ++p_;
           continue;
         }
@@ -547,13 +555,13 @@ class Parser
           if (p_ + 2 < s_.size() && strchr("*+?{", s_[p_ + 2]) != NULL)
             fail(UGPU_UNSUPPORTED, "repeated word boundary");
           const int m = word_assertion(p_);
-          // an assertion with atoms after it tests the match begin, one with
-          // none (also an alternative of assertions only: "\\b" compiles to
-          // META_WBE) the end.  \< at the end of a match is a begin of a word
-          // there (B of the end pair: no word before, a word after), \> an end (A)
-          const bool at_end = last;
-          const int cls = !at_end ? m : (m == 1 ? 2 : m == 2 ? 1 : m);
-          wmask_ &= !at_end ? (cls | 0x38) : (cls << 3 | 0x07);
+          // an assertion with atoms after it tests the match begin
+          // (META_WBB NWB BWB EWB), one with none the end (META_WBE NWE BWE
+          // EWE; also an alternative of assertions only: "\\b" compiles to
+          // META_WBE)
+          const uint8_t code = last ? (m == 3 ? 0x02 : m == 4 ? 0x04 : m == 1 ? 0x07 : 0x08)
+                                    : (m == 3 ? 0x01 : m == 4 ? 0x03 : m == 1 ? 0x05 : 0x06);
+          (last ? end_ : begin_).push_back(code);
           p_ += 2;
           continue;
         }
@@ -1309,8 +1317,7 @@ struct Glushkov
   std::vector<ByteSet> bytes;            // position -> bytes
   std::vector<std::vector<int>> follow;  // position -> follow positions
   std::vector<int> accept;               // position -> accept index (end markers), 0 otherwise
-  std::vector<int> anchor;               // end marker -> 1: needs a walk begun at a line begin, 2: needs a line end next
-  std::vector<int> wmask;                // end marker -> word-boundary classes allowed (Parser::wmasks)
+  std::vector<std::vector<uint8_t>> metas;  // end marker -> its alternative's meta edges (Parser::metaseqs)
 
   struct Info
   {
@@ -1338,8 +1345,7 @@ struct Glushkov
     bytes.push_back(b);
     follow.emplace_back();
     accept.push_back(acc);
-    anchor.push_back(0);
-    wmask.push_back(0x3F);
+    metas.emplace_back();
     return static_cast<int>(bytes.size() - 1);
   }
 
@@ -1427,6 +1433,80 @@ inline uint32_t ctx_of(int bc, int ec, bool bol, bool eol)
   return c | (bol ? CTX_BOL : 0u) | (eol ? CTX_EOL : 0u);
 }
 
+// Whether meta edge `m` (META - META_MIN) holds in context ctx: 4 line
+// contexts (bit 0 bol, bit 1 eol) or 64 (ctx_bits.hpp)
+inline bool meta_holds_ctx(uint8_t m, uint32_t ctx, bool word)
+{
+  if (!word)
+    return m == 0x09 ? (ctx & 1) != 0 : m == 0x0a ? (ctx & 2) != 0 : false;
+  const bool eol = ctx & CTX_EOL, ew = ctx & CTX_EW, we = ctx & CTX_WE, bol = ctx & CTX_BOL, wb = ctx & CTX_WB,
+             bw = ctx & CTX_BW;
+  switch (m)
+  {
+    case 0x01: return bw == wb;
+    case 0x02: return we == ew;
+    case 0x03: return bw != wb;
+    case 0x04: return we != ew;
+    case 0x05: return bw && wb;
+    case 0x06: return !bw && !wb;
+    case 0x07: return !we && !ew;
+    case 0x08: return we && ew;
+    case 0x09: return bol;
+    default: return eol;
+  }
+}
+
+// The accept of a DFA state whose ends are `acc` (accept index, meta edges),
+// as RE/flex builds and the interpreter evaluates it (lib/matcher.cpp:193-450):
+// the state's TAKE is its lowest index without meta edges; its meta edges,
+// one per distinct next meta, are tried in descending META code (the order
+// encode_dfa emits them, lib/pattern.cpp:2945-2990), the first that holds is
+// followed to the alternatives that wait for it, whose finished ones give the
+// TAKE there (lowest index), and so on (at most 5 jumps).  So the accept is not
+// the lowest satisfied index: in ^ab|ab$ with both anchors holding, EOL is
+// tried first and gives 2.
+uint32_t meta_accept(const std::vector<std::pair<uint32_t, const std::vector<uint8_t> *>> &acc, uint32_t ctx,
+                     bool word)
+{
+  uint32_t cap = 0;
+  std::vector<std::pair<uint32_t, size_t>> cur;  // (index into acc, next meta)
+  for (size_t i = 0; i < acc.size(); ++i)
+  {
+    if (acc[i].second->empty())
+      cap = cap == 0 || acc[i].first < cap ? acc[i].first : cap;
+    else
+      cur.emplace_back(static_cast<uint32_t>(i), 0);
+  }
+  for (int jumps = 0; jumps < 5 && !cur.empty(); ++jumps)
+  {
+    int best = -1;
+    for (auto &c : cur)
+    {
+      const uint8_t m = (*acc[c.first].second)[c.second];
+      if (m > best && meta_holds_ctx(m, ctx, word))
+        best = m;
+    }
+    if (best < 0)
+      break;
+    std::vector<std::pair<uint32_t, size_t>> nxt;
+    uint32_t done = 0;
+    for (auto &c : cur)
+    {
+      const std::vector<uint8_t> &ms = *acc[c.first].second;
+      if (ms[c.second] != best)
+        continue;
+      if (c.second + 1 == ms.size())
+        done = done == 0 || acc[c.first].first < done ? acc[c.first].first : done;
+      else
+        nxt.emplace_back(c.first, c.second + 1);
+    }
+    if (done)
+      cap = done;
+    cur.swap(nxt);
+  }
+  return cap;
+}
+
 struct Dfa
 {
   std::vector<std::vector<uint32_t>> next;  // state -> 256 targets (0 = dead state)
@@ -1472,27 +1552,21 @@ Dfa subsets(Glushkov &g, const std::vector<int> &start)
   for (int b = 0; b < 256; ++b)
     if (rep[cls[b]] < 0)
       rep[cls[b]] = b;
-  for (int m : g.wmask)
-    if (m != 0x3F)
-      d.nctx = 64;
+  for (const auto &ms : g.metas)
+    for (uint8_t m : ms)
+      if (m <= 0x08)
+        d.nctx = 64;
   for (size_t k = 0; k < sets.size(); ++k)
   {
     std::vector<int> cur = sets[k];  // copy: sets grows
     CtxN cx(d.nctx, 0);
-    for (uint32_t ctx = 0; ctx < d.nctx; ++ctx)
-      for (int p : cur)
-      {
-        if (!g.accept[p])
-          continue;
-        bool ok;
-        if (d.nctx == 4)
-          ok = (g.anchor[p] & ~static_cast<int>(ctx)) == 0;
-        else
-          ok = (!(g.anchor[p] & 1) || (ctx & CTX_BOL)) && (!(g.anchor[p] & 2) || (ctx & CTX_EOL)) &&
-               ((g.wmask[p] >> bcls_of(ctx)) & 1) && ((g.wmask[p] >> (3 + ecls_of(ctx))) & 1);
-        if (ok && (cx[ctx] == 0 || static_cast<uint32_t>(g.accept[p]) < cx[ctx]))
-          cx[ctx] = g.accept[p];
-      }
+    std::vector<std::pair<uint32_t, const std::vector<uint8_t> *>> acc;  // (accept index, meta edges) of the state's ends
+    for (int p : cur)
+      if (g.accept[p])
+        acc.emplace_back(static_cast<uint32_t>(g.accept[p]), &g.metas[p]);
+    if (!acc.empty())
+      for (uint32_t ctx = 0; ctx < d.nctx; ++ctx)
+        cx[ctx] = meta_accept(acc, ctx, d.nctx == 64);
     d.acc.push_back(cx[0]);
     for (uint32_t ctx = 1; ctx < d.nctx; ++ctx)
       d.anchored = d.anchored || cx[ctx] != cx[0];
@@ -1924,8 +1998,8 @@ int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, 
     {
       Glushkov::Info info = g.walk(alts[k]);
       int end = g.new_pos(ByteSet(), static_cast<int>(k + 1));
-      g.anchor[end] = k < parser.anchors.size() ? parser.anchors[k] : 0;
-      g.wmask[end] = k < parser.wmasks.size() ? parser.wmasks[k] : 0x3F;
+      if (k < parser.metaseqs.size())
+        g.metas[end] = parser.metaseqs[k];
       g.link(info.last, std::vector<int>{end});
       Glushkov::merge(start, info.first);
       if (info.nullable)

@@ -938,7 +938,7 @@ __global__ __launch_bounds__(256) void stage_copy_kernel(ScanParams P)
   for (uint32_t i = threadIdx.x; i < n; i += 256) {
     P.out_start[base + i] = P.st_start[s0 + i];
     P.out_len[base + i] = P.st_len[s0 + i];
-    P.out_cap[base + i] = P.st_cap[s0 + i];
+    if (P.out_cap) P.out_cap[base + i] = P.st_cap[s0 + i];
   }
   __syncthreads();
   if (threadIdx.x == 0) P.st_n[b] = kStageDone;

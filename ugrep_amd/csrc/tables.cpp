@@ -410,10 +410,13 @@ bool tables_equivalent(const DfaTables& a, const DfaTables& b)
     work.pop_back();
     if ((p.first == 0) != (p.second == 0)) return false;
     if (p.first == 0) continue;
-    if (a.caps[p.first] != b.caps[p.second]) return false;
-    if (a.anchored || b.anchored)
+    if (a.anchored || b.anchored) {
+      // (conditional accepts: caps is only a prefilter superset there)
       for (uint32_t ctx = 0; ctx < 64; ++ctx)
         if (acc(a, p.first, ctx) != acc(b, p.second, ctx)) return false;
+    } else if (a.caps[p.first] != b.caps[p.second]) {
+      return false;
+    }
     for (int c = 0; c < 256; ++c) {
       const std::pair<uint32_t, uint32_t> q(norm(la, step(a, p.first, c)), norm(lb, step(b, p.second, c)));
       if (seen.insert(q).second) work.push_back(q);

@@ -635,7 +635,7 @@ __device__ __forceinline__ void cwrite(const CLane& L, const uint32_t cb[4], con
       if (st & bit) {
         if (cur < o.capacity) {
           o.start[cur] = pos;
-          o.cap[cur] = o.cap1;
+          if (o.cap) o.cap[cur] = o.cap1;
         } else {
           o.over = 1;
         }
@@ -674,12 +674,10 @@ __device__ __forceinline__ void cflush(const CPend& p, const uint16_t* slot, COu
   if (p.cur + p.R <= o.capacity && p.E <= p.cur + p.R) {
     // (all in range: wave-uniform bases, 32-bit lane offsets, no checks)
     uint64_t* const st = o.start + p.cur;
-    uint32_t* const cp = o.cap + p.cur;
     uint32_t* const ln = o.len + (p.cur - p.open);
-    for (uint32_t t = lane; t < p.R; t += 64) {
-      st[t] = p.q0 + S[t];
-      cp[t] = o.cap1;
-    }
+    for (uint32_t t = lane; t < p.R; t += 64) st[t] = p.q0 + S[t];
+    if (o.cap)  // (NULL: 12-byte records)
+      for (uint32_t t = lane; t < p.R; t += 64) o.cap[p.cur + t] = o.cap1;
     uint32_t t = lane;
     if (p.open && t == 0 && t < p.E) {  // the end of the match open at the chunk start
       const uint64_t e = p.q0 + En[0];
@@ -697,7 +695,7 @@ __device__ __forceinline__ void cflush(const CPend& p, const uint16_t* slot, COu
       const uint64_t i = p.cur + t;
       if (i < o.capacity) {
         o.start[i] = p.q0 + S[t];
-        o.cap[i] = o.cap1;
+        if (o.cap) o.cap[i] = o.cap1;
       } else {
         o.over = 1;
       }
@@ -768,10 +766,17 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
   uint32_t sb[4];
   cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb, sb);
   if constexpr (BM) {
-    uint32_t in[4];
+    if constexpr (U) {
+      uint32_t in[4];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) in[d] = (L.E[d] | ((L.E[d] >> 1) & cb[d])) & kOnes;  // In_i = G_i | X_i & In_{i-1}
-    ib[q >> 4] = (uint16_t)nib16(in);
+      for (int d = 0; d < 4; ++d) in[d] = (L.E[d] | ((L.E[d] >> 1) & cb[d])) & kOnes;  // In_i = G_i | X_i & In_{i-1}
+      ib[q >> 4] = (uint16_t)nib16(in);
+    } else {
+      // the carry-in bits C_i = In_{i-1}, which cfinish has anyway (the adder
+      // codes die here: fewer live registers than In_i); xc_expand_kernel
+      // shifts them
+      ib[q >> 4] = (uint16_t)nib16(cb);
+    }
   }
   if constexpr (WR) {
     if (pd)
@@ -1230,24 +1235,26 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_bm_kernel(ScanParams P)
 // from that wave's output base, and the ends in the range, which close the
 // match open at wlo first (index base - 1; its start was written by an
 // earlier block: the raw end goes into len and out_fix names the index for
-// xc_fix_kernel, as in the WRITE pass).  64-bit words of In bits, 256 a round;
-// the round's starts and lengths are ordered by block scans and staged in LDS,
-// then stored by consecutive threads.  No table, no walk: the pass reads 1/8
-// of the input's bytes and writes the records.
+// xc_fix_kernel, as in the WRITE pass).  64-bit words of In bits, 64 a
+// wave-round; the round's starts and ends are ordered by DPP scans and staged
+// in LDS (u16 offsets from the round's first position), then stored by
+// consecutive lanes -- starts, caps (none for 12-byte records) and lengths
+// (the k-th end of the round closes the k-th start, or the match open at
+// the round start) all leave as coalesced stores.  No table, no walk: the pass
+// reads 1/8 of the input's bytes and writes the records.
 constexpr int kXeThreads = 256;
-constexpr uint32_t kXeCap = 64 * kXeThreads / 2;  // records a round can hold (a start needs a 0 before it)
 
 // The range is cut into 4 quarters of whole words, one per wave.  A first
 // pass counts each quarter's starts and ends and finds its last start; after
 // one block barrier every wave knows its output bases and writes its quarter
-// alone: per round 64 words, one per lane, ordered by DPP scans, the starts
-// staged in the wave's LDS slice for coalesced stores.
-constexpr uint32_t kXeWaveCap = 64 * 32;  // starts a wave-round can hold
+// alone.
+constexpr uint32_t kXeWaveCap = 64 * 32;  // starts (and ends) a wave-round can hold
 
 template <bool U>
 __global__ __launch_bounds__(kXeThreads) void xc_expand_kernel(ScanParams P)
 {
-  __shared__ uint32_t st_off[4][kXeWaveCap];  // a round's start positions, from the round's first position
+  __shared__ uint16_t st_off[4][kXeWaveCap];  // a round's start positions, from the round's first position
+  __shared__ uint16_t en_off[4][kXeWaveCap];  // its end positions
   __shared__ uint32_t qs[4], qe[4];
   __shared__ int64_t ql[4];
   __shared__ uint64_t fix_s;
@@ -1263,13 +1270,43 @@ __global__ __launch_bounds__(kXeThreads) void xc_expand_kernel(ScanParams P)
   const bool last = any && whi == P.hi;
   const uint64_t end = !any ? wlo : last ? P.totals->exit + 1 : whi;  // event positions [wlo, end)
   const uint64_t* words = reinterpret_cast<const uint64_t*>(P.inbits);
-  // the events of word wi (positions [wlo, end) only)
-  auto events = [&](uint64_t wi, uint64_t& st, uint64_t& en) __attribute__((always_inline)) {
+  // the events of word wi (positions [wlo, end) only).  U: the bits are In_i;
+  // two-state tables: C_i = In_{i-1} (cchunk), so In_i is bit i + 1
+  // (loads and arithmetic apart: the passes issue the loads of several words,
+  // or of the next round, before they use any -- the pass is latency-bound)
+  struct Raw {
+    uint64_t a = 0, b = 0;  // word wi, and its neighbour (U: wi - 1, else wi + 1)
+  };
+  auto load_raw = [&](uint64_t wi) __attribute__((always_inline)) {
+    Raw r;
+    const uint64_t pos = wi * 64;
+    if (pos >= end || pos + 64 <= wlo) return r;
+    r.a = words[wi];
+    if constexpr (U) {
+      if (pos > P.lo) r.b = words[wi - 1];
+    } else {
+      // (C_{pos + 64}: the next wave's first bit at whi; for the wave holding
+      // hi, In is 0 from position end - 1 -- the exit -- on)
+      if (last ? pos + 64 < end : pos + 64 <= end) r.b = words[wi + 1];
+    }
+    return r;
+  };
+  auto events = [&](uint64_t wi, const Raw& r, uint64_t& st, uint64_t& en) __attribute__((always_inline)) {
     const uint64_t pos = wi * 64;
     st = en = 0;
     if (pos >= end || pos + 64 <= wlo) return;
-    const uint64_t w = words[wi];
-    const uint64_t prev = (w << 1) | (pos > P.lo ? words[wi - 1] >> 63 : 0ull);
+    uint64_t w, prev;
+    if constexpr (U) {
+      w = r.a;
+      prev = (w << 1) | (r.b >> 63);
+    } else {
+      prev = r.a;
+      w = (prev >> 1) | (r.b << 63);
+      if (last) {
+        const uint64_t zi = end - 1 - pos;
+        if (zi < 64) w &= (1ull << zi) - 1ull;
+      }
+    }
     const uint64_t a = wlo > pos ? wlo - pos : 0, z = end - pos;
     const uint64_t lim = (~0ull << a) & (z >= 64 ? ~0ull : ((1ull << z) - 1ull));
     st = w & ~prev & lim;
@@ -1282,12 +1319,21 @@ __global__ __launch_bounds__(kXeThreads) void xc_expand_kernel(ScanParams P)
   {
     uint32_t ns = 0, ne = 0;
     int64_t ls = -1;
-    for (uint64_t wi = qb + lane; wi < qend; wi += 64) {
-      uint64_t st, en;
-      events(wi, st, en);
-      ns += (uint32_t)__builtin_popcountll(st);
-      ne += (uint32_t)__builtin_popcountll(en);
-      if (st) ls = (int64_t)(wi * 64 + 63 - __builtin_clzll(st));
+    for (uint64_t wi0 = qb + lane; wi0 < qend; wi0 += 256) {
+      Raw r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (wi0 + 64 * k < qend) r[k] = load_raw(wi0 + 64 * k);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t wi = wi0 + 64 * k;
+        if (wi >= qend) break;
+        uint64_t st, en;
+        events(wi, r[k], st, en);
+        ns += (uint32_t)__builtin_popcountll(st);
+        ne += (uint32_t)__builtin_popcountll(en);
+        if (st) ls = (int64_t)(wi * 64 + 63 - __builtin_clzll(st));
+      }
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -1305,65 +1351,79 @@ __global__ __launch_bounds__(kXeThreads) void xc_expand_kernel(ScanParams P)
   __syncthreads();
   if (any) {
     const uint64_t base = P.out_base[gw];
-    const uint32_t open0 = wlo > P.lo ? (uint32_t)((words[(wlo - 1) >> 6] >> ((wlo - 1) & 63)) & 1ull) : 0u;
+    // In_{wlo - 1}: U bit wlo - 1; two-state tables C_wlo
+    const uint32_t open0 = wlo <= P.lo ? 0u
+                           : U        ? (uint32_t)((words[(wlo - 1) >> 6] >> ((wlo - 1) & 63)) & 1ull)
+                                      : (uint32_t)((words[wlo >> 6] >> (wlo & 63)) & 1ull);
     uint64_t s_before = 0, e_before = 0;
-    int64_t last_start = -1;
+    int64_t last_start = -1;  // the last start so far (-1: none since wlo)
     for (uint32_t w = 0; w < wv; ++w) {
       s_before += qs[w];
       e_before += qe[w];
       if (ql[w] >= 0) last_start = ql[w];
     }
-    uint32_t* so = st_off[wv];
+    uint16_t* so = st_off[wv];
+    uint16_t* eo = en_off[wv];
+    const uint64_t cap_n = P.out_capacity;
+    Raw cur;
+    if (qb + lane < qend) cur = load_raw(qb + lane);
     for (uint64_t w0 = qb; w0 < qend; w0 += 64) {
       const uint64_t wi = w0 + lane, pos = wi * 64;
+      Raw nxt;  // (the next round's words, in flight during this round)
+      if (wi + 64 < qend) nxt = load_raw(wi + 64);
       uint64_t st = 0, en = 0;
-      if (wi < qend) events(wi, st, en);
+      if (wi < qend) events(wi, cur, st, en);
+      cur = nxt;
       const uint32_t ns = (uint32_t)__builtin_popcountll(st), ne = (uint32_t)__builtin_popcountll(en);
       const uint32_t is = cscan_add(ns), ie = cscan_add(ne);
       const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)is, 63);
       const uint32_t E = (uint32_t)__builtin_amdgcn_readlane((int)ie, 63);
-      // the last start before this lane's word: in the nearest lower lane with
-      // starts, else before the round
       const uint64_t hs = __ballot(st != 0);
-      const uint64_t lower = hs & ((1ull << lane) - 1ull);
       const int64_t myls = st ? (int64_t)(pos + 63 - __builtin_clzll(st)) : -1;
-      const int src = lower ? 63 - __builtin_clzll(lower) : 0;
-      const int64_t nb = __shfl(myls, src, 64);
-      const int64_t ls = lower ? nb : last_start;
       const uint64_t pb = w0 * 64;
+      const uint32_t lb = (uint32_t)(pos - pb);
       uint64_t m = st;
       for (uint32_t k = is - ns; m; ++k) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        so[k] = (uint16_t)(lb + (uint32_t)__builtin_ctzll(m));
         m &= m - 1;
-        so[k] = (uint32_t)(pos + j - pb);
       }
-      // the lengths, written by their lanes (end indices are consecutive)
       m = en;
-      for (uint64_t i = base - open0 + e_before + (ie - ne); m; ++i) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      for (uint32_t k = ie - ne; m; ++k) {
+        eo[k] = (uint16_t)(lb + (uint32_t)__builtin_ctzll(m));
         m &= m - 1;
-        const uint64_t e = pos + j;
-        const uint64_t sb = st & ((1ull << j) - 1ull);  // starts of the word before the end
-        const int64_t s = sb ? (int64_t)(pos + 63 - __builtin_clzll(sb)) : ls;
-        if (i < P.out_capacity) {
-          if (s >= 0) {
-            P.out_len[i] = (uint32_t)(e - (uint64_t)s);
-          } else {
-            P.out_len[i] = (uint32_t)(e + (uint64_t)P.delta);  // raw (reported): the match open at wlo
-            fix_s = i;
-          }
+      }
+      cwave_sync();
+      // (uniform) a match is open at the round start: its end is the round's first
+      const uint32_t open_r = (uint32_t)(open0 + s_before - e_before);
+      const uint64_t sb0 = base + s_before, eb0 = base - open0 + e_before;
+#if defined(UGPU_XE_ABL) && (UGPU_XE_ABL == 1 || UGPU_XE_ABL == 3)  // no start stores (benchmarking; wrong records)
+      if (R == ~0u)
+#endif
+      for (uint32_t t = lane; t < R; t += 64) {
+        const uint64_t i = sb0 + t;
+        if (i < cap_n) {
+          P.out_start[i] = pb + so[t] + (uint64_t)P.delta;
+          if (P.out_cap) P.out_cap[i] = P.cap1;
         } else {
           atomicOr(P.flags, UGPU_FLAG_CAPACITY);
         }
       }
-      cwave_sync();
-      for (uint32_t t = lane; t < R; t += 64) {
-        const uint64_t i = base + s_before + t;
-        if (i < P.out_capacity) {
-          P.out_start[i] = pb + so[t] + (uint64_t)P.delta;
-          P.out_cap[i] = P.cap1;
-        } else {
+#if defined(UGPU_XE_ABL) && (UGPU_XE_ABL == 1 || UGPU_XE_ABL == 2)  // no length stores (benchmarking; wrong records)
+      if (E == ~0u)
+#endif
+      for (uint32_t t = lane; t < E; t += 64) {
+        const uint64_t i = eb0 + t;
+        if (i >= cap_n) {
           atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+          continue;
+        }
+        if (t >= open_r) {
+          P.out_len[i] = (uint32_t)eo[t] - (uint32_t)so[t - open_r];
+        } else if (last_start >= 0) {
+          P.out_len[i] = (uint32_t)(pb + eo[t] - (uint64_t)last_start);
+        } else {
+          P.out_len[i] = (uint32_t)(pb + eo[t] + (uint64_t)P.delta);  // raw (reported): the match open at wlo
+          fix_s = i;
         }
       }
       s_before += R;

@@ -152,7 +152,8 @@ def gather_offsets(start, length, cap, group=None, dst=None):
 
     start (int64, global byte offsets), length and cap (int32) are this rank's
     records in chain order, on the collective's device.  The records are
-    packed 16 B each ((start, len << 32 | cap)), padded to the largest shard's
+    packed 16 B each ((start, len << 32 | cap)) -- 12 B (start, len) when cap is
+    None (tables with one accept index) -- padded to the largest shard's
     count and exchanged with one all_gather (dst None: every rank gets the
     whole list) or one gather to rank dst (others get None); the result is the
     concatenation in rank order, which is global chain order because shards
@@ -168,11 +169,17 @@ def gather_offsets(start, length, cap, group=None, dst=None):
     dist.all_gather(ns, n, group=group)
     counts = [int(x.item()) for x in ns]
     m = max(max(counts), 1)
-    pack = torch.zeros((m, 2), dtype=torch.int64, device=dev)
     k = counts[rank]
-    if k:
-        pack[:k, 0] = start[:k].to(torch.int64)
-        pack[:k, 1] = (length[:k].to(torch.int64) << 32) | (cap[:k].to(torch.int64) & 0xFFFFFFFF)
+    if cap is None:
+        pack = torch.zeros((m, 3), dtype=torch.int32, device=dev)
+        if k:
+            pack[:k, 0:2] = start[:k].to(torch.int64).contiguous().view(torch.int32).view(k, 2)
+            pack[:k, 2] = length[:k].to(torch.int32)
+    else:
+        pack = torch.zeros((m, 2), dtype=torch.int64, device=dev)
+        if k:
+            pack[:k, 0] = start[:k].to(torch.int64)
+            pack[:k, 1] = (length[:k].to(torch.int64) << 32) | (cap[:k].to(torch.int64) & 0xFFFFFFFF)
     if dst is None:
         parts = [torch.empty_like(pack) for _ in range(world)]
         dist.all_gather(parts, pack, group=group)
@@ -182,4 +189,7 @@ def gather_offsets(start, length, cap, group=None, dst=None):
         if rank != dst:
             return None
     allp = torch.cat([parts[r][:counts[r]] for r in range(world)])
+    if cap is None:
+        st = allp[:, 0:2].contiguous().view(torch.int64).reshape(-1)
+        return st, allp[:, 2].clone(), None
     return allp[:, 0].clone(), (allp[:, 1] >> 32).to(torch.int32), (allp[:, 1] & 0xFFFFFFFF).to(torch.int32)

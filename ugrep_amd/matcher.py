@@ -467,8 +467,10 @@ class Scanner:
         return ms.value
 
     def offsets(self, d_start, d_len, d_cap, capacity, stream=0):
+        """Write the last scan's records; d_cap 0/None: 12-byte records (tables
+        with one accept index, info()["shape"] & SHAPE_ONE_ACCEPT)."""
         check(lib.ugpu_scan_offsets(self._h, ctypes.c_void_p(d_start), ctypes.c_void_p(d_len),
-                                    ctypes.c_void_p(d_cap), capacity, ctypes.c_void_p(stream)))
+                                    ctypes.c_void_p(d_cap or None), capacity, ctypes.c_void_p(stream)))
 
     def chain_fix(self, dptr, lo, hi, read_end, at_eof, bias, old_entry, new_entry, stream=0):
         t = _lib.Totals()
