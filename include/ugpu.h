@@ -232,6 +232,15 @@ int ugpu_result_free(ugpu_result *res);
    ugpu_records_free, which waits for the pipeline. */
 typedef struct ugpu_records ugpu_records;
 int ugpu_find_records(const ugpu_dfa *dfa, const uint8_t *buf, uint64_t len, uint64_t start, ugpu_records **out);
+/* ugpu_find_records with flags.  UGPU_REC_BORROW: the caller keeps buf
+   readable until ugpu_records_free returns (which stops and joins the
+   pipeline), so the call returns at once and the first records can be popped
+   while the rest of the input is still crossing PCIe.  Plain
+   ugpu_find_records returns only once the last input byte is on the device
+   (ugrep may unmap a file as soon as it stops asking for matches). */
+#define UGPU_REC_BORROW 1u
+int ugpu_find_records_ex(const ugpu_dfa *dfa, const uint8_t *buf, uint64_t len, uint64_t start, uint32_t flags,
+                         ugpu_records **out);
 int ugpu_records_next(ugpu_records *r, uint64_t *start, uint32_t *len, uint32_t *cap);
 int ugpu_records_totals(ugpu_records *r, uint64_t *count, uint64_t *digest, uint64_t *dcap);
 /* Pop every remaining record, returning their number and digests (what a

@@ -548,13 +548,20 @@ static int orc_walk_ctx(const uint8_t *buf, uint64_t n, uint64_t p, uint64_t cur
   return bol | orc_at_wb_cur(buf, n, p, cur) << 1 | orc_at_bw(buf, n, p) << 2;
 }
 
-static uint32_t orc_accept_at(const orc_dfa *d, uint32_t s, int wctx, const uint8_t *buf, uint64_t n, uint64_t q)
+/* the accept index at q of a walk from p in state s (cur: the end of its last
+   accept so far, p before any), meta edges followed as above */
+static uint32_t orc_accept_at(const orc_dfa *d, uint32_t s, const uint8_t *buf, uint64_t n, uint64_t p, uint64_t cur,
+                              uint64_t q)
 {
   uint32_t cap = d->accept[s];
-  int bol = wctx & 1, wb = (wctx >> 1) & 1, bw = (wctx >> 2) & 1;
-  int eol = q >= n || buf[q] == '\n' || (buf[q] == '\r' && q + 1 < n && buf[q + 1] == '\n');
-  int ew = orc_at_ew(buf, n, q), we = orc_at_we_meta(buf, n, q);
+  int wctx, bol, wb, bw, eol, ew, we;
   int jumps;
+  if (d->meta[(size_t)s * ORC_MAXMETA] == 0)
+    return cap; /* no meta edge: the contexts are not needed */
+  wctx = orc_walk_ctx(buf, n, p, cur);
+  bol = wctx & 1, wb = (wctx >> 1) & 1, bw = (wctx >> 2) & 1;
+  eol = q >= n || buf[q] == '\n' || (buf[q] == '\r' && q + 1 < n && buf[q + 1] == '\n');
+  ew = orc_at_ew(buf, n, q), we = orc_at_we_meta(buf, n, q);
   for (jumps = 0; jumps < 5; ++jumps)
   {
     uint32_t t = 0, k;
@@ -605,7 +612,7 @@ uint64_t orc_find_a(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t s
     uint32_t s = d->start, a = 0, c;
     uint64_t q = p, last = p;
     int hit = 0;
-    if ((c = orc_accept_at(d, s, orc_walk_ctx(buf, n, p, p), buf, n, q)) != 0)
+    if ((c = orc_accept_at(d, s, buf, n, p, p, q)) != 0)
     {
       hit = 1;
       a = c;
@@ -617,7 +624,7 @@ uint64_t orc_find_a(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t s
         break;
       s = t;
       ++q;
-      if ((c = orc_accept_at(d, s, orc_walk_ctx(buf, n, p, last), buf, n, q)) != 0)
+      if ((c = orc_accept_at(d, s, buf, n, p, last, q)) != 0)
       {
         hit = 1;
         last = q;

@@ -13,11 +13,11 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-UNSUPPORTED = {"word_boundary", "lookahead"}
+UNSUPPORTED = {"lookahead"}
 # anchored tables are supported (tests/test_anchor.py); their cases.json
 # results are the reference as ugrep runs it without option N, where its match
 # predictor decides, so the case loops below skip them
-SKIP_CASES = UNSUPPORTED | {"anchor_bol", "anchor_eol"}
+SKIP_CASES = UNSUPPORTED | {"anchor_bol", "anchor_eol", "word_boundary"}  # word tables: tests/test_wordb.py
 
 
 @pytest.fixture(scope="module")

@@ -10,10 +10,11 @@ import ugrep_amd
 from ugrep_amd import _lib
 from oracle_lib import case_input
 
-# line anchors (anchor_bol, anchor_eol) are supported since round 3: per-context
-# accepts, tests/test_anchor.py; word boundaries and lookahead are not
-UNSUPPORTED = {"word_boundary", "lookahead"}
-ANCHORED = {"anchor_bol", "anchor_eol"}
+# line anchors (anchor_bol, anchor_eol) are supported since round 3 and word
+# boundaries since round 4 (per-context accepts: tests/test_anchor.py,
+# tests/test_wordb.py); lookahead is not
+UNSUPPORTED = {"lookahead"}
+ANCHORED = {"anchor_bol", "anchor_eol", "word_boundary"}
 
 
 def test_exports_every_declared_symbol():
@@ -141,7 +142,7 @@ def test_prefilter_selectivity_c2():
 
 def test_result_struct_layout():
     assert ctypes.sizeof(_lib.Totals) == 48
-    assert ctypes.sizeof(_lib.DfaInfo) == 36
+    assert ctypes.sizeof(_lib.DfaInfo) == 44
 
 
 def _xt_find(t, x, data):

@@ -9,8 +9,9 @@ import pytest
 
 from oracle_lib import OracleDfa, case_input, gen
 
-UNSUPPORTED = {"word_boundary", "lookahead"}
-ANCHORED = {"anchor_bol", "anchor_eol"}  # restated by orc_find_a (tests/test_anchor.py)
+UNSUPPORTED = {"lookahead"}
+# restated by orc_find_a (tests/test_anchor.py, tests/test_wordb.py)
+ANCHORED = {"anchor_bol", "anchor_eol", "word_boundary"}
 
 
 def test_unsupported_tables_rejected(patterns):

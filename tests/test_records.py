@@ -40,6 +40,17 @@ def _check(U, pat, data, start=0, nul=False, word=False):
     assert r.triples() == want[3]
     r2 = U.Records(pat, data, start=start)
     assert r2.drain() == tuple(want[:3])
+    # a borrowed buffer (UGPU_REC_BORROW): records popped while the input is
+    # still crossing; a few records by next(), then the parallel drain
+    r3 = U.Records(pat, data, start=start, borrow=True)
+    assert r3.triples() == want[3]
+    r4 = U.Records(pat, data, start=start, borrow=True)
+    head = [r4.next() for _ in range(min(3, len(want[3])))]
+    assert [list(t) for t in head] == want[3][:len(head)]
+    k, dg, dc = r4.drain()
+    m64 = (1 << 64) - 1
+    hk, hdg, hdc = len(head), sum(s * 31 + ln for s, ln, _ in head), sum((s + 1) * c for s, _, c in head)
+    assert (k + hk, (dg + hdg) & m64, (dc + hdc) & m64) == tuple(want[:3])
 
 
 @pytest.mark.parametrize("rx,kind", [("foo|bar|baz", 1), ("[A-Za-z_][A-Za-z0-9_]*", 3), (r"\w+", 4)])
@@ -55,6 +66,19 @@ def test_records_equal_oracle(U, small_chunks, rx, kind):
     r = U.Records(pat, dev)
     f = U.find_all(pat, dev, offsets=False)
     assert r.drain() == (f.count, f.digest, f.dcap)
+
+
+def test_records_drain_one_thread(U, small_chunks, monkeypatch):
+    """ugpu_records_drain with UGPU_REC_DRAIN_THREADS=1 (pieces decoded in
+    order on the calling thread) and with 3 (in flight at once)."""
+    from oracle_lib import gen
+    pat = U.Pattern(U.compile_regex(r"\w+"))
+    data = gen(4, 9, 0, (6 << 20) + 77)
+    f = U.find_all(pat, data, offsets=False)
+    for t in ("1", "3"):
+        monkeypatch.setenv("UGPU_REC_DRAIN_THREADS", t)
+        assert U.Records(pat, data).drain() == (f.count, f.digest, f.dcap)
+        assert U.Records(pat, data, borrow=True).drain() == (f.count, f.digest, f.dcap)
 
 
 def test_records_escapes_and_borders(U, small_chunks):

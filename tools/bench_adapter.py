@@ -66,6 +66,19 @@ def main():
             line["records_ms"] = round(bestr * 1e3, 4)
             line["records_gbps"] = round(n / bestr / 1e9, 3)
             line["records_equal"] = got == (r.count, r.digest, r.dcap)
+            # the same with a borrowed buffer (UGPU_REC_BORROW: the consumer
+            # starts at the first piece, not after the whole H2D; a native
+            # consumer that owns its buffer, not ugrep's mmap)
+            bestb = 1e30
+            for _ in range(a.reps):
+                t0 = time.perf_counter()
+                rr = U.Records(pat, buf, borrow=True)
+                gotb = rr.drain()
+                bestb = min(bestb, time.perf_counter() - t0)
+                rr.close()
+            line["records_borrow_ms"] = round(bestb * 1e3, 4)
+            line["records_borrow_gbps"] = round(n / bestb / 1e9, 3)
+            line["records_borrow_equal"] = gotb == (r.count, r.digest, r.dcap)
             if os.path.exists(exe):
                 j = json.loads(subprocess.run([exe, "bench", "re", rx, "gen:%d:1:0:%d" % (kind, n), "1", str(a.reps)],
                                               capture_output=True, check=True, timeout=600).stdout.decode()

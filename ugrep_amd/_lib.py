@@ -138,6 +138,8 @@ def _load():
         "ugpu_version": (ctypes.c_char_p, []),
         "ugpu_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
         "ugpu_find_records": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(V)]),
+        "ugpu_find_records_ex": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                                ctypes.POINTER(V)]),
         "ugpu_records_next": (ctypes.c_int, [V, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
                                              ctypes.POINTER(ctypes.c_uint32)]),
         "ugpu_records_totals": (ctypes.c_int, [V, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),

@@ -26,6 +26,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <future>
 #include <vector>
 
 #include "../../include/ugpu.h"
@@ -2081,6 +2082,7 @@ bool records_advance(ugpu_records* r, int* rc)
     return false;
   }
   ugpu_records::Piece& p = r->pieces[r->pi++];
+  r->cv.notify_all();  // (the pipeline may wait for the consumer to move on: R->ahead)
   if (p.landed) {
     // (the pipeline thread only appends to the deque: p stays put)
     hipEvent_t ev = p.landed;
@@ -2158,7 +2160,14 @@ int ugpu_warmup(int dev)
 
 int ugpu_find_records(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_t start, ugpu_records** out)
 {
+  return ugpu_find_records_ex(dfa, buf, len, start, 0, out);
+}
+
+int ugpu_find_records_ex(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_t start, uint32_t flags,
+                         ugpu_records** out)
+{
   if (!dfa || !out || (!buf && len)) return fail(UGPU_INVAL, "NULL argument");
+  if (flags & ~UGPU_REC_BORROW) return fail(UGPU_INVAL, "unknown records flags");
   *out = nullptr;
   if (start > len) start = len;
   int dev = 0;
@@ -2185,8 +2194,10 @@ int ugpu_find_records(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uin
     }
     // a host buffer may go away once this returns (ugrep unmaps a file when
     // it stops asking for matches): wait for the last input byte to be on the
-    // device; scans and record copies go on behind the consumer
-    if (!is_device_ptr(buf)) {
+    // device; scans and record copies go on behind the consumer.  Borrowed
+    // buffers (UGPU_REC_BORROW) stay readable until ugpu_records_free, which
+    // joins the pipeline: the consumer starts at the first piece.
+    if (!is_device_ptr(buf) && !(flags & UGPU_REC_BORROW)) {
       std::unique_lock<std::mutex> lk(R->mu);
       R->cv.wait(lk, [&] { return R->input_free; });
     }
@@ -2231,12 +2242,139 @@ int ugpu_records_next(ugpu_records* r, uint64_t* start, uint32_t* len, uint32_t*
   return 1;
 }
 
+namespace {
+
+// the count, digest and dcap of one whole piece, from its arrays (what a
+// native consumer's inlined loop computes)
+struct PieceSums {
+  uint64_t k = 0, dg = 0, dc = 0;
+};
+
+PieceSums decode_piece(const ugpu_records::Piece& p, int caps, uint32_t cap1)
+{
+  PieceSums out;
+  const uint64_t pn = p.n, base = p.base;
+  const std::pair<uint64_t, uint64_t>* esc = p.esc.data();
+  const uint64_t ne = p.esc.size();
+  if (p.dense) {
+    // a dense piece: start_i = so + sum of gaps up to i + lengths before i,
+    // so between escapes the sums of starts are weighted sums of the gaps
+    // and lengths (no serial chain; the loop vectorises); an escaped record
+    // carries its own start and restarts the sum after it
+    const uint8_t* g = p.host;
+    const uint8_t* l = p.host + pn;
+    uint64_t so = 0, ssum = 0, slen = 0, a = 0;
+    auto seg = [&](uint64_t b) {
+      // (blocks of 256: the in-block weights j * byte fit 16 bits, so the
+      // inner loop vectorises with 16-bit multiplies)
+      uint64_t sg = 0, skg = 0, sl = 0, skl = 0;
+      for (uint64_t kb = a; kb < b; kb += 256) {
+        const uint32_t m = b - kb < 256 ? (uint32_t)(b - kb) : 256u;
+        const uint8_t* gp = g + kb;
+        const uint8_t* lp = l + kb;
+        uint32_t bg = 0, bjg = 0, bl = 0, bjl = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+          bg += gp[j];
+          bjg += (uint16_t)((uint16_t)j * gp[j]);
+          bl += lp[j];
+          bjl += (uint16_t)((uint16_t)j * lp[j]);
+        }
+        sg += bg;
+        sl += bl;
+        skg += kb * bg + bjg;
+        skl += kb * bl + bjl;
+      }
+      ssum += (b - a) * so + (b * sg - skg) + (b ? (b - 1) * sl - skl : 0);
+      slen += sl;
+      so += sg + sl;
+    };
+    for (uint64_t j = 0; j < ne; ++j) {
+      const uint64_t e = esc[j].first, v = esc[j].second;
+      seg(e);
+      so = (uint32_t)v;
+      ssum += so;
+      slen += v >> 32;
+      so += v >> 32;
+      a = e + 1;
+    }
+    seg(pn);
+    out.dg = 31 * (ssum + pn * base) + slen;
+    out.dc = (ssum + pn * (base + 1)) * cap1;
+    out.k = pn;
+    return out;
+  }
+  const uint32_t* ps = reinterpret_cast<const uint32_t*>(p.host);
+  const uint16_t* pl = reinterpret_cast<const uint16_t*>(p.host + 4 * pn);
+  const uint16_t* pc = caps ? reinterpret_cast<const uint16_t*>(p.host + 6 * pn) : nullptr;
+  uint64_t sdg = 0, sdc = 0, ssum = 0;
+  for (uint64_t i = 0; i < pn; ++i) {
+    const uint64_t s0 = ps[i];
+    ssum += s0;
+    sdg += s0 * 31 + pl[i];
+    if (pc) sdc += (base + s0 + 1) * pc[i];
+  }
+  // starts are base + s0; caps are cap1 without a cap array
+  out.dg = sdg + pn * base * 31;
+  out.dc = pc ? sdc : (ssum + pn * (base + 1)) * cap1;
+  for (uint64_t j = 0; j < ne; ++j) {
+    // escaped records: replace the 0xFFFF placeholders by the true values
+    const uint64_t i = esc[j].first, s0 = base + ps[i];
+    const uint32_t l = (uint32_t)esc[j].second, c = pc ? (uint32_t)(esc[j].second >> 32) : cap1;
+    out.dg += (uint64_t)l - pl[i];
+    if (pc) out.dc += (s0 + 1) * ((uint64_t)c - pc[i]);
+  }
+  out.k = pn;
+  return out;
+}
+
+// the next whole piece for ugpu_records_drain, without releasing the one
+// before (its decode may still run); false at the end or on an error (*rc)
+bool records_take(ugpu_records* r, size_t* idx, int* rc)
+{
+  std::unique_lock<std::mutex> lk(r->mu);
+  r->cv.wait(lk, [&] { return r->pi < r->published || r->done; });
+  if (r->pi >= r->published) {
+    *rc = r->rc;
+    return false;
+  }
+  const size_t i = r->pi++;
+  r->cv.notify_all();  // (the pipeline may wait for the consumer to move on: R->ahead)
+  ugpu_records::Piece& p = r->pieces[i];
+  if (p.landed) {
+    hipEvent_t ev = p.landed;
+    lk.unlock();
+    const hipError_t e = hipEventSynchronize(ev);
+    (void)hipEventDestroy(ev);
+    lk.lock();
+    p.landed = nullptr;
+    if (e != hipSuccess) {
+      *rc = hip_fail(e, "records copy");
+      r->pi = r->published;
+      return false;
+    }
+  }
+  *idx = i;
+  return true;
+}
+
+void records_release(ugpu_records* r, size_t i)
+{
+  std::lock_guard<std::mutex> lk(r->mu);
+  ugpu_records::Piece& p = r->pieces[i];
+  pinned_put(p.host, p.host_bytes);
+  p.host = nullptr;
+  r->cv.notify_all();
+}
+
+}  // namespace
+
 int ugpu_records_drain(ugpu_records* r, uint64_t* n, uint64_t* digest, uint64_t* dcap)
 {
   if (!r) return fail(UGPU_INVAL, "NULL argument");
   // the rest of the current piece through ugpu_records_next, then whole
-  // pieces straight from their arrays as they are published (the loop a
-  // native consumer inlines)
+  // pieces straight from their arrays as they are published, decoded on up
+  // to UGPU_REC_DRAIN_THREADS threads at once (default 8; a piece's sums
+  // need nothing from the pieces before it)
   uint64_t k = 0, dg = 0, dc = 0, st = 0;
   uint32_t ln = 0, cp = 0;
   while (r->ri < r->n && ugpu_records_next(r, &st, &ln, &cp) == 1) {
@@ -2244,81 +2382,48 @@ int ugpu_records_drain(ugpu_records* r, uint64_t* n, uint64_t* digest, uint64_t*
     dg += st * 31 + ln;
     dc += (st + 1) * cp;
   }
-  int rc = UGPU_OK;
-  while (records_advance(r, &rc)) {
-    if (r->dg) {
-      // a dense piece: start_i = so + sum of gaps up to i + lengths before i,
-      // so between escapes the sums of starts are weighted sums of the gaps
-      // and lengths (no serial chain; the loop vectorises); an escaped record
-      // carries its own start and restarts the sum after it
-      const uint8_t* g = r->dg;
-      const uint8_t* l = r->dl;
-      const uint64_t pn = r->n, base = r->base;
-      uint64_t so = 0, ssum = 0, slen = 0, a = 0;
-      auto seg = [&](uint64_t b) {
-        // (blocks of 256: the in-block weights j * byte fit 16 bits, so the
-        // inner loop vectorises with 16-bit multiplies)
-        uint64_t sg = 0, skg = 0, sl = 0, skl = 0;
-        for (uint64_t kb = a; kb < b; kb += 256) {
-          const uint32_t m = b - kb < 256 ? (uint32_t)(b - kb) : 256u;
-          const uint8_t* gp = g + kb;
-          const uint8_t* lp = l + kb;
-          uint32_t bg = 0, bjg = 0, bl = 0, bjl = 0;
-          for (uint32_t j = 0; j < m; ++j) {
-            bg += gp[j];
-            bjg += (uint16_t)((uint16_t)j * gp[j]);
-            bl += lp[j];
-            bjl += (uint16_t)((uint16_t)j * lp[j]);
-          }
-          sg += bg;
-          sl += bl;
-          skg += kb * bg + bjg;
-          skl += kb * bl + bjl;
-        }
-        ssum += (b - a) * so + (b * sg - skg) + (b ? (b - 1) * sl - skl : 0);
-        slen += sl;
-        so += sg + sl;
-      };
-      for (uint64_t j = 0; j < r->ne; ++j) {
-        const uint64_t e = r->esc[j].first, v = r->esc[j].second;
-        seg(e);
-        so = (uint32_t)v;
-        ssum += so;
-        slen += v >> 32;
-        so += v >> 32;
-        a = e + 1;
-      }
-      seg(pn);
-      dg += 31 * (ssum + pn * base) + slen;
-      dc += (ssum + pn * (base + 1)) * r->cap1;
-      k += pn;
-      r->ri = r->n;
-      continue;
+  if (r->pi > 0) {
+    // (the current piece is used up: back to the pool)
+    std::lock_guard<std::mutex> lk(r->mu);
+    ugpu_records::Piece& prev = r->pieces[r->pi - 1];
+    if (prev.host && !prev.landed) {
+      pinned_put(prev.host, prev.host_bytes);
+      prev.host = nullptr;
     }
-    const uint32_t* ps = r->st;
-    const uint16_t* pl = r->ln;
-    const uint16_t* pc = r->cp;
-    const uint64_t pn = r->n, base = r->base;
-    uint64_t sdg = 0, sdc = 0, ssum = 0;
-    for (uint64_t i = 0; i < pn; ++i) {
-      const uint64_t s0 = ps[i];
-      ssum += s0;
-      sdg += s0 * 31 + pl[i];
-      if (pc) sdc += (base + s0 + 1) * pc[i];
-    }
-    // starts are base + s0; caps are cap1 without a cap array
-    dg += sdg + pn * base * 31;
-    dc += pc ? sdc : (ssum + pn * (base + 1)) * r->cap1;
-    for (uint64_t j = 0; j < r->ne; ++j) {
-      // escaped records: replace the 0xFFFF placeholders by the true values
-      const uint64_t i = r->esc[j].first, s0 = base + ps[i];
-      const uint32_t l = (uint32_t)r->esc[j].second, c = pc ? (uint32_t)(r->esc[j].second >> 32) : r->cap1;
-      dg += (uint64_t)l - pl[i];
-      if (pc) dc += (s0 + 1) * ((uint64_t)c - pc[i]);
-    }
-    k += pn;
-    r->ri = r->n;
+    r->dg = r->dl = nullptr;
+    r->st = nullptr;
+    r->ln = r->cp = nullptr;
+    r->n = r->ri = 0;
+    r->cv.notify_all();
   }
+  const size_t threads = (size_t)std::max<uint64_t>(env_u64("UGPU_REC_DRAIN_THREADS", 8), 1);
+  std::deque<std::pair<size_t, std::future<PieceSums>>> jobs;
+  auto retire = [&]() {
+    PieceSums s = jobs.front().second.get();
+    records_release(r, jobs.front().first);
+    jobs.pop_front();
+    k += s.k;
+    dg += s.dg;
+    dc += s.dc;
+  };
+  int rc = UGPU_OK;
+  size_t idx = 0;
+  while (records_take(r, &idx, &rc)) {
+    const ugpu_records::Piece* pp = &r->pieces[idx];  // (the deque only grows at its end: stable)
+    const int caps = r->caps;
+    const uint32_t cap1 = r->cap1;
+    if (threads == 1) {
+      jobs.emplace_back(idx, std::async(std::launch::deferred, [pp, caps, cap1] { return decode_piece(*pp, caps, cap1); }));
+    } else {
+      try {
+        jobs.emplace_back(idx, std::async(std::launch::async, [pp, caps, cap1] { return decode_piece(*pp, caps, cap1); }));
+      } catch (...) {
+        jobs.emplace_back(idx, std::async(std::launch::deferred, [pp, caps, cap1] { return decode_piece(*pp, caps, cap1); }));
+      }
+    }
+    while (jobs.size() >= threads) retire();
+  }
+  while (!jobs.empty()) retire();
   if (rc) return rc;
   if (n) *n = k;
   if (digest) *digest = dg;

@@ -277,11 +277,18 @@ class Records:
     """ugpu_find_records: the records of a buffer for a one-at-a-time consumer
     (pipelined H2D, scans and packed record copy-back; include/ugpu.h)."""
 
-    def __init__(self, pattern, data, start=0):
+    def __init__(self, pattern, data, start=0, borrow=False):
+        """borrow=True (UGPU_REC_BORROW): this object keeps `data` alive until
+        close(), and the first records can be popped while the rest of the
+        input is still on its way to the device."""
         ptr, n, keep = _buffer_ptr(data)
         h = ctypes.c_void_p()
-        check(lib.ugpu_find_records(pattern.handle, ctypes.c_void_p(ptr), n, start, ctypes.byref(h)))
-        del keep
+        if borrow:
+            check(lib.ugpu_find_records_ex(pattern.handle, ctypes.c_void_p(ptr), n, start, 1, ctypes.byref(h)))
+            self._keep = (keep, data)
+        else:
+            check(lib.ugpu_find_records(pattern.handle, ctypes.c_void_p(ptr), n, start, ctypes.byref(h)))
+            del keep
         self._h = h
 
     def next(self):
@@ -315,6 +322,7 @@ class Records:
         if getattr(self, "_h", None):
             lib.ugpu_records_free(self._h)
             self._h = None
+        self._keep = None  # (a borrowed buffer outlives the pipeline)
 
     def __del__(self):
         self.close()
