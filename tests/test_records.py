@@ -93,6 +93,21 @@ def test_records_escapes_and_borders(U, small_chunks):
         _check(U, U.Pattern(U.compile_regex(rx)), data)
 
 
+@pytest.mark.parametrize("dense", ["0", "1"])
+def test_records_dense_pieces(U, small_chunks, monkeypatch, dense):
+    """2-byte pieces (u8 gap + u8 len; chunks of one accept index with a record
+    per < 32 bytes, the default) against the 6-byte form: gaps and lengths of
+    255 bytes and more (escapes), a 70 000-byte match across a chunk border."""
+    monkeypatch.setenv("UGPU_REC_DENSE", dense)
+    rng = np.random.default_rng(8)
+    data = np.where(rng.random(3 << 20) < 0.4, ord("a"), ord("-")).astype(np.uint8)
+    for off, ln, ch in ((5000, 254, "-"), (9000, 255, "-"), (12000, 300, "-"), (20000, 254, "a"), (30000, 255, "a"),
+                        (40000, 1000, "a"), ((1 << 20) - 30000, 70000, "a"), ((2 << 20) + 5, 256, "-")):
+        data[off:off + ln] = ord(ch)
+    _check(U, U.Pattern(U.compile_regex("a+")), data)
+    _check(U, U.Pattern(U.compile_regex("a+")), data, start=12345)
+
+
 def test_records_word_and_anchors(U, small_chunks):
     from test_multi import _w_corpus
     data = _w_corpus(3 << 20)

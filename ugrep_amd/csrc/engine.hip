@@ -1629,6 +1629,7 @@ struct ugpu_records {
   bool cancel = false;      // ugpu_records_free before the end: the pipeline stops at its next chunk
   bool unbounded = false;   // ugpu_records_totals waits for the end: no limit on pieces ahead
   size_t ahead = 4;         // pieces the pipeline may publish ahead of the consumer (UGPU_REC_AHEAD)
+  uint64_t chunk = 32ull << 20;  // input bytes per piece (UGPU_REC_CHUNK)
   int rc = 0;
   std::mutex mu;
   std::condition_variable cv;
@@ -1878,7 +1879,7 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
     publish(nullptr, true);
     return;
   }
-  const uint64_t chunk = std::max<uint64_t>(env_u64("UGPU_REC_CHUNK", 64ull << 20), 1ull << 20);
+  const uint64_t chunk = R->chunk;
   const uint64_t halo = 1ull << 20;
   const bool host = !is_device_ptr(buf);
   // (the bytes before start are never read but for at_wb / at_bol, 4 back)
@@ -1939,7 +1940,7 @@ void records_pipeline(ugpu_records* R, const ugpu_dfa* dfa, int dev, const uint8
       ugpu_records::Piece pc;
       pc.base = lo;
       pc.n = tot.count;
-      pc.dense = !R->caps && pc.n * 32 >= hi - lo && env_u64("UGPU_REC_DENSE", 0) != 0;
+      pc.dense = !R->caps && pc.n * 32 >= hi - lo && env_u64("UGPU_REC_DENSE", 1) != 0;
       const uint64_t n = pc.n, bytes = n * (pc.dense ? 2 : R->caps ? 8 : 6);
       if ((e = ws->reserve_out(n)) != hipSuccess) {
         rc = hip_fail(e, "records output");
@@ -2181,7 +2182,12 @@ int ugpu_find_records_ex(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, 
   R->sync_d2h = env_u64("UGPU_REC_SYNC", 0) != 0;
   R->zero_copy = env_u64("UGPU_REC_ZC", 0) != 0;
   R->trace = env_u64("UGPU_REC_TRACE", 0) != 0;
-  R->ahead = (size_t)std::max<uint64_t>(env_u64("UGPU_REC_AHEAD", 4), 1);
+  // chunks of 32 MiB (16 MiB for a borrowed buffer, whose consumer starts at
+  // the first piece: tools/rec_sweep.py); the pipeline runs at
+  // most 256 MiB of input (and at least 4 pieces) ahead of the consumer
+  R->chunk = std::max<uint64_t>(env_u64("UGPU_REC_CHUNK", (flags & UGPU_REC_BORROW) ? 16ull << 20 : 32ull << 20),
+                                1ull << 20);
+  R->ahead = (size_t)std::max<uint64_t>(env_u64("UGPU_REC_AHEAD", std::max<uint64_t>(4, (256ull << 20) / R->chunk)), 1);
   R->t0 = std::chrono::steady_clock::now();
   if (len == start) {
     R->done = R->input_free = true;
@@ -2250,9 +2256,8 @@ struct PieceSums {
   uint64_t k = 0, dg = 0, dc = 0;
 };
 
-PieceSums decode_piece(const ugpu_records::Piece& p, int caps, uint32_t cap1)
+void decode_piece(const ugpu_records::Piece& p, int caps, uint32_t cap1, PieceSums& out)
 {
-  PieceSums out;
   const uint64_t pn = p.n, base = p.base;
   const std::pair<uint64_t, uint64_t>* esc = p.esc.data();
   const uint64_t ne = p.esc.size();
@@ -2301,7 +2306,7 @@ PieceSums decode_piece(const ugpu_records::Piece& p, int caps, uint32_t cap1)
     out.dg = 31 * (ssum + pn * base) + slen;
     out.dc = (ssum + pn * (base + 1)) * cap1;
     out.k = pn;
-    return out;
+    return;
   }
   const uint32_t* ps = reinterpret_cast<const uint32_t*>(p.host);
   const uint16_t* pl = reinterpret_cast<const uint16_t*>(p.host + 4 * pn);
@@ -2324,7 +2329,6 @@ PieceSums decode_piece(const ugpu_records::Piece& p, int caps, uint32_t cap1)
     if (pc) out.dc += (s0 + 1) * ((uint64_t)c - pc[i]);
   }
   out.k = pn;
-  return out;
 }
 
 // the next whole piece for ugpu_records_drain, without releasing the one
@@ -2413,12 +2417,24 @@ int ugpu_records_drain(ugpu_records* r, uint64_t* n, uint64_t* digest, uint64_t*
     const int caps = r->caps;
     const uint32_t cap1 = r->cap1;
     if (threads == 1) {
-      jobs.emplace_back(idx, std::async(std::launch::deferred, [pp, caps, cap1] { return decode_piece(*pp, caps, cap1); }));
+      jobs.emplace_back(idx, std::async(std::launch::deferred, [pp, caps, cap1] {
+        PieceSums o;
+        decode_piece(*pp, caps, cap1, o);
+        return o;
+      }));
     } else {
       try {
-        jobs.emplace_back(idx, std::async(std::launch::async, [pp, caps, cap1] { return decode_piece(*pp, caps, cap1); }));
+        jobs.emplace_back(idx, std::async(std::launch::async, [pp, caps, cap1] {
+        PieceSums o;
+        decode_piece(*pp, caps, cap1, o);
+        return o;
+      }));
       } catch (...) {
-        jobs.emplace_back(idx, std::async(std::launch::deferred, [pp, caps, cap1] { return decode_piece(*pp, caps, cap1); }));
+        jobs.emplace_back(idx, std::async(std::launch::deferred, [pp, caps, cap1] {
+        PieceSums o;
+        decode_piece(*pp, caps, cap1, o);
+        return o;
+      }));
       }
     }
     while (jobs.size() >= threads) retire();
