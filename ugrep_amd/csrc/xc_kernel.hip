@@ -1243,12 +1243,73 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_bm_kernel(ScanParams P)
 // the round start) all leave as coalesced stores.  No table, no walk: the pass
 // reads 1/8 of the input's bytes and writes the records.
 constexpr int kXeThreads = 256;
+#ifndef UGPU_XE_CAP
+#define UGPU_XE_CAP 1024
+#endif
+
+// a word load the compiler does not track (no s_waitcnt of its own); the
+// caller waits with xe_wait, whose count N must be at most the number of
+// vector-memory instructions issued after the load
+__device__ __forceinline__ uint64_t xe_load(const uint64_t* p)
+{
+  uint64_t v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void xe_wait(uint64_t& a, uint64_t& b)
+{
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
+// a lane's events (bits of m, positions lb + bit) staged at k0 .. k1 - 1 of
+// o in position order, two per step
+__device__ __forceinline__ void xe_stage(uint16_t* o, uint32_t k0, uint32_t k1, uint32_t lb, uint64_t m)
+{
+  while (m) {
+    const uint32_t lo = (uint32_t)__builtin_ctzll(m), hi = 63u - (uint32_t)__builtin_clzll(m);
+    o[k0++] = (uint16_t)(lb + lo);
+    o[--k1] = (uint16_t)(lb + hi);  // (lo == hi: the same slot, the same value)
+    m &= m - 1;
+    m &= ~(1ull << hi);
+  }
+}
+// the same with N the largest of 32, 16, 8, 4, 0 not above k (uniform): one
+// asm statement, so that a and b are never read (copied) before the wait
+__device__ __forceinline__ void xe_wait_k(uint64_t& a, uint64_t& b, uint32_t k)
+{
+  asm volatile(
+      "s_cmp_lt_u32 %2, 32\n\t"
+      "s_cbranch_scc1 1f\n\t"
+      "s_waitcnt vmcnt(32)\n\t"
+      "s_branch 5f\n"
+      "1:\n\t"
+      "s_cmp_lt_u32 %2, 16\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_waitcnt vmcnt(16)\n\t"
+      "s_branch 5f\n"
+      "2:\n\t"
+      "s_cmp_lt_u32 %2, 8\n\t"
+      "s_cbranch_scc1 3f\n\t"
+      "s_waitcnt vmcnt(8)\n\t"
+      "s_branch 5f\n"
+      "3:\n\t"
+      "s_cmp_lt_u32 %2, 4\n\t"
+      "s_cbranch_scc1 4f\n\t"
+      "s_waitcnt vmcnt(4)\n\t"
+      "s_branch 5f\n"
+      "4:\n\t"
+      "s_waitcnt vmcnt(0)\n"
+      "5:"
+      : "+v"(a), "+v"(b)
+      : "s"(__builtin_amdgcn_readfirstlane(k))
+      : "memory", "scc");
+}
 
 // The range is cut into 4 quarters of whole words, one per wave.  A first
 // pass counts each quarter's starts and ends and finds its last start; after
 // one block barrier every wave knows its output bases and writes its quarter
 // alone.
-constexpr uint32_t kXeWaveCap = 64 * 32;  // starts (and ends) a wave-round can hold
+constexpr uint32_t kXeWaveCap = UGPU_XE_CAP;  // starts (and ends) a wave-round stages at once (2 KiB each)
 
 template <bool U>
 __global__ __launch_bounds__(kXeThreads) void xc_expand_kernel(ScanParams P)
@@ -1365,71 +1426,159 @@ __global__ __launch_bounds__(kXeThreads) void xc_expand_kernel(ScanParams P)
     uint16_t* so = st_off[wv];
     uint16_t* eo = en_off[wv];
     const uint64_t cap_n = P.out_capacity;
-    Raw cur;
-    if (qb + lane < qend) cur = load_raw(qb + lane);
+    // the words of a round (a) and their neighbours (b) come in by loads the
+    // compiler does not track (xe_load): its own wait for them would be a
+    // vmcnt(0) -- the round's record stores lie between a prefetch and its use
+    // -- so every round would wait for its stores and its prefetch.  Here the
+    // next round's loads go out before this round's stores and the round ends
+    // with a wait that lets up to K of those stores stay in flight (xe_wait).
+    const uint64_t wlo6 = P.lo >> 6;
+    auto ia = [&](uint64_t wi) __attribute__((always_inline)) { return wi < qend ? wi : qend - 1; };
+    auto ib = [&](uint64_t wi) __attribute__((always_inline)) {
+      if constexpr (U) {
+        const uint64_t v = wi > 0 ? wi - 1 : 0;
+        return v > wlo6 ? v : wlo6;
+      } else {
+        return wi + 1 < (end >> 6) ? wi + 1 : (end >> 6);  // (every word read where b counts; inside the bitmap)
+      }
+    };
+    auto raw = [&](uint64_t wi, uint64_t a, uint64_t b) __attribute__((always_inline)) {
+      Raw r;
+      const uint64_t pos = wi * 64;
+      if (pos >= end || pos + 64 <= wlo) return r;
+      r.a = a;
+      if constexpr (U)
+        r.b = pos > P.lo ? b : 0;
+      else
+        r.b = (last ? pos + 64 < end : pos + 64 <= end) ? b : 0;
+      return r;
+    };
+    uint64_t A = 0, B = 0;
+    if (qb < qend) {
+      A = xe_load(words + ia(qb + lane));
+      B = xe_load(words + ib(qb + lane));
+      xe_wait<0>(A, B);
+    }
     for (uint64_t w0 = qb; w0 < qend; w0 += 64) {
       const uint64_t wi = w0 + lane, pos = wi * 64;
-      Raw nxt;  // (the next round's words, in flight during this round)
-      if (wi + 64 < qend) nxt = load_raw(wi + 64);
+      uint64_t An = xe_load(words + ia(wi + 64)), Bn = xe_load(words + ib(wi + 64));
       uint64_t st = 0, en = 0;
-      if (wi < qend) events(wi, cur, st, en);
-      cur = nxt;
-      const uint32_t ns = (uint32_t)__builtin_popcountll(st), ne = (uint32_t)__builtin_popcountll(en);
-      const uint32_t is = cscan_add(ns), ie = cscan_add(ne);
-      const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)is, 63);
-      const uint32_t E = (uint32_t)__builtin_amdgcn_readlane((int)ie, 63);
-      const uint64_t hs = __ballot(st != 0);
-      const int64_t myls = st ? (int64_t)(pos + 63 - __builtin_clzll(st)) : -1;
+      if (wi < qend) events(wi, raw(wi, A, B), st, en);
       const uint64_t pb = w0 * 64;
       const uint32_t lb = (uint32_t)(pos - pb);
-      uint64_t m = st;
-      for (uint32_t k = is - ns; m; ++k) {
-        so[k] = (uint16_t)(lb + (uint32_t)__builtin_ctzll(m));
-        m &= m - 1;
-      }
-      m = en;
-      for (uint32_t k = ie - ne; m; ++k) {
-        eo[k] = (uint16_t)(lb + (uint32_t)__builtin_ctzll(m));
-        m &= m - 1;
-      }
-      cwave_sync();
-      // (uniform) a match is open at the round start: its end is the round's first
-      const uint32_t open_r = (uint32_t)(open0 + s_before - e_before);
-      const uint64_t sb0 = base + s_before, eb0 = base - open0 + e_before;
+      // a round stages all its starts and ends at once unless one of them
+      // exceeds kXeWaveCap; then lanes 0-31 and 32-63 go as two rounds
+      // (at most 32 starts per word); K counts the store iterations
+      uint32_t K = 0;
+      auto part = [&](uint64_t pst, uint64_t pen) __attribute__((always_inline)) {
+        const uint32_t ns = (uint32_t)__builtin_popcountll(pst), ne = (uint32_t)__builtin_popcountll(pen);
+        const uint32_t is = cscan_add(ns), ie = cscan_add(ne);
+        const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)is, 63);
+        const uint32_t E = (uint32_t)__builtin_amdgcn_readlane((int)ie, 63);
+        const uint64_t hs = __ballot(pst != 0);
+        const int64_t myls = pst ? (int64_t)(pos + 63 - __builtin_clzll(pst)) : -1;
+        // (two events per step: the lowest from the front, the highest from the back)
+        xe_stage(so, is - ns, is, lb, pst);
+        xe_stage(eo, ie - ne, ie, lb, pen);
+        cwave_sync();
+        // (uniform) a match is open at the round start: its end is the round's first
+        const uint32_t open_r = (uint32_t)(open0 + s_before - e_before);
+        const uint64_t sb0 = base + s_before, eb0 = base - open0 + e_before;
 #if defined(UGPU_XE_ABL) && (UGPU_XE_ABL == 1 || UGPU_XE_ABL == 3)  // no start stores (benchmarking; wrong records)
-      if (R == ~0u)
+        if (R == ~0u)
 #endif
-      for (uint32_t t = lane; t < R; t += 64) {
-        const uint64_t i = sb0 + t;
-        if (i < cap_n) {
-          P.out_start[i] = pb + so[t] + (uint64_t)P.delta;
-          if (P.out_cap) P.out_cap[i] = P.cap1;
+        if (sb0 + R <= cap_n && !P.out_cap) {
+          // (the usual case: 4 staged starts read, then 4 stores)
+          const uint64_t sbase = pb + (uint64_t)P.delta;
+          uint64_t* const os = P.out_start + sb0;
+          for (uint32_t t0 = 0; t0 < R; t0 += 256) {
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const uint32_t t = t0 + 64 * j + lane;
+              v[j] = t < R ? so[t] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const uint32_t t = t0 + 64 * j + lane;
+              if (t < R) os[t] = sbase + v[j];
+            }
+          }
         } else {
-          atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+          for (uint32_t t = lane; t < R; t += 64) {
+            const uint64_t i = sb0 + t;
+            if (i < cap_n) {
+              P.out_start[i] = pb + so[t] + (uint64_t)P.delta;
+              if (P.out_cap) P.out_cap[i] = P.cap1;
+            } else {
+              atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+            }
+          }
         }
-      }
 #if defined(UGPU_XE_ABL) && (UGPU_XE_ABL == 1 || UGPU_XE_ABL == 2)  // no length stores (benchmarking; wrong records)
-      if (E == ~0u)
+        if (E == ~0u)
 #endif
-      for (uint32_t t = lane; t < E; t += 64) {
-        const uint64_t i = eb0 + t;
-        if (i >= cap_n) {
-          atomicOr(P.flags, UGPU_FLAG_CAPACITY);
-          continue;
+        uint32_t t1 = 0;  // the ends from t1 on close starts of this round
+        if (open_r && E) {
+          // (the one end that closes the match open at the round start)
+          if (lane == 0) {
+            const uint64_t i = eb0;
+            if (i >= cap_n) {
+              atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+            } else if (last_start >= 0) {
+              P.out_len[i] = (uint32_t)(pb + eo[0] - (uint64_t)last_start);
+            } else {
+              P.out_len[i] = (uint32_t)(pb + eo[0] + (uint64_t)P.delta);  // raw (reported): the match open at wlo
+              fix_s = i;
+            }
+          }
+          t1 = 1;
         }
-        if (t >= open_r) {
-          P.out_len[i] = (uint32_t)eo[t] - (uint32_t)so[t - open_r];
-        } else if (last_start >= 0) {
-          P.out_len[i] = (uint32_t)(pb + eo[t] - (uint64_t)last_start);
+        if (eb0 + E <= cap_n) {
+          uint32_t* const ol = P.out_len + eb0;
+          for (uint32_t t0 = t1; t0 < E; t0 += 256) {
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const uint32_t t = t0 + 64 * j + lane;
+              v[j] = t < E ? (uint32_t)eo[t] - (uint32_t)so[t - open_r] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const uint32_t t = t0 + 64 * j + lane;
+              if (t < E) ol[t] = v[j];
+            }
+          }
         } else {
-          P.out_len[i] = (uint32_t)(pb + eo[t] + (uint64_t)P.delta);  // raw (reported): the match open at wlo
-          fix_s = i;
+          for (uint32_t t = t1 + lane; t < E; t += 64) {
+            const uint64_t i = eb0 + t;
+            if (i >= cap_n)
+              atomicOr(P.flags, UGPU_FLAG_CAPACITY);
+            else
+              P.out_len[i] = (uint32_t)eo[t] - (uint32_t)so[t - open_r];
+          }
         }
+        s_before += R;
+        e_before += E;
+        const int64_t rl = __shfl(myls, hs ? 63 - __builtin_clzll(hs) : 0, 64);
+        if (hs) last_start = rl;
+#if !defined(UGPU_XE_ABL)  // (the ablations skip stores: K stays 0)
+        K += (R + 255) / 256 + (E > t1 ? (E - t1 + 255) / 256 : 0);  // (at least one store per 4-store step)
+#endif
+      };
+      const uint32_t cs = (uint32_t)__builtin_popcountll(st), ce = (uint32_t)__builtin_popcountll(en);
+      const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane((int)cscan_add(cs), 63);
+      const uint32_t re = (uint32_t)__builtin_amdgcn_readlane((int)cscan_add(ce), 63);
+      if (rs <= kXeWaveCap && re <= kXeWaveCap) {
+        part(st, en);
+      } else {
+        part(lane < 32 ? st : 0, lane < 32 ? en : 0);
+        cwave_sync();  // (the second half stages anew)
+        part(lane < 32 ? 0 : st, lane < 32 ? 0 : en);
       }
-      s_before += R;
-      e_before += E;
-      const int64_t rl = __shfl(myls, hs ? 63 - __builtin_clzll(hs) : 0, 64);
-      if (hs) last_start = rl;
+      xe_wait_k(An, Bn, K);
+      A = An;
+      B = Bn;
       cwave_sync();  // (the next round stages anew)
     }
   }
