@@ -747,7 +747,8 @@ __device__ __forceinline__ void cwrite_now(const CLane& L, const uint32_t cb[4],
 template <bool MASK, bool W, bool WR = false, bool U = false, bool BM = false>
 __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_t q, const CLim& lim, uint32_t& cw,
                                        uint32_t& cs, uint32_t& ws, uint32_t& ls, uint32_t cb[4], CW& wc, COut& o,
-                                       CU& u, CPend* pd = nullptr, uint16_t* slot = nullptr, uint16_t* ib = nullptr)
+                                       CU& u, CPend* pd = nullptr, uint16_t* slot = nullptr, uint16_t* ib = nullptr,
+                                       uint16_t* ibl = nullptr)
 {
 #if defined(UGPU_XC_ABL) && UGPU_XC_ABL == 1  // loads only (benchmarking; wrong counts)
   if (!MASK) {
@@ -770,12 +771,24 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
       uint32_t in[4];
 #pragma unroll
       for (int d = 0; d < 4; ++d) in[d] = (L.E[d] | ((L.E[d] >> 1) & cb[d])) & kOnes;  // In_i = G_i | X_i & In_{i-1}
-      ib[q >> 4] = (uint16_t)nib16(in);
+      if (ibl)
+        ibl[(q >> 4) & 63] = (uint16_t)nib16(in);
+      else
+        ib[q >> 4] = (uint16_t)nib16(in);
     } else {
       // the carry-in bits C_i = In_{i-1}, which cfinish has anyway (the adder
       // codes die here: fewer live registers than In_i); xc_expand_kernel
       // shifts them
-      ib[q >> 4] = (uint16_t)nib16(cb);
+#if defined(UGPU_XBM_ABL) && UGPU_XBM_ABL == 1  // bits stored into 32 KiB (benchmarking; wrong records)
+      ib[(q >> 4) & 0x3fff] = (uint16_t)nib16(cb);
+#elif defined(UGPU_XBM_ABL) && UGPU_XBM_ABL == 2  // bits not stored (benchmarking; wrong records)
+      cs += nib16(cb) == 0x12345u;
+#else
+      if (ibl)
+        ibl[(q >> 4) & 63] = (uint16_t)nib16(cb);  // (the tile's bits leave by wide stores)
+      else
+        ib[q >> 4] = (uint16_t)nib16(cb);
+#endif
     }
   }
   if constexpr (WR) {
@@ -793,7 +806,8 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
 // before the chunk (bit 24: the byte just before).
 template <bool UW, bool FAST, bool BM = false>
 __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q, uint32_t& mprev, uint32_t& cs,
-                                              uint32_t& ws, uint32_t& ls, uint16_t* ib = nullptr)
+                                              uint32_t& ws, uint32_t& ls, uint16_t* ib = nullptr,
+                                              uint16_t* ibl = nullptr)
 {
 #if defined(UGPU_XU_ABL) && UGPU_XU_ABL == 3  // loads only (benchmarking; wrong counts)
   cs += v.x ^ v.y ^ v.z ^ v.w;
@@ -814,7 +828,12 @@ __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q,
     const uint32_t wd = (4u * d) | ((4u * d + 1) << 8) | ((4u * d + 2) << 16) | ((4u * d + 3) << 24);
     ws = __builtin_amdgcn_udot4(st, wd, ws, false);
   }
-  if constexpr (BM) ib[q >> 4] = (uint16_t)nib16(m);  // (In = M here)
+  if constexpr (BM) {
+    if (ibl)
+      ibl[(q >> 4) & 63] = (uint16_t)nib16(m);  // (In = M here; the tile's bits leave by wide stores)
+    else
+      ib[q >> 4] = (uint16_t)nib16(m);
+  }
 }
 
 // U mode, OFFSETS (WRITE), a chunk wholly inside [wlo, hi): In = M here too,
@@ -895,6 +914,10 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
   __shared__ __attribute__((aligned(16))) uint32_t ubm3[U ? kXuBm3 : 1];
   constexpr uint32_t kStg = U ? kStageU : kStage;
   __shared__ __attribute__((aligned(16))) uint16_t wstage[WR ? kCWaves * 2 * 2 * kStg : 2];
+  // BM: a tile's In bits (64 lanes x 16 bits per chunk), gathered so that they
+  // leave as one store of kIt * 2 bytes per lane instead of a 2-byte store per
+  // lane and chunk (those ran at a fraction of the HBM write rate)
+  __shared__ __attribute__((aligned(16))) uint16_t bmst[BM ? kCWaves * 64 * kIt : 1];
   CU u;
   if constexpr (U) {
     // the pair table: entry (x, y) at x << 8 | (y ^ (x << 2 & 0xfc))
@@ -1089,8 +1112,9 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
           }
         }
         uint16_t* const slot = out.stage + (uint32_t)(j & 1) * 2u * kStg;
+        uint16_t* const ibl = BM ? bmst + ((uint32_t)wid * kIt + j) * 64u : nullptr;
         if constexpr (U && !WR)
-          uchunk_direct<W, FAST, BM>(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls, P.inbits);
+          uchunk_direct<W, FAST, BM>(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls, P.inbits, ibl);
         else if constexpr (U && WR)
           uchunk_write<FAST>(u, cur[j], ts + j * kCChunk + lo16, mprev, out, pend[j & 1], slot);
         else if constexpr (WR)
@@ -1098,7 +1122,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
                                   &pend[j & 1], slot);
         else
           cchunk<false, W, WR, U, BM>(cc, cur[j], ts + j * kCChunk + lo16, lim, cw, a.cs[j], a.ws, a.ls, cb, wc, out,
-                                      u, nullptr, nullptr, P.inbits);
+                                      u, nullptr, nullptr, P.inbits, ibl);
         if constexpr (WR) {
           // the stores of the staged slots: at the tile end after the next
           // tile's loads (cwrite: they then overlap the next tile's work),
@@ -1113,6 +1137,15 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
         }
       };
       cunroll<0, kIt>(chunk);
+      if constexpr (BM) {
+        // the tile's bits: kIt * 128 contiguous bytes at bit offset ts
+        using BmWord = typename std::conditional<kIt == 8, uint4, typename std::conditional<kIt == 4, uint2, uint32_t>::type>::type;
+        static_assert(sizeof(BmWord) == 2 * kIt, "one word per lane");
+        cwave_sync();
+        const BmWord v = reinterpret_cast<const BmWord*>(bmst + (uint32_t)wid * kIt * 64u)[lane];
+        reinterpret_cast<BmWord*>(P.inbits + (ts >> 4))[lane] = v;
+        cwave_sync();  // (the next tile's chunks write the slots anew)
+      }
       uint32_t c = 0, cj = 0;
 #pragma unroll
       for (int j = 0; j < kIt; ++j) {
@@ -1273,33 +1306,48 @@ __device__ __forceinline__ void xe_stage(uint16_t* o, uint32_t k0, uint32_t k1, 
     m &= ~(1ull << hi);
   }
 }
-// the same with N the largest of 32, 16, 8, 4, 0 not above k (uniform): one
+// the same with N the largest of 48, 32, 24, 16, 12, 8, 4, 0 not above k (uniform): one
 // asm statement, so that a and b are never read (copied) before the wait
 __device__ __forceinline__ void xe_wait_k(uint64_t& a, uint64_t& b, uint32_t k)
 {
   asm volatile(
-      "s_cmp_lt_u32 %2, 32\n\t"
+      "s_cmp_lt_u32 %2, 48\n\t"
       "s_cbranch_scc1 1f\n\t"
-      "s_waitcnt vmcnt(32)\n\t"
-      "s_branch 5f\n"
+      "s_waitcnt vmcnt(48)\n\t"
+      "s_branch 9f\n"
       "1:\n\t"
-      "s_cmp_lt_u32 %2, 16\n\t"
+      "s_cmp_lt_u32 %2, 32\n\t"
       "s_cbranch_scc1 2f\n\t"
-      "s_waitcnt vmcnt(16)\n\t"
-      "s_branch 5f\n"
+      "s_waitcnt vmcnt(32)\n\t"
+      "s_branch 9f\n"
       "2:\n\t"
-      "s_cmp_lt_u32 %2, 8\n\t"
+      "s_cmp_lt_u32 %2, 24\n\t"
       "s_cbranch_scc1 3f\n\t"
-      "s_waitcnt vmcnt(8)\n\t"
-      "s_branch 5f\n"
+      "s_waitcnt vmcnt(24)\n\t"
+      "s_branch 9f\n"
       "3:\n\t"
-      "s_cmp_lt_u32 %2, 4\n\t"
+      "s_cmp_lt_u32 %2, 16\n\t"
       "s_cbranch_scc1 4f\n\t"
-      "s_waitcnt vmcnt(4)\n\t"
-      "s_branch 5f\n"
+      "s_waitcnt vmcnt(16)\n\t"
+      "s_branch 9f\n"
       "4:\n\t"
+      "s_cmp_lt_u32 %2, 12\n\t"
+      "s_cbranch_scc1 5f\n\t"
+      "s_waitcnt vmcnt(12)\n\t"
+      "s_branch 9f\n"
+      "5:\n\t"
+      "s_cmp_lt_u32 %2, 8\n\t"
+      "s_cbranch_scc1 6f\n\t"
+      "s_waitcnt vmcnt(8)\n\t"
+      "s_branch 9f\n"
+      "6:\n\t"
+      "s_cmp_lt_u32 %2, 4\n\t"
+      "s_cbranch_scc1 7f\n\t"
+      "s_waitcnt vmcnt(4)\n\t"
+      "s_branch 9f\n"
+      "7:\n\t"
       "s_waitcnt vmcnt(0)\n"
-      "5:"
+      "9:"
       : "+v"(a), "+v"(b)
       : "s"(__builtin_amdgcn_readfirstlane(k))
       : "memory", "scc");
@@ -1312,7 +1360,10 @@ __device__ __forceinline__ void xe_wait_k(uint64_t& a, uint64_t& b, uint32_t k)
 constexpr uint32_t kXeWaveCap = UGPU_XE_CAP;  // starts (and ends) a wave-round stages at once (2 KiB each)
 
 template <bool U>
-__global__ __launch_bounds__(kXeThreads) void xc_expand_kernel(ScanParams P)
+#ifndef UGPU_XE_WAVES_PER_EU
+#define UGPU_XE_WAVES_PER_EU 6
+#endif
+__global__ __launch_bounds__(kXeThreads) __attribute__((amdgpu_waves_per_eu(UGPU_XE_WAVES_PER_EU))) void xc_expand_kernel(ScanParams P)
 {
   __shared__ uint16_t st_off[4][kXeWaveCap];  // a round's start positions, from the round's first position
   __shared__ uint16_t en_off[4][kXeWaveCap];  // its end positions
@@ -1563,7 +1614,9 @@ __global__ __launch_bounds__(kXeThreads) void xc_expand_kernel(ScanParams P)
         const int64_t rl = __shfl(myls, hs ? 63 - __builtin_clzll(hs) : 0, 64);
         if (hs) last_start = rl;
 #if !defined(UGPU_XE_ABL)  // (the ablations skip stores: K stays 0)
-        K += (R + 255) / 256 + (E > t1 ? (E - t1 + 255) / 256 : 0);  // (at least one store per 4-store step)
+        // (a store instruction goes out for every 64 records: lane 0 takes part
+        // in each; the one store of the match open at the round start aside)
+        K += (R + 63) / 64 + (E > t1 ? (E - t1 + 63) / 64 : 0);
 #endif
       };
       const uint32_t cs = (uint32_t)__builtin_popcountll(st), ce = (uint32_t)__builtin_popcountll(en);
