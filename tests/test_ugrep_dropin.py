@@ -160,3 +160,50 @@ def test_dropin_ugrep_reproduces_goldens():
         diff = sorted(k for k in set(cpu_cases) | set(want["cpu_cases"]) if cpu_cases.get(k) != want["cpu_cases"].get(k))
         assert not diff, [(k, cpu_cases.get(k), want["cpu_cases"].get(k)) for k in diff[:10]]
         assert served == want["served_by_gpu"]
+
+
+# word-boundary searches: ugrep_gpu against the reference
+# build on the same files, byte for byte; the finite patterns are served by the
+# GPU, a boundary after a loop stays on the CPU matcher (reason
+# anchor_predictor: the reference's match predictor decides there)
+WORDB_CMDS = [(["-co", r"\bdolor\b"], True), (["-on", r"\<con"], True), (["-c", r"um\>"], True),
+              (["-co", r"\Bor\B"], True), (["-io", r"\b(lorem|ipsum|sit)\b"], True), (["-o", r"\<(in|ut)\>"], True),
+              (["-co", r"\w+\b"], False)]
+
+
+@pytest.mark.gpu
+def test_dropin_word_boundaries_on_gpu(tmp_path):
+    exe_gpu = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")
+    exe_ref = os.path.join(ROOT, "oracle", "_ref", "ugrep")
+    if not (os.path.exists(exe_gpu) and os.path.exists(exe_ref)):
+        pytest.skip("ugrep builds missing (make -C oracle ref, build container)")
+    import numpy as np
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import gen
+    lorem = open(os.path.join(CWD, "lorem.utf8.txt"), "rb").read()
+    (tmp_path / "lorem1m.txt").write_bytes((lorem * (1 + (1 << 20) // len(lorem)))[:1 << 20])
+    (tmp_path / "words.txt").write_bytes(np.asarray(gen(4, 5, 0, 3 << 20)).tobytes())
+    files = ["lorem1m.txt", "words.txt"]
+    env = dict(os.environ, UGPU_ADAPTER_MIN_BYTES="0", UGPU_ADAPTER_STATS="1", UGPU_ADAPTER_WARM="0")
+    ledger = []
+    for args, on_gpu in WORDB_CMDS:
+        ref = subprocess.run([exe_ref, "--sort"] + args + files, cwd=tmp_path, capture_output=True, timeout=120, env=env)
+        got = subprocess.run([exe_gpu, "--sort"] + args + files, cwd=tmp_path, capture_output=True, timeout=120, env=env)
+        assert ref.returncode == got.returncode, args
+        assert got.stdout == ref.stdout, (args, len(got.stdout), len(ref.stdout))
+        st = _stats(got.stderr)
+        gpu_finds = sum(m["gpu"] for m in st)
+        ledger.append(dict(args=args, out_bytes=len(ref.stdout), gpu_finds=gpu_finds,
+                           cpu_finds=sum(m["cpu"] for m in st), why=[m["why"] for m in st if m["why"]]))
+        if on_gpu:
+            # (matchers ugrep built but never ran show table "none"; a FIND
+            # call past a file's last record may go to the CPU matcher)
+            assert gpu_finds > 0 and not any(m["table"] == "unsupported" for m in st), (args, st)
+            assert not any({"anchor_predictor", "table", "engine"} & set(m["why"]) for m in st), (args, st)
+        else:
+            assert gpu_finds == 0 and any("anchor_predictor" in m["why"] for m in st), (args, st)
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "dropin_wordb_ledger.json"), "w") as f:
+        json.dump(ledger, f, indent=1)
