@@ -20,7 +20,7 @@ def db(d, sub):
 
 def main(d, match=("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "xc_kernel", "xu_kernel", "scan_kernel")):
     kernels = []
-    c = db(d, "trace")
+    c = c_trace = db(d, "trace")
     if c:
         for name, calls, total, avg, pct in c.execute(
                 "select name, total_calls, total_duration, average, percentage from top_kernels"):
@@ -61,6 +61,17 @@ def main(d, match=("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "x
             bench = json.loads(fh.read().strip().splitlines()[-1])
     except (OSError, ValueError, IndexError):
         pass
+    # the timed steps' dispatches: the last `steps` full-size ones (before them
+    # come the warmup steps and the first launch, slower while clocks ramp)
+    if dom and bench and "main_dispatches" in dom and c_trace:
+        steps = int(bench.get("steps", 0))
+        durs = [r[0] / 1e3 for r in c_trace.execute("select duration from kernels where name = ? order by dispatch_id",
+                                                    (dom["name"],))]
+        top = max(durs)
+        main_ = [x for x in durs if x >= 0.75 * top]
+        if steps and len(main_) >= steps:
+            dom["timed_dispatches"] = steps
+            dom["timed_avg_us"] = round(sum(main_[-steps:]) / steps, 3)
     res = {"kernels": kernels, "dominant": dom, "counters_last_dispatch": counters}
     if bench:
         res["bench"] = {k: bench[k] for k in ("value", "ms_per_step", "matches", "roofline", "config") if k in bench} \
@@ -74,7 +85,7 @@ def main(d, match=("sparse_kernel", "dense_kernel", "xi_kernel", "xg_kernel", "x
     if "GRBM_GUI_ACTIVE" in counters and dom:
         res["effective_clock_ghz"] = round(counters["GRBM_GUI_ACTIVE"] / 8 / (dom.get("main_avg_us", dom["avg_us"]) * 1e3), 3)
     if dom and "main_avg_us" in dom:
-        res["kernel_ms"] = round(dom["main_avg_us"] / 1e3, 4)
+        res["kernel_ms"] = round(dom.get("timed_avg_us", dom["main_avg_us"]) / 1e3, 4)
         if bench and "roofline" in bench:
             # the trace's average against the bench line's HIP-event time of the same command
             res["kernel_ms_bench"] = bench["roofline"].get("kernel_ms")
