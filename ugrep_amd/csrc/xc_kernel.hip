@@ -1295,15 +1295,28 @@ __device__ __forceinline__ void xe_wait(uint64_t& a, uint64_t& b)
   asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
 }
 // a lane's events (bits of m, positions lb + bit) staged at k0 .. k1 - 1 of
-// o in position order, two per step
+// o in position order
 __device__ __forceinline__ void xe_stage(uint16_t* o, uint32_t k0, uint32_t k1, uint32_t lb, uint64_t m)
 {
-  while (m) {
-    const uint32_t lo = (uint32_t)__builtin_ctzll(m), hi = 63u - (uint32_t)__builtin_clzll(m);
-    o[k0++] = (uint16_t)(lb + lo);
-    o[--k1] = (uint16_t)(lb + hi);  // (lo == hi: the same slot, the same value)
-    m &= m - 1;
-    m &= ~(1ull << hi);
+  // (32-bit halves side by side, each from both ends: a step writes up to 4
+  // events, with 32-bit bit scans)
+  uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+  uint32_t a0 = k0, a1 = k0 + (uint32_t)__builtin_popcount(lo), b0 = a1, b1 = k1;
+  while (lo | hi) {
+    if (lo) {
+      const uint32_t f = (uint32_t)__builtin_ctz(lo), g = 31u - (uint32_t)__builtin_clz(lo);
+      o[a0++] = (uint16_t)(lb + f);
+      o[--a1] = (uint16_t)(lb + g);  // (f == g: the same slot, the same value)
+      lo &= lo - 1;
+      lo &= ~(1u << g);
+    }
+    if (hi) {
+      const uint32_t f = (uint32_t)__builtin_ctz(hi), g = 31u - (uint32_t)__builtin_clz(hi);
+      o[b0++] = (uint16_t)(lb + 32u + f);
+      o[--b1] = (uint16_t)(lb + 32u + g);
+      hi &= hi - 1;
+      hi &= ~(1u << g);
+    }
   }
 }
 // the same with N the largest of 48, 32, 24, 16, 12, 8, 4, 0 not above k (uniform): one
@@ -1541,7 +1554,11 @@ __global__ __launch_bounds__(kXeThreads) __attribute__((amdgpu_waves_per_eu(UGPU
         if (sb0 + R <= cap_n && !P.out_cap) {
           // (the usual case: 4 staged starts read, then 4 stores)
           const uint64_t sbase = pb + (uint64_t)P.delta;
+#if defined(UGPU_XE_ABL) && UGPU_XE_ABL == 4  // records into 3 MiB (L2-resident; benchmarking; wrong records)
+          uint64_t* const os = P.out_start + (sb0 & 0x3ffffu);
+#else
           uint64_t* const os = P.out_start + sb0;
+#endif
           for (uint32_t t0 = 0; t0 < R; t0 += 256) {
             uint32_t v[4];
 #pragma unroll
@@ -1586,7 +1603,11 @@ __global__ __launch_bounds__(kXeThreads) __attribute__((amdgpu_waves_per_eu(UGPU
           t1 = 1;
         }
         if (eb0 + E <= cap_n) {
+#if defined(UGPU_XE_ABL) && UGPU_XE_ABL == 4
+          uint32_t* const ol = P.out_len + (eb0 & 0x3ffffu);
+#else
           uint32_t* const ol = P.out_len + eb0;
+#endif
           for (uint32_t t0 = t1; t0 < E; t0 += 256) {
             uint32_t v[4];
 #pragma unroll
@@ -1613,16 +1634,21 @@ __global__ __launch_bounds__(kXeThreads) __attribute__((amdgpu_waves_per_eu(UGPU
         e_before += E;
         const int64_t rl = __shfl(myls, hs ? 63 - __builtin_clzll(hs) : 0, 64);
         if (hs) last_start = rl;
-#if !defined(UGPU_XE_ABL)  // (the ablations skip stores: K stays 0)
+#if !defined(UGPU_XE_ABL) || UGPU_XE_ABL == 4  // (ablations 1-3 skip stores: K stays 0)
         // (a store instruction goes out for every 64 records: lane 0 takes part
         // in each; the one store of the match open at the round start aside)
         K += (R + 63) / 64 + (E > t1 ? (E - t1 + 63) / 64 : 0);
 #endif
       };
       const uint32_t cs = (uint32_t)__builtin_popcountll(st), ce = (uint32_t)__builtin_popcountll(en);
-      const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane((int)cscan_add(cs), 63);
-      const uint32_t re = (uint32_t)__builtin_amdgcn_readlane((int)cscan_add(ce), 63);
-      if (rs <= kXeWaveCap && re <= kXeWaveCap) {
+      // (no lane above 16 events of a kind: the round fits; else count exactly)
+      bool fits = __ballot(cs > kXeWaveCap / 64 || ce > kXeWaveCap / 64) == 0;
+      if (!fits) {
+        const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane((int)cscan_add(cs), 63);
+        const uint32_t re = (uint32_t)__builtin_amdgcn_readlane((int)cscan_add(ce), 63);
+        fits = rs <= kXeWaveCap && re <= kXeWaveCap;
+      }
+      if (fits) {
         part(st, en);
       } else {
         part(lane < 32 ? st : 0, lane < 32 ? en : 0);
