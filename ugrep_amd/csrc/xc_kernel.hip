@@ -1374,7 +1374,7 @@ constexpr uint32_t kXeWaveCap = UGPU_XE_CAP;  // starts (and ends) a wave-round 
 
 template <bool U>
 #ifndef UGPU_XE_WAVES_PER_EU
-#define UGPU_XE_WAVES_PER_EU 6
+#define UGPU_XE_WAVES_PER_EU 7
 #endif
 __global__ __launch_bounds__(kXeThreads) __attribute__((amdgpu_waves_per_eu(UGPU_XE_WAVES_PER_EU))) void xc_expand_kernel(ScanParams P)
 {
@@ -1525,7 +1525,10 @@ __global__ __launch_bounds__(kXeThreads) __attribute__((amdgpu_waves_per_eu(UGPU
     }
     for (uint64_t w0 = qb; w0 < qend; w0 += 64) {
       const uint64_t wi = w0 + lane, pos = wi * 64;
-      uint64_t An = xe_load(words + ia(wi + 64)), Bn = xe_load(words + ib(wi + 64));
+      // (U: the neighbour words of the next round are this round's, one lane
+      // up -- no second load)
+      uint64_t An = xe_load(words + ia(wi + 64)), Bn = 0;
+      if constexpr (!U) Bn = xe_load(words + ib(wi + 64));
       uint64_t st = 0, en = 0;
       if (wi < qend) events(wi, raw(wi, A, B), st, en);
       const uint64_t pb = w0 * 64;
@@ -1656,8 +1659,20 @@ __global__ __launch_bounds__(kXeThreads) __attribute__((amdgpu_waves_per_eu(UGPU
         part(lane < 32 ? 0 : st, lane < 32 ? 0 : en);
       }
       xe_wait_k(An, Bn, K);
+      if constexpr (U) {
+        // b of lane l is word wi - 1: lane l - 1's, and for lane 0 this
+        // round's last word
+        const uint64_t a63 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(A >> 32), 63) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)A, 63);
+        const uint32_t blo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)a63, (int)(uint32_t)An, 0x138, 0xf, 0xf,
+                                                                   false);  // wave_shr:1
+        const uint32_t bhi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(a63 >> 32), (int)(uint32_t)(An >> 32),
+                                                                   0x138, 0xf, 0xf, false);
+        B = ((uint64_t)bhi << 32) | blo;
+      } else {
+        B = Bn;
+      }
       A = An;
-      B = Bn;
       cwave_sync();  // (the next round stages anew)
     }
   }
