@@ -19,6 +19,9 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 import ugrep_amd as U  # noqa: E402
 
 PATS = [("c3", "[A-Za-z_][A-Za-z0-9_]*", 3), ("c4", r"\w+", 4)]
+CHUNKS = [int(x) for x in os.environ.get("SWEEP_CHUNKS", "16,32,64").split(",")]
+DENSE = [int(x) for x in os.environ.get("SWEEP_DENSE", "0,1").split(",")]
+THREADS = [int(x) for x in os.environ.get("SWEEP_THREADS", "8,16").split(",")]
 
 
 def main():
@@ -33,7 +36,7 @@ def main():
         buf = gen(kind, 1, 0, n)
         want = U.find_all(pat, buf, offsets=False)
         want = (want.count, want.digest, want.dcap)
-        for chunk, dense, threads, borrow in itertools.product((16, 32, 64), (0, 1), (8, 16), (False, True)):
+        for chunk, dense, threads, borrow in itertools.product(CHUNKS, DENSE, THREADS, (False, True)):
             os.environ["UGPU_REC_CHUNK"] = str(chunk << 20)
             os.environ["UGPU_REC_DENSE"] = str(dense)
             os.environ["UGPU_REC_DRAIN_THREADS"] = str(threads)

@@ -1629,7 +1629,7 @@ struct ugpu_records {
   bool cancel = false;      // ugpu_records_free before the end: the pipeline stops at its next chunk
   bool unbounded = false;   // ugpu_records_totals waits for the end: no limit on pieces ahead
   size_t ahead = 4;         // pieces the pipeline may publish ahead of the consumer (UGPU_REC_AHEAD)
-  uint64_t chunk = 32ull << 20;  // input bytes per piece (UGPU_REC_CHUNK)
+  uint64_t chunk = 16ull << 20;  // input bytes per piece (UGPU_REC_CHUNK)
   int rc = 0;
   std::mutex mu;
   std::condition_variable cv;
@@ -1679,7 +1679,9 @@ uint8_t* pinned_get(size_t need, size_t& got)
       return p;
     }
   }
-  size_t c = 64u << 20;
+  // (power-of-two blocks from 4 MiB: a piece of a small chunk does not pin
+  // 64 MiB, which pushed the pool past kPinKeep and into a pin/unpin per piece)
+  size_t c = 4u << 20;
   while (c < need) c *= 2;
   void* p = nullptr;
   // (non-coherent: cached for the host reads that decode the records; every
@@ -2182,11 +2184,9 @@ int ugpu_find_records_ex(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, 
   R->sync_d2h = env_u64("UGPU_REC_SYNC", 0) != 0;
   R->zero_copy = env_u64("UGPU_REC_ZC", 0) != 0;
   R->trace = env_u64("UGPU_REC_TRACE", 0) != 0;
-  // chunks of 32 MiB (16 MiB for a borrowed buffer, whose consumer starts at
-  // the first piece: tools/rec_sweep.py); the pipeline runs at
-  // most 256 MiB of input (and at least 4 pieces) ahead of the consumer
-  R->chunk = std::max<uint64_t>(env_u64("UGPU_REC_CHUNK", (flags & UGPU_REC_BORROW) ? 16ull << 20 : 32ull << 20),
-                                1ull << 20);
+  // chunks of 16 MiB (tools/rec_sweep.py); the pipeline runs
+  // at most 256 MiB of input (and at least 4 pieces) ahead of the consumer
+  R->chunk = std::max<uint64_t>(env_u64("UGPU_REC_CHUNK", 16ull << 20), 1ull << 20);
   R->ahead = (size_t)std::max<uint64_t>(env_u64("UGPU_REC_AHEAD", std::max<uint64_t>(4, (256ull << 20) / R->chunk)), 1);
   R->t0 = std::chrono::steady_clock::now();
   if (len == start) {
