@@ -27,7 +27,7 @@ import torch.distributed as dist  # noqa: E402
 
 # the engine (libugrep_amd.so) is loaded by main() after the launcher decision,
 # so that a parent that only starts the rank processes never loads HIP code
-ugrep_amd = gather_offsets = scan_shard = shard_bounds = stitch = None
+ugrep_amd = gather_offsets = Shard = shard_bounds = stitch = None
 
 METRIC = "GB/s scanned + matches/s, 16 GiB synthetic buffer, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
@@ -272,11 +272,11 @@ def main():
     if args.launch_check:
         launch_check(backend)
         return
-    global ugrep_amd, gather_offsets, scan_shard, shard_bounds, stitch
+    global ugrep_amd, gather_offsets, Shard, shard_bounds, stitch
     import ugrep_amd as _u
     from ugrep_amd import dist as _d
-    ugrep_amd, gather_offsets, scan_shard, shard_bounds, stitch = (_u, _d.gather_offsets, _d.scan_shard,
-                                                                  _d.shard_bounds, _d.stitch)
+    ugrep_amd, gather_offsets, Shard, shard_bounds, stitch = (_u, _d.gather_offsets, _d.Shard, _d.shard_bounds,
+                                                             _d.stitch)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -302,8 +302,7 @@ def main():
     if args.config in STRONG and not args.bytes:
         per_gpu = size // world
     total = per_gpu * world
-    lo, hi, read_end, eof = shard_bounds(total, world, rank, args.halo)
-    n_read = read_end - lo
+    lo, hi, _, _ = shard_bounds(total, world, rank, args.halo)
     with open(os.path.join(REPO, "ugrep_amd", "data", "config_patterns.json")) as f:
         opc = json.load(f)[pkey]["opc"]
     if args.compile:
@@ -331,18 +330,15 @@ def main():
     if args.offsets:
         sc.stage(True)  # single-pass OFFSETS (prefiltered tables): the COUNT pass stages the records
     # one scan before the timed steps: a match longer than the halo grows it
-    # (dist.scan_shard), so the steps run on a shard that holds its matches
-    _, buf, read_end = scan_shard(sc, fetch, lo, hi, total, args.halo, stream=sptr)
-    eof = read_end == total
-    n_read = read_end - lo
-    log("rank %d: shard [%d, %d) read_end %d, pattern %s: %s" % (rank, lo, hi, read_end, rx, info))
-    ptr = buf.data_ptr()
+    # (dist.Shard), so the steps run on a shard that holds its matches; the
+    # chain fix and the true-entry re-scan grow it the same way, on the owner
+    # rank before any collective (a failure there is broadcast by stitch and
+    # every rank exits non-zero)
+    shard = Shard(sc, fetch, lo, hi, total, args.halo, stream=sptr)
+    shard.scan()
+    buf = shard.buf
+    log("rank %d: shard [%d, %d) read_end %d, pattern %s: %s" % (rank, lo, hi, shard.read_end, rx, info))
     kms = []
-
-    def fix_fn(old, new):
-        t = sc.chain_fix(ptr, 0, hi - lo, n_read, eof, lo, old - lo, new - lo, sptr)
-        return dict(count=t.count, digest=t.digest, dcap=t.dcap,
-                    exit=None if t.exit == (1 << 64) - 1 else t.exit + lo)
 
     recs_dev = {}  # --offsets: device record arrays, grown outside the timed steps when possible
 
@@ -362,23 +358,24 @@ def main():
         st, ln = recs_dev["start"][:count], recs_dev["len"][:count]
         ac = None if acc is None else acc[:count]
         if pg:
-            st, ln, ac = gather_offsets(st.to(xdev), ln.to(xdev), None if ac is None else ac.to(xdev))
-        return st, ln, ac
+            # to rank 0 only, as per-rank parts (dist.gather_offsets: an
+            # all_gather of dense tables' records would not fit at 8 ranks)
+            g = gather_offsets(st.to(xdev), ln.to(xdev), None if ac is None else ac.to(xdev), dst=0, concat=False)
+            return ([st], [ln], [ac]) if g is None else g  # (ranks > 0: their own, for the digest check)
+        return [st], [ln], [ac]
 
     def step():
-        sc.scan(ptr, 0, hi - lo, n_read, eof, lo, sptr)
-        t = sc.totals()
+        rec = shard.scan()
         kms.append(sc.kernel_ms())
-        rec = dict(entry=t.entry + lo, exit=t.exit + lo, count=t.count, digest=t.digest, dcap=t.dcap)
         if pg:
-            rec = stitch(rec, fix_fn, device=xdev)
+            rec = stitch(rec, shard.fix, device=xdev)
         if args.offsets:
-            count = t.count
+            count = rec["count"] if not pg else None
             if pg and rec["entries"][rank] != lo:  # chain re-entered this shard: re-scan from there
                 # (an entry at or past hi: the previous shard's last match covers this whole shard)
-                ent = min(rec["entries"][rank], hi)
-                sc.scan(ptr, ent - lo, hi - lo, n_read, eof, lo, sptr)
-                count = sc.totals().count
+                count = shard.scan(rec["entries"][rank])["count"]
+            elif pg:
+                count = rec["counts"][rank]
             rec["records"] = records(count)
         return rec
 
@@ -400,6 +397,7 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     pcie = None
+    buf = shard.buf  # (a grown halo replaced it)
     if rank == 0 and world == 1 and args.pcie_sample_mib > 0:
         pcie = pcie_inclusive(pat, buf, min(args.pcie_sample_mib << 20, hi - lo), dev)
     cpu_leg = (None, None)
@@ -432,6 +430,7 @@ def main():
     verified = None
     if args.verify:
         del buf
+        shard.buf = None
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
         if pg:
@@ -480,12 +479,15 @@ def main():
     if verified is not None:
         out["verified_whole_stream"] = verified
     if args.offsets:
-        st, ln, _ = res["records"]
+        sts, lns, _ = res["records"]
         m64 = (1 << 64) - 1
-        dg = int((st * 31 + ln.to(torch.int64)).sum().item()) & m64  # int64 sums wrap like the u64 digest
-        out["offsets"] = {"records": int(st.numel()), "bytes_per_record": 12 if one_accept else 16,
-                          "gathered_to": "all ranks" if pg else "local",
-                          "digest_matches_totals": int(st.numel()) == res["count"] and dg == res["digest"]}
+        nrec = sum(int(s_.numel()) for s_ in sts)
+        dg = sum(int((s_ * 31 + l_.to(torch.int64)).sum().item()) for s_, l_ in zip(sts, lns)) & m64  # (wraps as u64)
+        out["offsets"] = {"records": nrec, "bytes_per_record": 12 if one_accept else 16,
+                          "gathered_to": "rank 0 (per-rank parts)" if pg else "local",
+                          "digest_matches_totals": nrec == res["count"] and dg == res["digest"]}
+        if shard.grown:
+            out["offsets"]["halo_grown"] = shard.grown
     tr = measured_traffic(args.config, hi - lo, KERNELS[info["kernel"]])
     if tr and tr.get("kernel_ms") and abs(tr["kernel_ms"] - k_avg) > 0.05 * k_avg:
         # the counters were taken on a run whose kernel time differs from this one's

@@ -16,10 +16,13 @@
  * Semantics: identical match records (start, length, accept index) to
  * Matcher::find() on a fully buffered input (AbstractMatcher::buffer(),
  * include/reflex/absmatcher.h:542-591): leftmost-longest, non-overlapping,
- * empty matches rejected (option N off), options A/W off.  Tables with
- * anchors/word-boundary meta edges, lookahead HEAD/TAIL or REDO words return
- * UGPU_UNSUPPORTED; the caller keeps its CPU matcher for those
- * (include/reflex/pattern.h:1194-1217).
+ * empty matches rejected unless option N (UGPU_PAT_EMPTY), option A off;
+ * option W by UGPU_PAT_WORD.  Line anchors (META_BOL/META_EOL) and word
+ * boundaries (META_WBB/WBE/WEB/WEE/NWB/NWE/BWB/EWB) at the start or end of a
+ * match become per-context accepts.  Tables with
+ * lookahead HEAD/TAIL words, buffer anchors (META_BOB/EOB), assertions between
+ * consumed characters, or REDO words return UGPU_UNSUPPORTED; the caller keeps
+ * its CPU matcher for those (include/reflex/pattern.h:1194-1217).
  *
  * All functions return an int status; no exceptions cross this ABI (reference
  * errors: regex_error lib/pattern.cpp:162-169, std::bad_alloc absmatcher.h:401).
@@ -39,7 +42,7 @@ extern "C" {
 
 /* status codes */
 #define UGPU_OK 0
-#define UGPU_UNSUPPORTED 1 /* table needs anchors/lookahead/REDO/W: use the CPU matcher */
+#define UGPU_UNSUPPORTED 1 /* table needs lookahead/REDO/inner assertions: use the CPU matcher */
 #define UGPU_INVAL 2       /* bad argument or malformed opcode table */
 #define UGPU_NOMEM 3       /* host or device allocation failed */
 #define UGPU_DEVICE 4      /* HIP runtime error (see ugpu_last_error) */
@@ -49,6 +52,13 @@ extern "C" {
 /* scan modes */
 #define UGPU_MODE_COUNT 0   /* count + digests only */
 #define UGPU_MODE_OFFSETS 1 /* also materialize (start, len, cap) records */
+
+/* ABI version of this header: bumped whenever a struct below changes layout
+   (ugpu_dfa_info gained contexts/shape in ABI 2).  A caller compiled against
+   one header checks ugpu_abi_version() == UGPU_ABI_VERSION before passing a
+   struct to the library (integration/reflex_gpu_matcher.h does; on a mismatch
+   it keeps the CPU matcher). */
+#define UGPU_ABI_VERSION 2
 
 typedef struct ugpu_dfa ugpu_dfa;
 typedef struct ugpu_scanner ugpu_scanner;
@@ -419,6 +429,8 @@ const char *ugpu_compile_error(void);
 
 const char *ugpu_last_error(void);
 const char *ugpu_version(void);
+/* UGPU_ABI_VERSION of the header the library was built with */
+int ugpu_abi_version(void);
 
 /* Devices (no reference counterpart: its matchers are CPU threads).
    ugpu_select_device makes `dev` the calling thread's device (hipSetDevice):

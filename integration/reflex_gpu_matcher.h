@@ -85,6 +85,7 @@
 #include <thread>
 #include <vector>
 
+#include <dlfcn.h>
 #include <poll.h>
 
 #include <reflex/matcher.h>
@@ -92,6 +93,114 @@
 #include "ugpu.h"
 
 namespace reflex {
+
+// The engine's device half.  ugrep_gpu links only the host half
+// (libugpu_host.so: ugpu_compile, ugpu_dfa_plan_host, ugpu_last_error -- no HIP
+// runtime); the device half (libugrep_amd.so, which links libamdhip64) is
+// dlopen()ed from the directory the host half was loaded from
+// (UGPU_ENGINE_LIB overrides the path) at the first input the policy sends to
+// a device.  A run the CPU matcher serves end to end never loads the HIP
+// runtime: loading it cost every search ~14 ms on a host without a GPU and
+// ~55 ms on the GPU box.  The free functions below are
+// NULL-safe and do not load the device half for a NULL handle.
+struct GpuEngine {
+  bool ok = false;
+  decltype(&ugpu_dfa_create) dfa_create = NULL;
+  decltype(&ugpu_dfa_destroy) dfa_destroy = NULL;
+  decltype(&ugpu_device_count) device_count = NULL;
+  decltype(&ugpu_select_device) select_device = NULL;
+  decltype(&ugpu_warmup) warmup = NULL;
+  decltype(&ugpu_find_all_multi) find_all_multi = NULL;
+  decltype(&ugpu_find_records) find_records = NULL;
+  decltype(&ugpu_records_next) records_next = NULL;
+  decltype(&ugpu_records_free) records_free = NULL;
+  decltype(&ugpu_result_free) result_free = NULL;
+  decltype(&ugpu_stream_create) stream_create = NULL;
+  decltype(&ugpu_stream_destroy) stream_destroy = NULL;
+  decltype(&ugpu_stream_feed) stream_feed = NULL;
+  decltype(&ugpu_abi_version) abi_version = NULL;
+
+  static GpuEngine& get()
+  {
+    static GpuEngine e;
+    static std::once_flag once;
+    std::call_once(once, [] { e.load(); });
+    return e;
+  }
+  // loaded already (without loading it)
+  static bool loaded() { return loaded_flag().load(std::memory_order_acquire); }
+
+ private:
+  static std::atomic<bool>& loaded_flag()
+  {
+    static std::atomic<bool> f(false);
+    return f;
+  }
+  template <class F>
+  static bool sym(void* h, const char* name, F& f)
+  {
+    f = reinterpret_cast<F>(dlsym(h, name));
+    return f != NULL;
+  }
+  void load()
+  {
+    std::string path;
+    const char* env = std::getenv("UGPU_ENGINE_LIB");
+    if (env != NULL && *env)
+    {
+      path = env;
+    }
+    else
+    {
+      Dl_info di;
+      if (dladdr(reinterpret_cast<void*>(&ugpu_compile), &di) != 0 && di.dli_fname != NULL)
+      {
+        path = di.dli_fname;
+        const size_t slash = path.rfind('/');
+        path = (slash == std::string::npos ? std::string() : path.substr(0, slash + 1)) + "libugrep_amd.so";
+      }
+      else
+      {
+        path = "libugrep_amd.so";
+      }
+    }
+    void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (h == NULL)
+      return;
+    ok = sym(h, "ugpu_dfa_create", dfa_create) && sym(h, "ugpu_dfa_destroy", dfa_destroy) &&
+         sym(h, "ugpu_device_count", device_count) && sym(h, "ugpu_select_device", select_device) &&
+         sym(h, "ugpu_warmup", warmup) && sym(h, "ugpu_find_all_multi", find_all_multi) &&
+         sym(h, "ugpu_find_records", find_records) && sym(h, "ugpu_records_next", records_next) &&
+         sym(h, "ugpu_records_free", records_free) && sym(h, "ugpu_result_free", result_free) &&
+         sym(h, "ugpu_stream_create", stream_create) && sym(h, "ugpu_stream_destroy", stream_destroy) &&
+         sym(h, "ugpu_stream_feed", stream_feed) && sym(h, "ugpu_abi_version", abi_version) &&
+         abi_version() == UGPU_ABI_VERSION;
+    loaded_flag().store(true, std::memory_order_release);
+    // (the handle stays open for the process lifetime)
+  }
+};
+
+// NULL-safe frees that never load the device half for a NULL handle
+inline void e_result_free(ugpu_result* r)
+{
+  if (r != NULL)
+    (void)GpuEngine::get().result_free(r);
+}
+inline void e_stream_destroy(ugpu_stream* s)
+{
+  if (s != NULL)
+    (void)GpuEngine::get().stream_destroy(s);
+}
+inline void e_records_free(ugpu_records* r)
+{
+  if (r != NULL)
+    (void)GpuEngine::get().records_free(r);
+}
+inline void e_dfa_destroy(ugpu_dfa* d)
+{
+  if (d != NULL)
+    (void)GpuEngine::get().dfa_destroy(d);
+}
 
 class GpuMatcher : public Matcher {
  public:
@@ -131,10 +240,10 @@ class GpuMatcher : public Matcher {
                    why.empty() ? "-" : why.c_str());
     }
     src_.clear();
-    ugpu_result_free(gres_);
+    e_result_free(gres_);
     if (gst_ != NULL)
       on_device();
-    ugpu_stream_destroy(gst_);
+    e_stream_destroy(gst_);
     release_slot();
     --live();
   }
@@ -146,7 +255,7 @@ class GpuMatcher : public Matcher {
     release_slot();
     if (gst_ != NULL)
       on_device();
-    ugpu_stream_destroy(gst_);
+    e_stream_destroy(gst_);
     gst_ = NULL;
     cpu_stream_ = false;
     sopen_ = false;
@@ -275,7 +384,7 @@ class GpuMatcher : public Matcher {
     std::mutex mu;
     ugpu_dfa* d = NULL;
     bool failed = false;
-    ~Tables() { ugpu_dfa_destroy(d); }
+    ~Tables() { e_dfa_destroy(d); }
   };
   // whether the engine takes the table (false: unsupported, or anchors left to
   // the reference's predictor, tab_anchor_), and whether it is prefiltered --
@@ -291,7 +400,12 @@ class GpuMatcher : public Matcher {
       tab_anchor_ = false;
       tab_ok_ = false;
       sparse_ = false;
-      if (pat_ != NULL)
+      if (pat_ != NULL && ugpu_abi_version() != UGPU_ABI_VERSION)
+      {
+        // (a library built against another ugpu.h: its structs may differ)
+        tab_err_ = "engine library ABI differs from this ugpu.h";
+      }
+      else if (pat_ != NULL)
       {
         const std::string rx = (*pat_)[0];
         uint32_t* opc = NULL;
@@ -358,9 +472,9 @@ class GpuMatcher : public Matcher {
   }
   static void run_warm(Warm* w)
   {
-    bool ok = true;
-    for (int d = 0; d < devices(); ++d)
-      ok = ugpu_warmup(d) == UGPU_OK && ok;
+    bool ok = GpuEngine::get().ok;  // (the device half loads here, on the warm-up thread)
+    for (int d = 0; ok && d < devices(); ++d)
+      ok = GpuEngine::get().warmup(d) == UGPU_OK;
     w->state.store(ok ? 2 : 3, std::memory_order_release);
   }
   bool device_ready()
@@ -408,8 +522,9 @@ class GpuMatcher : public Matcher {
     if (tab_->d == NULL && !tab_->failed)
     {
       on_device();
-      if (ugpu_dfa_create(tab_->opc.data(), static_cast<uint32_t>(tab_->opc.size()), tab_->flags, &tab_->d) !=
-          UGPU_OK)
+      if (!GpuEngine::get().ok ||
+          GpuEngine::get().dfa_create(tab_->opc.data(), static_cast<uint32_t>(tab_->opc.size()), tab_->flags,
+                                      &tab_->d) != UGPU_OK)
       {
         tab_->d = NULL;
         tab_->failed = true;
@@ -594,7 +709,7 @@ class GpuMatcher : public Matcher {
   {
     static const int n = [] {
       int k = 0;
-      return ugpu_device_count(&k) == UGPU_OK && k > 0 ? k : 1;
+      return GpuEngine::get().ok && GpuEngine::get().device_count(&k) == UGPU_OK && k > 0 ? k : 1;
     }();
     return n;
   }
@@ -613,10 +728,14 @@ class GpuMatcher : public Matcher {
   }
   // this matcher's device current on the calling thread (ugrep calls a matcher
   // from the worker thread that owns it, but clones are made elsewhere)
-  void on_device() { (void)ugpu_select_device(dev()); }
+  void on_device()
+  {
+    if (GpuEngine::get().ok)
+      (void)GpuEngine::get().select_device(dev());
+  }
   void drop_records()
   {
-    ugpu_result_free(gres_);
+    e_result_free(gres_);
     gres_ = NULL;
     gi_ = 0;
     src_.clear();
@@ -684,14 +803,14 @@ class GpuMatcher : public Matcher {
     const uint8_t* b = reinterpret_cast<const uint8_t*>(buf_);
     int rc;
     if (devices() > 1 && end_ - cur_ >= multi_min_) {
-      rc = ugpu_find_all_multi(t, b, end_, cur_, UGPU_MODE_OFFSETS, 0, &gres_);
+      rc = GpuEngine::get().find_all_multi(t, b, end_, cur_, UGPU_MODE_OFFSETS, 0, &gres_);
       if (rc == UGPU_OK)
         src_.set(gres_);
     } else {
       // the pipelined host path: records popped from pinned memory as find()
       // asks for them (ugpu_find_records)
       ugpu_records* r = NULL;
-      rc = ugpu_find_records(t, b, end_, cur_, &r);
+      rc = GpuEngine::get().find_records(t, b, end_, cur_, &r);
       if (rc == UGPU_OK)
         src_.set(r);
     }
@@ -770,7 +889,7 @@ class GpuMatcher : public Matcher {
         cpu_stream_why_ = R_SMALL;
         if (gst_ != NULL)
           on_device();
-        ugpu_stream_destroy(gst_);
+        e_stream_destroy(gst_);
         gst_ = NULL;
         --gpu_finds_;
         return cpu(Const::FIND, R_SMALL);
@@ -794,7 +913,7 @@ class GpuMatcher : public Matcher {
         }
         on_device();
         const ugpu_dfa* t = tables();
-        if (t == NULL || ugpu_stream_create(t, 0, &gst_) != UGPU_OK)
+        if (t == NULL || GpuEngine::get().stream_create(t, 0, &gst_) != UGPU_OK)
         {
           gst_ = NULL;
           cpu_stream_ = true;
@@ -806,13 +925,13 @@ class GpuMatcher : public Matcher {
       const size_t from = static_cast<size_t>(sfed_ - num_);
       drop_records();
       on_device();
-      if (ugpu_stream_feed(gst_, reinterpret_cast<const uint8_t*>(buf_ + from), end_ - from,
+      if (GpuEngine::get().stream_feed(gst_, reinterpret_cast<const uint8_t*>(buf_ + from), end_ - from,
                            eof_ ? 1 : flush ? UGPU_FEED_FLUSH : 0, UGPU_MODE_OFFSETS, &gres_) != UGPU_OK)
       {
         // engine unavailable for this input: the CPU matcher takes over at the cursor
         cpu_stream_ = true;
         cpu_stream_why_ = R_ENGINE;
-        ugpu_stream_destroy(gst_);
+        e_stream_destroy(gst_);
         gst_ = NULL;
         --gpu_finds_;
         return cpu(Const::FIND, R_ENGINE);
@@ -856,7 +975,7 @@ class GpuMatcher : public Matcher {
     drop_records();
     if (gst_ != NULL)
       on_device();
-    ugpu_stream_destroy(gst_);
+    e_stream_destroy(gst_);
     gst_ = NULL;
     sopen_ = true;
     sbase_ = at;
@@ -878,7 +997,7 @@ class GpuMatcher : public Matcher {
     bool live() const { return rec != NULL || res != NULL; }
     void clear()
     {
-      ugpu_records_free(rec);
+      e_records_free(rec);
       rec = NULL;
       res = NULL;  // (owned by gres_)
       have = err = false;
@@ -900,7 +1019,7 @@ class GpuMatcher : public Matcher {
     {
       if (rec != NULL)
       {
-        const int rc = ugpu_records_next(rec, &start, &len, &cap);
+        const int rc = GpuEngine::get().records_next(rec, &start, &len, &cap);
         have = rc == 1;
         err = rc < 0;
       }

@@ -282,3 +282,73 @@ def test_multiprocess_gloo_four_ranks(U, patterns, streams):
         o = res[r]["out"]
         assert (o["count"], o["digest"], o["dcap"]) == want, r
     assert (res[0]["n"],) + tuple(res[0]["dg"]) == want
+
+
+def _halo_stream(n):
+    """"12 " filler; 'q' | 'x' 'a' + 6 MiB of 'b' across the 4 MiB cut
+    (tests/test_dist_halo.py's case)."""
+    mib = 1 << 20
+    data = np.frombuffer(b"12 " * (n // 3 + 1), np.uint8)[:n].copy()
+    data[4 * mib - 1] = ord("q")
+    data[4 * mib] = ord("x")
+    data[4 * mib + 1] = ord("a")
+    data[4 * mib + 2:10 * mib + 2] = ord("b")
+    return data
+
+
+def _halo_rank(rank, world, port, opc, q):
+    """One rank of the HALO case: dist.Shard over the HIP Scanner, stitch over gloo."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch as T
+        import ugrep_amd as U
+        from ugrep_amd.dist import Shard, shard_bounds, stitch
+        T.cuda.set_device(0)
+        st_ = T.cuda.current_stream().cuda_stream
+        data = _halo_stream(16 << 20)
+        lo, hi, _, _ = shard_bounds(data.size, world, rank, 64 << 10)
+
+        def fetch(a, z):
+            t = T.zeros(z - a + 16, dtype=T.uint8, device="cuda")
+            t[:z - a].copy_(T.from_numpy(data[a:z]))
+            T.cuda.synchronize()
+            return t
+
+        sh = Shard(U.Scanner(U.Pattern(opc)), fetch, lo, hi, data.size, 64 << 10, stream=st_)
+        out = stitch(sh.scan(), sh.fix)
+        cnt = sh.scan(out["entries"][rank])["count"] if out["entries"][rank] != lo else out["counts"][rank]
+        q.put((rank, dict(out=out, grown=sh.grown, cnt=cnt)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_multiprocess_fix_grows_the_halo(U):
+    """four processes on the one card, xa|ab+|qx, a 6 MiB
+    run of 'b' right after the first cut and a 64 KiB halo: rank 1's TRUE
+    chain (entered after shard 0's "qx") walks the 6 MiB "ab+" match past its
+    halo, ugpu_chain_fix fails with UGPU_HALO, and dist.Shard grows the halo on
+    that rank before the broadcast.  Totals equal the oracle's."""
+    import torch.multiprocessing as mp
+    from oracle_lib import OracleDfa
+    opc = U.compile_regex("xa|ab+|qx")
+    data = _halo_stream(16 << 20)
+    want = OracleDfa(opc).find(data)[:3]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 4
+    procs = [ctx.Process(target=_halo_rank, args=(r, world, port, opc, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(world):
+        o = res[r]["out"]
+        assert (o["count"], o["digest"], o["dcap"]) == want, r
+    assert res[1]["grown"] >= 1
+    assert sum(res[r]["cnt"] for r in range(world)) == want[0]

@@ -141,3 +141,26 @@ def test_records_early_free_and_bounded_pieces(U, patterns, monkeypatch):
     r2 = U.Records(pat, host)
     assert r2.totals() == tuple(OracleDfa(opc).find(host)[:3])
     r2.close()
+
+
+def test_records_free_stops_the_upload(U):
+    """free() on a BORROWED 4 GiB host buffer after the first pop
+    stops the input copy too (the uploader checks the cancel flag between
+    chunks) instead of copying the whole buffer to the device first.  The
+    whole copy alone takes longer than the bound (4 GiB of pageable H2D)."""
+    import time
+    host = np.frombuffer(b"abc de_f9 12+3 " * 16, np.uint8)
+    host = np.tile(host, (4 << 30) // host.size + 1)[:4 << 30]
+    pat = U.Pattern(U.compile_regex("[A-Za-z_][A-Za-z0-9_]*"))
+    r = U.Records(pat, host, borrow=True)
+    assert r.next() == (0, 3, 1)
+    t0 = time.perf_counter()
+    r.close()
+    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    d = torch.from_numpy(host).to("cuda")
+    torch.cuda.synchronize()
+    copy = time.perf_counter() - t1
+    del d
+    print("free %.3f s, whole H2D %.3f s" % (dt, copy))
+    assert dt < 0.5 * copy

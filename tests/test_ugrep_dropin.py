@@ -120,6 +120,23 @@ def test_dropin_default_policy_never_touches_a_device():
     assert why.get("small", 0) > 100, why
 
 
+def test_dropin_links_no_hip_runtime():
+    """ugrep_gpu links the engine's host half only
+    (libugpu_host.so); the device half and the HIP runtime are dlopen()ed at
+    the first input the adapter's policy sends to a GPU, so a CPU-served run
+    does not pay for loading them."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")
+    if not os.path.exists(exe):
+        pytest.skip("ugrep_gpu not built (make -C oracle ref, build container)")
+    out = subprocess.run(["readelf", "-d", exe], capture_output=True, check=True).stdout.decode()
+    needed = [ln.split("[")[1].split("]")[0] for ln in out.splitlines() if "(NEEDED)" in ln]
+    assert "libugpu_host.so" in needed, needed
+    assert not any("ugrep_amd" in n or "amdhip" in n or "hsa" in n for n in needed), needed
+    host = os.path.join(ROOT, "ugrep_amd", "libugpu_host.so")
+    out = subprocess.run(["readelf", "-d", host], capture_output=True, check=True).stdout.decode()
+    assert "amdhip" not in out and "hsa-runtime" not in out
+
+
 @pytest.mark.gpu
 def test_dropin_ugrep_reproduces_goldens():
     exe = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")

@@ -136,6 +136,7 @@ def _load():
         "ugpu_compile_error": (ctypes.c_char_p, []),
         "ugpu_last_error": (ctypes.c_char_p, []),
         "ugpu_version": (ctypes.c_char_p, []),
+        "ugpu_abi_version": (ctypes.c_int, []),
         "ugpu_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
         "ugpu_find_records": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(V)]),
         "ugpu_find_records_ex": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,

@@ -1,0 +1,274 @@
+// host_api.cpp -- the host half of the C ABI (libugpu_host.so, no HIP runtime):
+// table planning, the host-only table entry points and the error string.  See
+// plan.hpp.  The device half (engine.hip) calls dfa_plan / dfa_info_fill and
+// reports its errors through host_fail, so ugpu_last_error answers for both.
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../../include/ugpu.h"
+#include "plan.hpp"
+#include "tables.hpp"
+
+namespace {
+thread_local std::string g_err;
+int fail(int code, const std::string& msg)
+{
+  g_err = msg;
+  return code;
+}
+}  // namespace
+
+namespace ugpu {
+
+int host_fail(int code, const std::string& msg) { return fail(code, msg); }
+
+// \w+ as ugpu_compile builds it (language-equivalent to the reference's table,
+// tests/test_compile.py), compiled once
+bool is_word_plus(const DfaTables& t)
+{
+  static DfaTables wp;
+  static bool ok = [] {
+    uint32_t* opc = nullptr;
+    uint32_t nop = 0;
+    if (ugpu_compile("\\w+", 3, 0, &opc, &nop) != UGPU_OK) return false;
+    std::string err;
+    const bool built = build_tables(opc, nop, wp, err) == 0;
+    ugpu_opc_free(opc);
+    return built;
+  }();
+  return ok && tables_equivalent(t, wp);
+}
+
+DfaPlan dfa_plan(const DfaTables& t, uint32_t flags)
+{
+  DfaPlan p;
+  p.nul = (flags & UGPU_PAT_EMPTY) != 0;
+  p.amode = t.anchored || (p.nul && t.start_acc);
+  if (p.amode) {
+    p.ok = !(flags & UGPU_PAT_WORD);
+    return p;
+  }
+  if (flags & UGPU_PAT_WORD) {
+    p.wtab = true;
+    const bool wf = !(std::getenv("UGPU_WFAST") && std::getenv("UGPU_WFAST")[0] == '0');
+    p.wplus = wf && t.gap && !t.filter && t.cap1 != 0 && is_word_plus(t);
+    p.xcw = wf && t.xc && t.xc_w && !t.filter && t.cap1 != 0;
+    if (!p.wplus && !p.xcw) return p;  // option W runs wfind_kernel only: no transducer tables
+  }
+  const bool tx = !t.filter && t.cap1 != 0;
+  p.xtrans = t.restart_local && tx;
+  p.xid = t.immediate && tx;
+  p.xu = t.xu && tx;
+  p.xg = t.gap && tx;
+  return p;
+}
+
+void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* out)
+{
+  ugpu_dfa_info* info = static_cast<ugpu_dfa_info*>(out);
+  info->states = t.states;
+  info->classes = t.classes;
+  info->row = t.row;
+  info->format = t.format;
+  info->table_bytes = (uint32_t)(t.trans.size() * 2 + t.trans32.size() * 4 + (t.format != FMT_BYTE ? 256 : 0));
+  info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
+  info->first_bytes = t.first_bytes;
+  info->accepting = t.accepting;
+  info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;
+  info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u) |
+                (t.cap1 != 0 && !t.anchored ? UGPU_SHAPE_ONE_ACCEPT : 0u);
+  const char* xenv = std::getenv("UGPU_XI");
+  const char* genv = std::getenv("UGPU_XG");
+  const char* cenv = std::getenv("UGPU_XC");
+  const char* uenv = std::getenv("UGPU_XU");
+  const bool byte_filter = t.filter && t.format == FMT_BYTE;
+  // (dfa_xc and dfa_xu, from the plan instead of the uploaded tables)
+  const bool xc = t.xc && !t.filter && t.cap1 != 0 && (!p.wtab || p.xcw) && !(cenv && cenv[0] == '0');
+  const bool xu = p.xu && (!p.wtab || p.wplus) && !(uenv && uenv[0] == '0');
+  info->kernel = p.amode || t.format == FMT_WIDE || (p.wtab && !p.wplus && !p.xcw && !byte_filter) ? 4u
+                 : byte_filter                                                                  ? 0u
+                 : xc                                                                           ? 5u
+                 : xu                                                                           ? 6u
+                 : (p.xid && !(xenv && xenv[0] == '0'))                                          ? 2u
+                 : (p.xg && !(genv && genv[0] == '0'))                                           ? 3u
+                                                                                                  : 1u;
+}
+
+}  // namespace ugpu
+
+using namespace ugpu;
+
+extern "C" {
+
+const char* ugpu_last_error(void) { return g_err.c_str(); }
+
+const char* ugpu_version(void) { return "ugrep_amd 0.1 (gfx950)"; }
+int ugpu_abi_version(void) { return UGPU_ABI_VERSION; }
+
+int ugpu_dfa_plan_host(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa_info* info)
+{
+  if (!info) return fail(UGPU_INVAL, "info is NULL");
+  if (pattern_flags & ~(UGPU_PAT_WORD | UGPU_PAT_EMPTY)) return fail(UGPU_INVAL, "unknown pattern flags");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  const DfaPlan pl = dfa_plan(t, pattern_flags);
+  if (!pl.ok) return fail(UGPU_UNSUPPORTED, "option W with line anchors or empty matches");
+  dfa_info_fill(t, pl, info);
+  return UGPU_OK;
+}
+
+int ugpu_tables_build_host(const uint32_t* opc, uint32_t nop, ugpu_dfa_info* info, uint16_t* trans,
+                           uint32_t trans_cap, uint8_t* cls, uint32_t* caps, uint32_t caps_cap, uint32_t* start,
+                           uint32_t* accb)
+{
+  if (!info) return fail(UGPU_INVAL, "info is NULL");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  info->states = t.states;
+  info->classes = t.classes;
+  info->row = t.row;
+  info->format = t.format;
+  info->table_bytes = (uint32_t)(t.trans.size() * 2 + t.trans32.size() * 4 + (t.format != FMT_BYTE ? 256 : 0));
+  info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
+  info->first_bytes = t.first_bytes;
+  info->accepting = t.accepting;
+  info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;
+  info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u) |
+                (t.cap1 != 0 && !t.anchored ? UGPU_SHAPE_ONE_ACCEPT : 0u);
+  info->kernel = (t.filter && t.format == FMT_BYTE) ? 0u
+                 : t.format == FMT_WIDE              ? 4u
+                 : (t.xc && t.cap1 != 0)             ? 5u
+                 : (t.xu && t.cap1 != 0)             ? 6u
+                 : (t.immediate && t.cap1 != 0)      ? 2u
+                 : (t.gap && t.cap1 != 0)            ? 3u
+                                                     : 1u;
+  if (start) *start = t.start;
+  if (accb) *accb = t.accb;
+  if (trans) {
+    if (t.format == FMT_WIDE) return fail(UGPU_UNSUPPORTED, "wide table (u32 entries): no u16 host form");
+    if (trans_cap < t.trans.size()) return fail(UGPU_CAPACITY, "trans capacity");
+    std::copy(t.trans.begin(), t.trans.end(), trans);
+  }
+  if (cls) std::copy(t.cls.begin(), t.cls.end(), cls);
+  if (caps) {
+    if (caps_cap < t.caps.size()) return fail(UGPU_CAPACITY, "caps capacity");
+    std::copy(t.caps.begin(), t.caps.end(), caps);
+  }
+  return UGPU_OK;
+}
+
+int ugpu_tables_prefilter_host(const uint32_t* opc, uint32_t nop, uint8_t* ft, int* enabled)
+{
+  if (!ft || !enabled) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  std::copy(t.ft, t.ft + 20, ft);
+  *enabled = t.filter ? 1 : 0;
+  return UGPU_OK;
+}
+
+int ugpu_tables_transducer_host(const uint32_t* opc, uint32_t nop, uint16_t* xtrans, uint32_t xtrans_cap, int* local)
+{
+  if (!local) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *local = t.restart_local ? 1 : 0;
+  if (!t.restart_local) return UGPU_OK;
+  if (!xtrans || xtrans_cap < t.xtrans.size()) return fail(UGPU_INVAL, "xtrans capacity too small");
+  std::copy(t.xtrans.begin(), t.xtrans.end(), xtrans);
+  return UGPU_OK;
+}
+
+int ugpu_tables_immediate_host(const uint32_t* opc, uint32_t nop, uint8_t* xid, uint32_t xid_cap, uint32_t* rows,
+                               uint8_t* sync_byte, int* immediate)
+{
+  if (!immediate || !rows) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *immediate = t.immediate ? 1 : 0;
+  *rows = t.xid_rows;
+  if (sync_byte) *sync_byte = t.sync_byte;
+  if (!t.immediate || !xid) return UGPU_OK;
+  if (xid_cap < t.xid.size()) return fail(UGPU_INVAL, "xid capacity too small");
+  std::copy(t.xid.begin(), t.xid.end(), xid);
+  return UGPU_OK;
+}
+
+int ugpu_tables_gap_host(const uint32_t* opc, uint32_t nop, uint16_t* xg, uint32_t xg_cap, uint8_t* sync, int* gap)
+{
+  if (!gap) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *gap = t.gap ? 1 : 0;
+  if (!t.gap) return UGPU_OK;
+  if (!xg || xg_cap < t.xg.size()) return fail(UGPU_INVAL, "xg capacity too small");
+  std::copy(t.xg.begin(), t.xg.end(), xg);
+  if (sync) std::copy(t.xg_sync.begin(), t.xg_sync.end(), sync);
+  return UGPU_OK;
+}
+
+int ugpu_tables_xc_host(const uint32_t* opc, uint32_t nop, uint8_t* cls, int* ok)
+{
+  if (!ok) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *ok = t.xc ? 1 : 0;
+  if (cls && t.xc) std::copy(t.xc_tab.begin(), t.xc_tab.end(), cls);
+  return UGPU_OK;
+}
+
+int ugpu_tables_xu_host(const uint32_t* opc, uint32_t nop, uint8_t* tab, uint32_t* bm3, int* ok)
+{
+  if (!ok) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *ok = t.xu ? 1 : 0;
+  if (tab && t.xu) std::copy(t.xu_tab.begin(), t.xu_tab.end(), tab);
+  if (bm3 && t.xu) std::copy(t.xu_bm3.begin(), t.xu_bm3.end(), bm3);
+  return UGPU_OK;
+}
+
+int ugpu_tables_context_host(const uint32_t* opc, uint32_t nop, uint32_t* acap, uint32_t acap_cap, int* anchored,
+                             int* start_acc)
+{
+  DfaTables t;
+  std::string err;
+  const int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  if (acap && acap_cap < t.acap.size()) return fail(UGPU_INVAL, "acap too small");
+  if (acap) std::copy(t.acap.begin(), t.acap.end(), acap);
+  if (anchored) *anchored = t.anchored ? 1 : 0;
+  if (start_acc) *start_acc = t.start_acc ? 1 : 0;
+  return UGPU_OK;
+}
+
+int ugpu_tables_equivalent_host(const uint32_t* opc_a, uint32_t nop_a, const uint32_t* opc_b, uint32_t nop_b, int* eq)
+{
+  if (!eq) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables a, b;
+  std::string err;
+  int rc = build_tables(opc_a, nop_a, a, err);
+  if (rc == 0) rc = build_tables(opc_b, nop_b, b, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *eq = tables_equivalent(a, b) ? 1 : 0;
+  return UGPU_OK;
+}
+
+}  // extern "C"

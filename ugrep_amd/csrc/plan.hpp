@@ -1,0 +1,41 @@
+// plan.hpp -- the host half of the engine (libugpu_host.so), shared with the
+// device half (engine.hip in libugrep_amd.so).
+//
+// The host half holds everything a caller needs to decide, without a device,
+// whether and how a pattern runs on the GPU: the table builder (tables.cpp),
+// the regex compiler (regex_compile.cpp), the plan below, the host-only C ABI
+// (ugpu_compile, ugpu_dfa_plan_host, ugpu_tables_*_host) and the error string
+// of both halves (ugpu_last_error).  It does not link the HIP runtime, so the
+// drop-in matcher links only it and loads the device half at the first input
+// its policy sends to a GPU (integration/reflex_gpu_matcher.h).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "tables.hpp"
+
+// Unicode Word ranges as flat [lo, hi] pairs (regex_compile.cpp, the table of \w)
+void ugpu_word_ranges(std::vector<uint32_t>& out);
+
+namespace ugpu {
+
+// What ugpu_dfa_create uploads for a table under pattern flags, and so which
+// kernels its scans run: decided on the host alone (ugpu_dfa_plan_host answers
+// it without touching a device)
+struct DfaPlan {
+  bool ok = true;  // false: option W with line anchors or empty matches (UGPU_UNSUPPORTED)
+  bool nul = false, amode = false;
+  bool wtab = false, wplus = false, xcw = false;
+  bool xtrans = false, xid = false, xu = false, xg = false;
+};
+
+DfaPlan dfa_plan(const DfaTables& t, uint32_t flags);
+// ugpu_dfa_info from the tables and the plan (ugpu_dfa_plan_host, ugpu_dfa_info_get)
+void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* info /* ugpu_dfa_info* */);
+// \w+ as ugpu_compile builds it
+bool is_word_plus(const DfaTables& t);
+// sets the calling thread's error string (ugpu_last_error) and returns code
+int host_fail(int code, const std::string& msg);
+
+}  // namespace ugpu

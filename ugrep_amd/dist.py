@@ -36,6 +36,10 @@ def _to_u64(v):
 KEYS = ("entry", "exit", "count", "digest", "dcap")
 
 
+class ShardError(RuntimeError):
+    """Raised on every rank when one rank's shard correction failed."""
+
+
 def resolve(recs, fix):
     """Resolve per-shard chain records, left to right, into exact totals.
 
@@ -93,49 +97,107 @@ def stitch(rec, fix_fn, device="cpu", group=None):
     recs = [dict(zip(KEYS, (_to_u64(int(x)) for x in t.cpu().tolist()))) for t in allrec]
 
     def fix(r, old, new):
-        buf = torch.zeros(5, dtype=torch.int64, device=device)
+        # [count, digest, dcap, exit known, exit, failed]: the owner's failure
+        # travels in the same broadcast, so that no rank is left blocked in a
+        # collective when fix_fn raises; every rank then raises
+        buf = torch.zeros(6, dtype=torch.int64, device=device)
+        err = None
         if rank == r:
-            d = fix_fn(old, new)
-            ex = d.get("exit")
-            buf = torch.tensor([_to_i64(d["count"]), _to_i64(d["digest"]), _to_i64(d["dcap"]),
-                                1 if ex is not None else 0, _to_i64(ex if ex is not None else 0)],
-                               dtype=torch.int64, device=device)
+            try:
+                d = fix_fn(old, new)
+                ex = d.get("exit")
+                buf = torch.tensor([_to_i64(d["count"]), _to_i64(d["digest"]), _to_i64(d["dcap"]),
+                                    1 if ex is not None else 0, _to_i64(ex if ex is not None else 0), 0],
+                                   dtype=torch.int64, device=device)
+            except Exception as e:  # noqa: BLE001 - re-raised below, after the broadcast
+                err = e
+                buf[5] = 1
         # owner ranks r are visited in the same order on every rank
         dist.broadcast(buf, src=r, group=group)
         v = [_to_u64(int(x)) for x in buf.cpu().tolist()]
+        if v[5]:
+            if err is not None:
+                raise err
+            raise ShardError("rank %d failed to re-enter its shard at %d (see that rank's error)" % (r, new))
         return dict(count=v[0], digest=v[1], dcap=v[2], exit=v[4] if v[3] else None)
 
     return resolve(recs, fix)
 
 
+class Shard:
+    """One rank's shard [lo, hi) of a total-byte stream, in its own buffer
+    [lo, read_end), with every engine call that can meet UGPU_HALO retried on
+    a grown halo.
+
+    A match longer than the halo makes a scan fail with UGPU_HALO,
+    and so does ugpu_chain_fix when the TRUE chain (re-entered at the previous
+    shard's exit) walks into a match the speculative chain never saw.  Both
+    are handled here, on the owner rank, before any collective: the halo is
+    doubled, the shard fetched again, and the call repeated, up to the stream
+    end (where no match can run past).  fetch(lo, read_end) -> a uint8 CUDA
+    tensor holding the stream's bytes [lo, read_end) (with the 16 bytes of
+    padding the engine may read past them).  After a grown halo, .buf /
+    .ptr / .read_end name the new buffer: callers read them per call."""
+
+    def __init__(self, scanner, fetch, lo, hi, total, halo=1 << 20, stream=0):
+        self.sc, self.fetch, self.lo, self.hi, self.total = scanner, fetch, lo, hi, total
+        self.halo = max(int(halo), 1)
+        self.stream = stream
+        self.grown = 0
+        self._load()
+
+    def _load(self):
+        self.read_end = min(self.total, self.hi + self.halo)
+        self.eof = self.read_end == self.total
+        self.buf = None  # (release the old buffer before fetching the larger one)
+        self.buf = self.fetch(self.lo, self.read_end)
+        self.ptr = self.buf.data_ptr()
+
+    def _retry(self, call):
+        from ._lib import UGPU_HALO, UgpuError
+        while True:
+            try:
+                return call()
+            except UgpuError as err:
+                if err.code != UGPU_HALO or self.eof:
+                    raise
+                self.halo *= 2
+                self.grown += 1
+                self._load()
+
+    def scan(self, entry=None):
+        """Scan [max(entry, lo), hi) (entry None: lo; an entry at or past hi
+        scans nothing: the previous shard's last match covers this shard);
+        returns stitch()'s record, positions global."""
+        e = self.lo if entry is None else min(max(entry, self.lo), self.hi)
+
+        def go():
+            self.sc.scan(self.ptr, e - self.lo, self.hi - self.lo, self.read_end - self.lo, self.eof, self.lo,
+                         self.stream)
+            return self.sc.totals()
+        t = self._retry(go)
+        return dict(entry=t.entry + self.lo, exit=t.exit + self.lo, count=t.count, digest=t.digest, dcap=t.dcap)
+
+    def fix(self, old, new):
+        """stitch()'s fix_fn: the correction for this shard re-entered at new
+        instead of old (ugpu_chain_fix)."""
+        def go():
+            return self.sc.chain_fix(self.ptr, 0, self.hi - self.lo, self.read_end - self.lo, self.eof, self.lo,
+                                     old - self.lo, new - self.lo, self.stream)
+        t = self._retry(go)
+        return dict(count=t.count, digest=t.digest, dcap=t.dcap,
+                    exit=None if t.exit == MASK64 else t.exit + self.lo)
+
+
 def scan_shard(scanner, fetch, lo, hi, total, halo=1 << 20, entry=None, stream=0):
     """Scan shard [lo, hi) of a total-byte stream from `entry` (default lo),
-    growing the readable halo when a match runs past it.
-
-    fetch(lo, read_end) -> a uint8 CUDA tensor holding the stream's bytes
-    [lo, read_end) (with the 16 bytes of padding the engine may read past
-    them).  A match longer than the halo makes the scan fail with UGPU_HALO
-    (DESIGN §5): the halo is then doubled and the shard fetched and scanned
-    again, up to the stream end (where no match can run past).  Returns
+    growing the readable halo when a match runs past it (Shard).  Returns
     (record, buffer, read_end): the record in stitch()'s form with global
     positions, and the buffer and readable end the record was scanned on
     (fix_fn and the OFFSETS pass must use the same)."""
-    from ._lib import UGPU_HALO, UgpuError
-    h = max(int(halo), 1)
-    while True:
-        read_end = min(total, hi + h)
-        buf = fetch(lo, read_end)
-        e = lo if entry is None else min(max(entry, lo), hi)
-        try:
-            scanner.scan(buf.data_ptr(), e - lo, hi - lo, read_end - lo, read_end == total, lo, stream)
-            t = scanner.totals()
-        except UgpuError as err:
-            if err.code != UGPU_HALO or read_end == total:
-                raise
-            h *= 2
-            continue
-        rec = dict(entry=t.entry + lo, exit=t.exit + lo, count=t.count, digest=t.digest, dcap=t.dcap)
-        return rec, buf, read_end
+    sh = Shard(scanner, fetch, lo, hi, total, halo, stream)
+    rec = sh.scan(entry)
+    return rec, sh.buf, sh.read_end
 
 
 def shard_bounds(total, world, rank, halo):
@@ -147,7 +209,7 @@ def shard_bounds(total, world, rank, halo):
     return lo, hi, read_end, read_end == total
 
 
-def gather_offsets(start, length, cap, group=None, dst=None):
+def gather_offsets(start, length, cap, group=None, dst=None, concat=True):
     """Exchange the final match records of every shard.
 
     start (int64, global byte offsets), length and cap (int32) are this rank's
@@ -159,7 +221,15 @@ def gather_offsets(start, length, cap, group=None, dst=None):
     concatenation in rank order, which is global chain order because shards
     are contiguous and ordered.  RCCL has no all_gatherv; padding costs at most
     (world - 1) x the count spread, and the counts travel first in one
-    8-byte all_gather.
+    8-byte all_gather.  concat=False returns the per-rank parts as lists
+    (start, len, cap per rank, views into the received buffers) instead of
+    one concatenation, which would double the receiver's record memory.
+
+    Memory: a receiver holds world x max(count) x (12 or 16) B.
+    Dense tables at 8 x 16 GiB (C3: ~1.25 G records per shard, 12 B) make that
+    ~120 GB at the root -- which is why the bench gathers to one root
+    (dst=0) and never all-gathers records: an all_gather would put those
+    120 GB on every rank.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -188,6 +258,12 @@ def gather_offsets(start, length, cap, group=None, dst=None):
         dist.gather(pack, parts, dst=dst, group=group)
         if rank != dst:
             return None
+    if not concat:
+        ps = [parts[r][:counts[r]] for r in range(world)]
+        if cap is None:
+            return ([p[:, 0:2].contiguous().view(torch.int64).reshape(-1) for p in ps], [p[:, 2] for p in ps], None)
+        return ([p[:, 0] for p in ps], [(p[:, 1] >> 32).to(torch.int32) for p in ps],
+                [(p[:, 1] & 0xFFFFFFFF).to(torch.int32) for p in ps])
     allp = torch.cat([parts[r][:counts[r]] for r in range(world)])
     if cap is None:
         st = allp[:, 0:2].contiguous().view(torch.int64).reshape(-1)
