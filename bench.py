@@ -66,7 +66,7 @@ def _spec(kind, sample):
     return "gen:%d:1:0:%d" % (kind, sample)
 
 
-def cpu_baseline(cfg, sample, threads):
+def cpu_baseline(cfg, sample, threads, rx_override=None, word=False):
     """The reference CPU matcher on a bounded sample of the same corpus.
 
     `value` is the reference AVX2 path (oracle/_ref/ref_harness_avx2: libreflex
@@ -79,6 +79,10 @@ def cpu_baseline(cfg, sample, threads):
     with the GPU scan of the same bytes.  Falls back to the oracle restatement
     ("port") when the reference build is absent."""
     pkey, mode, rx, kind, _, _ = CONFIGS[cfg]
+    if rx_override is not None:
+        mode, rx, pkey = "re", rx_override, None
+    if word:
+        mode += "W"  # (the harness's Matcher option W, ugrep -w)
     avx2 = os.path.join(REPO, "oracle", "_ref", "ref_harness_avx2")
     avx512 = os.path.join(REPO, "oracle", "_ref", "ref_harness")
     if os.path.exists(avx2):
@@ -101,6 +105,8 @@ def cpu_baseline(cfg, sample, threads):
             return out, (j["count"], j["digest"], j["dcap"])
         except Exception as e:  # pragma: no cover - diagnostic path
             log("reference harness failed (%s); using the oracle restatement" % e)
+    if pkey is None or word:
+        return None, None  # (no reference build: the restatement leg covers the BASELINE patterns only)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_lib import OracleDfa, gen as host_gen
     with open(os.path.join(REPO, "ugrep_amd", "data", "config_patterns.json")) as f:
@@ -258,7 +264,10 @@ def main():
                     help="tables from the native regex compiler (ugpu_compile) instead of the reference's "
                          "dumped opcode words")
     ap.add_argument("--word", action="store_true",
-                    help="Matcher option W (ugrep -w) on the same pattern: wfind_kernel (not a BASELINE config)")
+                    help="Matcher option W (ugrep -w) on the same pattern (not a BASELINE config)")
+    ap.add_argument("--regex", default=None,
+                    help="another pattern (ERE, compiled by ugpu_compile) over the config's corpus, e.g. "
+                         "word boundaries '\\bfoo\\b' (not a BASELINE config)")
     ap.add_argument("--launch-check", action="store_true",
                     help="bring the ranks up (process group, all_gather, barrier) and report them; no GPU work")
     args = ap.parse_args()
@@ -305,7 +314,11 @@ def main():
     lo, hi, _, _ = shard_bounds(total, world, rank, args.halo)
     with open(os.path.join(REPO, "ugrep_amd", "data", "config_patterns.json")) as f:
         opc = json.load(f)[pkey]["opc"]
-    if args.compile:
+    if args.regex is not None:
+        rx, mode = args.regex, "re"
+        opc = ugrep_amd.compile_regex(rx)
+        desc = "'%s'%s over the corpus of %s (%s)" % (rx, " -w" if args.word else "", args.config, desc)
+    elif args.compile:
         opc = ugrep_amd.compile_regex(rx, fixed=(mode == "F"))
     pat = ugrep_amd.Pattern(opc, word=args.word)
     info = pat.info()
@@ -411,19 +424,21 @@ def main():
         threads = min(threads, visible)
         sample = min(args.cpu_sample_mib << 20, per_gpu)
         log("cpu baseline: %d MiB, %d threads (per-GPU share of %d visible CPUs)" % (sample >> 20, threads, visible))
-        base, ref = cpu_baseline(args.config, sample, threads)
+        base, ref = cpu_baseline(args.config, sample, threads, args.regex, args.word)
         allc = min(visible, 256)
         if base is not None and base.get("kind") == "reference" and allc > threads:
             try:
                 pkey_, mode_, rx_, kind_, _, _ = CONFIGS[args.config]
-                ja = _harness(os.path.join(REPO, "oracle", "_ref", "ref_harness_avx2"), mode_, rx_,
-                              _spec(kind_, sample), allc, 2)
+                if args.regex is not None:
+                    mode_, rx_ = "re", args.regex
+                ja = _harness(os.path.join(REPO, "oracle", "_ref", "ref_harness_avx2"), mode_ + ("W" if args.word else ""),
+                              rx_, _spec(kind_, sample), allc, 2)
                 base["all_cores"] = {"value": round(ja["bytes"] / ja["seconds"] / 1e9, 3), "unit": "GB/s",
                                      "cores": allc, "best_of": 2}
             except Exception as e:  # pragma: no cover - diagnostic path
                 log("all-cores reference leg failed: %s" % e)
         chk = None
-        if ref is not None and not args.word:  # the same bytes on the GPU, compared with the reference
+        if ref is not None:  # the same bytes on the GPU, compared with the reference
             chk = gpu_reference_check(pat, buf, sample, ref, sptr)
             log("reference parity on [0, %d): %s" % (sample, chk))
         cpu_leg = (base, chk)
@@ -464,7 +479,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc, "config": args.config, "pattern": rx, "bytes_per_gpu": per_gpu,
                    "total_bytes": total, "corpus_kind": kind, "parallelism": "shard%d" % world,
-                   "tables": "compiled" if args.compile else "reference", "word": args.word, "dfa_states": info["states"], "dfa_row": info["row"], "prefilter_ppm": info["prefilter_ppm"]},
+                   "tables": "compiled" if (args.compile or args.regex is not None) else "reference", "word": args.word, "dfa_states": info["states"], "dfa_row": info["row"], "prefilter_ppm": info["prefilter_ppm"]},
         "matches": res["count"],
         "matches_per_s": round(matches_per_s, 1),
         "digest": res["digest"],
@@ -488,7 +503,9 @@ def main():
                           "digest_matches_totals": nrec == res["count"] and dg == res["digest"]}
         if shard.grown:
             out["offsets"]["halo_grown"] = shard.grown
-    tr = measured_traffic(args.config, hi - lo, KERNELS[info["kernel"]])
+    # (the committed PMC traffic is per BASELINE config and pattern)
+    tr = None if (args.regex is not None or args.word) else measured_traffic(args.config, hi - lo,
+                                                                             KERNELS[info["kernel"]])
     if tr and tr.get("kernel_ms") and abs(tr["kernel_ms"] - k_avg) > 0.05 * k_avg:
         # the counters were taken on a run whose kernel time differs from this one's
         log("traffic.json %s: kernel %.4f ms there, %.4f ms here: not used" % (args.config, tr["kernel_ms"], k_avg))

@@ -15,16 +15,21 @@
  *     (lib/matcher.cpp:467-502) over the goto words whose format is
  *     include/reflex/pattern.h:1155-1247 (GOTO lo<<24|hi<<16|idx, HALT
  *     0x00FFFFFF, LONG idx 0xFFFE + next word, TAKE 0xFE..).  TAKE at the head
- *     of a block (lib/pattern.cpp:2945-2952) makes the state accepting.
- *     REDO/TAIL/HEAD and meta edges other than META_BOL / META_EOL and the
- *     word boundaries META_WBB .. META_EWE (pattern.h:933-943) are rejected
+ *     of a block (lib/pattern.cpp:2945-2952) makes the state accepting; so
+ *     does REDO (0xFD000000, a negative pattern's accept, ugrep -N
+ *     '(?^...)'), with the accept ORC_REDO.  TAIL/HEAD, meta edges other than
+ *     META_BOL / META_EOL and the word boundaries META_WBB .. META_EWE
+ *     (pattern.h:933-943), and REDO in a table with meta edges are rejected
  *     (ORC_UNSUPPORTED); meta edges are kept per state in block order
  *     (orc_find_a).
  *   orc_find -- the FIND driver of Matcher::match (lib/matcher.cpp:42-750) for
  *     tables without meta/lookahead, options A/N/W off: from p walk the DFA,
  *     remember the last TAKE (:139-150, :207-217), stop on HALT/EOF (:448-459,
  *     :528-541); emit the longest non-empty match and resume at its end
- *     (:681, :735-737), otherwise retry at p+1 (:635-661, :692-713).  The adv_
+ *     (:681, :735-737), otherwise retry at p+1 (:635-661, :692-713).  A match
+ *     whose last accept is REDO is not emitted and the search resumes at its
+ *     end (:732-738 "ignore accept and continue"; an empty one moves to p+1
+ *     as any empty match, :682-713).  The adv_
  *     prefilters (lib/matcher.cpp:797-954, lib/matcher_avx2.cpp) only skip
  *     positions that cannot start a match and are not restated -- except for
  *     tables with meta edges, where the Pattern's predictor can also reject
@@ -45,6 +50,7 @@
 #define ORC_NOMEM 3
 
 #define ORC_MAXMETA 4
+#define ORC_REDO 0xffffffffu /* the accept of a REDO state (never an accept index: those have 24 bits) */
 typedef struct orc_dfa
 {
   uint32_t nstates; /* including dead state 0 */
@@ -128,6 +134,8 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
         uint32_t w = opc[g], op = w >> 24;
         if (op == 0xfe)
           d->accept[s] = w & 0xffffff;
+        else if (w == 0xfd000000u)
+          d->accept[s] = ORC_REDO; /* REDO (lib/pattern.cpp:2945-2947): precedes any TAKE */
         else if (is_meta(w) && op >= 0x01 && op <= 0x0a && nm < ORC_MAXMETA)
         {
           uint32_t idx = w & 0xffff, tgt = idx == 0xfffe ? (g + 1 < nop ? opc[g + 1] & 0xffffff : nop) : idx;
@@ -212,6 +220,11 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
           if (d->next[(size_t)t * 256 + b] != 0)
             goto unsupported;
       }
+    /* REDO with meta edges: not restated (the engine refuses it too) */
+    if (d->anchored)
+      for (s = 1; s < ns; ++s)
+        if (d->accept[s] == ORC_REDO)
+          goto unsupported;
   }
   free(id);
   free(queue);
@@ -272,7 +285,11 @@ uint64_t orc_find(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t sta
   {
     uint32_t a;
     uint64_t len = orc_step(d, buf, n, p, &a);
-    if (len > 0)
+    if (len > 0 && a == ORC_REDO)
+    {
+      p += len; /* a negative pattern's match: consumed, not reported */
+    }
+    else if (len > 0)
     {
       uint64_t st = p + bias;
       if (list && cnt < list_cap)

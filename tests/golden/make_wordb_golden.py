@@ -14,7 +14,7 @@ semantics the engine implements), and, where it differs, "run": the Matcher
 as ugrep runs it.  The two differ where the Pattern's predictor rejects
 positions the DFA matches at (\\w+\\b and x\\b|xy print nothing in the
 reference CLI); the drop-in adapter keeps those patterns on the CPU matcher
-(integration/reflex_gpu_matcher.h word_predictor_exact).  Inputs: a hand-made
+(integration/reflex_gpu_matcher.h predictor_exact).  Inputs: a hand-made
 text with every boundary kind next to ASCII, '_', digits, UTF-8 word and
 non-word characters, invalid UTF-8, CR LF and a last line without newline;
 the reference's CLI inputs; corpus slices.
@@ -56,6 +56,12 @@ PATTERNS = [
     # the lowest satisfied index (^ab|ab$ with both: 2)
     r"\bé|é\b|\Bx\B", r"\bab|ab\b", r"ab\>|ab|\bab", r"\bab\b|ab\b", r"^ab|ab$", r"^ab$|ab$", r"\bfoo\b|foo",
     r"\<the|the\>|\Bthe",
+    # the adapter rule's boundary: finite alternations whose
+    # branches share a prefix under different boundary kinds, and \b after a
+    # fixed repeat of classes -- finite, so the rule sends them to the GPU
+    r"\bfoo\b|\bfoo\B", r"\bab\b|\Bab", r"foo\>|foob\b", r"\<fo|\<foo\>", r"\b(a|ab|abc)\b",
+    r"(foo|fo)\b", r"\b\w{3}\b", r"\b[a-z]{2}\d\b", r"\<\w{2}\>", r"\b\d{2,3}\b", r"\b.{2}\b",
+    r"\bx\w\b", r"\b[[:alpha:]]{3}\b|\bfoo",
 ]
 MODES = ["re", "reN", "reU"]
 

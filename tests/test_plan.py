@@ -17,8 +17,13 @@ def test_plan_known_tables():
     assert U.host_plan("foo|bar|baz")["kernel"] == 0
     assert U.host_plan("[A-Za-z_][A-Za-z0-9_]*")["kernel"] == 5
     assert U.host_plan(r"\w+")["kernel"] == 6
-    assert U.host_plan("^foo")["kernel"] == 4
-    assert U.host_plan("^foo", empty=True)["kernel"] == 4
+    # line anchors / word boundaries: prefiltered tables run sparse_kernel's
+    # context walks, the others wfind_kernel's chain of context walks
+    assert U.host_plan("^foo")["kernel"] == 0
+    assert U.host_plan("^foo", empty=True)["kernel"] == 0
+    assert U.host_plan(r"\bfoo\b")["kernel"] == 0
+    assert U.host_plan("^[a-z]+")["kernel"] == 4
+    assert U.host_plan(r"\b[a-z]+\b")["kernel"] == 4
     with pytest.raises(U.Unsupported):
         U.host_plan("^foo", word=True)
     with pytest.raises(U.Unsupported):

@@ -188,8 +188,25 @@ WORDB_CMDS = [(["-co", r"\bdolor\b"], True), (["-on", r"\<con"], True), (["-c", 
               (["-co", r"\w+\b"], False)]
 
 
+# negative patterns (ugrep -N: (?^...) alternatives, REDO accepts)
+NEG_CMDS = [(["-co", "-N", "dolor", "-e", r"dolor\w*"], True), (["-on", "-N", "sit", "-e", r"s[a-z]+"], True),
+            (["-c", "-N", "con", "-N", "in", "-e", r"[a-z]+"], True), (["-o", "-U", "-N", "ad", "-e", r"a[a-z]"], True),
+            (["-co", "-N", "lorem", "-e", r"\w+"], True)]
+
+
 @pytest.mark.gpu
 def test_dropin_word_boundaries_on_gpu(tmp_path):
+    _dropin_ledger(tmp_path, WORDB_CMDS, "dropin_wordb_ledger.json")
+
+
+@pytest.mark.gpu
+def test_dropin_negative_patterns_on_gpu(tmp_path):
+    """ugrep -N commands served by the GPU (REDO accepts),
+    byte-equal to the reference build."""
+    _dropin_ledger(tmp_path, NEG_CMDS, "dropin_redo_ledger.json")
+
+
+def _dropin_ledger(tmp_path, cmds, ledger_name):
     exe_gpu = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")
     exe_ref = os.path.join(ROOT, "oracle", "_ref", "ugrep")
     if not (os.path.exists(exe_gpu) and os.path.exists(exe_ref)):
@@ -204,7 +221,7 @@ def test_dropin_word_boundaries_on_gpu(tmp_path):
     files = ["lorem1m.txt", "words.txt"]
     env = dict(os.environ, UGPU_ADAPTER_MIN_BYTES="0", UGPU_ADAPTER_STATS="1", UGPU_ADAPTER_WARM="0")
     ledger = []
-    for args, on_gpu in WORDB_CMDS:
+    for args, on_gpu in cmds:
         ref = subprocess.run([exe_ref, "--sort"] + args + files, cwd=tmp_path, capture_output=True, timeout=120, env=env)
         got = subprocess.run([exe_gpu, "--sort"] + args + files, cwd=tmp_path, capture_output=True, timeout=120, env=env)
         assert ref.returncode == got.returncode, args
@@ -222,5 +239,5 @@ def test_dropin_word_boundaries_on_gpu(tmp_path):
             assert gpu_finds == 0 and any("anchor_predictor" in m["why"] for m in st), (args, st)
     out = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out, exist_ok=True)
-    with open(os.path.join(out, "dropin_wordb_ledger.json"), "w") as f:
+    with open(os.path.join(out, ledger_name), "w") as f:
         json.dump(ledger, f, indent=1)

@@ -67,6 +67,41 @@ def test_fixture_coverage():
     assert any(r["run"] is not None for c in CASES for r in c["results"])
 
 
+def _predictor_exact(opc):
+    """integration/reflex_gpu_matcher.h predictor_exact for word-boundary
+    tables without line anchors: the language is finite and no state whose
+    accept depends on the word context goes on with byte edges."""
+    import ugrep_amd as U
+    info = U.host_plan(opc)
+    sh = info["shape"]
+    return bool(sh & U._lib.SHAPE_FINITE) and not sh & U._lib.SHAPE_WORD_COND
+
+
+def test_reference_as_run_agrees_on_gpu_eligible_patterns():
+    """Where the adapter sends a word-boundary table to the GPU, the reference
+    as ugrep runs it (its match predictor on: the lookback cut lbk_ and the
+    needle pin_ of lib/pattern.cpp:3990-4290, applied by lib/matcher.cpp:52-86
+    and :640-660) gives the DFA semantics (predictor off) on every fixture
+    input.  The prediction can only reject a position the DFA matches at after
+    a cycle (the lookback cut) or where an accept waits for the context while
+    bytes may follow; the rule excludes both.  The fixtures include the rule's
+    boundary shapes: shared prefixes under different boundary kinds, \\b
+    after a fixed repeat of classes."""
+    seen = eligible_shapes = 0
+    for c in CASES:
+        if c["pattern"] in UNSUPPORTED or c["nul"] or "^" in c["pattern"] or "$" in c["pattern"]:
+            continue
+        if not any((w & 0x00FF0000) == 0 and 0 < (w >> 24) <= 8 for w in c["opc"]):
+            continue  # (no word-boundary edge in this table)
+        if _predictor_exact(c["opc"]):
+            seen += 1
+            eligible_shapes += c["pattern"] in (r"\bfoo\b|\bfoo\B", r"\b(a|ab|abc)\b", r"\b\w{3}\b",
+                                                r"\b[a-z]{2}\d\b", r"\b\d{2,3}\b")
+            for r in c["results"]:
+                assert r["run"] is None, (c["pattern"], c["mode"], r["input"])
+    assert seen >= 60 and eligible_shapes >= 5, (seen, eligible_shapes)
+
+
 def test_oracle_matches_reference():
     for c in CASES:
         o = OracleDfa(c["opc"])
@@ -271,7 +306,9 @@ def test_gpu_find_all_matches_reference():
                 U.Pattern(c["opc"], empty=c["nul"])
             continue
         pat = U.Pattern(c["opc"], empty=c["nul"])
-        assert pat.info()["kernel"] == 4
+        info = pat.info()
+        # prefiltered tables: sparse_kernel's context walks; the rest: wfind_kernel
+        assert info["kernel"] == (0 if info["prefilter_ppm"] and info["format"] == 0 else 4), c["pattern"]
         for r in c["results"]:
             data = _input(r["input"])
             dev = torch.from_numpy(data).to("cuda")
@@ -341,7 +378,9 @@ def test_compiler_word_boundaries_match_reference():
             opc = U.compile_regex(rx, reflex=form == "reflex")
             assert host_equivalent(opc, c["opc"]), (c["pattern"], c["mode"], form)
             info = U.host_plan(opc)
-            assert info == U.host_plan(c["opc"]) or info["states"] != U.host_plan(c["opc"])["states"], c["pattern"]
+            ref = U.host_plan(c["opc"])
+            assert (info["kernel"], info["contexts"]) == (ref["kernel"], ref["contexts"]) or \
+                info["states"] != ref["states"], c["pattern"]
             if info["format"] == 2:
                 continue
             tab = U.host_tables(opc)
@@ -353,3 +392,51 @@ def test_compiler_word_boundaries_match_reference():
                     (c["pattern"], c["mode"], form)
                 walked += 1
     assert walked >= 200
+
+
+SPARSE_CTX = [r"\bfoo\b", r"\<(in|ut)\>", r"\bdolor\b", r"\Boo\B", r"x\>", r"\<con", r"um\>", r"^foo", r"ing$",
+              r"\b(lorem|ipsum|sit)\b"]
+
+
+def _ctx_corpus(n):
+    """lorem text, C2 words and the C4 UTF-8 corpus in 64 KiB slices, with
+    CR LF line ends, '_' and digits next to the pattern words"""
+    from oracle_lib import gen, GOLDEN
+    lorem = np.frombuffer(open(os.path.join(GOLDEN, "lorem.utf8.txt"), "rb").read(), np.uint8)
+    parts = [np.tile(lorem, 8)[:64 << 10], gen(1, 3, 0, 64 << 10), gen(4, 3, 0, 64 << 10),
+             np.frombuffer(b"foo_foo 9foo foo9 \r\nfoo\r\n_in ut\xc3\xa9ut in\xe2\x82\xacin xing\n" * 512, np.uint8)]
+    out = np.concatenate(parts * (n // sum(p.size for p in parts) + 1))[:n]
+    return np.ascontiguousarray(out)
+
+
+@pytest.mark.gpu
+def test_gpu_sparse_context_walks_match_oracle():
+    """prefiltered word-boundary and line-anchor tables run
+    sparse_kernel with context walks (kernel 0).  Against the oracle's
+    restatement of the meta tests (pinned to the reference fixtures above)
+    on 6 MiB of mixed text: totals, match lists (OFFSETS, staged and WRITE
+    pass), three virtual shards, and the same scans on wfind_kernel
+    (UGPU_SPARSE=0)."""
+    torch = _torch()
+    import ugrep_amd as U
+    from oracle_lib import OracleDfa
+    data = _ctx_corpus(6 << 20)
+    dev = torch.from_numpy(data).to("cuda")
+    torch.cuda.synchronize()
+    for rx in SPARSE_CTX:
+        opc = U.compile_regex(rx)
+        pat = U.Pattern(opc)
+        assert pat.info()["kernel"] == 0, rx
+        cnt, dg, dc, lst = OracleDfa(opc).find(data, want_list=True)
+        got = U.find_all(pat, dev, offsets=True)
+        assert (got.count, got.digest, got.dcap) == (cnt, dg, dc), rx
+        assert [list(t) for t in got.triples()] == lst, rx
+        m = U.find_all_multi(pat, data, ndev=3, offsets=False)
+        assert (m.count, m.digest, m.dcap) == (cnt, dg, dc), rx
+        os.environ["UGPU_SPARSE"] = "0"
+        try:
+            pw = U.Pattern(opc)
+            g2 = U.find_all(pw, dev, offsets=False)
+        finally:
+            os.environ.pop("UGPU_SPARSE", None)
+        assert (g2.count, g2.digest, g2.dcap) == (cnt, dg, dc), rx

@@ -19,6 +19,17 @@ __device__ __forceinline__ uint32_t op(uint32_t a, uint32_t b)
   if constexpr (K == 5) return __builtin_amdgcn_udot4(a, 0x03020100u, b, false);
   if constexpr (K == 6) return __builtin_amdgcn_update_dpp(b, a, 0x130, 0xf, 0xf, false);
   if constexpr (K == 7) return (a << 3) + b;  // v_lshl_add_u32
+  if constexpr (K == 8) return (a << 8) | b;  // v_lshl_or_b32
+  if constexpr (K == 9) return a >> 7;        // v_lshrrev_b32 (dependent chain per lane: 8 chains)
+  if constexpr (K == 10) return (a | b) | (a >> 3);  // v_or3_b32 (+ shift)
+  if constexpr (K == 11) return __builtin_amdgcn_ubfe(a, 8, 16) ^ b;  // v_bfe_u32 (+ xor)
+  if constexpr (K == 12) return (a & 0x00ff00ffu) | (b & 0xff00ff00u);  // v_bfi_b32 or bitop3
+  if constexpr (K == 13) return a - b;  // v_sub_u32
+  if constexpr (K == 14) return a + b + 0x1234567u;  // v_add3_u32
+  if constexpr (K == 15) return (a & b) | 0x01010101u;  // v_and_or_b32
+  if constexpr (K == 16) { uint32_t r; asm volatile("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+  if constexpr (K == 17) { uint32_t r; asm volatile("v_or3_b32 %0, %1, %2, %1" : "=v"(r) : "v"(a), "v"(b)); return r; }
+  if constexpr (K == 18) { uint32_t r; asm volatile("v_lshlrev_b32 %0, 3, %1" : "=v"(r) : "v"(a)); return r ^ b; }
   return a;
 }
 
@@ -77,7 +88,7 @@ void run(const char* name, int waves_per_simd)
 
 int main()
 {
-  for (int w : {1, 2, 8}) {
+  for (int w : {8}) {
     run<0>("v_perm", w);
     run<1>("alignbit", w);
     run<2>("bitop3", w);
@@ -86,6 +97,17 @@ int main()
     run<5>("dot4", w);
     run<6>("dpp", w);
     run<7>("lshl_add", w);
+    run<8>("lshl_or", w);
+    run<9>("lshr", w);
+    run<10>("or3+lshr", w);
+    run<11>("bfe+xor", w);
+    run<12>("bfi", w);
+    run<13>("sub", w);
+    run<14>("add3", w);
+    run<15>("and_or", w);
+    run<16>("lshl_or(asm)", w);
+    run<17>("or3(asm)", w);
+    run<18>("lshl+xor", w);
   }
   return 0;
 }

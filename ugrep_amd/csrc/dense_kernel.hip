@@ -61,6 +61,9 @@ struct RelEm {
   uint32_t log_row;
   __device__ __forceinline__ void put(uint32_t p, uint32_t len, uint32_t le, int sign)
   {
+    if constexpr (!CAP1) {
+      if (caps[le >> log_row] == kCapRedo) return;  // (REDO: not reported; CAP1 tables have none)
+    }
     const uint32_t sg = (uint32_t)sign;  // +1 / -1 (wraps)
     r.cnt += sg;
     r.sst += sg * p;
@@ -86,10 +89,12 @@ struct AbsWriteEm {
   uint32_t overflow = 0;
   __device__ __forceinline__ void put(uint32_t p, uint32_t l, uint32_t le, int)
   {
+    const uint32_t a = caps[le >> log_row];
+    if (a == kCapRedo) return;  // (REDO: not reported)
     if (idx < capacity) {
       start[idx] = base + p;
       len[idx] = l;
-      if (cap) cap[idx] = caps[le >> log_row];  // (NULL: 12-byte records, one accept index)
+      if (cap) cap[idx] = a;  // (NULL: 12-byte records, one accept index)
     } else {
       overflow = 1;
     }

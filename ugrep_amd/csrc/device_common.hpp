@@ -364,12 +364,15 @@ struct Ctx {
   int64_t delta;
 };
 
+// (a match whose last accept is REDO, kCapRedo, is neither counted nor
+// written: the chain steps over it, lib/matcher.cpp:732-738)
 struct CountEm {
   uint64_t cnt = 0, dg = 0, dc = 0;
   __device__ __forceinline__ void put(const Ctx& c, uint64_t pos, uint64_t len, uint32_t le, int sign)
   {
     uint64_t st = pos + (uint64_t)c.delta;
     uint64_t cap = c.caps[le >> c.log_row];
+    if (cap == kCapRedo) return;
     uint64_t d1 = st * 31 + len, d2 = (st + 1) * cap;
     if (sign > 0) {
       ++cnt;
@@ -392,10 +395,12 @@ struct WriteEm {
   uint32_t overflow = 0;
   __device__ __forceinline__ void put(const Ctx& c, uint64_t pos, uint64_t l, uint32_t le, int)
   {
+    const uint32_t a = c.caps[le >> c.log_row];
+    if (a == kCapRedo) return;
     if (idx < capacity) {
       start[idx] = pos + (uint64_t)c.delta;
       len[idx] = (uint32_t)l;
-      if (cap) cap[idx] = c.caps[le >> c.log_row];  // (NULL: 12-byte records, one accept index)
+      if (cap) cap[idx] = a;  // (NULL: 12-byte records, one accept index)
     } else {
       overflow = 1;
     }

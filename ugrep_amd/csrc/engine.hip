@@ -444,7 +444,7 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
   const DfaPlan pl = dfa_plan(d->t, pattern_flags);
   if (!pl.ok) {
     delete d;
-    return fail(UGPU_UNSUPPORTED, "option W with line anchors or empty matches");
+    return fail(UGPU_UNSUPPORTED, "option W with line anchors, empty matches or negative patterns");
   }
   hipError_t e = hipGetDevice(&d->device);
   if (e != hipSuccess) {
@@ -627,7 +627,14 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   // the W rules); every other table runs wfind_kernel (tables through the caches)
   // line anchors / option N: every scan runs the context walk on wfind_kernel
   // wide tables: the exact walk on wfind_kernel, transitions from global memory
-  if (dfa->amode || dfa->t.format == FMT_WIDE || (dfa->d_wtab && !(dfa->t.filter && dfa->t.format == FMT_BYTE))) {
+  // context accepts (word boundaries, line anchors) on a prefiltered table:
+  // sparse_kernel's candidate walks run the context walk, the
+  // prefilter's candidates stay a superset; without a prefilter (or with
+  // UGPU_SPARSE=0) wfind_kernel's chain of context walks
+  const char* senv0 = std::getenv("UGPU_SPARSE");
+  const bool ctx_sparse = dfa->amode && dfa->t.filter && dfa->t.format == FMT_BYTE && !(senv0 && senv0[0] == '0');
+  if ((dfa->amode && !ctx_sparse) || dfa->t.format == FMT_WIDE ||
+      (dfa->d_wtab && !dfa->amode && !(dfa->t.filter && dfa->t.format == FMT_BYTE))) {
     const uint32_t nacap = !dfa->amode ? dfa->t.states
                            : dfa->t.ctx_word ? (uint32_t)dfa->t.acap_rows.size() : (uint32_t)dfa->t.acap.size();
     const uint32_t nmap = dfa->amode && dfa->t.ctx_word ? dfa->t.states : 0u;
@@ -845,10 +852,11 @@ int ugpu_scan(ugpu_scanner* s, const uint8_t* dbuf, uint64_t lo, uint64_t hi, ui
   // by fix_kernel): a long match costs each wave its own bytes only
   // (UGPU_TRUNC=0: walks run to the readable end)
   static const bool trunc = env_u64("UGPU_TRUNC", 1) != 0;
-  P.open = s->sparse && !P.wtab && trunc ? s->d_open : nullptr;
+  P.open = s->sparse && !P.wtab && !P.acap && trunc ? s->d_open : nullptr;
   // walks longer than their window: the wave suspends, a resume launch of
-  // the kernel completes it (coop_walk); option W keeps its per-lane walks
-  P.susp = s->sparse && !P.wtab ? s->d_susp : nullptr;
+  // the kernel completes it (coop_walk); option W and the context walks keep
+  // their per-lane walks
+  P.susp = s->sparse && !P.wtab && !P.acap ? s->d_susp : nullptr;
   P.srec = P.susp ? s->d_srec : nullptr;
   s->staged_last = false;
   if (s->sparse && (s->stage || s->stage_once)) {

@@ -45,6 +45,13 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags)
   DfaPlan p;
   p.nul = (flags & UGPU_PAT_EMPTY) != 0;
   p.amode = t.anchored || (p.nul && t.start_acc);
+  if (t.redo && ((flags & UGPU_PAT_WORD) || p.amode)) {
+    // (negative patterns under option W, or with empty matches under option
+    // N: the reference's REDO skips at_we and reports an empty REDO match;
+    // not modelled -- the CPU matcher keeps those)
+    p.ok = false;
+    return p;
+  }
   if (p.amode) {
     p.ok = !(flags & UGPU_PAT_WORD);
     return p;
@@ -82,11 +89,13 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* out)
   const char* genv = std::getenv("UGPU_XG");
   const char* cenv = std::getenv("UGPU_XC");
   const char* uenv = std::getenv("UGPU_XU");
-  const bool byte_filter = t.filter && t.format == FMT_BYTE;
+  const char* senv = std::getenv("UGPU_SPARSE");
+  const bool byte_filter = t.filter && t.format == FMT_BYTE && !(senv && senv[0] == '0');
   // (dfa_xc and dfa_xu, from the plan instead of the uploaded tables)
   const bool xc = t.xc && !t.filter && t.cap1 != 0 && (!p.wtab || p.xcw) && !(cenv && cenv[0] == '0');
   const bool xu = p.xu && (!p.wtab || p.wplus) && !(uenv && uenv[0] == '0');
-  info->kernel = p.amode || t.format == FMT_WIDE || (p.wtab && !p.wplus && !p.xcw && !byte_filter) ? 4u
+  // (context accepts on a prefiltered table: sparse_kernel's context walks)
+  info->kernel = (p.amode && !byte_filter) || t.format == FMT_WIDE || (p.wtab && !p.wplus && !p.xcw && !byte_filter) ? 4u
                  : byte_filter                                                                  ? 0u
                  : xc                                                                           ? 5u
                  : xu                                                                           ? 6u
@@ -115,7 +124,7 @@ int ugpu_dfa_plan_host(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags
   int rc = build_tables(opc, nop, t, err);
   if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
   const DfaPlan pl = dfa_plan(t, pattern_flags);
-  if (!pl.ok) return fail(UGPU_UNSUPPORTED, "option W with line anchors or empty matches");
+  if (!pl.ok) return fail(UGPU_UNSUPPORTED, "option W with line anchors, empty matches or negative patterns");
   dfa_info_fill(t, pl, info);
   return UGPU_OK;
 }

@@ -32,6 +32,8 @@
 // also tests on the accept side, lib/pattern.cpp:2527-2538 k->anchor()) or
 // after its last (META_WBE/NWE/BWE/EWE): per-context accepts over 64 contexts
 // (ctx_bits.hpp), encoded as exhaustive meta-edge splits (encode()).
+// Negative patterns (?^...) as whole top-level alternatives (ugrep -N,
+// src/ugrep.cpp:6487): their accepts become REDO words.
 // Returns UGPU_UNSUPPORTED for what the GPU tables cannot express or this
 // compiler does not cover (other anchors, word boundaries, lazy quantifiers,
 // lookaround, backreferences, other \p names, \p{Lu} under -i): the caller keeps
@@ -67,6 +69,10 @@ typedef std::vector<std::pair<uint32_t, uint32_t>> CpSet;  // sorted, disjoint, 
 typedef std::bitset<256> ByteSet;
 
 const uint32_t kMaxCp = 0x10FFFF;
+// the accept of a state that holds a negative pattern's end (encoded as a
+// REDO word; the reference emits REDO for such a state whatever else it
+// accepts, lib/pattern.cpp:2358-2363, :2945-2947)
+const uint32_t kRedoAcc = 0xFFFFFFu;
 const size_t kMaxPositions = 1u << 16;  // expansion guard ({n,m} of large subtrees)
 const size_t kMaxStates = 1u << 16;
 
@@ -430,7 +436,30 @@ class Parser
       eol_ = false;
       begin_.clear();
       end_.clear();
-      alts.push_back(parse_concat(true));
+      neg_node_ = -1;
+      const int a = parse_concat(true);
+      alts.push_back(a);
+      // a negative pattern (?^...) (ugrep -N, src/ugrep.cpp:6487): the whole
+      // alternative, besides modifiers -- its accept is REDO.  The reference
+      // negates the positions that follow a negated one too
+      // (lib/pattern.cpp:2421-2432), so (?^...) inside a sequence negates its
+      // tail: not modelled, refused.
+      bool neg = false;
+      if (neg_node_ >= 0)
+      {
+        bool whole = a == neg_node_;
+        if (!whole && t_.nodes[a].kind == CAT)
+        {
+          int others = 0;
+          for (int k : t_.nodes[a].kids)
+            others += k != neg_node_ && t_.nodes[k].kind != EMPTY;
+          whole = others == 0;
+        }
+        if (!whole)
+          fail(UGPU_UNSUPPORTED, "(?^...) inside a sequence");
+        neg = true;
+      }
+      negs.push_back(neg);
       // the alternative's meta edges in the order RE/flex chains them after
       // its last byte: the end assertions as written, then the begin ones
       // (^ \< ... moved to the accept side), e.g. ^\<ab\>$ -> EWE EOL BOL BWB
@@ -443,8 +472,19 @@ class Parser
     }
     if (p_ != s_.size())
       fail(UGPU_INVAL, "unbalanced ')'");
+    bool any_neg = false, any_meta = false;
+    for (size_t k = 0; k < negs.size(); ++k)
+    {
+      any_neg = any_neg || negs[k];
+      any_meta = any_meta || !metaseqs[k].empty();
+    }
+    if (any_neg && any_meta)
+      fail(UGPU_UNSUPPORTED, "(?^...) with anchors or word boundaries");
     return alts;
   }
+
+  // per top-level alternative: a negative pattern (?^...), whose accept is REDO
+  std::vector<bool> negs;
 
   // per top-level alternative: the meta edges (META - META_MIN) its accept
   // passes through, in chain order
@@ -459,6 +499,8 @@ class Parser
   bool dotall_ = false;  // REFLEX mode (?s): '.' matches '\n'
   bool multiline_ = false;  // REFLEX mode (?m): ^ and $ are line anchors
   bool eol_ = false;  // the top-level alternative being parsed ended with $
+  int depth_ = 0;      // group nesting
+  int neg_node_ = -1;  // the (?^...) group of the top-level alternative being parsed
   std::vector<uint8_t> begin_, end_;  // its begin / end assertions (META - META_MIN), as written
 
   // a word-boundary assertion at p_ (\b \B \< \>): its class mask (for the
@@ -488,6 +530,25 @@ class Parser
     if (icase() && ((c | 0x20) >= 'a' && (c | 0x20) <= 'z'))
       b.set(c ^ 0x20);
     return t_.leaf(b);
+  }
+
+  // "(?^" at p_ - 1 .. p_ + 1: a negative pattern, at the top level only
+  int negative_group()
+  {
+    if (depth_ != 0 || neg_node_ >= 0)
+      fail(UGPU_UNSUPPORTED, "(?^...) inside a group");
+    p_ += 2;
+    ++depth_;
+    const bool ic = ic_, dot = dotall_;
+    const int a = parse_alt();
+    ic_ = ic;
+    dotall_ = dot;
+    --depth_;
+    if (p_ >= s_.size() || s_[p_] != ')')
+      fail(UGPU_INVAL, "missing ')'");
+    ++p_;
+    neg_node_ = a;
+    return a;
   }
 
   int parse_alt()
@@ -1122,6 +1183,8 @@ class Parser
       {
         ++p_;
         const bool ic = ic_, dot = dotall_;
+        if (p_ + 1 < s_.size() && s_[p_] == '?' && s_[p_ + 1] == '^')
+          return negative_group();
         if (p_ < s_.size() && s_[p_] == '?')
         {
           // (?imsx-imsx) modifies the rest of the enclosing group,
@@ -1155,7 +1218,9 @@ class Parser
           ic_ = i;
           dotall_ = d;
         }
+        ++depth_;
         int a = parse_alt();
+        --depth_;
         if (p_ >= s_.size() || s_[p_] != ')')
           fail(UGPU_INVAL, "missing ')'");
         ++p_;
@@ -1228,6 +1293,8 @@ class Parser
       case '(':
       {
         ++p_;
+        if (p_ + 1 < s_.size() && s_[p_] == '?' && s_[p_ + 1] == '^')
+          return negative_group();
         if (p_ < s_.size() && s_[p_] == '?')
         {
           if (p_ + 1 < s_.size() && s_[p_ + 1] == ':')
@@ -1235,7 +1302,9 @@ class Parser
           else
             fail(UGPU_UNSUPPORTED, "(? group");
         }
+        ++depth_;
         int a = parse_alt();
+        --depth_;
         if (p_ >= s_.size() || s_[p_] != ')')
           fail(UGPU_INVAL, "missing ')'");
         ++p_;
@@ -1318,6 +1387,7 @@ struct Glushkov
   std::vector<std::vector<int>> follow;  // position -> follow positions
   std::vector<int> accept;               // position -> accept index (end markers), 0 otherwise
   std::vector<std::vector<uint8_t>> metas;  // end marker -> its alternative's meta edges (Parser::metaseqs)
+  std::vector<bool> neg;                    // end marker of a negative pattern (Parser::negs): REDO
 
   struct Info
   {
@@ -1346,6 +1416,7 @@ struct Glushkov
     follow.emplace_back();
     accept.push_back(acc);
     metas.emplace_back();
+    neg.push_back(false);
     return static_cast<int>(bytes.size() - 1);
   }
 
@@ -1561,12 +1632,16 @@ Dfa subsets(Glushkov &g, const std::vector<int> &start)
     std::vector<int> cur = sets[k];  // copy: sets grows
     CtxN cx(d.nctx, 0);
     std::vector<std::pair<uint32_t, const std::vector<uint8_t> *>> acc;  // (accept index, meta edges) of the state's ends
+    bool redo = false;
     for (int p : cur)
       if (g.accept[p])
+      {
         acc.emplace_back(static_cast<uint32_t>(g.accept[p]), &g.metas[p]);
+        redo = redo || g.neg[p];
+      }
     if (!acc.empty())
       for (uint32_t ctx = 0; ctx < d.nctx; ++ctx)
-        cx[ctx] = meta_accept(acc, ctx, d.nctx == 64);
+        cx[ctx] = redo ? kRedoAcc : meta_accept(acc, ctx, d.nctx == 64);
     d.acc.push_back(cx[0]);
     for (uint32_t ctx = 1; ctx < d.nctx; ++ctx)
       d.anchored = d.anchored || cx[ctx] != cx[0];
@@ -1932,7 +2007,9 @@ std::vector<uint32_t> encode(const Dfa &d)
     for (size_t i = 0; i < nb; ++i)
     {
       const Block &k = blocks[i];
-      if (k.take)
+      if (k.take == kRedoAcc)
+        out.push_back(0xFD000000u);  // REDO (lib/pattern.cpp:2945-2947)
+      else if (k.take)
         out.push_back(0xFE000000u | k.take);
       for (auto &m : k.metas)
       {
@@ -2000,6 +2077,7 @@ int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, 
       int end = g.new_pos(ByteSet(), static_cast<int>(k + 1));
       if (k < parser.metaseqs.size())
         g.metas[end] = parser.metaseqs[k];
+      g.neg[end] = k < parser.negs.size() && parser.negs[k];
       g.link(info.last, std::vector<int>{end});
       Glushkov::merge(start, info.first);
       if (info.nullable)

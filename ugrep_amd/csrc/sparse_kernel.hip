@@ -198,18 +198,21 @@ __device__ __forceinline__ void resolve(bool valid, uint64_t c, uint64_t len, ui
   }
   const uint64_t kb = __ballot(kept);
   if (!kb) return;
+  // the reported ones: a kept match whose last accept is REDO moves the chain
+  // but is not reported (WriteEm / CountEm skip it)
+  const uint64_t rb = __ballot(kept && C.caps[le >> C.log_row] != kCapRedo);
   if constexpr (WRITE) {
-    WriteEm we{w.widx + lanes_below(kb), P.out_capacity, P.out_start, P.out_len, P.out_cap};
+    WriteEm we{w.widx + lanes_below(rb), P.out_capacity, P.out_start, P.out_len, P.out_cap};
     if (kept) we.put(C, c, len, le, +1);
     w.wover |= we.overflow;
-    w.widx += __popcll(kb);
+    w.widx += __popcll(rb);
   } else {
     if (kept) w.acc.put(C, c, len, le, +1);
     if constexpr (STAGE) {
-      WriteEm se{w.sg.n + lanes_below(kb), P.st_per, w.sg.start, w.sg.len, w.sg.cap};
+      WriteEm se{w.sg.n + lanes_below(rb), P.st_per, w.sg.start, w.sg.len, w.sg.cap};
       if (kept) se.put(C, c, len, le, +1);
       w.sg.over |= se.overflow;
-      w.sg.n += __popcll(kb);
+      w.sg.n += __popcll(rb);
     }
     if (!w.first) {
       const int f = __builtin_ctzll(kb);
@@ -444,8 +447,10 @@ __device__ __forceinline__ void batch_finish(BatchLane& L, int lane, uint8_t* sc
 // after, completes the batch and the rest of the wave's tiles -- so the long
 // path's registers never count against the main kernel's occupancy.  `lim`
 // bounds every walk: the wave's range end when walks are truncated (P.open),
-// else the readable end.  Option W keeps its per-lane walks (walk<0, true>).
-template <bool WRITE, int ABL, bool W = false, bool STAGE = false, bool RESUME = false>
+// else the readable end.  Option W (W = kWalkWord) and tables whose accepts
+// depend on the context (W = kWalkCtx: word boundaries, line anchors) keep
+// per-lane walks through global memory (walk<0, W>).
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false>
 __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr, uint32_t dn, int lane, const Tab<0>& T,
                                             const Ctx& C, const ScanParams& P, WaveChain& w, uint64_t lim,
                                             uint64_t gw)
@@ -460,22 +465,16 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
   *reinterpret_cast<uint4*>(scr + 32 * lane) = v0;
   *reinterpret_cast<uint4*>(scr + 32 * lane + 16) = v1;
   wave_lds_sync();
-  if constexpr (W) {
+  if constexpr (W != kWalkPlain) {
     uint64_t len = 0;
     uint32_t le = 0;
     if (valid && ABL != 3) {
-      Win win;
-      win.lds = scr + 32 * lane;
-      win.base = a;
-      win.lend = a + 32;
-      win.g = P.g;
-      win.rend = P.rend;
-      win.eof = P.at_eof;
-      win.wtab = P.wtab;
-      win.nwtab = P.nwtab;
-      win.bob = P.bob;
-      // option W: the walk checks at_wb/at_we (device_common.hpp); candidates
-      // stay a superset (W only removes matches), so the prefilter is unchanged
+      // option W: the walk checks at_wb/at_we (device_common.hpp); context
+      // accepts: the walk bits at c, the position bits at each accepting
+      // state (ctx_accept).  Either way the candidates stay a superset (W and
+      // the contexts only remove matches, the first bytes are the table's),
+      // so the prefilter is unchanged.
+      const Win win = win_of(P);
       len = walk<0, W>(T, win, c, le, w.ovf);
     }
     resolve<WRITE, STAGE>(valid, c, len, le, lane, C, P, w);
@@ -533,7 +532,7 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
 // by the wave's range [wlo, whi).
 // ABL (benchmarking only; results are not matches): 1 loads alone, 2 loads +
 // prefilter, 3 everything but the walks.
-template <bool WRITE, int ABL, bool W = false, bool STAGE = false, bool RESUME = false>
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false>
 __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3,
                                           uint64_t ts, bool edge, uint64_t wlo, uint64_t whi, int lane,
                                           const FTab& F, const Tab<0>& T, const Ctx& C, const ScanParams& P,
@@ -669,7 +668,7 @@ __device__ __forceinline__ TileLoad wave_tile(const uint8_t* wbase, uint32_t i, 
 
 }  // namespace
 
-template <bool WRITE, int ABL, bool W = false, bool STAGE = false, bool RESUME = false>
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false>
 __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -699,7 +698,8 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
   __syncthreads();  // the only workgroup barrier: tables staged
   if (!mine) return;
   const Tab<0> T{ltrans, nullptr, P.start, P.accb};
-  const Ctx C{lcaps, P.log_row, P.delta};
+  // (context accepts: a walk's `le` is the acap index, whose entry is the accept index)
+  const Ctx C = W == kWalkCtx ? Ctx{P.acap, 0u, P.delta} : Ctx{lcaps, P.log_row, P.delta};
   const FTab F{P.ft[0], P.ft[1], P.ft[2], P.ft[3], P.ft[4]};
 
   uint64_t tb = P.t0 + gw * P.tpb;
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
   // walk limit: with truncation (P.open) a walk still alive at the range end
   // of any wave but the last becomes the wave's open walk (fix_kernel); the
   // last wave's walks run to the readable end, as the range's exit needs
-  const uint64_t lim = (!W && P.open && whi < P.hi) ? whi : P.rend;
+  const uint64_t lim = (W == kWalkPlain && P.open && whi < P.hi) ? whi : P.rend;
   if constexpr (WRITE && !RESUME) {  // single-pass OFFSETS: this wave's records were staged and copied already
     if (P.st_n && P.st_n[gw] == kStageDone) {
       if (P.susp && lane == 0) P.susp[gw] = 0;
@@ -866,7 +866,7 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
       rec.dg = d;
       rec.dc = dc;
       rec.pad0 = rec.pad1 = rec.pad2 = 0;
-      if (!W) {  // the first kept match (fix_kernel shortcuts), the open walk
+      if (W == kWalkPlain) {  // the first kept match (fix_kernel shortcuts), the open walk
         rec.pad0 = w.c1;
         rec.pad1 = w.first ? w.e1 : 0;
         rec.pad2 = (uint64_t)w.le1 | (w.open ? kRecOpen : 0) | kRecFirst;
@@ -885,7 +885,7 @@ size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates)
 
 namespace {
 
-template <bool WRITE, int ABL, bool W = false, bool STAGE = false, bool RESUME = false>
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false>
 hipError_t sparse_launch(const ScanParams& P, size_t smem, hipStream_t stream)
 {
   static size_t attr_smem = 65536;
@@ -902,12 +902,12 @@ hipError_t sparse_launch(const ScanParams& P, size_t smem, hipStream_t stream)
 
 // The main launch, then (plain walks) the resume launch for the waves it
 // suspended at long walks.
-template <bool WRITE, int ABL, bool W = false, bool STAGE = false>
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false>
 hipError_t sparse_one(const ScanParams& P, size_t smem, hipStream_t stream)
 {
   hipError_t e = sparse_launch<WRITE, ABL, W, STAGE>(P, smem, stream);
-  if constexpr (!W && ABL == 0) {
-    if (e == hipSuccess && P.susp) e = sparse_launch<WRITE, 0, false, STAGE, true>(P, smem, stream);
+  if constexpr (W == kWalkPlain && ABL == 0) {
+    if (e == hipSuccess && P.susp) e = sparse_launch<WRITE, 0, kWalkPlain, STAGE, true>(P, smem, stream);
   }
   return e;
 }
@@ -954,9 +954,15 @@ hipError_t launch_stage_copy(const ScanParams& P, hipStream_t stream)
 
 hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream_t stream)
 {
+  if (P.acap) {  // (word boundaries, line anchors: context accepts)
+    if (write) return sparse_one<true, 0, kWalkCtx>(P, smem, stream);
+    return P.st_n ? sparse_one<false, 0, kWalkCtx, true>(P, smem, stream)
+                  : sparse_one<false, 0, kWalkCtx>(P, smem, stream);
+  }
   if (P.wtab) {
-    if (write) return sparse_one<true, 0, true>(P, smem, stream);
-    return P.st_n ? sparse_one<false, 0, true, true>(P, smem, stream) : sparse_one<false, 0, true>(P, smem, stream);
+    if (write) return sparse_one<true, 0, kWalkWord>(P, smem, stream);
+    return P.st_n ? sparse_one<false, 0, kWalkWord, true>(P, smem, stream)
+                  : sparse_one<false, 0, kWalkWord>(P, smem, stream);
   }
   if (write) return sparse_one<true, 0>(P, smem, stream);
   if (P.st_n) return sparse_one<false, 0, false, true>(P, smem, stream);

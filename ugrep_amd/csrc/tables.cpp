@@ -446,6 +446,8 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       const uint32_t w = opc[k], op = w >> 24;
       if (op == 0xfe) {
         cap = w & 0xffffff;
+      } else if (w == 0xFD000000u) {
+        cap = kCapRedo;  // REDO (lib/pattern.cpp:2945-2947): a negative pattern's accept
       } else if (word_is_meta(w)) {
         const uint32_t idx = w & 0xffff;
         if (op != kMetaBol && op != kMetaEol && !(op >= kMetaWordMin && op <= kMetaWordMax)) {
@@ -471,7 +473,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
           raw.push_back(RawState{(uint32_t)t, 0, {}, {}});
         }
       } else {
-        err = "opcode table uses REDO/TAIL/HEAD/indent words";
+        err = "opcode table uses TAIL/HEAD (lookahead) or indent words";
         return 1;
       }
       ++k;
@@ -537,10 +539,15 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   // supported (the reference would continue that walk from the same byte)
   // (word boundaries: 64 contexts, tables.hpp CTX_*; line anchors only: 4)
   const uint32_t n = (uint32_t)raw.size();
-  bool anchored = false, word = false;
+  bool anchored = false, word = false, redo = false;
   for (uint32_t i = 0; i < n; ++i) {
     anchored = anchored || !raw[i].metas.empty();
+    redo = redo || raw[i].cap == kCapRedo;
     for (const auto& m : raw[i].metas) word = word || (m.first >= kMetaWordMin && m.first <= kMetaWordMax);
+  }
+  if (redo && anchored) {
+    err = "REDO (a negative pattern) in a table with anchors or word boundaries";
+    return 1;
   }
   const uint32_t nctx = word ? 64u : 4u;
   std::vector<uint32_t> acc4((size_t)n * nctx, 0);
@@ -941,6 +948,10 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       t.cap1 = 0;
   }
   if (anchored) t.cap1 = 0;  // (conditional accepts: the accept index comes from acap)
+  // (REDO: the matches that end in it are not reported, which the one-index
+  // kernels -- transducers, carry chains, code-point runs -- do not model)
+  t.redo = redo;
+  if (redo) t.cap1 = 0;
   if (!t.xc && !wide && t.cap1 != 0 && start_sid < first_acc) build_xu(nxt, S, first_acc, start_sid, t);
   // prefilter (see tables.hpp): per first byte c, the bytes that can follow
   // it (second) and follow those (third); "all" once a prefix accepts

@@ -35,6 +35,7 @@ struct DfaTables {
   uint32_t accb = 0;     // first accepting entry (A * R)
   uint32_t accepting = 0;
   uint32_t cap1 = 0;     // the accept index when every accepting state has the same one, else 0
+  bool redo = false;     // some state accepts with REDO (caps = kCapRedo, ctx_bits.hpp); cap1 is then 0
   // Candidate prefilter (replaces the reference's needle/pin prefilters,
   // lib/matcher_avx2.cpp:303-799): the first bytes of the pattern are split
   // into two groups g; a position p can start a match only if for some g

@@ -66,6 +66,9 @@ constexpr uint32_t kCTile = kCChunk * kCIter;
 #ifndef UGPU_XU_ITER
 #define UGPU_XU_ITER 2
 #endif
+#ifndef UGPU_XU_PACK
+#define UGPU_XU_PACK 0
+#endif
 constexpr int kUIter = UGPU_XU_ITER;  // U mode: fewer chunks in flight per wave, twice the waves
 static_assert(kCIter <= 4 && kUIter <= 4, "CIt");
 constexpr int kCLook = 8;                 // look-back chunks before giving up
@@ -248,6 +251,21 @@ __device__ __forceinline__ void ucode_lane(const CU& u, const uint32_t w[4], uin
 #pragma unroll
     for (int k = 0; k < 4; ++k) a[4 * d + k] = __builtin_amdgcn_perm(x, sw, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
   }
+#if UGPU_XU_PACK
+  // (the four bytes of a dword packed by three v_lshl_or_b32 -- full-rate
+  // VALU -- instead of two v_perm_b32, which issue at half rate on gfx950:
+  // tools/probe/valu_rate.hip)
+  uint32_t b[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) b[k] = u.tab[a[k]];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    uint32_t lo, hi;
+    asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(lo) : "v"(b[4 * d + 1]), "v"(b[4 * d]));
+    asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(hi) : "v"(b[4 * d + 3]), "v"(b[4 * d + 2]));
+    asm("v_lshl_or_b32 %0, %1, 16, %2" : "=v"(c[d]) : "v"(hi), "v"(lo));
+  }
+#else
   v2u16 r[8];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
@@ -259,6 +277,7 @@ __device__ __forceinline__ void ucode_lane(const CU& u, const uint32_t w[4], uin
 #pragma unroll
   for (int d = 0; d < 4; ++d)
     c[d] = __builtin_bit_cast(uint32_t, r[2 * d]) | (__builtin_bit_cast(uint32_t, r[2 * d + 1]) << 8);
+#endif
 }
 
 // the code of byte 0 of x (byte 1 of x follows it)
@@ -441,7 +460,21 @@ __device__ __forceinline__ uint64_t clook(uint64_t gen, uint64_t prop, uint32_t 
 struct CIt {
   uint32_t cs[4] = {};
   uint32_t ws = 0, ls = 0;
+  // U mode COUNT (kXuCnt): byte-wise sums of the tile's start bits per dword
+  // (sacc) and of its M bits (macc), folded into ws / ls once per tile
+  uint32_t sacc[4] = {}, macc = 0;
 };
+
+// U mode COUNT: sums per byte instead of v_bcnt / v_dot4 per dword.  Those
+// two issue at half rate on gfx950 (4 cycles per wave-instruction at 8 waves
+// per SIMD, against 2 for v_add / v_bitop3: tools/probe/valu_rate.hip), so
+// the start bits and M bits of a chunk are added byte-wise (a byte counts at
+// most 4 per chunk) and folded by one v_dot4 each per chunk (starts: the
+// chunk's count) or per tile (positions, In bytes).
+#ifndef UGPU_XU_CNT
+#define UGPU_XU_CNT 1
+#endif
+constexpr bool kXuCnt = UGPU_XU_CNT != 0;
 
 // Finish one chunk: final adds with the lane carry-in, then the events.
 // cb = the lane's carry-in bits (bit 0 of each byte: In_{i-1}).
@@ -807,7 +840,7 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
 template <bool UW, bool FAST, bool BM = false>
 __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q, uint32_t& mprev, uint32_t& cs,
                                               uint32_t& ws, uint32_t& ls, uint16_t* ib = nullptr,
-                                              uint16_t* ibl = nullptr)
+                                              uint16_t* ibl = nullptr, CIt* acc = nullptr)
 {
 #if defined(UGPU_XU_ABL) && UGPU_XU_ABL == 3  // loads only (benchmarking; wrong counts)
   cs += v.x ^ v.y ^ v.z ^ v.w;
@@ -818,6 +851,25 @@ __device__ __forceinline__ void uchunk_direct(CU& u, const uint4& v, uint64_t q,
   const uint32_t mp = __builtin_amdgcn_update_dpp(mprev, m[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
   mprev = __builtin_amdgcn_readlane(m[3], 63);
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  if (kXuCnt && acc) {
+    uint32_t st[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t pm = __builtin_amdgcn_alignbit(m[d], d ? m[d - 1] : mp, 24);  // M of the byte before
+      st[d] = m[d] & ~pm;
+      if constexpr (UW) u.risk |= ustray(w[d], m[d], pm);
+      acc->sacc[d] += st[d];
+    }
+    cs = __builtin_amdgcn_udot4((st[0] + st[1]) + (st[2] + st[3]), kOnes, cs, false);
+    acc->macc += (m[0] + m[1]) + (m[2] + m[3]);
+    if constexpr (BM) {
+      if (ibl)
+        ibl[(q >> 4) & 63] = (uint16_t)nib16(m);
+      else
+        ib[q >> 4] = (uint16_t)nib16(m);
+    }
+    return;
+  }
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t pm = __builtin_amdgcn_alignbit(m[d], d ? m[d - 1] : mp, 24);  // M of the byte before
@@ -1114,7 +1166,8 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
         uint16_t* const slot = out.stage + (uint32_t)(j & 1) * 2u * kStg;
         uint16_t* const ibl = BM ? bmst + ((uint32_t)wid * kIt + j) * 64u : nullptr;
         if constexpr (U && !WR)
-          uchunk_direct<W, FAST, BM>(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls, P.inbits, ibl);
+          uchunk_direct<W, FAST, BM>(u, cur[j], ts + j * kCChunk + lo16, mprev, a.cs[j], a.ws, a.ls, P.inbits, ibl,
+                                     &a);
         else if constexpr (U && WR)
           uchunk_write<FAST>(u, cur[j], ts + j * kCChunk + lo16, mprev, out, pend[j & 1], slot);
         else if constexpr (WR)
@@ -1145,6 +1198,15 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
         const BmWord v = reinterpret_cast<const BmWord*>(bmst + (uint32_t)wid * kIt * 64u)[lane];
         reinterpret_cast<BmWord*>(P.inbits + (ts >> 4))[lane] = v;
         cwave_sync();  // (the next tile's chunks write the slots anew)
+      }
+      if constexpr (U && !WR && kXuCnt) {
+        // (the byte sums of the tile: kIt <= 4 chunks, at most 4 per byte each)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t wd = (4u * d) | ((4u * d + 1) << 8) | ((4u * d + 2) << 16) | ((4u * d + 3) << 24);
+          a.ws = __builtin_amdgcn_udot4(a.sacc[d], wd, a.ws, false);
+        }
+        a.ls = __builtin_amdgcn_udot4(a.macc, kOnes, a.ls, false);
       }
       uint32_t c = 0, cj = 0;
 #pragma unroll
