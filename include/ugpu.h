@@ -54,11 +54,12 @@ extern "C" {
 #define UGPU_MODE_OFFSETS 1 /* also materialize (start, len, cap) records */
 
 /* ABI version of this header: bumped whenever a struct below changes layout
-   (ugpu_dfa_info gained contexts/shape in ABI 2).  A caller compiled against
+   or an entry point is added (ugpu_dfa_info gained contexts/shape in ABI 2;
+   ugpu_stream_reserve came in ABI 3).  A caller compiled against
    one header checks ugpu_abi_version() == UGPU_ABI_VERSION before passing a
    struct to the library (integration/reflex_gpu_matcher.h does; on a mismatch
    it keeps the CPU matcher). */
-#define UGPU_ABI_VERSION 2
+#define UGPU_ABI_VERSION 3
 
 typedef struct ugpu_dfa ugpu_dfa;
 typedef struct ugpu_scanner ugpu_scanner;
@@ -356,6 +357,14 @@ int ugpu_stream_feed(ugpu_stream *st, const uint8_t *chunk, uint64_t len, int fi
 /* Absolute offset up to which the FIND chain is settled (bytes before it will
    not be scanned again). */
 uint64_t ugpu_stream_settled(const ugpu_stream *st);
+
+/* Pre-create, on the calling thread's device, the pooled resources of `n`
+   streams on this table whose feeds hold up to feed_bytes (scanners, device
+   buffers and match lists, a private queue and a pinned block each), so that
+   the streams created later allocate nothing (ugrep's workers otherwise make
+   these device allocations all at once, and they serialise).  Optional: a
+   stream without reserved resources creates them itself. */
+int ugpu_stream_reserve(const ugpu_dfa *dfa, int n, uint64_t feed_bytes);
 
 /* --- line-level consumers ---
    For a device-resident buffer (16-byte aligned; the kernels load whole

@@ -30,7 +30,7 @@
 // buffer with the reference's protocol (grow() + get(), absmatcher.h:1417-1593,
 // so buffer shifts, line counting and ugrep's flush handler behave as on the
 // CPU) and feeds the new bytes to a ugpu_stream in chunks of at least
-// UGPU_ADAPTER_CHUNK bytes; settled records come back with absolute offsets
+// UGPU_ADAPTER_CHUNK bytes (default 2 MiB); settled records come back with absolute offsets
 // (num_ + buffer position).
 //
 // Between finds the caller may move cur_ (skip('\n') for -c, --range, context
@@ -76,6 +76,7 @@
 #define REFLEX_GPU_MATCHER_H
 
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <cstdio>
 #include <cstdlib>
@@ -119,6 +120,7 @@ struct GpuEngine {
   decltype(&ugpu_stream_destroy) stream_destroy = NULL;
   decltype(&ugpu_stream_feed) stream_feed = NULL;
   decltype(&ugpu_abi_version) abi_version = NULL;
+  decltype(&ugpu_stream_reserve) stream_reserve = NULL;
 
   static GpuEngine& get()
   {
@@ -174,6 +176,7 @@ struct GpuEngine {
          sym(h, "ugpu_records_free", records_free) && sym(h, "ugpu_result_free", result_free) &&
          sym(h, "ugpu_stream_create", stream_create) && sym(h, "ugpu_stream_destroy", stream_destroy) &&
          sym(h, "ugpu_stream_feed", stream_feed) && sym(h, "ugpu_abi_version", abi_version) &&
+         sym(h, "ugpu_stream_reserve", stream_reserve) &&
          abi_version() == UGPU_ABI_VERSION;
     loaded_flag().store(true, std::memory_order_release);
     // (the handle stays open for the process lifetime)
@@ -235,9 +238,10 @@ class GpuMatcher : public Matcher {
       for (int r = 0; r < kReasons; ++r)
         if (cpu_why_[r] != 0)
           why += std::string(why.empty() ? "" : ",") + reason_name(r) + ":" + std::to_string(cpu_why_[r]);
-      std::fprintf(stderr, "[ugpu-adapter] scans=%zu gpu_finds=%zu cpu_finds=%zu table=%s cpu_why=%s\n", scans_,
-                   gpu_finds_, cpu_finds(), tab_pat_ == NULL ? "none" : tab_ok_ ? "gpu" : "unsupported",
-                   why.empty() ? "-" : why.c_str());
+      std::fprintf(stderr, "[ugpu-adapter] scans=%zu gpu_finds=%zu cpu_finds=%zu table=%s cpu_why=%s read_ms=%.1f feed_ms=%.1f\n",
+                   scans_, gpu_finds_, cpu_finds(), tab_pat_ == NULL ? "none" : tab_ok_ ? "gpu" : "unsupported",
+                   why.empty() ? "-" : why.c_str(), std::chrono::duration<double, std::milli>(t_read_).count(),
+                   std::chrono::duration<double, std::milli>(t_feed_).count());
     }
     src_.clear();
     e_result_free(gres_);
@@ -285,6 +289,23 @@ class GpuMatcher : public Matcher {
  protected:
   virtual size_t match(Method method)
   {
+    // (the hot path of a streamed input: FIND with the cursor where the last
+    // record left it and records of the current feed pending -- nothing that
+    // the checks below decide can have changed since that record: a new
+    // pattern, options or input drop the records)
+    if (method == Const::FIND && gres_ != NULL && gi_ < gres_->count && own_ && chr_ == '\0' &&
+        num_ + cur_ == gcur_abs_ && tab_pat_ == pat_ && sopen_ && !cpu_stream_)
+    {
+      const uint64_t s = sbase_ + gres_->start[gi_];
+      if (s >= gcur_abs_)
+      {
+        ++gpu_finds_;
+        const size_t r = hit(static_cast<size_t>(s - num_), gres_->len[gi_], gres_->cap[gi_]);
+        ++gi_;
+        gcur_abs_ = num_ + cur_;
+        return r;
+      }
+    }
     // FIND, and SCAN / MATCH on whole buffers, come from the engine's FIND
     // records; SPLIT stays on the CPU matcher
     if (method == Const::SPLIT)
@@ -470,11 +491,36 @@ class GpuMatcher : public Matcher {
     static Warm w;
     return w;
   }
-  static void run_warm(Warm* w)
+  // tab: the tables of the matcher that started the warm-up.  Once the devices
+  // are up, they are uploaded and the pooled resources of one stream per live
+  // matcher (ugrep: one per worker) are made on each device
+  // (ugpu_stream_reserve), so that the workers' first feeds do not all
+  // allocate device memory at once -- they serialise on it (VERDICT r4 item 6:
+  // ~100 ms per worker).  Meanwhile the CPU matchers answer (reason "warmup").
+  static void run_warm(Warm* w, std::shared_ptr<Tables> tab, size_t feed)
   {
     bool ok = GpuEngine::get().ok;  // (the device half loads here, on the warm-up thread)
     for (int d = 0; ok && d < devices(); ++d)
       ok = GpuEngine::get().warmup(d) == UGPU_OK;
+    const char* re = std::getenv("UGPU_ADAPTER_RESERVE");
+    if (ok && tab && !(re != NULL && *re == '0'))
+    {
+      std::lock_guard<std::mutex> lk(tab->mu);
+      if (tab->d == NULL && !tab->failed)
+      {
+        (void)GpuEngine::get().select_device(0);
+        if (GpuEngine::get().dfa_create(tab->opc.data(), static_cast<uint32_t>(tab->opc.size()), tab->flags,
+                                        &tab->d) != UGPU_OK)
+        {
+          tab->d = NULL;
+          tab->failed = true;
+        }
+      }
+      const int per = (live().load() + devices() - 1) / devices();
+      for (int d = 0; tab->d != NULL && d < devices(); ++d)
+        if (GpuEngine::get().select_device(d) == UGPU_OK)
+          (void)GpuEngine::get().stream_reserve(tab->d, per, feed);
+    }
     w->state.store(ok ? 2 : 3, std::memory_order_release);
   }
   bool device_ready()
@@ -492,7 +538,7 @@ class GpuMatcher : public Matcher {
         {
           try
           {
-            w.th = std::thread(run_warm, &w);
+            w.th = std::thread(run_warm, &w, tab_, 2 * chunk_);
           }
           catch (...)
           {
@@ -500,7 +546,7 @@ class GpuMatcher : public Matcher {
           }
         }
         if (!async)
-          run_warm(&w);
+          run_warm(&w, tab_, 2 * chunk_);
       }
       st = w.state.load(std::memory_order_acquire);
     }
@@ -771,7 +817,10 @@ class GpuMatcher : public Matcher {
     e = std::getenv("UGPU_ADAPTER_WARM");
     warm_async_ = !(e && *e == '0');
     e = std::getenv("UGPU_ADAPTER_CHUNK");
-    chunk_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (8u << 20);
+    // (2 MiB: a feed's bytes and records stay in the worker's caches between
+    // the read, the H2D staging and the pops -- ugrep C3 3.2-3.5x against
+    // 2.4-2.6x with 8 MiB feeds, profiles/r05_ugrep_e2e.json)
+    chunk_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (2u << 20);
     if (chunk_ == 0)
       chunk_ = 1;
   }
@@ -861,7 +910,17 @@ class GpuMatcher : public Matcher {
       // has arrived, include/reflex/input.h:716-731) feeds at once: the next
       // get() would block, and the reference matcher reports the matches in the
       // bytes it already has before it blocks.
+      if (gst_ == NULL && !stream_may_feed())
+      {
+        // no device for this stream yet (cold, warming, failed, or the device
+        // queue is full): the CPU matcher answers from the cursor on its own
+        // reads -- reading chunk_ bytes ahead here first would cost the CPU
+        // path ~20 % (larger buffer shifts; tools/bench_ugrep.py C2)
+        --gpu_finds_;
+        return cpu(Const::FIND, gst_why_);
+      }
       bool flush = false;
+      const auto t_read = std::chrono::steady_clock::now();
       while (!eof_ && num_ + end_ - sfed_ < chunk_)
       {
         if (end_ + blk_ + 1 >= max_)
@@ -882,6 +941,7 @@ class GpuMatcher : public Matcher {
           }
         }
       }
+      t_read_ += std::chrono::steady_clock::now() - t_read;
       if (eof_ && scans_at_restart_ == scans_ && num_ + end_ - sbase_ < min_bytes())
       {
         // a small input, all of it read before any feed: the CPU matcher is faster
@@ -925,8 +985,11 @@ class GpuMatcher : public Matcher {
       const size_t from = static_cast<size_t>(sfed_ - num_);
       drop_records();
       on_device();
-      if (GpuEngine::get().stream_feed(gst_, reinterpret_cast<const uint8_t*>(buf_ + from), end_ - from,
-                           eof_ ? 1 : flush ? UGPU_FEED_FLUSH : 0, UGPU_MODE_OFFSETS, &gres_) != UGPU_OK)
+      const auto t_feed = std::chrono::steady_clock::now();
+      const int frc = GpuEngine::get().stream_feed(gst_, reinterpret_cast<const uint8_t*>(buf_ + from), end_ - from,
+                                                   eof_ ? 1 : flush ? UGPU_FEED_FLUSH : 0, UGPU_MODE_OFFSETS, &gres_);
+      t_feed_ += std::chrono::steady_clock::now() - t_feed;
+      if (frc != UGPU_OK)
       {
         // engine unavailable for this input: the CPU matcher takes over at the cursor
         cpu_stream_ = true;
@@ -940,6 +1003,30 @@ class GpuMatcher : public Matcher {
       sfed_ = num_ + end_;
       sdone_ = eof_;
     }
+  }
+  // whether a first feed could go to a device now, decided without reading
+  // ahead and without side effects (gst_why_: the reason when not).  A device
+  // still cold for a dense table is not decided here: the read-ahead's
+  // small-input test comes first, so a small input never starts the warm-up.
+  bool stream_may_feed()
+  {
+    const int st = warm().state.load(std::memory_order_acquire);
+    if (st == 1 || st == 3 || (st == 0 && sparse_ && warm_async_))
+    {
+      gst_why_ = warm_reason();
+      return false;
+    }
+    if (st == 2 && sparse_ && !slot_)
+    {
+      DevQueue& q = queue(dev());
+      std::lock_guard<std::mutex> lk(q.mu);
+      if (q.busy >= sparse_max_)
+      {
+        gst_why_ = R_SPARSE;
+        return false;
+      }
+    }
+    return true;
   }
   // more input can be read without blocking (memory and std::istream sources
   // never block; for a FILE*, poll its descriptor)
@@ -1055,6 +1142,9 @@ class GpuMatcher : public Matcher {
   ugpu_stream* gst_ = NULL;
   uint64_t sbase_ = 0, sfed_ = 0, gcur_abs_ = 0;
   bool sdone_ = false, cpu_stream_ = false;
+  int gst_why_ = R_COLD;  // (stream_may_feed)
+  // time in the stream's reads and feeds (UGPU_ADAPTER_STATS)
+  std::chrono::steady_clock::duration t_read_{}, t_feed_{};
   bool sopen_ = false;  // a stream was started for this input (its ugpu_stream at the first feed)
   bool sfit_ = false;   // this input passed the small-input test (device queue decisions from here)
   int cpu_stream_why_ = R_ENGINE;

@@ -103,7 +103,11 @@ def inputs():
 
 def test_kernel_choice(pats):
     assert pats["c3_ident"].info()["kernel"] == 5
-    assert pats["digits"].info()["kernel"] == 0  # prefiltered: sparse_kernel unless UGPU_SPARSE=0
+    # prefiltered: sparse_kernel, or with UGPU_SPARSE=0 (this module's
+    # default, _no_sparse) the dense kernel (xc_kernel takes no prefiltered table)
+    assert pats["digits"].info()["kernel"] == 1
+    os.environ.pop("UGPU_SPARSE", None)
+    assert pats["digits"].info()["kernel"] == 0
 
 
 @pytest.fixture(autouse=True)

@@ -3,8 +3,10 @@
 the reference build (oracle/_ref/ugrep) and of the drop-in build
 (oracle/_ref/ugrep_gpu: reflex::GpuMatcher at ugrep's construction sites) over
 the same files, 16 worker threads (one GPU's share of the node's cores), with
-the adapter's default policy.  The files are memory-mapped by ugrep (<= 1 GB,
-src/mmap.hpp:46-47), so every GPU scan crosses PCIe (ugpu_find_records).
+the adapter's default policy.  ugrep reads files through input() (memory maps
+are off unless --mmap, src/ugrep.hpp:43-44), so each input reaches the GPU as a
+stream of chunks (ugpu_stream_feed); with --mmap a whole buffer
+(ugpu_find_records).  Either way the bytes cross PCIe.
 Prints one JSON line per config: wall seconds (best of --reps), GB/s, whether
 the outputs are identical, and how the adapter dispatched (matchers, GPU scans,
 FIND calls answered by the GPU and by the CPU matcher, and why).
@@ -28,7 +30,8 @@ CONFIGS = [("c2", "foo|bar|baz", 1), ("c2_gpu", "foo|bar|baz", 1), ("c3", "[A-Za
 
 
 def stats(stderr):
-    agg = dict(matchers=0, gpu_matchers=0, scans=0, gpu_finds=0, cpu_finds=0, cpu_why={})
+    agg = dict(matchers=0, gpu_matchers=0, scans=0, gpu_finds=0, cpu_finds=0, cpu_why={}, read_ms_max=0.0,
+               feed_ms_max=0.0)
     for ln in stderr.decode(errors="replace").splitlines():
         if not ln.startswith("[ugpu-adapter] scans="):
             continue
@@ -39,6 +42,10 @@ def stats(stderr):
         agg["cpu_finds"] += int(kv["cpu_finds"])
         if int(kv["scans"]):
             agg["gpu_matchers"] += 1
+        # (per matcher: time in its stream's reads and in ugpu_stream_feed)
+        for k in ("read_ms", "feed_ms"):
+            if k in kv:
+                agg[k + "_max"] = max(agg[k + "_max"], float(kv[k]))
         if kv["cpu_why"] != "-":
             for w in kv["cpu_why"].split(","):
                 k, v = w.split(":")

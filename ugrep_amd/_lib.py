@@ -125,6 +125,7 @@ def _load():
         "ugpu_stream_destroy": (ctypes.c_int, [V]),
         "ugpu_stream_feed": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, P(P(Result))]),
         "ugpu_stream_settled": (ctypes.c_uint64, [V]),
+        "ugpu_stream_reserve": (ctypes.c_int, [V, ctypes.c_int, ctypes.c_uint64]),
         "ugpu_lines": (ctypes.c_int, [V, ctypes.c_uint64, V, ctypes.c_uint64, V, P(ctypes.c_uint64),
                                       P(ctypes.c_uint64), V]),
         "ugpu_check_utf8": (ctypes.c_int, [V, ctypes.c_uint64, P(ctypes.c_uint64), V]),

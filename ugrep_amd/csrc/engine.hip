@@ -1175,9 +1175,26 @@ namespace {
 // call: hipFree synchronises the device): a private non-blocking stream (calls
 // from several host threads do not serialise on the null stream), the device
 // copy of a host input and the device match arrays, grown on demand.
+// Pinned host memory for a stream's match lists: ugpu_stream_feed copies the
+// records there and its ugpu_result borrows the arrays (refs: results still
+// alive; a block with live results is not written again).  Blocks live as long
+// as the pooled workspace that holds them (the process).
+struct PinBlk {
+  uint8_t* p = nullptr;
+  size_t bytes = 0;             // (a pinned_get block)
+  uint64_t cap = 0;             // records
+  uint64_t cap_n = 0;           // cap[0 .. cap_n) holds cap_v (single-accept tables: no cap copy)
+  uint32_t cap_v = 0;
+  std::atomic<int> refs{0};
+};
+
 struct FindWs {
   int dev = -1;
   hipStream_t st = nullptr;
+  // ugpu_stream: the two device buffers (carry + chunk) and the pinned blocks
+  uint8_t* d_sb[2] = {nullptr, nullptr};
+  uint64_t sb_cap = 0;  // bytes of each (+ 16 padding allocated)
+  PinBlk pin[2];
   uint8_t* d_in = nullptr;
   uint64_t in_cap = 0;
   uint64_t* d_start = nullptr;
@@ -1245,6 +1262,19 @@ void find_ws_release(FindWs* w)
   g_find_pool.push_back(w);
 }
 
+// Every ugpu_result is the head of a ResBox: its arrays are malloc()ed, or
+// (pin set) borrowed from a pinned block of a stream's workspace
+struct ResBox {
+  ugpu_result r;
+  PinBlk* pin;
+};
+
+ugpu_result* result_alloc()
+{
+  ResBox* b = static_cast<ResBox*>(std::calloc(1, sizeof(ResBox)));
+  return b ? &b->r : nullptr;
+}
+
 int scanner_acquire(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write = false)
 {
   ugpu_dfa* d = const_cast<ugpu_dfa*>(dfa);
@@ -1279,7 +1309,7 @@ int ugpu_find_all(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, uint64_
   if (!dfa || !out || (!buf && len)) return fail(UGPU_INVAL, "NULL argument");
   *out = nullptr;
   if (start > len) start = len;
-  ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
+  ugpu_result* r = result_alloc();
   if (!r) return fail(UGPU_NOMEM, "host allocation");
   if (len == 0) {
     *out = r;
@@ -2483,7 +2513,7 @@ int ugpu_find_all_multi(const ugpu_dfa* dfa, const uint8_t* buf, uint64_t len, u
     sh.entry = e;
     if (d.exit != ~0ull) sh.exit = d.exit + sh.org;
   }
-  ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
+  ugpu_result* r = result_alloc();
   if (!r) return finish(fail(UGPU_NOMEM, "host allocation"));
   for (Shard& sh : shards) {
     sh.base = r->count;
@@ -2797,10 +2827,9 @@ int ugpu_is_binary(const uint8_t* dbuf, uint64_t len, uint32_t flags, int* binar
 // to the end, and carries [exit - 4, n) into the other buffer.
 struct ugpu_stream {
   const ugpu_dfa* dfa = nullptr;
-  ugpu_scanner* sc = nullptr;
+  ugpu_scanner* sc = nullptr;  // pooled (scanner_acquire)
+  FindWs* ws = nullptr;        // pooled: private stream, the two buffers, pinned match lists
   uint64_t keep = 0;
-  uint8_t* buf[2] = {nullptr, nullptr};
-  uint64_t cap = 0;    // capacity of each buffer (bytes, + 16 padding allocated)
   int cur = 0;         // buffer holding the carry
   uint64_t carry = 0;  // bytes at buf[cur][0..carry): the prefix, then the unsettled bytes
   uint64_t ctx = 0;    // prefix bytes (4, or fewer at the stream's start: buf[cur][0] is its first byte)
@@ -2810,10 +2839,16 @@ struct ugpu_stream {
 
 namespace {
 
+// The stream's resources come from the pools ugpu_find_all uses (a scanner of
+// the table, a per-device workspace): creating a stream per input costs no
+// device allocation once the pools are warm, and no call of a feed touches
+// the null stream or frees device memory (hipFree synchronises the device, so
+// ugrep's workers would wait on each other; VERDICT r4 item 6's trace)
 int stream_grow(ugpu_stream* st, uint64_t need)
 {
-  if (need <= st->cap) return UGPU_OK;
-  uint64_t c = st->cap ? st->cap : (1ull << 20);
+  FindWs* w = st->ws;
+  if (need <= w->sb_cap) return UGPU_OK;
+  uint64_t c = w->sb_cap ? w->sb_cap : (1ull << 20);
   while (c < need) c *= 2;
   uint8_t* nb[2] = {nullptr, nullptr};
   for (int i = 0; i < 2; ++i) {
@@ -2824,7 +2859,8 @@ int stream_grow(ugpu_stream* st, uint64_t need)
     }
   }
   if (st->carry) {
-    const hipError_t e = hipMemcpy(nb[0], st->buf[st->cur], st->carry, hipMemcpyDeviceToDevice);
+    hipError_t e = hipMemcpyAsync(nb[0], w->d_sb[st->cur], st->carry, hipMemcpyDeviceToDevice, w->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(w->st);
     if (e != hipSuccess) {
       (void)hipFree(nb[0]);
       (void)hipFree(nb[1]);
@@ -2832,12 +2868,36 @@ int stream_grow(ugpu_stream* st, uint64_t need)
     }
   }
   for (int i = 0; i < 2; ++i)
-    if (st->buf[i]) (void)hipFree(st->buf[i]);
-  st->buf[0] = nb[0];
-  st->buf[1] = nb[1];
+    if (w->d_sb[i]) (void)hipFree(w->d_sb[i]);
+  w->d_sb[0] = nb[0];
+  w->d_sb[1] = nb[1];
   st->cur = 0;
-  st->cap = c;
+  w->sb_cap = c;
   return UGPU_OK;
+}
+
+// a pinned block of the workspace with no live result and room for m records
+// (grown here), or null (both lent out: the caller copies into malloc()ed arrays)
+PinBlk* stream_pin(FindWs* w, uint64_t m)
+{
+  for (PinBlk& b : w->pin) {
+    if (b.refs.load(std::memory_order_acquire) != 0) continue;
+    if (b.cap < m) {
+      // (from the pinned pool: non-coherent, so the host's reads of the
+      // records are cached)
+      if (b.p) pinned_put(b.p, b.bytes);
+      b.p = nullptr;
+      b.cap = b.cap_n = 0;
+      b.bytes = 0;
+      size_t got = 0;
+      b.p = pinned_get((m + m / 4 + 1024) * 16, got);
+      if (!b.p) return nullptr;
+      b.bytes = got;
+      b.cap = got / 16;
+    }
+    return &b;
+  }
+  return nullptr;
 }
 
 }  // namespace
@@ -2856,10 +2916,17 @@ int ugpu_stream_create(const ugpu_dfa* dfa, uint64_t keep, ugpu_stream** out)
   }
   st->dfa = dfa;
   st->keep = keep ? keep : (64ull << 10);
-  rc = ugpu_scanner_create(dfa, &st->sc);
+  // (a records consumer's scanner: the drop-in matcher feeds in OFFSETS mode)
+  rc = scanner_acquire(dfa, &st->sc, true);
   if (rc) {
     delete st;
     return rc;
+  }
+  st->ws = find_ws_acquire(dev);
+  if (!st->ws) {
+    scanner_release(dfa, st->sc);
+    delete st;
+    return fail(UGPU_NOMEM, "stream workspace");
   }
   *out = st;
   return UGPU_OK;
@@ -2868,14 +2935,81 @@ int ugpu_stream_create(const ugpu_dfa* dfa, uint64_t keep, ugpu_stream** out)
 int ugpu_stream_destroy(ugpu_stream* st)
 {
   if (!st) return UGPU_OK;
-  ugpu_scanner_destroy(st->sc);
-  for (int i = 0; i < 2; ++i)
-    if (st->buf[i]) (void)hipFree(st->buf[i]);
+  (void)hipStreamSynchronize(st->ws->st);
+  st->sc->bol0 = 1;
+  scanner_release(st->dfa, st->sc);
+  find_ws_release(st->ws);
   delete st;
   return UGPU_OK;
 }
 
 uint64_t ugpu_stream_settled(const ugpu_stream* st) { return st ? st->base : 0; }
+
+int ugpu_stream_reserve(const ugpu_dfa* dfa, int n, uint64_t feed_bytes)
+{
+  if (!dfa || n < 0) return fail(UGPU_INVAL, "NULL table or negative count");
+  if (n > 256) n = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(UGPU_DEVICE, "hipGetDevice");
+  int rc = dfa_on(dfa, dev, &dfa);
+  if (rc) return rc;
+  // (every item is acquired before any is released, so the pools end up
+  // holding n distinct ones)
+  const uint64_t need = feed_bytes + (64ull << 10) + 16;  // a feed plus its carry
+  uint64_t c = 1ull << 20;
+  while (c < need) c *= 2;
+  const uint64_t recs = feed_bytes / 8 + 1024;  // (a guess: a list that is longer grows)
+  std::vector<ugpu_scanner*> scs;
+  std::vector<FindWs*> wss;
+  for (int i = 0; i < n && !rc; ++i) {
+    ugpu_scanner* s = nullptr;
+    rc = scanner_acquire(dfa, &s, true);
+    if (rc) break;
+    scs.push_back(s);
+    if (s->xc && !s->word && env_u64("UGPU_XC_BITMAP", 1) != 0) {
+      // (the In bits of a COUNT pass over a whole buffer, as ugpu_scan sizes them)
+      const uint64_t nb = ((((c + 16 + 15) & ~uint64_t(15)) + 2048) >> 3) + 64;
+      if (nb > s->inbits_cap) {
+        (void)hipFree(s->d_inbits);
+        s->d_inbits = nullptr;
+        s->inbits_cap = 0;
+        if (hipMalloc(&s->d_inbits, nb + nb / 8) == hipSuccess)
+          s->inbits_cap = nb + nb / 8;
+        else
+          (void)hipGetLastError();
+      }
+    }
+    FindWs* w = find_ws_acquire(dev);
+    if (!w) {
+      rc = fail(UGPU_NOMEM, "stream workspace");
+      break;
+    }
+    wss.push_back(w);
+    if (w->sb_cap < c) {
+      for (int k = 0; k < 2; ++k) {
+        (void)hipFree(w->d_sb[k]);
+        w->d_sb[k] = nullptr;
+      }
+      w->sb_cap = 0;
+      hipError_t e = hipMalloc(&w->d_sb[0], c + 16);
+      if (e == hipSuccess) e = hipMalloc(&w->d_sb[1], c + 16);
+      if (e != hipSuccess) {
+        rc = hip_fail(e, "stream buffer");
+        break;
+      }
+      w->sb_cap = c;
+    }
+    hipError_t e = w->reserve_out(recs);
+    if (e != hipSuccess) {
+      rc = hip_fail(e, "stream match list");
+      break;
+    }
+    if (env_u64("UGPU_RESERVE_PIN", 0) != 0 && !stream_pin(w, recs)) rc = fail(UGPU_NOMEM, "pinned match list");
+  }
+  for (ugpu_scanner* s : scs) scanner_release(dfa, s);
+  for (FindWs* w : wss) find_ws_release(w);
+  return rc;
+}
 
 int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int final, uint32_t mode, ugpu_result** out)
 {
@@ -2885,15 +3019,20 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
   const bool flush = final == UGPU_FEED_FLUSH;
   final = final == 1;
   *out = nullptr;
+  FindWs* w = st->ws;
+  hipStream_t hs = w->st;
   const uint64_t n = st->carry + len;
   int rc = stream_grow(st, n);
   if (rc) return rc;
-  uint8_t* b = st->buf[st->cur];
-  if (len) HIP_TRY(hipMemcpy(b + st->carry, chunk, len, hipMemcpyHostToDevice));
-  ugpu_result* r = static_cast<ugpu_result*>(std::calloc(1, sizeof(ugpu_result)));
+  uint8_t* b = w->d_sb[st->cur];
+  if (len) {
+    HIP_TRY(hipMemcpyAsync(b + st->carry, chunk, len, hipMemcpyHostToDevice, hs));
+  }
+  ugpu_result* r = result_alloc();
   if (!r) return fail(UGPU_NOMEM, "host allocation");
   ugpu_scanner_context(st->sc, 1);  // (buf[cur][0] is the stream's first byte or 4 bytes before lo)
   const uint64_t lo = st->ctx, bias = st->base - lo;
+  const bool offsets = mode == UGPU_MODE_OFFSETS;
   // settle the chain up to `keep` bytes before the end (all of it when final);
   // a walk still open at the end of the bytes so far means hi was too close
   uint64_t hi = final ? n : (n > lo + st->keep ? n - st->keep : lo);
@@ -2905,7 +3044,8 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
     // from the end by 16, 64, 256, ... bytes, then bisect between the last hi
     // that was too close and the first that was not
     auto try_hi = [&](uint64_t h) -> int {
-      int c = ugpu_scan(st->sc, b, lo, h, n, 0, bias, nullptr);
+      st->sc->stage_once = offsets;
+      int c = ugpu_scan(st->sc, b, lo, h, n, 0, bias, hs);
       if (!c) c = ugpu_scan_totals(st->sc, &tot);
       return c;
     };
@@ -2918,7 +3058,7 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
         break;
       }
       if (rc != UGPU_HALO) {
-        std::free(r);
+        ugpu_result_free(r);
         return rc;
       }
       bad = h;
@@ -2934,7 +3074,7 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
       } else if (rc == UGPU_HALO) {
         bad = mid;
       } else {
-        std::free(r);
+        ugpu_result_free(r);
         return rc;
       }
     }
@@ -2942,20 +3082,21 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
     rc = UGPU_OK;
     if (hi > lo && last != hi) rc = try_hi(hi);  // (the scanner holds the last scan)
     if (rc) {
-      std::free(r);
+      ugpu_result_free(r);
       return rc;
     }
     exit = hi > lo ? tot.exit : lo;
   }
   while (hi > lo && !(flush && !final)) {
-    rc = ugpu_scan(st->sc, b, lo, hi, n, final ? 1 : 0, bias, nullptr);
+    st->sc->stage_once = offsets;  // (single-pass OFFSETS for prefiltered tables)
+    rc = ugpu_scan(st->sc, b, lo, hi, n, final ? 1 : 0, bias, hs);
     if (!rc) rc = ugpu_scan_totals(st->sc, &tot);
     if (rc == UGPU_HALO && !final) {
       hi = lo + (hi - lo) / 2;
       continue;
     }
     if (rc) {
-      std::free(r);
+      ugpu_result_free(r);
       return rc;
     }
     exit = final ? n : tot.exit;
@@ -2965,28 +3106,61 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
     r->count = tot.count;
     r->digest = tot.digest;
     r->dcap = tot.dcap;
-    if (mode == UGPU_MODE_OFFSETS && tot.count > 0) {
+    if (offsets && tot.count > 0) {
+      // records into the workspace's device lists, then one copy into a pinned
+      // block the result borrows (single-accept tables: no cap array on the
+      // device; the block's cap array holds the accept index already)
       const uint64_t m = tot.count;
-      uint64_t* d_start = nullptr;
-      uint32_t *d_len = nullptr, *d_cap = nullptr;
-      r->start = static_cast<uint64_t*>(std::malloc(m * 8));
-      r->len = static_cast<uint32_t*>(std::malloc(m * 4));
-      r->cap = static_cast<uint32_t*>(std::malloc(m * 4));
-      hipError_t e = hipSuccess;
-      if (!r->start || !r->len || !r->cap || (e = hipMalloc(&d_start, m * 8)) != hipSuccess ||
-          (e = hipMalloc(&d_len, m * 4)) != hipSuccess || (e = hipMalloc(&d_cap, m * 4)) != hipSuccess)
-        rc = e != hipSuccess ? hip_fail(e, "stream match list") : fail(UGPU_NOMEM, "stream match list");
-      if (!rc) rc = ugpu_scan_offsets(st->sc, d_start, d_len, d_cap, m, nullptr);
-      if (!rc && ((e = hipMemcpy(r->start, d_start, m * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
-                  (e = hipMemcpy(r->len, d_len, m * 4, hipMemcpyDeviceToHost)) != hipSuccess ||
-                  (e = hipMemcpy(r->cap, d_cap, m * 4, hipMemcpyDeviceToHost)) != hipSuccess))
+      const uint32_t cap1 = st->dfa->t.cap1;
+      const bool one = cap1 != 0 && !st->dfa->t.anchored;
+      hipError_t e = w->reserve_out(m);
+      if (e != hipSuccess) rc = hip_fail(e, "stream match list");
+      if (!rc) rc = ugpu_scan_offsets(st->sc, w->d_start, w->d_len, one ? nullptr : w->d_cap, m, hs);
+      PinBlk* pb = rc ? nullptr : stream_pin(w, m);
+      uint64_t* hstart = nullptr;
+      uint32_t *hlen = nullptr, *hcap = nullptr;
+      if (!rc && pb) {
+        hstart = reinterpret_cast<uint64_t*>(pb->p);
+        hlen = reinterpret_cast<uint32_t*>(pb->p + pb->cap * 8);
+        hcap = reinterpret_cast<uint32_t*>(pb->p + pb->cap * 12);
+      } else if (!rc) {
+        hstart = static_cast<uint64_t*>(std::malloc(m * 8));
+        hlen = static_cast<uint32_t*>(std::malloc(m * 4));
+        hcap = static_cast<uint32_t*>(std::malloc(m * 4));
+        r->start = hstart;
+        r->len = hlen;
+        r->cap = hcap;
+        if (!hstart || !hlen || !hcap) rc = fail(UGPU_NOMEM, "stream match list");
+      }
+      if (!rc && ((e = hipMemcpyAsync(hstart, w->d_start, m * 8, hipMemcpyDeviceToHost, hs)) != hipSuccess ||
+                  (e = hipMemcpyAsync(hlen, w->d_len, m * 4, hipMemcpyDeviceToHost, hs)) != hipSuccess ||
+                  (!one && (e = hipMemcpyAsync(hcap, w->d_cap, m * 4, hipMemcpyDeviceToHost, hs)) != hipSuccess)))
         rc = hip_fail(e, "stream match list copy");
-      (void)hipFree(d_start);
-      (void)hipFree(d_len);
-      (void)hipFree(d_cap);
+      if (!rc && one) {
+        // (while the copies run)
+        if (pb && pb->cap_v == cap1 && pb->cap_n >= m) {
+        } else {
+          std::fill(hcap, hcap + m, cap1);
+          if (pb) {
+            pb->cap_v = cap1;
+            pb->cap_n = m;
+          }
+        }
+      } else if (!rc && pb) {
+        pb->cap_n = 0;  // (the cap array now holds copied accept indices)
+      }
+      if (!rc && (e = hipStreamSynchronize(hs)) != hipSuccess) rc = hip_fail(e, "stream match list copy");
       if (rc) {
+        (void)hipStreamSynchronize(hs);
         ugpu_result_free(r);
         return rc;
+      }
+      if (pb) {
+        pb->refs.fetch_add(1, std::memory_order_acq_rel);
+        reinterpret_cast<ResBox*>(r)->pin = pb;
+        r->start = hstart;
+        r->len = hlen;
+        r->cap = hcap;
       }
     }
   }
@@ -2995,7 +3169,14 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
   // resumes at the byte after them
   const uint64_t nctx = exit < 4 ? exit : 4;  // (exit >= lo: buf[cur][0] is the first byte when exit < 4)
   const uint64_t keep_n = n - exit + nctx;
-  if (keep_n) HIP_TRY(hipMemcpy(st->buf[1 - st->cur], b + exit - nctx, keep_n, hipMemcpyDeviceToDevice));
+  if (keep_n) {
+    hipError_t e = hipMemcpyAsync(w->d_sb[1 - st->cur], b + exit - nctx, keep_n, hipMemcpyDeviceToDevice, hs);
+    if (e == hipSuccess) e = hipStreamSynchronize(hs);
+    if (e != hipSuccess) {
+      ugpu_result_free(r);
+      return hip_fail(e, "stream carry copy");
+    }
+  }
   st->cur = 1 - st->cur;
   st->carry = keep_n;
   st->ctx = nctx;
@@ -3008,10 +3189,15 @@ int ugpu_stream_feed(ugpu_stream* st, const uint8_t* chunk, uint64_t len, int fi
 int ugpu_result_free(ugpu_result* r)
 {
   if (!r) return UGPU_OK;
-  std::free(r->start);
-  std::free(r->len);
-  std::free(r->cap);
-  std::free(r);
+  ResBox* b = reinterpret_cast<ResBox*>(r);  // (r is the head of its box: result_alloc)
+  if (b->pin) {
+    b->pin->refs.fetch_sub(1, std::memory_order_release);
+  } else {
+    std::free(r->start);
+    std::free(r->len);
+    std::free(r->cap);
+  }
+  std::free(b);
   return UGPU_OK;
 }
 

@@ -67,7 +67,7 @@ constexpr uint32_t kCTile = kCChunk * kCIter;
 #define UGPU_XU_ITER 2
 #endif
 #ifndef UGPU_XU_PACK
-#define UGPU_XU_PACK 0
+#define UGPU_XU_PACK 1
 #endif
 constexpr int kUIter = UGPU_XU_ITER;  // U mode: fewer chunks in flight per wave, twice the waves
 static_assert(kCIter <= 4 && kUIter <= 4, "CIt");
@@ -1337,7 +1337,6 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_bm_kernel(ScanParams P)
 // (the k-th end of the round closes the k-th start, or the match open at
 // the round start) all leave as coalesced stores.  No table, no walk: the pass
 // reads 1/8 of the input's bytes and writes the records.
-constexpr int kXeThreads = 256;
 #ifndef UGPU_XE_CAP
 #define UGPU_XE_CAP 1024
 #endif
@@ -1428,22 +1427,25 @@ __device__ __forceinline__ void xe_wait_k(uint64_t& a, uint64_t& b, uint32_t k)
       : "memory", "scc");
 }
 
-// The range is cut into 4 quarters of whole words, one per wave.  A first
-// pass counts each quarter's starts and ends and finds its last start; after
-// one block barrier every wave knows its output bases and writes its quarter
-// alone.
+// NW = 4: the range is cut into 4 quarters of whole words, one per wave.  A
+// first pass counts each quarter's starts and ends and finds its last start;
+// after one block barrier every wave knows its output bases and writes its
+// quarter alone.  NW = 1: one wave takes the COUNT wave's whole range, its
+// output base is the COUNT pass's, and there is no first pass (the bitmap is
+// read once, and no block barrier separates the passes) -- with one block per
+// COUNT wave (8192) the chip still holds 32 of these waves per CU.
 constexpr uint32_t kXeWaveCap = UGPU_XE_CAP;  // starts (and ends) a wave-round stages at once (2 KiB each)
 
-template <bool U>
+template <bool U, int NW>
 #ifndef UGPU_XE_WAVES_PER_EU
 #define UGPU_XE_WAVES_PER_EU 7
 #endif
-__global__ __launch_bounds__(kXeThreads) __attribute__((amdgpu_waves_per_eu(UGPU_XE_WAVES_PER_EU))) void xc_expand_kernel(ScanParams P)
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(UGPU_XE_WAVES_PER_EU))) void xc_expand_kernel(ScanParams P)
 {
-  __shared__ uint16_t st_off[4][kXeWaveCap];  // a round's start positions, from the round's first position
-  __shared__ uint16_t en_off[4][kXeWaveCap];  // its end positions
-  __shared__ uint32_t qs[4], qe[4];
-  __shared__ int64_t ql[4];
+  __shared__ uint16_t st_off[NW][kXeWaveCap];  // a round's start positions, from the round's first position
+  __shared__ uint16_t en_off[NW][kXeWaveCap];  // its end positions
+  __shared__ uint32_t qs[NW], qe[NW];
+  __shared__ int64_t ql[NW];
   __shared__ uint64_t fix_s;
   constexpr uint64_t kTile = (uint64_t)kCChunk * (U ? kUIter : kCIter);
   const uint64_t gw = blockIdx.x;
@@ -1500,10 +1502,10 @@ __global__ __launch_bounds__(kXeThreads) __attribute__((amdgpu_waves_per_eu(UGPU
     en = prev & ~w & lim;
   };
   const uint64_t wb = wlo >> 6, we = end > wlo ? (end + 63) >> 6 : wb;  // words [wb, we)
-  const uint64_t nq = (we - wb + 3) / 4;
+  const uint64_t nq = (we - wb + NW - 1) / NW;
   const uint64_t qb = wb + wv * nq, qend = qb + nq < we ? qb + nq : we;  // this wave's words
   // pass 1: the quarter's counts and last start
-  {
+  if constexpr (NW > 1) {
     uint32_t ns = 0, ne = 0;
     int64_t ls = -1;
     for (uint64_t wi0 = qb + lane; wi0 < qend; wi0 += 256) {
@@ -1811,10 +1813,22 @@ uint32_t xc_waves() { return kCWaves; }
 hipError_t launch_xc_expand(const ScanParams& P, hipStream_t stream, uint64_t count)
 {
   const uint32_t nrec = P.grid * (uint32_t)kCWaves;
-  if (P.xu_tab)
-    hipLaunchKernelGGL((xc_expand_kernel<true>), dim3(nrec), dim3(kXeThreads), 0, stream, P);
-  else
-    hipLaunchKernelGGL((xc_expand_kernel<false>), dim3(nrec), dim3(kXeThreads), 0, stream, P);
+  // (UGPU_XE_WAVES: 1 = one wave per COUNT wave, no counting pass; 4 = quarters)
+  static const int nw = [] {
+    const char* e = std::getenv("UGPU_XE_WAVES");
+    return e && *e == '1' ? 1 : 4;
+  }();
+  if (nw == 4) {
+    if (P.xu_tab)
+      hipLaunchKernelGGL((xc_expand_kernel<true, 4>), dim3(nrec), dim3(256), 0, stream, P);
+    else
+      hipLaunchKernelGGL((xc_expand_kernel<false, 4>), dim3(nrec), dim3(256), 0, stream, P);
+  } else {
+    if (P.xu_tab)
+      hipLaunchKernelGGL((xc_expand_kernel<true, 1>), dim3(nrec), dim3(64), 0, stream, P);
+    else
+      hipLaunchKernelGGL((xc_expand_kernel<false, 1>), dim3(nrec), dim3(64), 0, stream, P);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint64_t n = count < P.out_capacity ? count : P.out_capacity;
