@@ -90,6 +90,8 @@ struct ugpu_dfa {
   // (wfind_kernel, device_common.hpp kWalkCtx) on the per-context accepts
   bool nul = false, amode = false;
   uint32_t* d_acap = nullptr;  // acap, or (word boundaries) acap_rows then acap_map
+  // no match starts right after a word character (ScanParams::wstart)
+  bool wstart = false;
   // idle scanners of ugpu_find_all calls on this table (reused: creating one
   // costs device allocations and property queries)
   std::mutex pool_mu;
@@ -274,6 +276,7 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.acap_n = (uint32_t)(P.ctx_word ? d->t.acap_rows.size() : d->t.acap.size());
   P.amap = P.ctx_word ? d->d_acap + d->t.acap_rows.size() : nullptr;
   P.nul = d->nul ? 1u : 0u;
+  P.wstart = d->wstart && env_u64("UGPU_WSTART", 1) != 0 ? 1u : 0u;
   P.bol0 = 1;
   // chain bytes one stitch merge may cross before the chains count as not
   // resynchronising (two chains of a resynchronising table meet within a match
@@ -457,6 +460,30 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
   d->amode = pl.amode;
   d->wplus = pl.wplus;
   d->xcw = pl.xcw;
+  // option W: every match begins where at_wb holds (lib/matcher.cpp:107);
+  // word-boundary tables: when no state accepts in a context without CTX_WB
+  if (pattern_flags & UGPU_PAT_WORD) {
+    d->wstart = !d->amode;
+  } else if (d->amode && d->t.ctx_word && d->t.format != FMT_WIDE) {
+    // a candidate right after a letter has WB = 0 and BW = whether its first
+    // character is a word character: droppable when no state accepts in such
+    // a context.  BW = 1 for every first byte of the pattern that is an ASCII
+    // word byte; any other first byte (non-ASCII included) may give BW = 0.
+    auto asc_word = [](uint32_t b) {
+      return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_';
+    };
+    bool bw0 = false;
+    for (uint32_t b = 0; b < 256 && !bw0; ++b) {
+      const uint32_t col = d->t.format == FMT_BYTE ? b : d->t.cls[b];
+      if (d->t.trans[d->t.start + col] != 0 && !asc_word(b)) bw0 = true;
+    }
+    bool any = false;
+    for (size_t i = 0; i < d->t.acap.size() && !any; ++i) {
+      const uint32_t c = (uint32_t)(i & 63);
+      any = !(c & CTX_WB) && ((c & CTX_BW) || bw0) && d->t.acap[i] != 0;
+    }
+    d->wstart = !any && !d->t.acap.empty();
+  }
   const size_t n = d->t.trans.size();
   d->ntrans_pad = (uint32_t)((n + 7) & ~size_t(7));
   std::vector<uint16_t> tr(d->ntrans_pad, 0);

@@ -210,6 +210,10 @@ struct ScanParams {
   // buffer is '\n', or the buffer begins the input); nul: option N, empty
   // matches are reported
   const uint32_t* acap;
+  // sparse_kernel: no match starts after a word character (option W's at_wb
+  // at the match begin, lib/matcher.cpp:107; or a table whose every accept
+  // needs CTX_WB), so candidates right after an ASCII letter are dropped
+  uint32_t wstart;
   uint32_t bol0;
   uint32_t nul;
   uint32_t ctx_word;

@@ -61,6 +61,17 @@ __device__ __forceinline__ uint32_t flags4(uint32_t X)
   return ((((X | (X >> 1)) & 0x01010101u) * 0x01020408u) >> 24);
 }
 
+// 4-bit mask (bit i = byte i is an ASCII letter) of a dword: lower-case the
+// letters (| 0x20), then t >= 'a' and t <= 'z' per byte with the bytes' top
+// bits as the comparison results (t <= 0x7f, so no carry crosses a byte);
+// bytes >= 0x80 are no letters.
+__device__ __forceinline__ uint32_t letters4(uint32_t x)
+{
+  const uint32_t t = (x | 0x20202020u) & 0x7f7f7f7fu;
+  const uint32_t m = (t + 0x1f1f1f1fu) & ~(t + 0x05050505u) & ~x & 0x80808080u;
+  return ((m >> 7) * 0x01020408u) >> 24;
+}
+
 // Wave-wide inclusive scans by DPP row shifts + row broadcasts (no LDS round
 // trip): row_shr 1,2,4,8 then row_bcast:15 (rows 1,3) and row_bcast:31 (rows 2,3).
 __device__ __forceinline__ uint32_t dpp_scan_add(uint32_t v)
@@ -597,6 +608,15 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
   for (int k = 0; k < 4; ++k) {
     if (!tail && !__ballot(anyk[k] != 0)) continue;
     uint32_t mk = flags4(X[k][0]) | (flags4(X[k][1]) << 4) | (flags4(X[k][2]) << 8) | (flags4(X[k][3]) << 12);
+    if (P.wstart) {
+      // no match starts right after a word character: drop the candidates
+      // that follow an ASCII letter in the lane's 16 bytes (its first byte's
+      // predecessor is another lane's: it stays; a digit, '_' or a non-ASCII
+      // byte before a candidate keeps it too -- a superset)
+      const uint4& v = k == 0 ? v0 : k == 1 ? v1 : k == 2 ? v2 : v3;
+      const uint32_t lt = letters4(v.x) | (letters4(v.y) << 4) | (letters4(v.z) << 8) | (letters4(v.w) << 12);
+      mk &= ~(lt << 1);
+    }
     const uint64_t p0 = ts + 1024u * k + 16u * lane;
     if (!P.at_eof && p0 + 18 > P.rend && p0 < P.rend) {
       // the last two readable positions of a non-final range: their prefilter
