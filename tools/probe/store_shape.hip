@@ -6,6 +6,7 @@
 //   shape 1: 16 B per lane for both arrays (2 starts, 4 lengths a lane)
 //   shape 2: shape 1 but rounds not aligned to 4 records (head/tail lanes narrow)
 //   shape 3: a plain linear 16-B-per-lane fill of the same 12 GB
+//   shape 4: shape 0 with non-temporal stores
 // hipcc --offload-arch=gfx950 -O3 store_shape.hip -o store_shape
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -34,6 +35,10 @@ __global__ __launch_bounds__(64) void k(uint64_t* st, uint32_t* ln, uint64_t nre
     if constexpr (SHAPE == 0) {
       for (uint32_t t = lane; t < R; t += 64) st[r + t] = r + t;
       for (uint32_t t = lane; t < R; t += 64) ln[r + t] = (uint32_t)t;
+    } else if constexpr (SHAPE == 4) {
+      // shape 0 with non-temporal stores
+      for (uint32_t t = lane; t < R; t += 64) __builtin_nontemporal_store((uint64_t)(r + t), &st[r + t]);
+      for (uint32_t t = lane; t < R; t += 64) __builtin_nontemporal_store((uint32_t)t, &ln[r + t]);
     } else {
       // head records up to 4-alignment of r, then 16-B lanes, then the tail
       const uint32_t h = SHAPE == 1 ? 0u : (uint32_t)((4 - (r & 3)) & 3);
@@ -69,9 +74,9 @@ int main(int argc, char** argv)
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int shape = 0; shape < 4; ++shape) {
+  for (int shape = 0; shape < 5; ++shape) {
     for (uint32_t per : {476u, 475u}) {
-      if ((shape == 1 && per & 3) || (shape == 3 && per != 476u)) continue;
+      if ((shape == 1 && per & 3) || (shape >= 3 && per != 476u)) continue;
       float best = 1e9f;
       for (int rep = 0; rep < 6; ++rep) {
         CK(hipEventRecord(a));
@@ -79,7 +84,8 @@ int main(int argc, char** argv)
           case 0: hipLaunchKernelGGL(k<0>, dim3(nblk), dim3(64), 0, 0, st, ln, nrec, per_blk, per); break;
           case 1: hipLaunchKernelGGL(k<1>, dim3(nblk), dim3(64), 0, 0, st, ln, nrec, per_blk, per); break;
           case 2: hipLaunchKernelGGL(k<2>, dim3(nblk), dim3(64), 0, 0, st, ln, nrec, per_blk, per); break;
-          default: hipLaunchKernelGGL(k<3>, dim3(nblk), dim3(64), 0, 0, st, ln, nrec, per_blk, per); break;
+          case 3: hipLaunchKernelGGL(k<3>, dim3(nblk), dim3(64), 0, 0, st, ln, nrec, per_blk, per); break;
+          default: hipLaunchKernelGGL(k<4>, dim3(nblk), dim3(64), 0, 0, st, ln, nrec, per_blk, per); break;
         }
         CK(hipGetLastError());
         CK(hipEventRecord(b));

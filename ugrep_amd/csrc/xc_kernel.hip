@@ -1340,6 +1340,13 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_bm_kernel(ScanParams P)
 #ifndef UGPU_XE_CAP
 #define UGPU_XE_CAP 1024
 #endif
+// non-temporal record stores: 1 starts, 2 lengths, 3 both.  Starts only is
+// the default: C4 OFFSETS 5.03 / 5.82 against 5.49 / 6.11 ms per step, C3
+// 9.05 against 9.33 (two runs on one box); lengths too was slower on C3
+// (profiles/r05_offsets_ab.json)
+#ifndef UGPU_XE_NT
+#define UGPU_XE_NT 1
+#endif
 
 // a word load the compiler does not track (no s_waitcnt of its own); the
 // caller waits with xe_wait, whose count N must be at most the number of
@@ -1636,7 +1643,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(UGPU_XE
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const uint32_t t = t0 + 64 * j + lane;
+#if UGPU_XE_NT & 1
+              if (t < R) __builtin_nontemporal_store(sbase + v[j], &os[t]);
+#else
               if (t < R) os[t] = sbase + v[j];
+#endif
             }
           }
         } else {
@@ -1685,7 +1696,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(UGPU_XE
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const uint32_t t = t0 + 64 * j + lane;
+#if UGPU_XE_NT & 2
+              if (t < E) __builtin_nontemporal_store(v[j], &ol[t]);
+#else
               if (t < E) ol[t] = v[j];
+#endif
             }
           }
         } else {
