@@ -66,6 +66,12 @@ constexpr uint32_t kCTile = kCChunk * kCIter;
 #ifndef UGPU_XU_ITER
 #define UGPU_XU_ITER 2
 #endif
+// the COUNT pass's In-bit stores non-temporal: C3 OFFSETS 8.54 against 8.70 ms
+// (xc_bm_kernel 3.57 against 3.72), C4 even; non-temporal loads of the bits in
+// the expansion were slower (profiles/r05_offsets_ab.json)
+#ifndef UGPU_XBM_NT
+#define UGPU_XBM_NT 1
+#endif
 #ifndef UGPU_XU_PACK
 #define UGPU_XU_PACK 1
 #endif
@@ -1196,7 +1202,17 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
         static_assert(sizeof(BmWord) == 2 * kIt, "one word per lane");
         cwave_sync();
         const BmWord v = reinterpret_cast<const BmWord*>(bmst + (uint32_t)wid * kIt * 64u)[lane];
+#if UGPU_XBM_NT
+        if constexpr (kIt == 4) {
+          __builtin_nontemporal_store(__builtin_bit_cast(uint64_t, v), reinterpret_cast<uint64_t*>(P.inbits + (ts >> 4)) + lane);
+        } else if constexpr (kIt == 2) {
+          __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(P.inbits + (ts >> 4)) + lane);
+        } else {
+          reinterpret_cast<BmWord*>(P.inbits + (ts >> 4))[lane] = v;
+        }
+#else
         reinterpret_cast<BmWord*>(P.inbits + (ts >> 4))[lane] = v;
+#endif
         cwave_sync();  // (the next tile's chunks write the slots anew)
       }
       if constexpr (U && !WR && kXuCnt) {
@@ -1354,7 +1370,11 @@ __global__ __launch_bounds__(kCWaves * 64) void xc_bm_kernel(ScanParams P)
 __device__ __forceinline__ uint64_t xe_load(const uint64_t* p)
 {
   uint64_t v;
+#if UGPU_XE_LNT
+  asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+#else
   asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+#endif
   return v;
 }
 template <int N>
