@@ -263,7 +263,13 @@ __device__ __forceinline__ void ucode_lane(const CU& u, const uint32_t w[4], uin
   // tools/probe/valu_rate.hip)
   uint32_t b[16];
 #pragma unroll
+#if defined(UGPU_XU_ABL) && UGPU_XU_ABL == 1  // broadcast lookups: no bank conflicts (benchmarking; wrong counts)
+  for (int k = 0; k < 16; ++k) b[k] = u.tab[a[k] & 3u];
+#elif defined(UGPU_XU_ABL) && UGPU_XU_ABL == 2  // no LDS lookups (benchmarking; wrong counts)
+  for (int k = 0; k < 16; ++k) b[k] = (a[k] >> 13) & 1u;
+#else
   for (int k = 0; k < 16; ++k) b[k] = u.tab[a[k]];
+#endif
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     uint32_t lo, hi;
