@@ -502,7 +502,11 @@ class GpuMatcher : public Matcher {
     bool ok = GpuEngine::get().ok;  // (the device half loads here, on the warm-up thread)
     for (int d = 0; ok && d < devices(); ++d)
       ok = GpuEngine::get().warmup(d) == UGPU_OK;
+    // (UGPU_ADAPTER_RESERVE: 0 = no reserve, 2 = the devices count as ready
+    // before the reserve runs, so the workers' first feeds overlap it)
     const char* re = std::getenv("UGPU_ADAPTER_RESERVE");
+    const bool late = re != NULL && *re == '2';
+    ugpu_dfa* t = NULL;
     if (ok && tab && !(re != NULL && *re == '0'))
     {
       std::lock_guard<std::mutex> lk(tab->mu);
@@ -516,12 +520,16 @@ class GpuMatcher : public Matcher {
           tab->failed = true;
         }
       }
-      const int per = (live().load() + devices() - 1) / devices();
-      for (int d = 0; tab->d != NULL && d < devices(); ++d)
-        if (GpuEngine::get().select_device(d) == UGPU_OK)
-          (void)GpuEngine::get().stream_reserve(tab->d, per, feed);
+      t = tab->d;  // (tab keeps it alive)
     }
-    w->state.store(ok ? 2 : 3, std::memory_order_release);
+    if (late)
+      w->state.store(ok ? 2 : 3, std::memory_order_release);
+    const int per = (live().load() + devices() - 1) / devices();
+    for (int d = 0; t != NULL && d < devices(); ++d)
+      if (GpuEngine::get().select_device(d) == UGPU_OK)
+        (void)GpuEngine::get().stream_reserve(t, per, feed);
+    if (!late)
+      w->state.store(ok ? 2 : 3, std::memory_order_release);
   }
   bool device_ready()
   {

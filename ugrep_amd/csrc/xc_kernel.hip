@@ -72,6 +72,14 @@ constexpr uint32_t kCTile = kCChunk * kCIter;
 #ifndef UGPU_XBM_NT
 #define UGPU_XBM_NT 1
 #endif
+// U mode pair-table layout: 1 = entry (x, y) at x << 8 | (y ^ (x << 2 & 0xfc))
+// (the swizzle spread ASCII lanes over the LDS banks); 0 = at x << 8 | y, so a
+// lookup address is one v_perm of the lane's bytes (no next-byte dword, no
+// XOR) -- bank conflicts no longer cost time
+#ifndef UGPU_XU_SWZ
+#define UGPU_XU_SWZ 1
+#endif
+__device__ __forceinline__ uint32_t xu_swz(uint32_t x) { return UGPU_XU_SWZ ? ((x << 2) & 0xfcu) : 0u; }
 #ifndef UGPU_XU_PACK
 #define UGPU_XU_PACK 1
 #endif
@@ -224,12 +232,18 @@ __device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t n
   // spreads the lanes of ASCII text over the banks.  (Addressing the host
   // tables directly, ASCII and continuation lanes on few dwords, had fewer
   // bank conflicts but 26 instead of 11 VALU per dword: 3.57 vs 3.17 ms on C4.)
+#if UGPU_XU_SWZ
   const uint32_t y = __builtin_amdgcn_alignbit(nx, x, 8);
   const uint32_t sw = y ^ ((x << 2) & 0xfcfcfcfcu);
+#endif
   uint32_t r = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
+#if UGPU_XU_SWZ
     const uint32_t a = __builtin_amdgcn_perm(x, sw, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
+#else
+    const uint32_t a = __builtin_amdgcn_perm(nx, x, 0x0c0c0000u | (uint32_t)k << 8 | (uint32_t)(k + 1));
+#endif
 #if defined(UGPU_XU_ABL) && UGPU_XU_ABL == 1  // broadcast lookups: no bank conflicts (benchmarking; wrong counts)
     r |= (uint32_t)u.tab[a & 3u] << (8 * k);
 #elif defined(UGPU_XU_ABL) && UGPU_XU_ABL == 2  // no LDS lookups (benchmarking; wrong counts)
@@ -252,10 +266,17 @@ __device__ __forceinline__ void ucode_lane(const CU& u, const uint32_t w[4], uin
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t x = w[d];
+#if UGPU_XU_SWZ
     const uint32_t y = __builtin_amdgcn_alignbit(d < 3 ? w[d + 1] : nx, x, 8);
     const uint32_t sw = y ^ ((x << 2) & 0xfcfcfcfcu);
 #pragma unroll
     for (int k = 0; k < 4; ++k) a[4 * d + k] = __builtin_amdgcn_perm(x, sw, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
+#else
+    // (bytes k + 1 and k of the lane's stream, k + 1 = 4 being the next dword's first)
+    const uint32_t xn = d < 3 ? w[d + 1] : nx;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[4 * d + k] = __builtin_amdgcn_perm(xn, x, 0x0c0c0000u | (uint32_t)k << 8 | (uint32_t)(k + 1));
+#endif
   }
 #if UGPU_XU_PACK
   // (the four bytes of a dword packed by three v_lshl_or_b32 -- full-rate
@@ -295,7 +316,7 @@ __device__ __forceinline__ void ucode_lane(const CU& u, const uint32_t w[4], uin
 // the code of byte 0 of x (byte 1 of x follows it)
 __device__ __forceinline__ uint32_t ucode_b0(const CU& u, uint32_t x)
 {
-  const uint32_t a = ((x & 0xffu) << 8) | (((x >> 8) & 0xffu) ^ ((x << 2) & 0xfcu));
+  const uint32_t a = ((x & 0xffu) << 8) | (((x >> 8) & 0xffu) ^ xu_swz(x & 0xffu));
   return u.tab[a];
 }
 
@@ -984,11 +1005,11 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
   __shared__ __attribute__((aligned(16))) uint16_t bmst[BM ? kCWaves * 64 * kIt : 1];
   CU u;
   if constexpr (U) {
-    // the pair table: entry (x, y) at x << 8 | (y ^ (x << 2 & 0xfc))
+    // the pair table: entry (x, y) at x << 8 | (y ^ xu_swz(x))
     for (uint32_t i = threadIdx.x; i < 65536 / 4; i += kCWaves * 64) {
       uint32_t w = 0;
       for (uint32_t b = 0; b < 4; ++b) {
-        const uint32_t a = 4 * i + b, x = a >> 8, y = (a & 0xffu) ^ ((x << 2) & 0xfcu);
+        const uint32_t a = 4 * i + b, x = a >> 8, y = (a & 0xffu) ^ xu_swz(x);
         uint32_t e = x < 0x80   ? P.xu_tab[x]
                      : x < 0xc0 ? P.xu_tab[kXuCls + y]
                                 : P.xu_tab[256 + (x & 63) * 256 + y];
