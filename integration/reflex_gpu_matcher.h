@@ -491,23 +491,27 @@ class GpuMatcher : public Matcher {
     static Warm w;
     return w;
   }
-  // tab: the tables of the matcher that started the warm-up.  Once the devices
-  // are up, they are uploaded and the pooled resources of one stream per live
-  // matcher (ugrep: one per worker) are made on each device
-  // (ugpu_stream_reserve), so that the workers' first feeds do not all
-  // allocate device memory at once -- they serialise on it (VERDICT r4 item 6:
-  // ~100 ms per worker).  Meanwhile the CPU matchers answer (reason "warmup").
+  // tab: the tables of the matcher that started the warm-up.  With
+  // UGPU_ADAPTER_RESERVE, once the devices are up the tables are uploaded and
+  // the pooled resources of one stream per live matcher (ugrep: one per
+  // worker) are made on each device (ugpu_stream_reserve), so that the
+  // workers' first feeds allocate nothing.  Meanwhile the CPU matchers answer
+  // (reason "warmup").
   static void run_warm(Warm* w, std::shared_ptr<Tables> tab, size_t feed)
   {
     bool ok = GpuEngine::get().ok;  // (the device half loads here, on the warm-up thread)
     for (int d = 0; ok && d < devices(); ++d)
       ok = GpuEngine::get().warmup(d) == UGPU_OK;
-    // (UGPU_ADAPTER_RESERVE: 0 = no reserve, 2 = the devices count as ready
-    // before the reserve runs, so the workers' first feeds overlap it)
+    // UGPU_ADAPTER_RESERVE: 1 = reserve before the devices count as ready,
+    // 2 = after (the workers' first feeds overlap it), unset/0 = no reserve.
+    // Off by default: on ugrep -J16 over 16 files the serial reserve lengthens
+    // the warm-up by about as much as it saves the workers (C3 3.26x with it,
+    // 3.41x without, means of 4 and 2 runs; profiles/r05_ugrep_e2e.json).
+    // A long-running process with many inputs per worker is where it pays.
     const char* re = std::getenv("UGPU_ADAPTER_RESERVE");
     const bool late = re != NULL && *re == '2';
     ugpu_dfa* t = NULL;
-    if (ok && tab && !(re != NULL && *re == '0'))
+    if (ok && tab && re != NULL && (*re == '1' || *re == '2'))
     {
       std::lock_guard<std::mutex> lk(tab->mu);
       if (tab->d == NULL && !tab->failed)
