@@ -72,6 +72,12 @@ __device__ __forceinline__ uint32_t letters4(uint32_t x)
   return ((m >> 7) * 0x01020408u) >> 24;
 }
 
+// 16-bit mask of the ASCII letters among a lane's 16 bytes
+__device__ __forceinline__ uint32_t letters16(const uint4& v)
+{
+  return letters4(v.x) | (letters4(v.y) << 4) | (letters4(v.z) << 8) | (letters4(v.w) << 12);
+}
+
 // Wave-wide inclusive scans by DPP row shifts + row broadcasts (no LDS round
 // trip): row_shr 1,2,4,8 then row_bcast:15 (rows 1,3) and row_bcast:31 (rows 2,3).
 __device__ __forceinline__ uint32_t dpp_scan_add(uint32_t v)
@@ -598,6 +604,16 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
     X[3][2] = cand_flags(z, u);
     X[3][3] = cand_flags(u, e3);
   }
+  // no match starts right after a word character (P.wstart): the candidates
+  // that follow an ASCII letter in the lane's 16 bytes are dropped below (the
+  // first byte's predecessor is another lane's: it stays; a digit, '_' or a
+  // non-ASCII byte before a candidate keeps it too -- a superset).  The
+  // letter masks are taken here, so that the tile's bytes die early.
+  uint32_t lt01 = 0, lt23 = 0;
+  if (P.wstart) {
+    lt01 = letters16(v0) | (letters16(v1) << 16);
+    lt23 = letters16(v2) | (letters16(v3) << 16);
+  }
   const uint32_t any0 = X[0][0] | X[0][1] | X[0][2] | X[0][3], any1 = X[1][0] | X[1][1] | X[1][2] | X[1][3];
   const uint32_t any2 = X[2][0] | X[2][1] | X[2][2] | X[2][3], any3 = X[3][0] | X[3][1] | X[3][2] | X[3][3];
   // (tail: the tile holds the last two readable positions of a non-final range)
@@ -608,15 +624,7 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
   for (int k = 0; k < 4; ++k) {
     if (!tail && !__ballot(anyk[k] != 0)) continue;
     uint32_t mk = flags4(X[k][0]) | (flags4(X[k][1]) << 4) | (flags4(X[k][2]) << 8) | (flags4(X[k][3]) << 12);
-    if (P.wstart) {
-      // no match starts right after a word character: drop the candidates
-      // that follow an ASCII letter in the lane's 16 bytes (its first byte's
-      // predecessor is another lane's: it stays; a digit, '_' or a non-ASCII
-      // byte before a candidate keeps it too -- a superset)
-      const uint4& v = k == 0 ? v0 : k == 1 ? v1 : k == 2 ? v2 : v3;
-      const uint32_t lt = letters4(v.x) | (letters4(v.y) << 4) | (letters4(v.z) << 8) | (letters4(v.w) << 12);
-      mk &= ~(lt << 1);
-    }
+    if (P.wstart) mk &= ~(((k < 2 ? lt01 : lt23) >> (16 * (k & 1))) << 1) & 0xffffu;
     const uint64_t p0 = ts + 1024u * k + 16u * lane;
     if (!P.at_eof && p0 + 18 > P.rend && p0 < P.rend) {
       // the last two readable positions of a non-final range: their prefilter
