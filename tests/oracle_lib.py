@@ -51,6 +51,44 @@ def _load():
 L = _load()
 
 
+_DFA_CACHE = {}
+
+
+def oracle_dfa(opc):
+    """OracleDfa of opc, cached (tests build the same tables many times)."""
+    key = bytes(np.ascontiguousarray(np.asarray(opc, dtype=np.uint32)).tobytes())
+    d = _DFA_CACHE.get(key)
+    if d is None:
+        d = _DFA_CACHE[key] = OracleDfa(opc)
+    return d
+
+
+def range_totals(opc, host, lo, hi):
+    """(count, digest, dcap, exit) of the FIND chain entering at lo over the
+    whole of host, counting the matches that start before hi; exit is the end
+    of the last such match when it runs past hi, else hi.  (The scanners'
+    ugpu_scan(lo, hi) totals; numpy sums wrap mod 2**64 like the digests.)"""
+    o = oracle_dfa(opc)
+    if o.anchored:
+        _, _, _, lst = o.find(host, start=lo, want_list=True)
+        a = np.asarray(lst, dtype=np.uint64).reshape(-1, 3)
+        st, ln, cp = a[:, 0], a[:, 1], a[:, 2]
+    else:
+        st, ln, cp = o.find_arrays(host, start=lo)
+    k = int(np.searchsorted(st, np.uint64(hi), side="left"))
+    ex = hi
+    if not k:
+        return 0, 0, 0, ex
+    s, l, c = st[:k], ln[:k], cp[:k]
+    with np.errstate(over="ignore"):
+        dg = int((s * np.uint64(31) + l).sum(dtype=np.uint64))
+        dc = int(((s + np.uint64(1)) * c).sum(dtype=np.uint64))
+    end = int(s[-1]) + int(l[-1])
+    if end > hi:
+        ex = end
+    return k, dg, dc, ex
+
+
 class OracleDfa:
     def __init__(self, opc):
         self.opc = np.ascontiguousarray(np.asarray(opc, dtype=np.uint32))

@@ -116,18 +116,9 @@ def xc_restated(cls, cap, data, lo, hi, rend, at_eof):
 
 
 def _oracle_range(opc, host, lo, hi):
-    _, _, _, lst = OracleDfa(opc).find(host, start=lo, want_list=True)
-    cnt = dg = dc = 0
-    ex = hi
-    for s, ln, cap in lst:
-        if s >= hi:
-            break
-        cnt += 1
-        dg = (dg + 31 * s + ln) & M
-        dc = (dc + (s + 1) * cap) & M
-        if s + ln > hi:
-            ex = s + ln
-    return cnt, dg, dc, ex
+    """(count, digest, dcap, exit) of the chain entering at lo, matches starting before hi."""
+    from oracle_lib import range_totals
+    return range_totals(opc, host, lo, hi)
 
 
 def _inputs():

@@ -46,19 +46,8 @@ def _dev(arr):
 
 def _oracle_range(opc, host, lo, hi):
     """(count, digest, dcap, exit) of the chain entering at lo, matches starting before hi."""
-    from oracle_lib import OracleDfa
-    _, _, _, lst = OracleDfa(opc).find(host, start=lo, want_list=True)
-    cnt = dg = dc = 0
-    ex = hi
-    for s, ln, cap in lst:
-        if s >= hi:
-            break
-        cnt += 1
-        dg = (dg + 31 * s + ln) & M
-        dc = (dc + (s + 1) * cap) & M
-        if s + ln > hi:
-            ex = s + ln
-    return cnt, dg, dc, ex
+    from oracle_lib import range_totals
+    return range_totals(opc, host, lo, hi)
 
 
 def _scan(U, pat, t, lo, hi, n):

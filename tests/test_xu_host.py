@@ -73,20 +73,9 @@ def xu_restated(tab, bm3, cap, data, lo, hi, rend, at_eof):
 
 
 def _oracle_range(opc, host, lo, hi):
-    _, _, _, lst = OracleDfa(opc).find(host, start=lo, want_list=True)
-    cnt = dg = dc = 0
-    ex = hi
-    cap = 1
-    for s, ln, c in lst:
-        if s >= hi:
-            break
-        cap = c
-        cnt += 1
-        dg = (dg + 31 * s + ln) & M
-        dc = (dc + (s + 1) * c) & M
-        if s + ln > hi:
-            ex = s + ln
-    return cnt, dg, dc, ex
+    """(count, digest, dcap, exit) of the chain entering at lo, matches starting before hi."""
+    from oracle_lib import range_totals
+    return range_totals(opc, host, lo, hi)
 
 
 def _inputs():
