@@ -226,3 +226,44 @@ def test_gpu_w_identifiers_on_xc():
             assert (res.count, res.digest, res.dcap) == (cnt, dg, dc), (ch, border)
             assert res.triples() == lst, (ch, border)
             assert (lst[0][0] == border) == (ch != "\u00e9"), (ch, border, lst[:2])
+
+
+@pytest.mark.gpu
+def test_gpu_w_word_start_filter():
+    """Option W on prefiltered tables drops the candidates that follow an
+    ASCII letter (ScanParams::wstart, DESIGN 3.13).  Patterns whose first
+    bytes are letters, digits, '_' and non-word bytes, over text where they
+    follow letters, digits, '_', UTF-8 letters and separators, at lane and
+    chunk borders: equal to the oracle with the filter on and off
+    (UGPU_WSTART=0), whole buffers and OFFSETS."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import ugrep_amd as U
+    rng = np.random.default_rng(11)
+    toks = ["ing", "xing", "_ing", "9ing", "éing", "ing9", "sing", "-ing", "ing-", "ing_", "ingé", "a", " ", " ", "\n",
+            "-", "_", "é", "ж", "7", "walking", "sing ing", "in g"]
+    parts = [toks[int(i)] for i in rng.integers(0, len(toks), 400000)]
+    host = np.frombuffer("".join(parts).encode(), np.uint8).copy()
+    # planted at 16-byte lane and 1 KiB chunk borders
+    for p in range(1024 - 3, host.size - 8, 4096):
+        host[p:p + 5] = np.frombuffer(b"aing ", np.uint8)
+    for p in range(16 * 7 - 1, host.size - 8, 16 * 61):
+        host[p:p + 4] = np.frombuffer(b"ing ", np.uint8)
+    dev = torch.from_numpy(host).to("cuda")
+    torch.cuda.synchronize()
+    n_sparse = 0
+    for rx in ("[a-z]+ing", "ing", "-ing", "_ing|ing", "[0-9]ing", "ing|[a-z]ing", "é?ing"):
+        opc = U.compile_regex(rx)
+        want = OracleDfa(opc).find_w(host, want_list=True)
+        for ws in ("1", "0"):
+            os.environ["UGPU_WSTART"] = ws
+            try:
+                pat = U.Pattern(opc, word=True)
+                n_sparse += pat.info()["kernel"] == 0
+                res = U.find_all(pat, dev, offsets=True)
+            finally:
+                os.environ.pop("UGPU_WSTART", None)
+            assert (res.count, res.digest, res.dcap) == want[:3], (rx, ws)
+            assert res.triples() == want[3], (rx, ws)
+    assert n_sparse >= 6  # (the filter is sparse_kernel's)

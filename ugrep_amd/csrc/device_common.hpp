@@ -58,7 +58,20 @@ struct Win {
   uint32_t nul = 0;
   uint32_t cword = 0;  // word-boundary meta edges: 64 contexts (ctx_bits.hpp), Word ranges in wtab
   const uint32_t* amap = nullptr;  // cword: each state's row of acap (tables.hpp acap_map)
+  // an LDS copy of bytes [wa, wa + wn) that the W / context walks read instead
+  // of global memory (sparse_kernel's per-lane candidate window; wn = 0: none)
+  const uint8_t* wl = nullptr;
+  uint64_t wa = 0;
+  uint32_t wn = 0;
 };
+
+// the byte at k (< rend) for the W and context walks: from the LDS window when
+// it holds k, else from global memory
+__device__ __forceinline__ uint32_t wbyte(const struct Win& w, uint64_t k)
+{
+  const uint64_t o = k - w.wa;  // (below the window: wraps to a large value)
+  return o < w.wn ? (uint32_t)w.wl[o] : (uint32_t)w.g[k];
+}
 
 // Walk modes (template argument W of walk / chain_step / merge)
 constexpr int kWalkPlain = 0, kWalkWord = 1, kWalkCtx = 2;
@@ -92,7 +105,7 @@ __device__ __forceinline__ Win win_of(const ScanParams& P)
 // global memory; at and past the readable end they read as 0 (the reference
 // buffer's NUL terminator).  iswword = binary search over the Unicode 15.1
 // Word ranges (matcher.h:457-1192).
-__device__ __forceinline__ uint32_t wrd(const Win& w, uint64_t k) { return k < w.rend ? w.g[k] : 0u; }
+__device__ __forceinline__ uint32_t wrd(const Win& w, uint64_t k) { return k < w.rend ? wbyte(w, k) : 0u; }
 
 __device__ __forceinline__ bool wisword(const Win& w, uint32_t c)
 {
@@ -133,13 +146,13 @@ __device__ __forceinline__ bool walnum(uint32_t c) { return (c - '0' < 10u) || (
 __device__ __forceinline__ bool at_wb(const Win& w, uint64_t p)
 {
   if (p <= w.bob) return true;  // BOB
-  const uint32_t c = w.g[p - 1];
+  const uint32_t c = wbyte(w, p - 1);
   if (c == '\n') return true;
   if (c == '_') return false;
   if ((c & 0xC0) == 0x80) {
     uint64_t k = p - 1;
-    if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
-      if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
+    if (k > w.bob && (wbyte(w, --k) & 0xC0) == 0x80)
+      if (k > w.bob && (wbyte(w, --k) & 0xC0) == 0x80)
         if (k > w.bob) --k;
     return !wisword(w, wutf8(w, k));
   }
@@ -153,7 +166,7 @@ __device__ __forceinline__ bool at_we(const Win& w, uint64_t q, uint32_t& ovf)
     if (!w.eof) ovf = 1;
     return true;
   }
-  const uint32_t c = w.g[q];
+  const uint32_t c = wbyte(w, q);
   if (c == '_') return false;
   if ((c & 0xC0) == 0xC0) {
     // the code point after the match decides; when its bytes run past a readable
@@ -179,14 +192,14 @@ __device__ __forceinline__ uint32_t at_eol(const Win& w, uint64_t q, uint32_t& o
     if (!w.eof) ovf = 1;
     return 1u;
   }
-  const uint32_t c = w.g[q];
+  const uint32_t c = wbyte(w, q);
   if (c == '\n') return 1u;
   if (c != '\r') return 0u;
   if (q + 1 >= w.rend) {
     if (!w.eof) ovf = 1;
     return 0u;
   }
-  return w.g[q + 1] == '\n' ? 1u : 0u;
+  return wbyte(w, q + 1) == '\n' ? 1u : 0u;
 }
 
 // Word-boundary meta edges (META_WBB .. META_EWE, include/reflex/pattern.h:
@@ -214,14 +227,14 @@ __device__ __forceinline__ bool at_bw(const Win& w, uint64_t p, uint32_t& ovf)
 __device__ __forceinline__ bool at_ew(const Win& w, uint64_t q)
 {
   if (q <= w.bob) return false;
-  const uint32_t c = w.g[q - 1];
+  const uint32_t c = wbyte(w, q - 1);
   if (c == '\n') return false;
   if (c == '_') return true;
   if ((c & 0xC0) == 0x80 && q - w.bob >= 2) {
     // back over at most two more continuation bytes to the lead byte
     uint64_t k = q - 2;
-    if ((w.g[k] & 0xC0) == 0x80)
-      if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
+    if ((wbyte(w, k) & 0xC0) == 0x80)
+      if (k > w.bob && (wbyte(w, --k) & 0xC0) == 0x80)
         if (k > w.bob) --k;
     return wisword(w, wutf8(w, k));
   }
@@ -238,7 +251,7 @@ __device__ __forceinline__ bool at_we_meta(const Win& w, uint64_t q, uint32_t& o
     if (!w.eof) ovf = 1;
     return true;
   }
-  const uint32_t c = w.g[q];
+  const uint32_t c = wbyte(w, q);
   if (c == '_') return false;
   if ((c & 0xC0) == 0xC0) {
     if (q + 5 > w.rend && !w.eof) ovf = 1;
@@ -254,8 +267,8 @@ __device__ __forceinline__ bool at_we_meta(const Win& w, uint64_t q, uint32_t& o
 __device__ __forceinline__ bool at_wb_cur(const Win& w, uint64_t cur)
 {
   uint64_t k = cur - 1;
-  if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
-    if (k > w.bob && (w.g[--k] & 0xC0) == 0x80)
+  if (k > w.bob && (wbyte(w, --k) & 0xC0) == 0x80)
+    if (k > w.bob && (wbyte(w, --k) & 0xC0) == 0x80)
       if (k > w.bob) --k;
   return !wisword(w, wutf8(w, k));
 }
@@ -264,7 +277,7 @@ __device__ __forceinline__ bool at_wb_cur(const Win& w, uint64_t cur)
 // line contexts bol << 1; word contexts CTX_BOL | CTX_WB | CTX_BW
 __device__ __forceinline__ uint32_t ctx_walk_bits(const Win& w, uint64_t p, uint32_t& ovf)
 {
-  const uint32_t bol = p <= w.bob ? w.bol0 : (w.g[p - 1] == '\n' ? 1u : 0u);
+  const uint32_t bol = p <= w.bob ? w.bol0 : (wbyte(w, p - 1) == '\n' ? 1u : 0u);
   if (!w.cword) return bol << 1;
   return (bol ? CTX_BOL : 0u) | (at_wb(w, p) ? CTX_WB : 0u) | (at_bw(w, p, ovf) ? CTX_BW : 0u);
 }
@@ -299,10 +312,10 @@ __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64
   if constexpr (W == kWalkCtx) {
     uint32_t bol = ctx_walk_bits(w, p, ovf);
     // (a continuation byte before p: at_wb follows the last accept, at_wb_cur)
-    const bool wbc = w.cword && p > w.bob && (w.g[p - 1] & 0xC0) == 0x80;
+    const bool wbc = w.cword && p > w.bob && (wbyte(w, p - 1) & 0xC0) == 0x80;
     le = ctx_accept(w, s, bol, q, ovf);
     while (q < w.rend) {
-      const uint32_t e = T.step(s, w.g[q]);
+      const uint32_t e = T.step(s, wbyte(w, q));
       if (e == 0) return last - p;
       s = e;
       ++q;
@@ -321,7 +334,7 @@ __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64
   if constexpr (W == kWalkWord) {
     if (!at_wb(w, p)) return 0;
     while (q < w.rend) {
-      const uint32_t e = T.step(s, w.g[q]);
+      const uint32_t e = T.step(s, wbyte(w, q));
       if (e == 0) return last - p;
       s = e;
       ++q;

@@ -466,7 +466,8 @@ __device__ __forceinline__ void batch_finish(BatchLane& L, int lane, uint8_t* sc
 // bounds every walk: the wave's range end when walks are truncated (P.open),
 // else the readable end.  Option W (W = kWalkWord) and tables whose accepts
 // depend on the context (W = kWalkCtx: word boundaries, line anchors) keep
-// per-lane walks through global memory (walk<0, W>).
+// per-lane walks (walk<0, W>): option W's read the lane's window and, around
+// it, global memory; the context walks read global memory.
 template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false>
 __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr, uint32_t dn, int lane, const Tab<0>& T,
                                             const Ctx& C, const ScanParams& P, WaveChain& w, uint64_t lim,
@@ -491,7 +492,17 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
       // state (ctx_accept).  Either way the candidates stay a superset (W and
       // the contexts only remove matches, the first bytes are the table's),
       // so the prefilter is unchanged.
-      const Win win = win_of(P);
+      // (option W: the walk reads its lane's 32-byte LDS window [a, a + 32)
+      // where it can, global memory around it -- -w '[a-z]+ing' 54.6 -> 45.1
+      // ms per 16 GiB.  The context walks keep global memory: with the window
+      // their kernel spills 66 instead of 36 VGPRs, and \bfoo\b, whose time
+      // is the main loop's, went 2.57 -> 2.84 ms; profiles/r05_sparse_walks_ab.json)
+      Win win = win_of(P);
+      if constexpr (W == kWalkWord) {
+        win.wl = scr + 32 * lane;
+        win.wa = a;
+        win.wn = 32;
+      }
       len = walk<0, W>(T, win, c, le, w.ovf);
     }
     resolve<WRITE, STAGE>(valid, c, len, le, lane, C, P, w);
