@@ -30,6 +30,8 @@ __device__ __forceinline__ uint32_t op(uint32_t a, uint32_t b)
   if constexpr (K == 16) { uint32_t r; asm volatile("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
   if constexpr (K == 17) { uint32_t r; asm volatile("v_or3_b32 %0, %1, %2, %1" : "=v"(r) : "v"(a), "v"(b)); return r; }
   if constexpr (K == 18) { uint32_t r; asm volatile("v_lshlrev_b32 %0, 3, %1" : "=v"(r) : "v"(a)); return r ^ b; }
+  if constexpr (K == 19) { uint32_t r; asm volatile("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(256u), "v"(b)); return r; }
+  if constexpr (K == 20) { uint32_t r; asm volatile("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
   return a;
 }
 
@@ -108,6 +110,8 @@ int main()
     run<16>("lshl_or(asm)", w);
     run<17>("or3(asm)", w);
     run<18>("lshl+xor", w);
+    run<19>("mad_u24(asm)", w);
+    run<20>("mul_u24(asm)", w);
   }
   return 0;
 }
