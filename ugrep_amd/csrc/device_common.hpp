@@ -58,6 +58,8 @@ struct Win {
   uint32_t nul = 0;
   uint32_t cword = 0;  // word-boundary meta edges: 64 contexts (ctx_bits.hpp), Word ranges in wtab
   const uint32_t* amap = nullptr;  // cword: each state's row of acap (tables.hpp acap_map)
+  // loop-needle tables (ScanParams::lb_cls): the 256-bit set C of C+ N
+  const uint32_t* lb = nullptr;
   // an LDS copy of bytes [wa, wa + wn) that the W / context walks read instead
   // of global memory (sparse_kernel's per-lane candidate window; wn = 0: none)
   const uint8_t* wl = nullptr;
@@ -95,6 +97,7 @@ __device__ __forceinline__ Win win_of(const ScanParams& P)
   w.nul = P.nul;
   w.cword = P.ctx_word;
   w.amap = P.amap;
+  w.lb = P.lb_cls;
   return w;
 }
 
@@ -425,15 +428,27 @@ struct WriteEm {
 // `sign`, then the chain continues at its end) or p+1.
 // Mode kWalkCtx with option N: an empty match at p is reported (the chain
 // still moves to p+1, lib/matcher.cpp:682-728).
+// Loop-needle tables (w.lb) and cap != 0: a failed walk from a byte of C
+// means no needle in the rest of its C-run, so no position of the run starts
+// a match: the chain skips to the run's end (at most to cap), which keeps the
+// serial re-walks of fix_kernel linear over long runs without a needle.
 template <int FMT, class Em, int W = kWalkPlain>
 __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t p, Em& em,
-                                               int sign, uint32_t& ovf)
+                                               int sign, uint32_t& ovf, uint64_t cap = 0)
 {
   uint32_t le;
   const uint64_t len = walk<FMT, W>(T, w, p, le, ovf);
   if (len) {
     em.put(c, p, len, le, sign);
     return p + len;
+  }
+  if constexpr (W != kWalkCtx) {
+    auto in_c = [&w](uint32_t b) { return (w.lb[b >> 5] >> (b & 31)) & 1u; };
+    if (cap && w.lb && p < w.rend && in_c(w.g[p])) {
+      uint64_t q = p + 1;
+      while (q < cap && q < w.rend && in_c(w.g[q])) ++q;
+      return q;
+    }
   }
   if constexpr (W == kWalkCtx) {
     if (le && w.nul) em.put(c, p, 0, le, sign);
@@ -463,9 +478,9 @@ __device__ __forceinline__ bool merge(const Tab<FMT>& T, const Win& w, const Ctx
       return false;
     }
     if (po < pn)
-      po = chain_step<FMT, CountEm, W>(T, w, c, po, em, -1, ovf);
+      po = chain_step<FMT, CountEm, W>(T, w, c, po, em, -1, ovf, e);
     else
-      pn = chain_step<FMT, CountEm, W>(T, w, c, pn, em, +1, ovf);
+      pn = chain_step<FMT, CountEm, W>(T, w, c, pn, em, +1, ovf, e);
   }
 }
 

@@ -92,6 +92,11 @@ struct ugpu_dfa {
   uint32_t* d_acap = nullptr;  // acap, or (word boundaries) acap_rows then acap_map
   // no match starts right after a word character (ScanParams::wstart)
   bool wstart = false;
+  // loop-needle tables (C+N, ScanParams::lb): the prefilter finds N, and each
+  // candidate walks back to its C-run's start (loop_needle below)
+  bool lb = false;
+  uint8_t lb_ft[20] = {};
+  uint32_t* d_lbcls = nullptr;  // 256-bit mask of C
   // idle scanners of ugpu_find_all calls on this table (reused: creating one
   // costs device allocations and property queries)
   std::mutex pool_mu;
@@ -282,9 +287,12 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   // resynchronising (two chains of a resynchronising table meet within a match
   // or two; longer merges go to the forest FIND)
   P.merge_budget = env_u64("UGPU_MERGE_BUDGET", 4096);
+  const uint8_t* ft = d->lb ? d->lb_ft : d->t.ft;
   for (int i = 0; i < 5; ++i)
-    P.ft[i] = (uint32_t)d->t.ft[4 * i] | ((uint32_t)d->t.ft[4 * i + 1] << 8) | ((uint32_t)d->t.ft[4 * i + 2] << 16) |
-              ((uint32_t)d->t.ft[4 * i + 3] << 24);
+    P.ft[i] = (uint32_t)ft[4 * i] | ((uint32_t)ft[4 * i + 1] << 8) | ((uint32_t)ft[4 * i + 2] << 16) |
+              ((uint32_t)ft[4 * i + 3] << 24);
+  P.lb_cls = d->lb ? d->d_lbcls : nullptr;
+  if (d->lb) P.wstart = 0;  // (the candidates are needle positions, not match starts)
 }
 
 // Translate a byte range of dbuf into the 16-byte aligned base coordinates
@@ -484,6 +492,25 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     }
     d->wstart = !any && !d->t.acap.empty();
   }
+  const uint32_t* lbcls = pl.lb_cls;
+  const std::string& needle = pl.lb_needle;
+  if (pl.lb) {
+    // the needle's first three bytes, one per prefilter set, group 0 (tables.hpp
+    // ft: bit 2 s + g of T0[b & 7], T1[(b >> 3) & 7], T2[b >> 6]); group 1 empty
+    d->lb = true;
+    for (int s3 = 0; s3 < 3; ++s3) {
+      const uint8_t bit = (uint8_t)(1u << (2 * s3));
+      if (s3 >= (int)needle.size()) {
+        for (int v = 0; v < 8; ++v) d->lb_ft[v] |= bit, d->lb_ft[8 + v] |= bit;
+        for (int v = 0; v < 4; ++v) d->lb_ft[16 + v] |= bit;
+        continue;
+      }
+      const uint32_t b = (unsigned char)needle[s3];
+      d->lb_ft[b & 7] |= bit;
+      d->lb_ft[8 + ((b >> 3) & 7)] |= bit;
+      d->lb_ft[16 + (b >> 6)] |= bit;
+    }
+  }
   const size_t n = d->t.trans.size();
   d->ntrans_pad = (uint32_t)((n + 7) & ~size_t(7));
   std::vector<uint16_t> tr(d->ntrans_pad, 0);
@@ -498,6 +525,11 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       (e = hipMemcpy(d->d_caps, d->t.caps.data(), d->t.caps.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
     ugpu_dfa_destroy(d);
     return hip_fail(e, "table upload");
+  }
+  if (d->lb && ((e = hipMalloc(&d->d_lbcls, 32)) != hipSuccess ||
+                (e = hipMemcpy(d->d_lbcls, lbcls, 32, hipMemcpyHostToDevice)) != hipSuccess)) {
+    ugpu_dfa_destroy(d);
+    return hip_fail(e, "loop class upload");
   }
   if (d->t.format == FMT_WIDE &&
       ((e = hipMalloc(&d->d_trans32, d->t.trans32.size() * 4)) != hipSuccess ||
@@ -596,6 +628,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   if (d->d_cls) (void)hipFree(d->d_cls);
   if (d->d_caps) (void)hipFree(d->d_caps);
   if (d->d_acap) (void)hipFree(d->d_acap);
+  if (d->d_lbcls) (void)hipFree(d->d_lbcls);
   delete d;
   return UGPU_OK;
 }
@@ -604,6 +637,8 @@ int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
 {
   if (!d || !info) return fail(UGPU_INVAL, "NULL argument");
   dfa_info_fill(d->t, dfa_plan(d->t, d->pflags), info);
+  // (the lookback the tables were uploaded with, whatever UGPU_LB says now)
+  info->shape = (info->shape & ~UGPU_SHAPE_LOOP_NEEDLE) | (d->lb ? UGPU_SHAPE_LOOP_NEEDLE : 0u);
   return UGPU_OK;
 }
 

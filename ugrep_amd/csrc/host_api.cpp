@@ -40,6 +40,92 @@ bool is_word_plus(const DfaTables& t)
   return ok && tables_equivalent(t, wp);
 }
 
+// Loop-needle tables: the language is C+ N for a byte set C and a string N
+// of >= 2 bytes of C (e.g. [a-z]+ing).  Then every FIND match is a whole C-run
+// prefix: it starts at a C-run's first byte (or at the scan start, inside a
+// run) and ends at the end of the run's last N -- after which no position of
+// the run starts a match -- so the chain enters every run at its start, and
+// a run holds a match iff N occurs in it after its first byte.  The sparse
+// kernel's prefilter then looks for N (3 bytes) instead of the first bytes
+// (here, common ones), and each candidate walks back over C to its run's
+// start (the reference's lookback, lib/matcher.cpp:636-656 lbk_ / cbk_,
+// restated for the FIND chain).  Recognised on the DFA: C = the start state's
+// live bytes, c N = the shortest accepted word, then the table must be
+// equivalent to the KMP automaton of C+ N (product walk over bytes).
+bool loop_needle(const DfaTables& t, uint32_t cls[8], std::string& needle)
+{
+  if (t.format != FMT_BYTE || t.anchored || t.redo || t.cap1 == 0 || t.start >= t.accb || t.row != 256) return false;
+  const uint32_t R = t.row;
+  for (int i = 0; i < 8; ++i) cls[i] = 0;
+  for (uint32_t b = 0; b < 256; ++b)
+    if (t.trans[t.start + b]) cls[b >> 5] |= 1u << (b & 31);
+  auto inC = [&](uint32_t b) { return (cls[b >> 5] >> (b & 31)) & 1u; };
+  // the shortest accepted word (BFS over entries, bytes in order)
+  const uint32_t S = t.states;
+  std::vector<int32_t> par(S, -1);
+  std::vector<uint8_t> pb(S, 0);
+  std::vector<uint32_t> q{t.start / R};
+  par[t.start / R] = (int32_t)(t.start / R);
+  uint32_t hit = ~0u;
+  for (size_t qi = 0; qi < q.size() && hit == ~0u; ++qi) {
+    const uint32_t s = q[qi];
+    for (uint32_t b = 0; b < 256 && hit == ~0u; ++b) {
+      const uint32_t e = t.trans[(size_t)s * R + b];
+      if (!e) continue;
+      const uint32_t s2 = e / R;
+      if (par[s2] >= 0) continue;
+      par[s2] = (int32_t)s;
+      pb[s2] = (uint8_t)b;
+      if (e >= t.accb) hit = s2;
+      q.push_back(s2);
+    }
+  }
+  if (hit == ~0u) return false;
+  std::string w;
+  for (uint32_t s = hit; s != t.start / R; s = (uint32_t)par[s]) w.insert(w.begin(), (char)pb[s]);
+  if (w.size() < 3 || w.size() > 64) return false;
+  needle = w.substr(1);
+  const uint32_t m = (uint32_t)needle.size();
+  for (unsigned char c : needle)
+    if (!inC(c)) return false;
+  // KMP over the needle: the longest prefix of N that is a suffix of
+  // N[0, k) + b; state m (matched) continues like the failure of m
+  std::vector<uint32_t> fail(m + 1, 0);
+  for (uint32_t i = 1, k = 0; i < m; ++i) {
+    while (k && needle[i] != needle[k]) k = fail[k];
+    if (needle[i] == needle[k]) ++k;
+    fail[i + 1] = k;
+  }
+  auto delta = [&](uint32_t k, uint32_t b) {
+    if (k == m) k = fail[m];
+    while (k && (unsigned char)needle[k] != b) k = fail[k];
+    return (unsigned char)needle[k] == b ? k + 1 : 0u;
+  };
+  // product walk: (table entry, automaton state), automaton state m + 1 = start
+  const uint32_t K0 = m + 1;
+  std::vector<uint8_t> seen((size_t)S * (m + 2), 0);
+  std::vector<std::pair<uint32_t, uint32_t>> st{{t.start, K0}};
+  seen[(size_t)(t.start / R) * (m + 2) + K0] = 1;
+  while (!st.empty()) {
+    const auto [e, k] = st.back();
+    st.pop_back();
+    for (uint32_t b = 0; b < 256; ++b) {
+      const uint32_t e2 = t.trans[e + b];
+      const bool alive = inC(b) != 0;
+      if (!e2 != !alive) return false;  // one side dead, the other not
+      if (!e2) continue;
+      const uint32_t k2 = k == K0 ? 0u : delta(k, b);
+      if ((e2 >= t.accb) != (k2 == m)) return false;
+      uint8_t& v = seen[(size_t)(e2 / R) * (m + 2) + k2];
+      if (!v) {
+        v = 1;
+        st.push_back({e2, k2});
+      }
+    }
+  }
+  return true;
+}
+
 DfaPlan dfa_plan(const DfaTables& t, uint32_t flags)
 {
   DfaPlan p;
@@ -55,6 +141,16 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags)
   if (p.amode) {
     p.ok = !(flags & UGPU_PAT_WORD);
     return p;
+  }
+  // loop-needle tables on the sparse kernel; under option W the run bytes must
+  // be word bytes (then no match starts inside a run: at_wb fails there)
+  const char* lenv = std::getenv("UGPU_LB");
+  if (t.filter && t.format == FMT_BYTE && !(lenv && lenv[0] == '0') && loop_needle(t, p.lb_cls, p.lb_needle)) {
+    p.lb = true;
+    if (flags & UGPU_PAT_WORD)
+      for (uint32_t b = 0; b < 256 && p.lb; ++b)
+        if ((p.lb_cls[b >> 5] >> (b & 31)) & 1u)
+          p.lb = (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_';
   }
   if (flags & UGPU_PAT_WORD) {
     p.wtab = true;
@@ -84,7 +180,7 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* out)
   info->accepting = t.accepting;
   info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;
   info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u) |
-                (t.cap1 != 0 && !t.anchored ? UGPU_SHAPE_ONE_ACCEPT : 0u);
+                (t.cap1 != 0 && !t.anchored ? UGPU_SHAPE_ONE_ACCEPT : 0u) | (p.lb ? UGPU_SHAPE_LOOP_NEEDLE : 0u);
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
   const char* cenv = std::getenv("UGPU_XC");

@@ -28,6 +28,11 @@ struct DfaPlan {
   bool nul = false, amode = false;
   bool wtab = false, wplus = false, xcw = false;
   bool xtrans = false, xid = false, xu = false, xg = false;
+  // loop-needle table (C+ N, host_api.cpp loop_needle): the sparse kernel's
+  // prefilter looks for N and its candidates walk back to their C-run's start
+  bool lb = false;
+  uint32_t lb_cls[8] = {};
+  std::string lb_needle;
 };
 
 DfaPlan dfa_plan(const DfaTables& t, uint32_t flags);

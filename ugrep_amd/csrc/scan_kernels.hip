@@ -187,7 +187,7 @@ __device__ __forceinline__ void resolve_open(const ScanParams& P, const Tab<FMT>
         over = 1;
         break;
       }
-      p = chain_step<FMT, CountEm>(T, w, C, p, d, +1, ovf);
+      p = chain_step<FMT, CountEm>(T, w, C, p, d, +1, ovf, bhi);
     }
     exi[b] = p;
     rec_add(P, (uint64_t)b, d.cnt, d.dg, d.dc);

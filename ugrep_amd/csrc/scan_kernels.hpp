@@ -214,6 +214,10 @@ struct ScanParams {
   // at the match begin, lib/matcher.cpp:107; or a table whose every accept
   // needs CTX_WB), so candidates right after an ASCII letter are dropped
   uint32_t wstart;
+  // sparse_kernel, loop-needle tables (engine.hip loop_needle): the prefilter
+  // (ft) finds the needle N; each candidate walks back over the bytes of C
+  // (256-bit mask) to its run's start.  NULL: ft finds first bytes.
+  const uint32_t* lb_cls;
   uint32_t bol0;
   uint32_t nul;
   uint32_t ctx_word;

@@ -174,6 +174,10 @@ struct WaveChain {
   // the position the tile loop resumes from (earlier candidates are consumed)
   uint32_t pend;
   uint64_t rs, ptile;  // (ptile: start of the tile the wave suspended in)
+  // loop-needle tables (lb_batch): the range start, the last list entry's
+  // position and run start
+  uint64_t wlo;
+  uint64_t lbr, lbs;
 };
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
@@ -455,6 +459,81 @@ __device__ __forceinline__ void batch_finish(BatchLane& L, int lane, uint8_t* sc
   wave_lds_sync();  // the aux region is reused
 }
 
+// Loop-needle tables (ScanParams::lb_cls, host_api.cpp loop_needle).  A list
+// entry is a needle position, or (kLbStart set) a run start already: the
+// wave's range start inside a run, and the run that reaches its range end.
+constexpr uint64_t kLbStart = 1ull << 63;
+__device__ __forceinline__ bool lb_in(const ScanParams& P, uint32_t b) { return (P.lb_cls[b >> 5] >> (b & 31)) & 1u; }
+
+// The whole wave walks back from position pl (exclusive) over bytes of C, 64
+// a step, not below bl: the start of the C-run that ends at pl (bl when the
+// run reaches it)
+__device__ __forceinline__ uint64_t lb_back_wave(const ScanParams& P, uint64_t pl, uint64_t bl, int lane)
+{
+  while (pl > bl) {
+    const bool inr = (uint64_t)lane < pl - bl;
+    const uint32_t b = inr ? (uint32_t)P.g[pl - 1 - lane] : 0u;
+    const uint64_t stop = __ballot(inr && !lb_in(P, b));
+    if (stop) return pl - (uint64_t)__builtin_ctzll(stop);
+    if (pl - bl <= 64) return bl;
+    pl -= 64;
+  }
+  return pl;
+}
+
+// The run starts of a batch of list entries (one per lane): each needle walks
+// back over C to the previous entry (at most 64 bytes alone, then with the
+// whole wave), so the walks of a batch cover the bytes between its entries
+// once; a needle that reaches the previous entry is in its run.  Run starts
+// never decrease along the list, so a max-scan hands each lane the start of
+// the nearest entry on its left that found one (or the wave's carried run).
+// A run begun before the wave's range starts at the range start: the wave's
+// chain is FIND from there, as every kernel's speculative chain (fix_kernel
+// stitches the true entries; the previous wave's range-end run converges with
+// it within a few bytes).
+__device__ __forceinline__ uint64_t lb_batch(const ScanParams& P, uint64_t e, bool listed, int lane, uint32_t dn,
+                                             WaveChain& w)
+{
+  const bool fixed = listed && (e >> 63) != 0;
+  const uint64_t n = listed ? (e & ~kLbStart) : w.lbr;
+  // the previous entry's position (lane 0: the last entry of the previous batch)
+  const uint32_t plo = (uint32_t)__shfl_up((int)(uint32_t)n, 1, 64);
+  const uint32_t phi = (uint32_t)__shfl_up((int)(uint32_t)(n >> 32), 1, 64);
+  uint64_t bound = lane == 0 ? w.lbr : (((uint64_t)phi << 32) | plo);
+  if (bound < w.wlo) bound = w.wlo;
+  if (bound > n) bound = n;
+  uint64_t p = n;
+  uint32_t steps = 0;
+  if (listed && !fixed)
+    while (p > bound && steps < 64 && lb_in(P, P.g[p - 1])) {
+      --p;
+      ++steps;
+    }
+  const bool longl = listed && !fixed && p > bound && lb_in(P, P.g[p - 1]);
+  for (uint64_t lm = __ballot(longl); lm; lm &= lm - 1) {
+    const int L = __builtin_ctzll(lm);
+    const uint64_t r = lb_back_wave(P, readlane64(p, L), readlane64(bound, L), lane);
+    if (lane == L) p = r;
+  }
+  // found: a run start of its own (a non-C byte before p, or a fixed entry)
+  const bool found = fixed || (listed && p > bound) || (listed && p == bound && bound == w.wlo);
+  uint64_t st = found ? p : 0;
+  // inclusive max-scan over the wave (64-bit, as two 32-bit halves ordered by the high one)
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t lo2 = (uint32_t)__shfl_up((int)(uint32_t)st, d, 64);
+    const uint32_t hi2 = (uint32_t)__shfl_up((int)(uint32_t)(st >> 32), d, 64);
+    const uint64_t o = ((uint64_t)hi2 << 32) | lo2;
+    if (lane >= d && o > st) st = o;
+  }
+  if (w.lbs > st) st = w.lbs;
+  // carry: the batch's last entry and its run
+  const int last = (int)dn - 1;
+  w.lbr = readlane64(n, last);
+  w.lbs = readlane64(st, last);
+  return st;
+}
+
 // Walk the deferred candidates (one per lane) and resolve them.  Each lane
 // copies the 32 bytes from c & ~15 into its LDS window (the tiles are gone
 // from registers) and walks its candidate there.  A walk still alive at the
@@ -468,14 +547,17 @@ __device__ __forceinline__ void batch_finish(BatchLane& L, int lane, uint8_t* sc
 // depend on the context (W = kWalkCtx: word boundaries, line anchors) keep
 // per-lane walks (walk<0, W>): option W's read the lane's window and, around
 // it, global memory; the context walks read global memory.
-template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false>
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false, bool LB = false>
 __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr, uint32_t dn, int lane, const Tab<0>& T,
                                             const Ctx& C, const ScanParams& P, WaveChain& w, uint64_t lim,
                                             uint64_t gw)
 {
   wave_lds_sync();
-  const bool valid = (uint32_t)lane < dn;
-  const uint64_t c = valid ? dl[lane] : 0;
+  const bool listed = (uint32_t)lane < dn;
+  const uint64_t craw = listed ? dl[lane] : 0;
+  bool valid = listed;
+  uint64_t c = craw;
+  if constexpr (LB) c = lb_batch(P, craw, listed, lane, dn, w);
   const uint64_t last16 = (P.rend - 1) & ~uint64_t(15);
   const uint64_t a = c & ~uint64_t(15);
   const uint4 v0 = load16(P.g, a, last16), v1 = load16(P.g, a + 16, last16);
@@ -549,7 +631,7 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
     ps.pad = 0;
     P.srec[gw].lanes[lane] = ps;
     w.pend = 1;
-    w.rs = readlane64(c, (int)dn - 1) + 1;  // the batch's candidates are consumed
+    w.rs = readlane64(LB ? craw & ~kLbStart : craw, (int)dn - 1) + 1;  // the batch's candidates are consumed (list positions)
   }
 }
 
@@ -560,7 +642,7 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
 // by the wave's range [wlo, whi).
 // ABL (benchmarking only; results are not matches): 1 loads alone, 2 loads +
 // prefilter, 3 everything but the walks.
-template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false>
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false, bool LB = false>
 __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3,
                                           uint64_t ts, bool edge, uint64_t wlo, uint64_t whi, int lane,
                                           const FTab& F, const Tab<0>& T, const Ctx& C, const ScanParams& P,
@@ -672,7 +754,7 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
     const uint32_t rank = incl - cnt;
     for (uint32_t done = 0; done < tot;) {
       if (w.dn == (uint32_t)kDefer) {
-        flush_deferred<WRITE, ABL, W, STAGE, RESUME>(dl, scr, w.dn, lane, T, C, P, w, lim, gw);
+        flush_deferred<WRITE, ABL, W, STAGE, RESUME, LB>(dl, scr, w.dn, lane, T, C, P, w, lim, gw);
         w.dn = 0;
         if (!RESUME && w.pend) {  // the wave suspends (the resume launch repeats this tile)
           w.ptile = ts;
@@ -707,7 +789,7 @@ __device__ __forceinline__ TileLoad wave_tile(const uint8_t* wbase, uint32_t i, 
 
 }  // namespace
 
-template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false>
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false, bool LB = false>
 __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -757,6 +839,8 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
   w.le1 = 0;
   w.pend = 0;
   w.rs = w.ptile = 0;
+  w.wlo = wlo;
+  w.lbr = w.lbs = wlo;
   // walk limit: with truncation (P.open) a walk still alive at the range end
   // of any wave but the last becomes the wave's open walk (fix_kernel); the
   // last wave's walks run to the readable end, as the range's exit needs
@@ -810,6 +894,15 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
                 (ps.packed >> 24) != 0};
     batch_finish<WRITE, STAGE>(L, lane, scr, T, C, P, w, lim, gw);
   }
+  if constexpr (!RESUME && W != kWalkCtx) {
+    // loop-needle tables: the range start inside a C-run is a candidate of its
+    // own (the chain from there may match; no needle before it says so)
+    if (LB && whi > wlo && lb_in(P, P.g[wlo])) {
+      if (lane == 0) dl[0] = wlo | kLbStart;
+      wave_lds_sync();
+      w.dn = 1;
+    }
+  }
   uint4 a0, a1, a2, a3, b0, b1, b2, b3;
   {
     const TileLoad La = wave_tile(wbase, i, rel);
@@ -828,7 +921,7 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
   // rest of its range without processing it); an odd last tile follows
   if (n >= i + 2) {
     do {
-      tile_pass<WRITE, ABL, W, STAGE, RESUME>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, i == 0 && clip_lo, wlo, whi,
+      tile_pass<WRITE, ABL, W, STAGE, RESUME, LB>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile, i == 0 && clip_lo, wlo, whi,
                                               lane, F, T, C, P, dl, scr, w, lim, gw);
       {
         const TileLoad L = wave_tile(wbase, i + 2, rel);
@@ -837,7 +930,7 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
         a2 = stream16(L, lo16 + 2048);
         a3 = stream16(L, lo16 + 3072);
       }
-      tile_pass<WRITE, ABL, W, STAGE, RESUME>(b0, b1, b2, b3, wb + (uint64_t)(i + 1) * kWaveTile, i + 2 == n && clip_hi,
+      tile_pass<WRITE, ABL, W, STAGE, RESUME, LB>(b0, b1, b2, b3, wb + (uint64_t)(i + 1) * kWaveTile, i + 2 == n && clip_hi,
                                               wlo, whi, lane, F, T, C, P, dl, scr, w, lim, gw);
       {
         const TileLoad L = wave_tile(wbase, i + 3, rel);
@@ -850,11 +943,30 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
     } while (i + 1 < n);
   }
   if (i < n)  // a* holds tile i = n - 1
-    tile_pass<WRITE, ABL, W, STAGE, RESUME>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile,
+    tile_pass<WRITE, ABL, W, STAGE, RESUME, LB>(a0, a1, a2, a3, wb + (uint64_t)i * kWaveTile,
                                             (i == 0 && clip_lo) || clip_hi, wlo, whi, lane, F, T, C, P, dl, scr, w,
                                             lim, gw);
+  if constexpr (LB) {
+    // loop-needle tables: the C-run that reaches the range end is this wave's
+    // candidate (its needles may all lie in the next waves' ranges)
+    if (!w.pend && whi > wlo && lb_in(P, P.g[whi - 1])) {
+      const uint64_t r = lb_back_wave(P, whi, wlo, lane);
+      {
+        if (w.dn == (uint32_t)kDefer) {
+          flush_deferred<WRITE, ABL, W, STAGE, RESUME, LB>(dl, scr, w.dn, lane, T, C, P, w, lim, gw);
+          w.dn = 0;
+        }
+        if (!w.pend) {
+          wave_lds_sync();
+          if (lane == 0) dl[w.dn] = r | kLbStart;
+          wave_lds_sync();
+          ++w.dn;
+        }
+      }
+    }
+  }
   if (!w.pend && w.dn) {
-    flush_deferred<WRITE, ABL, W, STAGE, RESUME>(dl, scr, w.dn, lane, T, C, P, w, lim, gw);
+    flush_deferred<WRITE, ABL, W, STAGE, RESUME, LB>(dl, scr, w.dn, lane, T, C, P, w, lim, gw);
     w.ptile = te * kWaveTile;  // (no tile left to repeat)
   }
   if constexpr (!RESUME) {
@@ -924,29 +1036,29 @@ size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates)
 
 namespace {
 
-template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false>
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false, bool LB = false>
 hipError_t sparse_launch(const ScanParams& P, size_t smem, hipStream_t stream)
 {
   static size_t attr_smem = 65536;
   if (smem > attr_smem) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE, ABL, W, STAGE, RESUME>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sparse_kernel<WRITE, ABL, W, STAGE, RESUME, LB>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_smem = smem;
   }
-  hipLaunchKernelGGL((sparse_kernel<WRITE, ABL, W, STAGE, RESUME>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream,
+  hipLaunchKernelGGL((sparse_kernel<WRITE, ABL, W, STAGE, RESUME, LB>), dim3(P.grid), dim3(kSpWaves * 64), smem, stream,
                      P);
   return hipGetLastError();
 }
 
 // The main launch, then (plain walks) the resume launch for the waves it
 // suspended at long walks.
-template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false>
+template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool LB = false>
 hipError_t sparse_one(const ScanParams& P, size_t smem, hipStream_t stream)
 {
-  hipError_t e = sparse_launch<WRITE, ABL, W, STAGE>(P, smem, stream);
+  hipError_t e = sparse_launch<WRITE, ABL, W, STAGE, false, LB>(P, smem, stream);
   if constexpr (W == kWalkPlain && ABL == 0) {
-    if (e == hipSuccess && P.susp) e = sparse_launch<WRITE, 0, kWalkPlain, STAGE, true>(P, smem, stream);
+    if (e == hipSuccess && P.susp) e = sparse_launch<WRITE, 0, kWalkPlain, STAGE, true, LB>(P, smem, stream);
   }
   return e;
 }
@@ -997,6 +1109,16 @@ hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream
     if (write) return sparse_one<true, 0, kWalkCtx>(P, smem, stream);
     return P.st_n ? sparse_one<false, 0, kWalkCtx, true>(P, smem, stream)
                   : sparse_one<false, 0, kWalkCtx>(P, smem, stream);
+  }
+  if (P.lb_cls) {  // (loop-needle tables: lb_batch)
+    if (P.wtab) {
+      if (write) return sparse_one<true, 0, kWalkWord, false, true>(P, smem, stream);
+      return P.st_n ? sparse_one<false, 0, kWalkWord, true, true>(P, smem, stream)
+                    : sparse_one<false, 0, kWalkWord, false, true>(P, smem, stream);
+    }
+    if (write) return sparse_one<true, 0, kWalkPlain, false, true>(P, smem, stream);
+    return P.st_n ? sparse_one<false, 0, kWalkPlain, true, true>(P, smem, stream)
+                  : sparse_one<false, 0, kWalkPlain, false, true>(P, smem, stream);
   }
   if (P.wtab) {
     if (write) return sparse_one<true, 0, kWalkWord>(P, smem, stream);
