@@ -2,7 +2,7 @@
 looks for the needle N and each candidate walks back over C to its run's start
 (ugrep_amd/csrc/host_api.cpp loop_needle, sparse_kernel.hip lb_batch; the
 reference's lookback, lib/matcher.cpp:636-656, restated for the FIND chain;
-DESIGN.md 3.14).
+DESIGN.md 3.15).
 
 CPU: which tables the plan recognises (ugpu_dfa_plan_host shape bit
 UGPU_SHAPE_LOOP_NEEDLE), with and without option W.
