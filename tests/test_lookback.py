@@ -37,6 +37,15 @@ def test_plan_loop_needle():
     assert U.host_plan("[a-z]+ing", word=True)["shape"] & LB
     assert U.host_plan("[a-z@]+ing")["shape"] & LB
     assert not U.host_plan("[a-z@]+ing", word=True)["shape"] & LB
+    assert not U.host_plan("[a-z-]+ing", word=True)["shape"] & LB
+    assert U.host_plan("[A-Za-z]+tion", word=True)["shape"] & LB
+    # without the lookback these have no prefilter and run other kernels
+    os.environ["UGPU_LB"] = "0"
+    try:
+        assert U.host_plan("[A-Za-z]+tion")["kernel"] != 0
+        assert U.host_plan("[a-z-]+ing")["kernel"] != 0
+    finally:
+        os.environ.pop("UGPU_LB", None)
     os.environ["UGPU_LB"] = "0"
     try:
         assert not U.host_plan("[a-z]+ing")["shape"] & LB
@@ -48,7 +57,10 @@ def test_plan_loop_needle():
 # its lookback: a C-run's bytes after its last needle cost it quadratic time,
 # so the long runs below end in a needle and needle-free runs stay short.
 CASES = [("[a-z]+ing", "ing", "q"), ("[a-z]+aa", "aa", "q"), ("[a-z]+abab", "abab", "q"), ("[0-9]+00", "00", "7"),
-         ("x+xx", "xx", "x"), ("[a-z_]+ing", "ing", "_"), ("[a-z@]+ing", "ing", "@")]
+         ("x+xx", "xx", "x"), ("[a-z_]+ing", "ing", "_"), ("[a-z@]+ing", "ing", "@"),
+         # (no first-byte prefilter: 52 and 27 first bytes; the lookback alone
+         # puts them on the sparse kernel)
+         ("[A-Za-z]+tion", "tion", "Q"), ("[a-z-]+ing", "ing", "-")]
 
 
 def _text(seed, n_tok, needle, f):
@@ -127,7 +139,7 @@ def test_gpu_lookback_whole_and_starts(U):
 def test_gpu_lookback_shards_streams_records(U):
     import torch
     rng = np.random.default_rng(9)
-    for k in (0, 2, 3):
+    for k in (0, 2, 3, 7):
         rx, needle, f = CASES[k]
         host = _text(20 + k, 300000, needle, f)
         dev = torch.from_numpy(host).to("cuda")
@@ -154,7 +166,7 @@ def test_gpu_lookback_shards_streams_records(U):
 @pytest.mark.gpu
 def test_gpu_lookback_word(U):
     import torch
-    for k in (0, 3, 1, 6, 5):
+    for k in (0, 3, 1, 6, 5, 7, 8):
         rx, needle, f = CASES[k]
         host = _text(30 + k, 300000, needle, f)
         dev = torch.from_numpy(host).to("cuda")
@@ -162,7 +174,7 @@ def test_gpu_lookback_word(U):
         want = o.find_w(host, want_list=True)
         for lb in ("1", "0"):
             pat, on = _pattern(U, rx, lb, word=True)
-            assert on == (lb == "1" and rx != "[a-z@]+ing"), rx
+            assert on == (lb == "1" and rx not in ("[a-z@]+ing", "[a-z-]+ing")), rx
             r = U.find_all(pat, dev, offsets=True)
             assert (r.count, r.digest, r.dcap) == want[:3], (rx, lb)
             assert r.triples() == want[3], (rx, lb)

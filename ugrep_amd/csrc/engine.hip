@@ -232,7 +232,7 @@ int utf8_scan(const uint8_t* dbuf, uint64_t len, bool nul, uint64_t* pos, void* 
 bool dfa_xc(const ugpu_dfa* d)
 {
   const char* env = std::getenv("UGPU_XC");
-  return d->t.xc && !d->t.filter && d->t.cap1 != 0 && (!d->d_wtab || d->xcw) && !(env && env[0] == '0');
+  return d->t.xc && !d->t.filter && !d->lb && d->t.cap1 != 0 && (!d->d_wtab || d->xcw) && !(env && env[0] == '0');
 }
 
 // code-point run tables run xc_kernel's U mode for COUNT and OFFSETS scans
@@ -636,9 +636,8 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
 int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
 {
   if (!d || !info) return fail(UGPU_INVAL, "NULL argument");
-  dfa_info_fill(d->t, dfa_plan(d->t, d->pflags), info);
   // (the lookback the tables were uploaded with, whatever UGPU_LB says now)
-  info->shape = (info->shape & ~UGPU_SHAPE_LOOP_NEEDLE) | (d->lb ? UGPU_SHAPE_LOOP_NEEDLE : 0u);
+  dfa_info_fill(d->t, dfa_plan(d->t, d->pflags, d->lb ? 1 : 0), info);
   return UGPU_OK;
 }
 
@@ -696,7 +695,7 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   const char* senv0 = std::getenv("UGPU_SPARSE");
   const bool ctx_sparse = dfa->amode && dfa->t.filter && dfa->t.format == FMT_BYTE && !(senv0 && senv0[0] == '0');
   if ((dfa->amode && !ctx_sparse) || dfa->t.format == FMT_WIDE ||
-      (dfa->d_wtab && !dfa->amode && !(dfa->t.filter && dfa->t.format == FMT_BYTE))) {
+      (dfa->d_wtab && !dfa->amode && !((dfa->t.filter || dfa->lb) && dfa->t.format == FMT_BYTE))) {
     const uint32_t nacap = !dfa->amode ? dfa->t.states
                            : dfa->t.ctx_word ? (uint32_t)dfa->t.acap_rows.size() : (uint32_t)dfa->t.acap.size();
     const uint32_t nmap = dfa->amode && dfa->t.ctx_word ? dfa->t.states : 0u;
@@ -736,7 +735,7 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   }
   // (UGPU_SPARSE=0: prefiltered tables take the dense-pattern kernels; testing)
   const char* senv = std::getenv("UGPU_SPARSE");
-  s->sparse = dfa->t.filter && dfa->t.format == FMT_BYTE && !(senv && senv[0] == '0');
+  s->sparse = (dfa->t.filter || dfa->lb) && dfa->t.format == FMT_BYTE && !(senv && senv[0] == '0');
   s->smem = s->sparse ? sparse_smem_bytes(dfa->ntrans_pad, dfa->t.states)
                       : dense_smem_bytes(dfa->t.format, dfa->ntrans_pad, dfa->t.states);
   if (s->smem > 160 * 1024) {

@@ -126,7 +126,7 @@ bool loop_needle(const DfaTables& t, uint32_t cls[8], std::string& needle)
   return true;
 }
 
-DfaPlan dfa_plan(const DfaTables& t, uint32_t flags)
+DfaPlan dfa_plan(const DfaTables& t, uint32_t flags, int lb)
 {
   DfaPlan p;
   p.nul = (flags & UGPU_PAT_EMPTY) != 0;
@@ -142,10 +142,12 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags)
     p.ok = !(flags & UGPU_PAT_WORD);
     return p;
   }
-  // loop-needle tables on the sparse kernel; under option W the run bytes must
-  // be word bytes (then no match starts inside a run: at_wb fails there)
+  // loop-needle tables run the sparse kernel, with or without a first-byte
+  // prefilter; under option W the run bytes must be word bytes (then no match
+  // starts inside a run: at_wb fails there)
   const char* lenv = std::getenv("UGPU_LB");
-  if (t.filter && t.format == FMT_BYTE && !(lenv && lenv[0] == '0') && loop_needle(t, p.lb_cls, p.lb_needle)) {
+  if (lb < 0) lb = !(lenv && lenv[0] == '0');
+  if (lb && t.format == FMT_BYTE && loop_needle(t, p.lb_cls, p.lb_needle)) {
     p.lb = true;
     if (flags & UGPU_PAT_WORD)
       for (uint32_t b = 0; b < 256 && p.lb; ++b)
@@ -155,11 +157,11 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags)
   if (flags & UGPU_PAT_WORD) {
     p.wtab = true;
     const bool wf = !(std::getenv("UGPU_WFAST") && std::getenv("UGPU_WFAST")[0] == '0');
-    p.wplus = wf && t.gap && !t.filter && t.cap1 != 0 && is_word_plus(t);
-    p.xcw = wf && t.xc && t.xc_w && !t.filter && t.cap1 != 0;
+    p.wplus = wf && t.gap && !t.filter && !p.lb && t.cap1 != 0 && is_word_plus(t);
+    p.xcw = wf && t.xc && t.xc_w && !t.filter && !p.lb && t.cap1 != 0;
     if (!p.wplus && !p.xcw) return p;  // option W runs wfind_kernel only: no transducer tables
   }
-  const bool tx = !t.filter && t.cap1 != 0;
+  const bool tx = !t.filter && !p.lb && t.cap1 != 0;
   p.xtrans = t.restart_local && tx;
   p.xid = t.immediate && tx;
   p.xu = t.xu && tx;
@@ -175,7 +177,9 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* out)
   info->row = t.row;
   info->format = t.format;
   info->table_bytes = (uint32_t)(t.trans.size() * 2 + t.trans32.size() * 4 + (t.format != FMT_BYTE ? 256 : 0));
-  info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0;
+  // (loop-needle tables without a first-byte prefilter: 1, the needle's
+  // candidates are not estimated)
+  info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : p.lb ? 1u : 0u;
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
   info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;
@@ -186,9 +190,9 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* out)
   const char* cenv = std::getenv("UGPU_XC");
   const char* uenv = std::getenv("UGPU_XU");
   const char* senv = std::getenv("UGPU_SPARSE");
-  const bool byte_filter = t.filter && t.format == FMT_BYTE && !(senv && senv[0] == '0');
+  const bool byte_filter = (t.filter || p.lb) && t.format == FMT_BYTE && !(senv && senv[0] == '0');
   // (dfa_xc and dfa_xu, from the plan instead of the uploaded tables)
-  const bool xc = t.xc && !t.filter && t.cap1 != 0 && (!p.wtab || p.xcw) && !(cenv && cenv[0] == '0');
+  const bool xc = t.xc && !t.filter && !p.lb && t.cap1 != 0 && (!p.wtab || p.xcw) && !(cenv && cenv[0] == '0');
   const bool xu = p.xu && (!p.wtab || p.wplus) && !(uenv && uenv[0] == '0');
   // (context accepts on a prefiltered table: sparse_kernel's context walks)
   info->kernel = (p.amode && !byte_filter) || t.format == FMT_WIDE || (p.wtab && !p.wplus && !p.xcw && !byte_filter) ? 4u

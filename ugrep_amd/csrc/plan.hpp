@@ -35,7 +35,8 @@ struct DfaPlan {
   std::string lb_needle;
 };
 
-DfaPlan dfa_plan(const DfaTables& t, uint32_t flags);
+// lb: loop-needle lookback 1 / 0, or -1 for the UGPU_LB default (on)
+DfaPlan dfa_plan(const DfaTables& t, uint32_t flags, int lb = -1);
 // ugpu_dfa_info from the tables and the plan (ugpu_dfa_plan_host, ugpu_dfa_info_get)
 void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* info /* ugpu_dfa_info* */);
 // \w+ as ugpu_compile builds it
