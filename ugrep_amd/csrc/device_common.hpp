@@ -316,7 +316,8 @@ __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64
     uint32_t bol = ctx_walk_bits(w, p, ovf);
     // (a continuation byte before p: at_wb follows the last accept, at_wb_cur)
     const bool wbc = w.cword && p > w.bob && (wbyte(w, p - 1) & 0xC0) == 0x80;
-    le = ctx_accept(w, s, bol, q, ovf);
+    // (a start state below accb accepts in no context: no lookups)
+    le = s >= T.accb ? ctx_accept(w, s, bol, q, ovf) : 0u;
     while (q < w.rend) {
       const uint32_t e = T.step(s, wbyte(w, q));
       if (e == 0) return last - p;

@@ -213,6 +213,15 @@ uint64_t env_u64(const char* name, uint64_t dflt)
   return v && *v ? std::strtoull(v, nullptr, 0) : dflt;
 }
 
+// context tables on sparse_kernel: the acap (+ amap) entries it stages in LDS
+// (0: too large, or no context accepts; they stay in global memory)
+uint32_t acap_lds_n(const ugpu_dfa* d)
+{
+  if (!d->amode) return 0;
+  const size_t n = d->t.ctx_word ? d->t.acap_rows.size() + d->t.states : d->t.acap.size();
+  return n <= kSpAcapLds ? (uint32_t)n : 0u;
+}
+
 // fix_kernel rounds allowed for a geometry before it gives up and the forest
 // FIND (forest.hip) resolves the range: resynchronising tables need 0-1 rounds
 // (more only for matches spanning several records), each round walks serially,
@@ -279,6 +288,7 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.acap = d->amode ? d->d_acap : nullptr;
   P.ctx_word = d->amode && d->t.ctx_word ? 1u : 0u;
   P.acap_n = (uint32_t)(P.ctx_word ? d->t.acap_rows.size() : d->t.acap.size());
+  P.acap_lds = acap_lds_n(d) != 0 && env_u64("UGPU_SP_ACAP_LDS", 1) != 0 ? 1u : 0u;
   P.amap = P.ctx_word ? d->d_acap + d->t.acap_rows.size() : nullptr;
   P.nul = d->nul ? 1u : 0u;
   P.wstart = d->wstart && env_u64("UGPU_WSTART", 1) != 0 ? 1u : 0u;
@@ -736,7 +746,7 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   // (UGPU_SPARSE=0: prefiltered tables take the dense-pattern kernels; testing)
   const char* senv = std::getenv("UGPU_SPARSE");
   s->sparse = (dfa->t.filter || dfa->lb) && dfa->t.format == FMT_BYTE && !(senv && senv[0] == '0');
-  s->smem = s->sparse ? sparse_smem_bytes(dfa->ntrans_pad, dfa->t.states)
+  s->smem = s->sparse ? sparse_smem_bytes(dfa->ntrans_pad, dfa->t.states, acap_lds_n(dfa))
                       : dense_smem_bytes(dfa->t.format, dfa->ntrans_pad, dfa->t.states);
   if (s->smem > 160 * 1024) {
     delete s;

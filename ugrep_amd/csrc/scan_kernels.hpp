@@ -225,6 +225,8 @@ struct ScanParams {
   // and, ctx_word, each state's row (tables.hpp acap_rows / acap_map)
   uint32_t acap_n;
   const uint32_t* amap;
+  // sparse_kernel: acap and amap are staged in LDS (small context tables)
+  uint32_t acap_lds;
   // sparse_kernel walk truncation: per wave, the open walk (COUNT pass writes,
   // fix_kernel resolves, the WRITE pass reads); NULL: walks run to rend
   OpenRec* open;
@@ -263,7 +265,9 @@ hipError_t launch_gen(int kind, uint64_t seed, uint64_t off, uint8_t* dbuf, uint
 hipError_t launch_sparse(const ScanParams& P, bool write, size_t smem, hipStream_t stream);
 hipError_t launch_stage_copy(const ScanParams& P, hipStream_t stream);
 hipError_t sparse_occupancy(const ScanParams& P, size_t smem, int* blocks_per_cu);
-size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates);
+size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nlds_acap = 0);
+// context tables whose acap (+ amap) entries sparse_kernel stages in LDS
+constexpr uint32_t kSpAcapLds = 2048;
 // line-level consumers, lines.hip
 struct LineRec {
   uint64_t first_line, last_line;  // lines of the wave's first / last match start (0: none)

@@ -24,6 +24,19 @@
 // Per-wave chain records (entry, exit, counts) are stitched by fix_kernel.
 #include "device_common.hpp"
 
+// The context-walk instantiations (word boundaries, line anchors) are built
+// for UGPU_SP_CTX_OCC blocks of kSpWaves waves per CU: at 4 they hold their
+// 95 VGPRs without spills (at 6: 80 VGPRs and 36 spilled) and their walks read
+// the candidate's LDS window (UGPU_SP_CTX_WIN), with acap/amap in LDS
+// (ScanParams::acap_lds): C2 \<(in|ut)\> 4.65 -> 4.24 ms, \bfoo\b 2.63 ->
+// 2.58 ms (profiles/r05_ctx_walks_ab.json)
+#ifndef UGPU_SP_CTX_OCC
+#define UGPU_SP_CTX_OCC 4
+#endif
+#ifndef UGPU_SP_CTX_WIN
+#define UGPU_SP_CTX_WIN 1
+#endif
+
 namespace ugpu {
 
 namespace {
@@ -558,12 +571,14 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
   bool valid = listed;
   uint64_t c = craw;
   if constexpr (LB) c = lb_batch(P, craw, listed, lane, dn, w);
-  const uint64_t last16 = (P.rend - 1) & ~uint64_t(15);
   const uint64_t a = c & ~uint64_t(15);
-  const uint4 v0 = load16(P.g, a, last16), v1 = load16(P.g, a + 16, last16);
-  wave_lds_sync();  // every lane has read its list entry before the windows overwrite it
-  *reinterpret_cast<uint4*>(scr + 32 * lane) = v0;
-  *reinterpret_cast<uint4*>(scr + 32 * lane + 16) = v1;
+  if constexpr (W != kWalkCtx || UGPU_SP_CTX_WIN) {
+    const uint64_t last16 = (P.rend - 1) & ~uint64_t(15);
+    const uint4 v0 = load16(P.g, a, last16), v1 = load16(P.g, a + 16, last16);
+    wave_lds_sync();  // every lane has read its list entry before the windows overwrite it
+    *reinterpret_cast<uint4*>(scr + 32 * lane) = v0;
+    *reinterpret_cast<uint4*>(scr + 32 * lane + 16) = v1;
+  }
   wave_lds_sync();
   if constexpr (W != kWalkPlain) {
     uint64_t len = 0;
@@ -574,13 +589,18 @@ __device__ __forceinline__ void flush_deferred(const uint64_t* dl, uint8_t* scr,
       // state (ctx_accept).  Either way the candidates stay a superset (W and
       // the contexts only remove matches, the first bytes are the table's),
       // so the prefilter is unchanged.
-      // (option W: the walk reads its lane's 32-byte LDS window [a, a + 32)
-      // where it can, global memory around it -- -w '[a-z]+ing' 54.6 -> 45.1
-      // ms per 16 GiB.  The context walks keep global memory: with the window
-      // their kernel spills 66 instead of 36 VGPRs, and \bfoo\b, whose time
-      // is the main loop's, went 2.57 -> 2.84 ms; profiles/r05_sparse_walks_ab.json)
+      // (the walk reads its lane's 32-byte LDS window [a, a + 32) where it
+      // can, global memory around it -- option W: -w '[a-z]+ing' 54.6 -> 45.1
+      // ms per 16 GiB, profiles/r05_sparse_walks_ab.json; the context walks:
+      // UGPU_SP_CTX_WIN above)
       Win win = win_of(P);
-      if constexpr (W == kWalkWord) {
+      if constexpr (W == kWalkCtx) {
+        if (P.acap_lds) {  // (C.caps: the LDS copy of acap, amap after it)
+          win.acap = C.caps;
+          win.amap = C.caps + P.acap_n;
+        }
+      }
+      if constexpr (W == kWalkWord || UGPU_SP_CTX_WIN) {
         win.wl = scr + 32 * lane;
         win.wa = a;
         win.wn = 32;
@@ -790,7 +810,7 @@ __device__ __forceinline__ TileLoad wave_tile(const uint8_t* wbase, uint32_t i, 
 }  // namespace
 
 template <bool WRITE, int ABL, int W = kWalkPlain, bool STAGE = false, bool RESUME = false, bool LB = false>
-__global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(ScanParams P)
+__global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : (W == kWalkCtx ? UGPU_SP_CTX_OCC : 6)) void sparse_kernel(ScanParams P)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -815,12 +835,22 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
     uint4* dst = reinterpret_cast<uint4*>(ltrans);
     for (uint32_t i = tid; i < P.ntrans_pad / 8; i += kSpWaves * 64) dst[i] = src[i];
     for (uint32_t i = tid; i < P.nstates; i += kSpWaves * 64) lcaps[i] = P.caps[i];
+    if constexpr (W == kWalkCtx) {
+      // (small context tables: acap, then amap, after the accept indices)
+      if (P.acap_lds) {
+        uint32_t* la = lcaps + P.nstates;
+        for (uint32_t i = tid; i < P.acap_n; i += kSpWaves * 64) la[i] = P.acap[i];
+        if (P.ctx_word)
+          for (uint32_t i = tid; i < P.nstates; i += kSpWaves * 64) la[P.acap_n + i] = P.amap[i];
+      }
+    }
   }
   __syncthreads();  // the only workgroup barrier: tables staged
   if (!mine) return;
   const Tab<0> T{ltrans, nullptr, P.start, P.accb};
   // (context accepts: a walk's `le` is the acap index, whose entry is the accept index)
-  const Ctx C = W == kWalkCtx ? Ctx{P.acap, 0u, P.delta} : Ctx{lcaps, P.log_row, P.delta};
+  const Ctx C = W == kWalkCtx ? Ctx{P.acap_lds ? lcaps + P.nstates : P.acap, 0u, P.delta}
+                              : Ctx{lcaps, P.log_row, P.delta};
   const FTab F{P.ft[0], P.ft[1], P.ft[2], P.ft[3], P.ft[4]};
 
   uint64_t tb = P.t0 + gw * P.tpb;
@@ -1028,9 +1058,9 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : 6) void sparse_kernel(S
 }
 
 // ---------------------------------------------------------------- launchers
-size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates)
+size_t sparse_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nlds_acap)
 {
-  size_t b = (size_t)kSpWaves * kAux + 2 * (size_t)ntrans_pad + 4 * (size_t)nstates;
+  size_t b = (size_t)kSpWaves * kAux + 2 * (size_t)ntrans_pad + 4 * (size_t)nstates + 4 * (size_t)nlds_acap;
   return (b + 15) & ~size_t(15);
 }
 
