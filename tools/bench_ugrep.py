@@ -26,7 +26,9 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 # -co: count every match (the FIND chain), not matching lines (plain -c stops
 # at a line's first match, src/ugrep.cpp:10536-10565)
-CONFIGS = [("c2", "foo|bar|baz", 1), ("c2_gpu", "foo|bar|baz", 1), ("c3", "[A-Za-z_][A-Za-z0-9_]*", 3), ("c4", r"\w+", 4)]
+CONFIGS = [("c2", "foo|bar|baz", 1), ("c2_gpu", "foo|bar|baz", 1), ("c3", "[A-Za-z_][A-Za-z0-9_]*", 3), ("c4", r"\w+", 4),
+           # loop-needle tables on the C2 corpus, -co and -cow
+           ("c2_ing", "[a-z]+ing", 1), ("c2_ing_gpu", "[a-z]+ing", 1), ("c2_wing_gpu", "[a-z]+ing", 1, ["-w"])]
 
 
 def stats(stderr):
@@ -88,7 +90,9 @@ def main():
         t_gpu, o_gpu, e_gpu = run(gpu, ["-co", "foo|bar|baz", p], env, a.reps)
         print(json.dumps({"config": "startup", "bytes": 1 << 16, "cpu_s": round(t_cpu, 4), "gpu_s": round(t_gpu, 4),
                           "outputs_equal": o_cpu == o_gpu, "adapter": stats(e_gpu)}), flush=True)
-    for name, rx, kind in CONFIGS:
+    for cfg in CONFIGS:
+        name, rx, kind = cfg[:3]
+        flags = cfg[3] if len(cfg) > 3 else []
         if name not in a.configs.split(","):
             continue
         with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
@@ -97,7 +101,7 @@ def main():
                 p = os.path.join(d, "%s_%03d.txt" % (name, k))
                 gen(kind, 1, k * n, n).tofile(p)
                 files.append(p)
-            args = ["-co", "-J%d" % a.workers, rx] + files
+            args = ["-co", "-J%d" % a.workers] + flags + [rx] + files
             env = dict(os.environ)
             env.pop("UGPU_ADAPTER_SPARSE_MAX", None)
             env.pop("UGPU_ADAPTER_MIN_BYTES", None)
@@ -114,7 +118,7 @@ def main():
             # -J: files finish in any order
             s_cpu, s_gpu = sorted(o_cpu.splitlines()), sorted(o_gpu.splitlines())
             diff = [(x.decode(), y.decode()) for x, y in zip(s_cpu, s_gpu) if x != y][:4]
-            print(json.dumps({"config": name, "pattern": rx, "files": a.files, "bytes": total,
+            print(json.dumps({"config": name, "pattern": rx, "flags": flags, "files": a.files, "bytes": total,
                               "workers": a.workers, "cpu_s": round(t_cpu, 4), "gpu_s": round(t_gpu, 4),
                               "cpu_gbps": round(total / t_cpu / 1e9, 2), "gpu_gbps": round(total / t_gpu / 1e9, 2),
                               "speedup": round(t_cpu / t_gpu, 2), "outputs_equal": s_cpu == s_gpu, "diff": diff,
