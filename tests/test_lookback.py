@@ -202,3 +202,82 @@ def test_gpu_lookback_giant_runs(U):
         dt = time.perf_counter() - t0
         assert r.triples() == want[3], rx
         assert dt < 2.0, (rx, dt)
+
+
+def _fuzz_cases(seed, n):
+    """Random C+ N patterns (and near misses that must not take the lookback)
+    with texts of C-runs around needles."""
+    rng = np.random.default_rng(seed)
+    pools = ["abcdefghijklmnopqrstuvwxyz", "abc", "ab", "0123456789", "xyz_", "aeiou", "ABCabc", "a@b#"]
+    out = []
+    for _ in range(n):
+        pool = pools[int(rng.integers(0, len(pools)))]
+        k = int(rng.integers(1, len(pool) + 1))
+        cset = sorted(set(rng.choice(list(pool), k, replace=True)))
+        m = int(rng.integers(2, 6))
+        needle = "".join(rng.choice(cset, m))
+        cls = "[" + "".join(c if c not in "^]-\\" else "\\" + c for c in cset) + "]"
+        rx = cls + "+" + needle
+        # (C+ (N)+ is no near miss: N is in C*, so it is the language C+ N)
+        near = [cls + "*" + needle, cls + "+" + needle + cls + "*"]
+        if len(cset) == 1:  # (c* c^m and c+ c^m c* are c+ c^(m-1), c+ c^m: loop-needle languages)
+            near = []
+        same = cls + "+(" + needle + ")+"
+        # text: runs of C (geometric lengths, a few long) holding needles, and separators
+        parts = []
+        for _ in range(4000):
+            r = rng.random()
+            if r < 0.5:
+                parts.append("".join(rng.choice(cset, int(rng.geometric(0.2)))))
+            elif r < 0.8:
+                parts.append(needle)
+            elif r < 0.995:
+                parts.append(str(rng.choice([" ", "\n", ".", "-", "Z", "é", "\0"])))
+            else:
+                parts.append("".join(rng.choice(cset, int(rng.integers(100, 3000)))) + needle)
+        out.append((rx, near, "".join(parts).encode(), set(cset), same))
+    return out
+
+
+def test_plan_fuzz_near_misses():
+    """Near misses of C+ N never take the lookback (their languages differ)."""
+    import ugrep_amd as U
+    from ugrep_amd._lib import SHAPE_LOOP_NEEDLE as LB
+    for rx, near, _, _, same in _fuzz_cases(7, 60):
+        assert U.host_plan(rx)["shape"] & LB, rx
+        assert U.host_plan(same)["shape"] & LB, same
+        for nr in near:
+            try:
+                assert not U.host_plan(nr)["shape"] & LB, nr
+            except U.Unsupported:
+                pass
+
+
+@pytest.mark.gpu
+def test_gpu_lookback_fuzz(U):
+    """100 random C+ N patterns (C from letters, digits, '_', punctuation;
+    needles of 2-5 bytes, often self-overlapping) over texts of C-runs, with
+    and without option W, and their near misses: equal to the oracle record by
+    record."""
+    import torch
+    word = set("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_")
+    for rx, near, text, cset, _ in _fuzz_cases(11, 100):
+        host = np.frombuffer(text, np.uint8).copy()
+        dev = torch.from_numpy(host).to("cuda")
+        o = OracleDfa(U.compile_regex(rx))
+        want = o.find(host, want_list=True)
+        pat, on = _pattern(U, rx, "1")
+        assert on, rx
+        r = U.find_all(pat, dev, offsets=True)
+        assert r.triples() == want[3], rx
+        r = U.find_all_multi(pat, dev, ndev=3, offsets=True)
+        assert r.triples() == want[3], (rx, "shards")
+        w = o.find_w(host, want_list=True)
+        patw, onw = _pattern(U, rx, "1", word=True)
+        assert onw == cset.issubset(word), rx
+        assert U.find_all(patw, dev, offsets=True).triples() == w[3], (rx, "W")
+        for nr in near[:2]:
+            want = OracleDfa(U.compile_regex(nr)).find(host, want_list=True)
+            pat, on = _pattern(U, nr, "1")
+            assert not on, nr
+            assert U.find_all(pat, dev, offsets=True).triples() == want[3], nr
