@@ -82,6 +82,7 @@ struct ugpu_dfa {
   // option W on a table equivalent to \w+: on valid UTF-8 the W
   // rules remove nothing, so such scans run the non-W kernels (xg_kernel)
   bool wplus = false;
+  bool wsparse = false;  // option W on the sparse kernel without a selective prefilter (DfaPlan::wsparse)
   // option W on a two-state table whose X is the ASCII word bytes: xc_kernel
   // applies the W rules itself (non-ASCII input falls back to wfind_kernel)
   bool xcw = false;
@@ -477,6 +478,7 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
   d->nul = pl.nul;
   d->amode = pl.amode;
   d->wplus = pl.wplus;
+  d->wsparse = pl.wsparse;
   d->xcw = pl.xcw;
   // option W: every match begins where at_wb holds (lib/matcher.cpp:107);
   // word-boundary tables: when no state accepts in a context without CTX_WB
@@ -705,7 +707,7 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   const char* senv0 = std::getenv("UGPU_SPARSE");
   const bool ctx_sparse = dfa->amode && dfa->t.filter && dfa->t.format == FMT_BYTE && !(senv0 && senv0[0] == '0');
   if ((dfa->amode && !ctx_sparse) || dfa->t.format == FMT_WIDE ||
-      (dfa->d_wtab && !dfa->amode && !((dfa->t.filter || dfa->lb) && dfa->t.format == FMT_BYTE))) {
+      (dfa->d_wtab && !dfa->amode && !((dfa->t.filter || dfa->lb || dfa->wsparse) && dfa->t.format == FMT_BYTE))) {
     const uint32_t nacap = !dfa->amode ? dfa->t.states
                            : dfa->t.ctx_word ? (uint32_t)dfa->t.acap_rows.size() : (uint32_t)dfa->t.acap.size();
     const uint32_t nmap = dfa->amode && dfa->t.ctx_word ? dfa->t.states : 0u;
@@ -745,7 +747,7 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   }
   // (UGPU_SPARSE=0: prefiltered tables take the dense-pattern kernels; testing)
   const char* senv = std::getenv("UGPU_SPARSE");
-  s->sparse = (dfa->t.filter || dfa->lb) && dfa->t.format == FMT_BYTE && !(senv && senv[0] == '0');
+  s->sparse = (dfa->t.filter || dfa->lb || dfa->wsparse) && dfa->t.format == FMT_BYTE && !(senv && senv[0] == '0');
   s->smem = s->sparse ? sparse_smem_bytes(dfa->ntrans_pad, dfa->t.states, acap_lds_n(dfa))
                       : dense_smem_bytes(dfa->t.format, dfa->ntrans_pad, dfa->t.states);
   if (s->smem > 160 * 1024) {

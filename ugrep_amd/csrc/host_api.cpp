@@ -159,6 +159,16 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags, int lb)
     const bool wf = !(std::getenv("UGPU_WFAST") && std::getenv("UGPU_WFAST")[0] == '0');
     p.wplus = wf && t.gap && !t.filter && !p.lb && t.cap1 != 0 && is_word_plus(t);
     p.xcw = wf && t.xc && t.xc_w && !t.filter && !p.lb && t.cap1 != 0;
+    // option W without a selective prefilter: the sparse kernel when every
+    // first byte is an ASCII word byte (then the word-start filter leaves about
+    // the word starts: C2 -w '[A-Za-z]+' 229.7 -> 89.0 ms against
+    // wfind_kernel; profiles/r05_wsparse_ab.json).  UGPU_WSPARSE=0: wfind_kernel.
+    const char* wsenv = std::getenv("UGPU_WSPARSE");
+    p.wsparse = !(wsenv && wsenv[0] == '0') && !t.filter && !p.lb && !p.wplus && !p.xcw && t.format == FMT_BYTE &&
+                t.row == 256 && t.first_bytes > 0 && !t.start_acc;
+    for (uint32_t b = 0; b < 256 && p.wsparse; ++b)
+      if (t.trans[t.start + b])
+        p.wsparse = (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_';
     if (!p.wplus && !p.xcw) return p;  // option W runs wfind_kernel only: no transducer tables
   }
   const bool tx = !t.filter && !p.lb && t.cap1 != 0;
@@ -190,7 +200,7 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* out)
   const char* cenv = std::getenv("UGPU_XC");
   const char* uenv = std::getenv("UGPU_XU");
   const char* senv = std::getenv("UGPU_SPARSE");
-  const bool byte_filter = (t.filter || p.lb) && t.format == FMT_BYTE && !(senv && senv[0] == '0');
+  const bool byte_filter = (t.filter || p.lb || p.wsparse) && t.format == FMT_BYTE && !(senv && senv[0] == '0');
   // (dfa_xc and dfa_xu, from the plan instead of the uploaded tables)
   const bool xc = t.xc && !t.filter && !p.lb && t.cap1 != 0 && (!p.wtab || p.xcw) && !(cenv && cenv[0] == '0');
   const bool xu = p.xu && (!p.wtab || p.wplus) && !(uenv && uenv[0] == '0');

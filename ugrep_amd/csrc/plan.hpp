@@ -31,6 +31,10 @@ struct DfaPlan {
   // loop-needle table (C+ N, host_api.cpp loop_needle): the sparse kernel's
   // prefilter looks for N and its candidates walk back to their C-run's start
   bool lb = false;
+  // option W on a byte table without a selective prefilter: the sparse
+  // kernel's W walks from the first-byte candidates that follow no ASCII
+  // letter (ScanParams::wstart) instead of wfind_kernel (UGPU_WSPARSE)
+  bool wsparse = false;
   uint32_t lb_cls[8] = {};
   std::string lb_needle;
 };
