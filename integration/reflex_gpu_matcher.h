@@ -443,7 +443,10 @@ class GpuMatcher : public Matcher {
           else if (planned)
           {
             tab_ok_ = true;
-            sparse_ = info.kernel == 0;
+            // (a prefiltered table: the reference's own needle search is fast on
+            // it; option W without a selective prefilter also runs sparse_kernel,
+            // prefilter_ppm 0, but is dense work for the CPU matcher)
+            sparse_ = info.kernel == 0 && info.prefilter_ppm != 0;
             tab_ = std::make_shared<Tables>();
             tab_->opc.assign(opc, opc + nop);
             tab_->flags = flags;
