@@ -180,6 +180,13 @@ def test_gpu_lookback_word(U):
             assert r.triples() == want[3], (rx, lb)
         w = o.find_w(host, start=3, want_list=True)
         assert U.find_all(pat, dev, start=3).triples() == w[3], rx
+        # (UGPU_SPARSE=0: wfind_kernel, which applies the W rules itself)
+        os.environ["UGPU_SPARSE"] = "0"
+        try:
+            pat0 = U.Pattern(rx, word=True)
+            assert U.find_all(pat0, dev, offsets=True).triples() == want[3], (rx, "wfind")
+        finally:
+            os.environ.pop("UGPU_SPARSE", None)
 
 
 @pytest.mark.gpu

@@ -93,8 +93,8 @@ struct ugpu_dfa {
   uint32_t* d_acap = nullptr;  // acap, or (word boundaries) acap_rows then acap_map
   // no match starts right after a word character (ScanParams::wstart)
   bool wstart = false;
-  // loop-needle tables (C+N, ScanParams::lb): the prefilter finds N, and each
-  // candidate walks back to its C-run's start (loop_needle below)
+  // loop-needle tables (C+N, ScanParams::lb_cls): the prefilter finds N, and
+  // each candidate walks back to its C-run's start (host_api.cpp loop_needle)
   bool lb = false;
   uint8_t lb_ft[20] = {};
   uint32_t* d_lbcls = nullptr;  // 256-bit mask of C
@@ -704,10 +704,13 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   // sparse_kernel's candidate walks run the context walk, the
   // prefilter's candidates stay a superset; without a prefilter (or with
   // UGPU_SPARSE=0) wfind_kernel's chain of context walks
+  // (option W: also loop-needle tables and DfaPlan::wsparse; UGPU_SPARSE=0:
+  // wfind_kernel, which applies the W rules)
   const char* senv0 = std::getenv("UGPU_SPARSE");
-  const bool ctx_sparse = dfa->amode && dfa->t.filter && dfa->t.format == FMT_BYTE && !(senv0 && senv0[0] == '0');
-  if ((dfa->amode && !ctx_sparse) || dfa->t.format == FMT_WIDE ||
-      (dfa->d_wtab && !dfa->amode && !((dfa->t.filter || dfa->lb || dfa->wsparse) && dfa->t.format == FMT_BYTE))) {
+  const bool sp_off = senv0 && senv0[0] == '0';
+  const bool ctx_sparse = dfa->amode && dfa->t.filter && dfa->t.format == FMT_BYTE && !sp_off;
+  const bool w_sparse = (dfa->t.filter || dfa->lb || dfa->wsparse) && dfa->t.format == FMT_BYTE && !sp_off;
+  if ((dfa->amode && !ctx_sparse) || dfa->t.format == FMT_WIDE || (dfa->d_wtab && !dfa->amode && !w_sparse)) {
     const uint32_t nacap = !dfa->amode ? dfa->t.states
                            : dfa->t.ctx_word ? (uint32_t)dfa->t.acap_rows.size() : (uint32_t)dfa->t.acap.size();
     const uint32_t nmap = dfa->amode && dfa->t.ctx_word ? dfa->t.states : 0u;
