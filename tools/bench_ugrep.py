@@ -28,7 +28,9 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 # at a line's first match, src/ugrep.cpp:10536-10565)
 CONFIGS = [("c2", "foo|bar|baz", 1), ("c2_gpu", "foo|bar|baz", 1), ("c3", "[A-Za-z_][A-Za-z0-9_]*", 3), ("c4", r"\w+", 4),
            # loop-needle tables on the C2 corpus, -co and -cow
-           ("c2_ing", "[a-z]+ing", 1), ("c2_ing_gpu", "[a-z]+ing", 1), ("c2_wing_gpu", "[a-z]+ing", 1, ["-w"])]
+           ("c2_ing", "[a-z]+ing", 1), ("c2_ing_gpu", "[a-z]+ing", 1), ("c2_wing_gpu", "[a-z]+ing", 1, ["-w"]),
+           # option W without a selective prefilter (sparse_kernel, DfaPlan::wsparse) on the C3 corpus
+           ("c3_wazAZ", "[A-Za-z]+", 3, ["-w"])]
 
 
 def stats(stderr):
