@@ -207,6 +207,17 @@ int ugpu_tables_xc_host(const uint32_t *opc, uint32_t nop, uint8_t *cls, int *ok
    lib/matcher.cpp:460-545.) */
 int ugpu_tables_xu_host(const uint32_t *opc, uint32_t nop, uint8_t *tab, uint32_t *bm3, int *ok);
 
+/* Host-only: the dominated-restart bits of the dense tables (bit s of
+   dom[s / 32], state numbering as ugpu_tables_build_host): L(start) is a
+   subset of L(s), so a failed FIND walk that crosses position q in state s
+   shows that no match starts at q (the chain skips it; ugrep_amd/csrc/
+   tables.hpp dom).  *n = the number of u32 words (0: not computed, no skips);
+   *all (may be NULL) = 1 when every non-accepting state reachable from the
+   start has its bit (then a failed walk skips up to the byte it died on).
+   (Replaces the reference's position-by-position restart after a failed
+   match, lib/matcher.cpp:692-713, for the stitching re-walks.) */
+int ugpu_tables_dom_host(const uint32_t *opc, uint32_t nop, uint32_t *dom, uint32_t dom_cap, uint32_t *n, int *all);
+
 /* Host-only: the per-context accept indices of the dense tables (states * 4
    u32: acap[state * 4 + bol * 2 + eol], state numbering as
    ugpu_tables_build_host), whether the table has line anchors, and whether its

@@ -105,6 +105,8 @@ def _load():
         "ugpu_scanner_context": (ctypes.c_int, [V, ctypes.c_int]),
         "ugpu_tables_xc_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, c_u8p, P(ctypes.c_int)]),
         "ugpu_tables_xu_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, c_u8p, c_u32p, P(ctypes.c_int)]),
+        "ugpu_tables_dom_host": (ctypes.c_int, [c_u32p, ctypes.c_uint32, c_u32p, ctypes.c_uint32,
+                                                P(ctypes.c_uint32), P(ctypes.c_int)]),
         "ugpu_find_all": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P(P(Result))]),
         "ugpu_find_all_multi": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int,
                                                P(P(Result))]),

@@ -60,6 +60,8 @@ struct Win {
   const uint32_t* amap = nullptr;  // cword: each state's row of acap (tables.hpp acap_map)
   // loop-needle tables (ScanParams::lb_cls): the 256-bit set C of C+ N
   const uint32_t* lb = nullptr;
+  // dominated restarts (ScanParams::dom): bit = state id
+  const uint32_t* dom = nullptr;
   // an LDS copy of bytes [wa, wa + wn) that the W / context walks read instead
   // of global memory (sparse_kernel's per-lane candidate window; wn = 0: none)
   const uint8_t* wl = nullptr;
@@ -98,6 +100,7 @@ __device__ __forceinline__ Win win_of(const ScanParams& P)
   w.cword = P.ctx_word;
   w.amap = P.amap;
   w.lb = P.lb_cls;
+  w.dom = P.dom;
   return w;
 }
 
@@ -375,6 +378,60 @@ __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64
   return last - p;
 }
 
+// A plain walk from p (walk<FMT>) that also finds where a failed walk lets
+// the FIND chain go on (w.dom, tables.hpp dom): `skip` = the first position
+// q > p whose state does not dominate the start state, or one past the byte
+// the walk died on, or the position where it stopped.  If the walk from p
+// accepts nowhere, no walk from a position in (p, skip) accepts either: its
+// accepted strings would be accepted by p's walk from the dominating state it
+// is in there.
+template <int FMT>
+__device__ __forceinline__ uint64_t walk_dom(const Tab<FMT>& T, const Win& w, uint64_t p, uint32_t& le, uint32_t& ovf,
+                                             uint64_t& skip)
+{
+  uint32_t s = T.start;
+  uint64_t q = p, last = p;
+  le = 0;
+  skip = 0;
+  auto dom = [&w](uint32_t e) { return (w.dom[e >> (w.log_row + 5)] >> ((e >> w.log_row) & 31)) & 1u; };
+  const uint64_t l1 = w.lend < w.rend ? w.lend : w.rend;
+  while (q < w.rend) {
+    const uint32_t e = T.step(s, q < l1 ? (uint32_t)w.lds[q - w.base] : (uint32_t)w.g[q]);
+    if (e == 0) {
+      if (!skip) skip = q + 1;
+      return last - p;
+    }
+    s = e;
+    ++q;
+    if (e >= T.accb) {
+      last = q;
+      le = e;
+    }
+    if (!skip && !dom(e)) skip = q;
+  }
+  if (!w.eof) ovf = 1;  // a live walk ran into the end of this shard's readable bytes
+  if (!skip) skip = q;
+  return last - p;
+}
+
+// Where the FIND chain goes on after a walk from c that is known to accept
+// nowhere (fix_kernel's resolved open walks; w.dom set): walk_dom's skip,
+// looking no further than lim.
+template <int FMT>
+__device__ __forceinline__ uint64_t dom_restart(const Tab<FMT>& T, const Win& w, uint64_t c, uint64_t lim)
+{
+  uint32_t s = T.start;
+  uint64_t q = c;
+  while (q < lim && q < w.rend) {
+    const uint32_t e = T.step(s, (uint32_t)w.g[q]);
+    if (e == 0) return q + 1;
+    s = e;
+    ++q;
+    if (!((w.dom[e >> (w.log_row + 5)] >> ((e >> w.log_row) & 31)) & 1u)) return q;
+  }
+  return q > c + 1 ? q : c + 1;
+}
+
 struct Ctx {
   const uint32_t* caps;
   uint32_t log_row;
@@ -433,11 +490,25 @@ struct WriteEm {
 // means no needle in the rest of its C-run, so no position of the run starts
 // a match: the chain skips to the run's end (at most to cap), which keeps the
 // serial re-walks of fix_kernel linear over long runs without a needle.
+// Tables with dominated restarts (w.dom) and cap != 0: a failed plain walk
+// moves the chain to walk_dom's skip (at most to cap), so a needle-free run
+// costs one walk, not one per position.
 template <int FMT, class Em, int W = kWalkPlain>
 __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, const Ctx& c, uint64_t p, Em& em,
                                                int sign, uint32_t& ovf, uint64_t cap = 0)
 {
   uint32_t le;
+  if constexpr (W == kWalkPlain) {
+    if (cap && w.dom) {
+      uint64_t skip;
+      const uint64_t len = walk_dom<FMT>(T, w, p, le, ovf, skip);
+      if (len) {
+        em.put(c, p, len, le, sign);
+        return p + len;
+      }
+      return skip < cap ? skip : (cap > p + 1 ? cap : p + 1);
+    }
+  }
   const uint64_t len = walk<FMT, W>(T, w, p, le, ovf);
   if (len) {
     em.put(c, p, len, le, sign);

@@ -66,6 +66,10 @@ using namespace ugpu;
 
 struct ugpu_dfa {
   DfaTables t;
+  // the plan the tables were uploaded with (lookback, option-W route); the
+  // kernel-choice test knobs (UGPU_SPARSE, UGPU_XI, ...) stay live: scanners
+  // and ugpu_dfa_info_get read them when they are called
+  DfaPlan plan;
   int device = 0;
   uint32_t ntrans_pad = 0;
   uint16_t* d_trans = nullptr;
@@ -98,6 +102,7 @@ struct ugpu_dfa {
   bool lb = false;
   uint8_t lb_ft[20] = {};
   uint32_t* d_lbcls = nullptr;  // 256-bit mask of C
+  uint32_t* d_dom = nullptr;    // dominated restarts (tables.hpp dom), or NULL
   // idle scanners of ugpu_find_all calls on this table (reused: creating one
   // costs device allocations and property queries)
   std::mutex pool_mu;
@@ -303,6 +308,8 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
     P.ft[i] = (uint32_t)ft[4 * i] | ((uint32_t)ft[4 * i + 1] << 8) | ((uint32_t)ft[4 * i + 2] << 16) |
               ((uint32_t)ft[4 * i + 3] << 24);
   P.lb_cls = d->lb ? d->d_lbcls : nullptr;
+  P.dom = d->d_dom;
+  P.dom_all = d->d_dom && d->t.dom_all ? 1u : 0u;
   if (d->lb) P.wstart = 0;  // (the candidates are needle positions, not match starts)
 }
 
@@ -474,6 +481,7 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     return hip_fail(e, "hipGetDevice");
   }
   d->opc.assign(opc, opc + nop);
+  d->plan = pl;
   d->pflags = pattern_flags;
   d->nul = pl.nul;
   d->amode = pl.amode;
@@ -542,6 +550,14 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
                 (e = hipMemcpy(d->d_lbcls, lbcls, 32, hipMemcpyHostToDevice)) != hipSuccess)) {
     ugpu_dfa_destroy(d);
     return hip_fail(e, "loop class upload");
+  }
+  // (UGPU_DOM=0: no dominated-restart skips; testing)
+  const char* domenv = std::getenv("UGPU_DOM");
+  if (!d->t.dom.empty() && !(domenv && domenv[0] == '0') &&
+      ((e = hipMalloc(&d->d_dom, d->t.dom.size() * 4)) != hipSuccess ||
+       (e = hipMemcpy(d->d_dom, d->t.dom.data(), d->t.dom.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)) {
+    ugpu_dfa_destroy(d);
+    return hip_fail(e, "dominance upload");
   }
   if (d->t.format == FMT_WIDE &&
       ((e = hipMalloc(&d->d_trans32, d->t.trans32.size() * 4)) != hipSuccess ||
@@ -641,6 +657,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   if (d->d_caps) (void)hipFree(d->d_caps);
   if (d->d_acap) (void)hipFree(d->d_acap);
   if (d->d_lbcls) (void)hipFree(d->d_lbcls);
+  if (d->d_dom) (void)hipFree(d->d_dom);
   delete d;
   return UGPU_OK;
 }
@@ -648,8 +665,9 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
 int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
 {
   if (!d || !info) return fail(UGPU_INVAL, "NULL argument");
-  // (the lookback the tables were uploaded with, whatever UGPU_LB says now)
-  dfa_info_fill(d->t, dfa_plan(d->t, d->pflags, d->lb ? 1 : 0), info);
+  // (the plan the tables were uploaded with -- lookback and option-W route,
+  // whatever UGPU_LB / UGPU_WSPARSE / UGPU_WFAST say now)
+  dfa_info_fill(d->t, d->plan, info);
   return UGPU_OK;
 }
 

@@ -364,6 +364,20 @@ int ugpu_tables_xu_host(const uint32_t* opc, uint32_t nop, uint8_t* tab, uint32_
   return UGPU_OK;
 }
 
+int ugpu_tables_dom_host(const uint32_t* opc, uint32_t nop, uint32_t* dom, uint32_t dom_cap, uint32_t* n, int* all)
+{
+  if (!n) return fail(UGPU_INVAL, "NULL argument");
+  DfaTables t;
+  std::string err;
+  const int rc = build_tables(opc, nop, t, err);
+  if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
+  *n = (uint32_t)t.dom.size();
+  if (all) *all = t.dom_all ? 1 : 0;
+  if (dom && dom_cap < t.dom.size()) return fail(UGPU_INVAL, "dom too small");
+  if (dom) std::copy(t.dom.begin(), t.dom.end(), dom);
+  return UGPU_OK;
+}
+
 int ugpu_tables_context_host(const uint32_t* opc, uint32_t nop, uint32_t* acap, uint32_t acap_cap, int* anchored,
                              int* start_acc)
 {

@@ -17,7 +17,14 @@ namespace ugpu {
 //      V's: V's end e1 (a closed first match) or, when V is wave k+1's own
 //      open walk, that walk's resolved end.  W may die first (kOpenDead).
 //      A walk that neither dies nor converges within kOpenConvBudget bytes
-//      gives up (kOpenUnres: UGPU_FLAG_BUDGET, the forest FIND).
+//      is left to R1b.
+//   R1b (one wave per such walk, when there are few): W walked on by the whole
+//      wave, 1 KiB a round (coop_continue), until it dies or reaches the end
+//      of the readable bytes (kOpenDead), within kOpenCoopBudget bytes; past
+//      that it gives up (kOpenUnres: UGPU_FLAG_BUDGET, the forest FIND).  The
+//      last open wave of a run of candidate bytes that crosses many waves
+//      (a needle-free letter run under [a-z]+(ing|ed)) is resolved here; the
+//      waves before it converge with their successors in R1.
 //   R2 (wave 0, open waves in descending order, 64 at a time): the ends, each
 //      from the next one's (a run of candidate bytes across many waves is one
 //      chain of converged open walks).
@@ -37,6 +44,90 @@ __device__ __forceinline__ void rec_add(const ScanParams& P, uint64_t b, uint64_
   r[3] += ddg;
   r[4] += ddc;
 }
+
+// R1b: walk W on with the whole wave from DFA entry s before byte q, up to
+// lim (<= rend).  Each round lane l walks the 16 bytes at (q & ~15) + 16 l
+// from a guessed entry (W's entry run over the 4 bytes before them: exact when
+// the state depends on the last few bytes, as in a letter loop); the guesses
+// are checked in lane order against the previous lane's exit, and W advances
+// to the first lane whose guess was wrong, or dies in the first dying lane
+// before it (as sparse_kernel's coop_walk, bytes from registers instead of
+// LDS).  Returns true when W died (q = the byte it died on) or reached the
+// readable end (q = rend); lastw / lew = W's last accept (unchanged if none).
+template <int FMT>
+__device__ __forceinline__ bool coop_continue(const Tab<FMT>& T, const Win& w, uint32_t& s, uint64_t& q, uint64_t lim,
+                                              uint64_t& lastw, uint32_t& lew)
+{
+  const int lane = threadIdx.x & 63;
+  while (q < lim) {
+    const uint64_t base = q & ~uint64_t(15);
+    const uint64_t sa = base + 16u * (uint32_t)lane;
+    uint32_t d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint64_t i = sa + 4 * k + b;
+        x |= (i < w.rend ? (uint32_t)w.g[i] : 0u) << (8 * b);
+      }
+      d[k] = x;
+    }
+    const uint32_t pw = (uint32_t)__shfl_up((int)d[3], 1, 64);  // the 4 bytes before the lane's 16
+    uint32_t spec = s;
+    if (lane != 0) {
+      uint32_t t = s;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) t = t ? T.step(t, (pw >> (8 * b)) & 0xffu) : 0u;
+      spec = t ? t : s;
+    }
+    const uint64_t a = sa > q ? sa : q;
+    const uint64_t z = sa + 16 < lim ? sa + 16 : lim;
+    uint32_t cur = spec, lel = 0;
+    uint64_t lastl = 0, dl = 0;
+    for (uint64_t i = a; i < z; ++i) {
+      const uint32_t byte = (d[(i - sa) >> 2] >> (8 * ((i - sa) & 3))) & 0xffu;
+      const uint32_t e = T.step(cur, byte);
+      if (e == 0) {
+        dl = i + 1;
+        break;
+      }
+      cur = e;
+      if (e >= T.accb) {
+        lastl = i + 1;
+        lel = e;
+      }
+    }
+    const uint32_t prev = (uint32_t)__shfl_up((int)cur, 1, 64);
+    const bool seg = a < z;
+    const int nl = __popcll(__ballot(seg));
+    const uint64_t bad = __ballot(seg && lane != 0 && spec != prev);
+    const uint64_t dead = __ballot(seg && dl != 0);
+    const uint64_t accm = __ballot(lastl != 0);
+    const int j = bad ? __builtin_ctzll(bad) : nl;
+    const int dd = dead ? __builtin_ctzll(dead) : 64;
+    const uint64_t m = accm & lowbits((uint64_t)(dd < j ? dd + 1 : j));
+    if (m) {
+      const int k = 63 - __builtin_clzll(m);
+      lastw = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(lastl >> 32), k, 64) << 32) |
+              (uint32_t)__shfl((int)(uint32_t)lastl, k, 64);
+      lew = (uint32_t)__shfl((int)lel, k, 64);
+    }
+    if (dd < j) {
+      const uint64_t dp = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(dl >> 32), dd, 64) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)dl, dd, 64);
+      q = dp - 1;
+      return true;
+    }
+    s = (uint32_t)__shfl((int)cur, j - 1, 64);
+    const uint64_t qn = base + 16u * (uint32_t)j;
+    q = (j < nl || qn < lim) ? qn : lim;
+  }
+  return q >= w.rend;
+}
+
+constexpr uint64_t kOpenCoopBudget = 64ull << 20;  // bytes R1b walks one open walk on
+constexpr int kOpenCoopMax = 256;                  // open walks R1b takes at most (else the forest FIND)
 
 template <int FMT>
 __device__ __forceinline__ void resolve_open(const ScanParams& P, const Tab<FMT>& T, const Ctx& C, const Win& w, int G,
@@ -91,10 +182,44 @@ __device__ __forceinline__ void resolve_open(const ScanParams& P, const Tab<FMT>
     o->q = q;
     o->lastw = lastw;
     o->lew = lew;
+    o->sq = s;  // (R1b goes on from here)
     o->type = type;
   }
   __threadfence_block();
   __syncthreads();
+  // R1b: the walks R1 left unresolved, one wave each, when there are few
+  {
+    __shared__ uint32_t nunres;
+    if (tid == 0) nunres = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int b = j * kFixThreads + tid;
+      if (b < G && ((openm[b >> 5] >> (b & 31)) & 1u) && P.open[b].type == kOpenUnres) atomicAdd(&nunres, 1u);
+    }
+    __syncthreads();
+    if (nunres && nunres <= (uint32_t)kOpenCoopMax) {
+      for (int b = 0, k = 0; b < G; ++b) {
+        if (!((openm[b >> 5] >> (b & 31)) & 1u)) continue;
+        OpenRec* o = P.open + b;
+        if (o->type != kOpenUnres) continue;
+        if ((k++ % (kFixThreads / 64)) != wid) continue;
+        uint32_t s = o->sq, lew = o->lew;
+        uint64_t q = o->q, lastw = o->lastw;
+        const uint64_t lim = q + kOpenCoopBudget < w.rend ? q + kOpenCoopBudget : w.rend;
+        const bool done = s != 0 && coop_continue<FMT>(T, w, s, q, lim, lastw, lew);
+        if (lane == 0 && done) {
+          if (q >= w.rend && !w.eof) ovf = 1;
+          o->q = q;
+          o->lastw = lastw;
+          o->lew = lew;
+          o->type = kOpenDead;
+        }
+      }
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
   // R2
   if (wid == 0) {
     uint64_t carry = 0;
@@ -178,6 +303,12 @@ __device__ __forceinline__ void resolve_open(const ScanParams& P, const Tab<FMT>
     if (o.e > o.c) {
       d.put(C, o.c, o.e - o.c, o.le_e, +1);
       p = o.e;
+    } else if (w.dom && !P.acap && !P.wtab) {
+      // the open walk accepts nowhere: the positions it crossed in dominating
+      // states start nothing either (tables.hpp dom), up to the block end --
+      // all of them when every non-accepting state dominates (dom_all: the
+      // walk never accepted, so it crossed the block in such states)
+      p = P.dom_all ? (bhi > o.c + 1 ? bhi : o.c + 1) : dom_restart<FMT>(T, w, o.c, bhi);
     }
     // an end before the range end: the chain goes on from there (those
     // candidates were dropped by the COUNT pass)

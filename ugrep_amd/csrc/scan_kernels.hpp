@@ -83,7 +83,7 @@ struct OpenRec {
   uint32_t type;   // R1: kOpenDead / kOpenConv / kOpenUnres
   uint64_t e;      // R2: the walk's last accept overall (== c: it never accepts)
   uint32_t le_e;   // R2: its accepting entry
-  uint32_t pad;
+  uint32_t sq;     // R1: the walk's DFA entry at q (R1b goes on from there)
 };
 constexpr uint32_t kOpenDead = 1, kOpenConv = 2, kOpenUnres = 3;
 
@@ -96,6 +96,7 @@ struct PendSlot {
 };
 struct SuspRec {
   uint64_t x, widx, cnt, dg, dc, c1, e1, rs, sgn;
+  uint64_t lbr, lbs;  // loop-needle tables: the lookback carry (sparse_kernel.hip lb_batch)
   uint32_t wover, ovf, first, open, le1, sgover, tile, dn;
   PendSlot lanes[64];
 };
@@ -218,6 +219,13 @@ struct ScanParams {
   // (ft) finds the needle N; each candidate walks back over the bytes of C
   // (256-bit mask) to its run's start.  NULL: ft finds first bytes.
   const uint32_t* lb_cls;
+  // plain walks: the states that dominate the start state (tables.hpp dom;
+  // bit = state id), or NULL: a failed walk skips the positions it crossed in
+  // such states (device_common.hpp chain_step)
+  const uint32_t* dom;
+  // sparse_kernel: every non-accepting state dominates the start (tables.hpp
+  // dom_all): a failed long walk moves the chain past the byte it died on
+  uint32_t dom_all;
   uint32_t bol0;
   uint32_t nul;
   uint32_t ctx_word;

@@ -191,6 +191,7 @@ struct WaveChain {
   // position and run start
   uint64_t wlo;
   uint64_t lbr, lbs;
+  uint64_t whi;  // the range end (dominated restarts stop there)
 };
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
@@ -267,6 +268,7 @@ struct CoopWalk {
   uint32_t le;    // entry of the last accepting state
   uint32_t done;  // the walk ended: it died, or reached the end of the stream
   uint32_t ovf;   // it reached a readable end that is not the end of the stream
+  uint64_t dpos;  // it died: one past the byte it died on (else 0)
 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -291,7 +293,7 @@ __device__ __forceinline__ CoopWalk coop_walk(const lds_u16* trans, uint32_t acc
 {
   const int lane = threadIdx.x & 63;
   const uint64_t last16 = (rend - 1) & ~uint64_t(15);
-  CoopWalk r{last, s, le, 0u, 0u};
+  CoopWalk r{last, s, le, 0u, 0u, 0ull};
   while (q < lim) {
     const uint64_t base = q & ~uint64_t(15);
     const uint64_t sa = base + 16u * (uint32_t)lane;
@@ -318,11 +320,13 @@ __device__ __forceinline__ CoopWalk coop_walk(const lds_u16* trans, uint32_t acc
     }
     uint32_t cur = spec, lel = 0;
     uint64_t lastl = 0;  // (an accept position follows a consumed byte: never 0)
+    uint64_t dl = 0;
     bool died = false;
     for (uint64_t i = a; i < z; ++i) {
       const uint32_t e = trans[cur | scr[i - base]];
       if (e == 0) {
         died = true;
+        dl = i + 1;
         break;
       }
       cur = e;
@@ -348,6 +352,7 @@ __device__ __forceinline__ CoopWalk coop_walk(const lds_u16* trans, uint32_t acc
         r.le = (uint32_t)__builtin_amdgcn_readlane(lel, k);
       }
       r.done = 1;
+      r.dpos = readlane64(dl, d);
       return r;
     }
     const uint64_t m = accm & lowbits((uint64_t)j);
@@ -404,7 +409,7 @@ __device__ __forceinline__ void long_lane(int i, const BatchLane& L, int lane, u
 {
   const uint64_t ci = readlane64(L.c, i);
   CoopWalk r{ci + (uint32_t)__builtin_amdgcn_readlane(L.lr, i), (uint32_t)__builtin_amdgcn_readlane(L.s, i),
-             (uint32_t)__builtin_amdgcn_readlane(L.le, i), 0u, 0u};
+             (uint32_t)__builtin_amdgcn_readlane(L.le, i), 0u, 0u, 0ull};
   if (__builtin_amdgcn_readlane(L.st, i) == 1)
     r = coop_walk((const lds_u16*)T.trans, T.accb, P.g, P.rend, P.at_eof, (lds_u8*)scr, r.s,
                   ci + (uint32_t)__builtin_amdgcn_readlane(L.qr, i), r.last, r.le, lim);
@@ -454,6 +459,16 @@ __device__ __forceinline__ void long_lane(int i, const BatchLane& L, int lane, u
     }
   }
   resolve<WRITE, STAGE>(lane == i, L.c, r.last - ci, r.le, lane, C, P, w);
+  // dominated restarts (tables.hpp dom_all): the failed walk from ci (on the
+  // chain: batch_resolve hands over no candidate below w.x) crossed only
+  // states that dominate the start, so no position up to the byte it died on
+  // (or up to the end of the stream) starts a match: the chain resumes there,
+  // at most at the range end (the exit the position-by-position chain has)
+  if (P.dom_all && r.done && r.last == ci && !r.ovf) {
+    const uint64_t sk = r.dpos ? r.dpos : P.rend;
+    const uint64_t s2 = sk < w.whi ? sk : w.whi;
+    if (s2 > w.x) w.x = s2;
+  }
 }
 
 // Resolve a walked batch completely: in position order, each lane whose walk
@@ -870,6 +885,7 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : (W == kWalkCtx ? UGPU_S
   w.pend = 0;
   w.rs = w.ptile = 0;
   w.wlo = wlo;
+  w.whi = whi;
   w.lbr = w.lbs = wlo;
   // walk limit: with truncation (P.open) a walk still alive at the range end
   // of any wave but the last becomes the wave's open walk (fix_kernel); the
@@ -918,6 +934,8 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : (W == kWalkCtx ? UGPU_S
     w.e1 = sr.e1;
     w.le1 = sr.le1;
     w.rs = sr.rs;
+    w.lbr = sr.lbr;  // (the lookback carry: lane 0's walk-back stays bounded by the previous entry)
+    w.lbs = sr.lbs;
     i = sr.tile;
     const PendSlot ps = sr.lanes[lane];
     BatchLane L{ps.c, ps.s, ps.packed & 0xffu, (ps.packed >> 8) & 0xffu, ps.le, (ps.packed >> 16) & 0xffu,
@@ -983,6 +1001,9 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : (W == kWalkCtx ? UGPU_S
       const uint64_t r = lb_back_wave(P, whi, wlo, lane);
       {
         if (w.dn == (uint32_t)kDefer) {
+          // (a suspension in this flush resumes straight into this block: no
+          // tile is left to repeat)
+          w.ptile = te * kWaveTile;
           flush_deferred<WRITE, ABL, W, STAGE, RESUME, LB>(dl, scr, w.dn, lane, T, C, P, w, lim, gw);
           w.dn = 0;
         }
@@ -1013,6 +1034,8 @@ __global__ __launch_bounds__(kSpWaves * 64, RESUME ? 1 : (W == kWalkCtx ? UGPU_S
           sr->c1 = w.c1;
           sr->e1 = w.e1;
           sr->rs = w.rs;
+          sr->lbr = w.lbr;
+          sr->lbs = w.lbs;
           sr->sgn = w.sg.n;
           sr->wover = w.wover;
           sr->ovf = w.ovf;

@@ -207,6 +207,54 @@ bool restart_local(const std::vector<uint32_t>& nxt, uint32_t start, uint32_t fi
 // or more, the same strings as the start state (then a word of the language
 // splits greedily into tokens, and the longest match at p is the longest run
 // of consecutive tokens from p).
+// DfaTables::dom.  For each state s, a lock-step walk of the pairs (a, b)
+// reachable from (start, s) over one byte per column class: L(start) is not a
+// subset of L(s) iff some reachable pair has a accepting and b not (the dead
+// state 0 is the non-accepting sink; a pair with a dead is fine).  A search
+// that finds no bad pair proves every pair it visited (the inclusion is
+// closed under the successor relation), and those pairs are not searched
+// again.  Bounded work: past the budget the remaining states stay unset (no
+// skip, which is always safe).
+void build_dom(const std::vector<uint32_t>& nxt, uint32_t S, uint32_t first_acc, uint32_t start_sid,
+               const std::vector<int>& reps, std::vector<uint32_t>& dom)
+{
+  dom.assign((S + 31) / 32, 0u);
+  if (S > 1024) {
+    dom.clear();
+    return;
+  }
+  std::vector<uint8_t> good((size_t)S * S, 0);
+  std::vector<uint32_t> stamp((size_t)S * S, 0);
+  std::vector<uint32_t> todo;
+  uint64_t budget = 1ull << 25;  // pair x class steps over all states
+  for (uint32_t s = 1; s < S && budget; ++s) {
+    const uint32_t tag = s;
+    bool bad = false;
+    todo.clear();
+    auto visit = [&](uint32_t a, uint32_t b) {
+      if (a == 0) return;  // nothing accepted from the dead state
+      const size_t k = (size_t)a * S + b;
+      if (good[k] || stamp[k] == tag) return;
+      if (b == 0 || (a >= first_acc && b < first_acc)) {
+        bad = true;
+        return;
+      }
+      stamp[k] = tag;
+      todo.push_back((uint32_t)k);
+    };
+    visit(start_sid, s);
+    for (size_t i = 0; i < todo.size() && !bad; ++i) {
+      const uint32_t a = todo[i] / S, b = todo[i] % S;
+      for (int c : reps) visit(nxt[(size_t)a * 256 + c], nxt[(size_t)b * 256 + c]);
+      budget = budget > reps.size() ? budget - reps.size() : 0;
+      if (!budget) bad = true;
+    }
+    if (bad) continue;
+    for (uint32_t k : todo) good[k] = 1;
+    dom[s >> 5] |= 1u << (s & 31);
+  }
+}
+
 void build_xu(const std::vector<uint32_t>& nxt, uint32_t S, uint32_t first_acc, uint32_t start_sid, DfaTables& t)
 {
   auto acc = [&](uint32_t s) { return s >= first_acc; };
@@ -741,6 +789,34 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
             t.xtrans[(size_t)s * R + col] = (uint16_t)x;
           }
         }
+    }
+  }
+  // dominated restarts (tables.hpp dom) for the plain walks
+  if (!anchored && !word) {
+    std::vector<int> reps;
+    std::vector<bool> seen_cls(256, false);
+    for (int c = 0; c < 256; ++c)
+      if (!seen_cls[cls[c]]) {
+        seen_cls[cls[c]] = true;
+        reps.push_back(c);
+      }
+    build_dom(nxt, S, first_acc, start_sid, reps, t.dom);
+    if (!t.dom.empty()) {
+      std::vector<bool> seen(S, false);
+      std::vector<uint32_t> order{start_sid};
+      seen[start_sid] = true;
+      t.dom_all = true;
+      for (size_t i = 0; i < order.size() && t.dom_all; ++i) {
+        const uint32_t a = order[i];
+        if (a != start_sid && a < first_acc && !((t.dom[a >> 5] >> (a & 31)) & 1u)) t.dom_all = false;
+        for (int c : reps) {
+          const uint32_t n = nxt[(size_t)a * 256 + c];
+          if (n && !seen[n]) {
+            seen[n] = true;
+            order.push_back(n);
+          }
+        }
+      }
     }
   }
   // immediate transducer (tables.hpp, xi_kernel.hip)

@@ -144,6 +144,18 @@ struct DfaTables {
   // shape: the language is finite (acyclic DFA); a state whose accept depends
   // on the word context also has byte edges
   bool finite = false, word_cond_edges = false;
+  // Dominated restarts (device_common.hpp chain_step): bit s (state id) is set
+  // when L(start) is a subset of L(s), i.e. every string a walk from the start
+  // state accepts is accepted from s too.  A walk from p that fails (no
+  // accept) and is in such a state at q shows that the walk from q fails as
+  // well, so the FIND chain may skip q: a needle-free run is crossed with one
+  // walk instead of one walk per position.  Empty: not computed (anchored or
+  // word-context tables, or more states than the budget allows).
+  std::vector<uint32_t> dom;
+  // every non-accepting state reachable from the start dominates it: a failed
+  // walk (it never accepts) then lets the chain skip every position it
+  // crossed, up to the byte it died on (sparse_kernel's long walks)
+  bool dom_all = false;
   std::vector<uint32_t> acap;  // states * 4, or states * 64 (ctx_word)
 };
 

@@ -171,6 +171,22 @@ def host_xu(opc):
     return (tab, bm3) if ok.value else None
 
 
+def host_dom(opc, want_all=False):
+    """Dominated-restart bits of the dense tables (tables.hpp dom): a bool
+    numpy array over state ids (ugpu_tables_build_host numbering), or None
+    when they were not computed; want_all: (bits, dom_all)."""
+    a, p = _as_u32(opc)
+    n = ctypes.c_uint32(0)
+    al = ctypes.c_int(0)
+    check(lib.ugpu_tables_dom_host(p, len(a), None, 0, ctypes.byref(n), ctypes.byref(al)))
+    bits = None
+    if n.value:
+        w = np.zeros(n.value, np.uint32)
+        check(lib.ugpu_tables_dom_host(p, len(a), w.ctypes.data_as(_lib.c_u32p), n.value, ctypes.byref(n), None))
+        bits = np.unpackbits(w.view(np.uint8), bitorder="little").astype(bool)
+    return (bits, bool(al.value)) if want_all else bits
+
+
 class Pattern:
     """Compiled pattern (opcode words) with its device tables."""
 
