@@ -255,6 +255,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pcie-sample-mib", type=int, default=2048,
                     help="host-buffer sample for the PCIe-inclusive leg (0 = skip)")
+    ap.add_argument("--offsets-exchange", choices=("auto", "gather", "sharded"), default="auto",
+                    help="N>1 --offsets: gather the records to rank 0 (SURVEY 8e step 4), keep them on their ranks "
+                         "and exchange only their sums (dist.verify_sharded), or auto: gather when all records "
+                         "fit in %d GiB at the root, else sharded (dense tables at 8 ranks: ~120 GB)" % 8)
     ap.add_argument("--offsets", action="store_true",
                     help="each step also materialises the match records (start, len, accept) in HBM and, "
                          "for N > 1, all-gathers them to every rank (SURVEY.md §8e step 4)")
@@ -286,6 +290,7 @@ def main():
     from ugrep_amd import dist as _d
     ugrep_amd, gather_offsets, Shard, shard_bounds, stitch = (_u, _d.gather_offsets, _d.Shard, _d.shard_bounds,
                                                              _d.stitch)
+    verify_sharded = _d.verify_sharded
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -359,7 +364,10 @@ def main():
     # (C3, C4); 16 bytes with the accept index otherwise (C2: 3)
     one_accept = bool(info["shape"] & ugrep_amd._lib.SHAPE_ONE_ACCEPT)
 
-    def records(count):
+    rec_bytes = 12 if one_accept else 16
+    gather_limit = 8 << 30  # record bytes at the root that --offsets-exchange auto still gathers
+
+    def records(count, total_count=None):
         if recs_dev.get("cap", -1) < count:
             cap = count + count // 8 + 1024
             recs_dev.update(cap=cap, start=torch.empty(cap, dtype=torch.int64, device=dev),
@@ -371,11 +379,18 @@ def main():
         st, ln = recs_dev["start"][:count], recs_dev["len"][:count]
         ac = None if acc is None else acc[:count]
         if pg:
+            ex = args.offsets_exchange
+            if ex == "auto":
+                ex = "gather" if (total_count or 0) * rec_bytes <= gather_limit else "sharded"
+            if ex == "sharded":
+                # records stay on their ranks; their sums travel (one all_gather of
+                # 4 x 8 B per rank) and are checked against the stitched totals
+                return ([st], [ln], [ac], "sharded")
             # to rank 0 only, as per-rank parts (dist.gather_offsets: an
             # all_gather of dense tables' records would not fit at 8 ranks)
             g = gather_offsets(st.to(xdev), ln.to(xdev), None if ac is None else ac.to(xdev), dst=0, concat=False)
-            return ([st], [ln], [ac]) if g is None else g  # (ranks > 0: their own, for the digest check)
-        return [st], [ln], [ac]
+            return (([st], [ln], [ac]) if g is None else g) + ("gather",)  # (ranks > 0: their own)
+        return [st], [ln], [ac], "local"
 
     def step():
         rec = shard.scan()
@@ -389,7 +404,11 @@ def main():
                 count = shard.scan(rec["entries"][rank])["count"]
             elif pg:
                 count = rec["counts"][rank]
-            rec["records"] = records(count)
+            rec["records"] = records(count, rec["count"])
+            if rec["records"][3] == "sharded":
+                sts, lns, acs, _ = rec["records"]
+                # (the sums are taken where the records are; only they move)
+                rec["verify"] = verify_sharded(sts[0], lns[0], acs[0], rec, device=xdev)
         return rec
 
     for _ in range(args.warmup):
@@ -494,13 +513,20 @@ def main():
     if verified is not None:
         out["verified_whole_stream"] = verified
     if args.offsets:
-        sts, lns, _ = res["records"]
+        sts, lns, _, how = res["records"]
         m64 = (1 << 64) - 1
-        nrec = sum(int(s_.numel()) for s_ in sts)
-        dg = sum(int((s_ * 31 + l_.to(torch.int64)).sum().item()) for s_, l_ in zip(sts, lns)) & m64  # (wraps as u64)
-        out["offsets"] = {"records": nrec, "bytes_per_record": 12 if one_accept else 16,
-                          "gathered_to": "rank 0 (per-rank parts)" if pg else "local",
-                          "digest_matches_totals": nrec == res["count"] and dg == res["digest"]}
+        if how == "sharded":
+            ver = res["verify"]
+            out["offsets"] = {"records": ver["count"], "bytes_per_record": rec_bytes,
+                              "gathered_to": "none: records stay on their ranks, their sums are all-gathered "
+                                             "(dist.verify_sharded)",
+                              "digest_matches_totals": bool(ver["ok"])}
+        else:
+            nrec = sum(int(s_.numel()) for s_ in sts)
+            dg = sum(int((s_ * 31 + l_.to(torch.int64)).sum().item()) for s_, l_ in zip(sts, lns)) & m64  # (wraps as u64)
+            out["offsets"] = {"records": nrec, "bytes_per_record": rec_bytes,
+                              "gathered_to": "rank 0 (per-rank parts)" if pg else "local",
+                              "digest_matches_totals": nrec == res["count"] and dg == res["digest"]}
         if shard.grown:
             out["offsets"]["halo_grown"] = shard.grown
     # (the committed PMC traffic is per BASELINE config and pattern)

@@ -451,6 +451,10 @@ const char *ugpu_compile_error(void);
 
 const char *ugpu_last_error(void);
 const char *ugpu_version(void);
+/* Provenance of the device library: "src:<hash of ugrep_amd/csrc and this
+   header (tools/srchash.py)> git:<commit it was built at>".  The Python
+   binding warns when the hash differs from the sources beside the library. */
+const char *ugpu_build_id(void);
 /* UGPU_ABI_VERSION of the header the library was built with */
 int ugpu_abi_version(void);
 

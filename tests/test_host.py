@@ -2,6 +2,7 @@
 builder (opcode words -> dense device tables) reproduces the reference's
 matches when walked on the CPU with the exact FIND chain."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -9,6 +10,8 @@ import pytest
 import ugrep_amd
 from ugrep_amd import _lib
 from oracle_lib import case_input
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # line anchors (anchor_bol, anchor_eol) are supported since round 3 and word
 # boundaries since round 4 (per-context accepts: tests/test_anchor.py,
@@ -23,6 +26,19 @@ def test_exports_every_declared_symbol():
     for n in names:
         assert hasattr(_lib.lib, n), n
     assert ugrep_amd.lib.ugpu_version().startswith(b"ugrep_amd")
+
+
+def test_build_id_matches_sources():
+    """Provenance: the loaded libugrep_amd.so embeds the hash of the sources it
+    was built from (ugpu_build_id, tools/srchash.py); _lib warns on a stale one."""
+    import subprocess
+    import sys
+    from ugrep_amd import _lib
+    bid, ok = _lib.build_id()
+    assert bid.startswith("src:") and " git:" in bid, bid
+    assert ok, (bid, _lib._source_hash())
+    here = subprocess.check_output([sys.executable, os.path.join(REPO, "tools", "srchash.py"), REPO], text=True)
+    assert bid.split()[0] == "src:" + here.strip()
 
 
 def test_unsupported_patterns(patterns):

@@ -139,6 +139,7 @@ def _load():
         "ugpu_compile_error": (ctypes.c_char_p, []),
         "ugpu_last_error": (ctypes.c_char_p, []),
         "ugpu_version": (ctypes.c_char_p, []),
+        "ugpu_build_id": (ctypes.c_char_p, []),
         "ugpu_abi_version": (ctypes.c_int, []),
         "ugpu_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
         "ugpu_find_records": (ctypes.c_int, [V, V, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(V)]),
@@ -162,6 +163,45 @@ def _load():
 
 
 lib = _load()
+
+
+def _source_hash():
+    """tools/srchash.py's hash of the sources beside this package (None when
+    they are not there, e.g. an installed copy)."""
+    import hashlib
+    repo = os.path.dirname(HERE)
+    csrc = os.path.join(HERE, "csrc")
+    hdr = os.path.join(repo, "include", "ugpu.h")
+    if not os.path.isdir(csrc) or not os.path.exists(hdr):
+        return None
+    h = hashlib.sha256()
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc)
+                   if f.endswith((".hip", ".hpp", ".cpp", ".inc", ".h")))
+    for f in files + [hdr]:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id():
+    """(library build id, whether it matches the sources beside it): the id is
+    "src:<hash> git:<commit>" (ugpu_build_id, ugrep_amd/Makefile)."""
+    bid = lib.ugpu_build_id().decode()
+    src = _source_hash()
+    return bid, src is None or bid.startswith("src:%s " % src)
+
+
+def _check_provenance():
+    import warnings
+    bid, ok = build_id()
+    if not ok:
+        warnings.warn("%s was not built from the sources beside it (%s, sources src:%s): rebuild with "
+                      "make -C ugrep_amd" % (os.path.basename(LIB_PATH), bid, _source_hash()), RuntimeWarning)
+
+
+if os.path.basename(LIB_PATH) == "libugrep_amd.so":  # (variant builds share the id of the default one)
+    _check_provenance()
 
 
 def check(rc):

@@ -662,6 +662,9 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   return UGPU_OK;
 }
 
+extern const char* ugpu_build_id_str;  // (build/build_id.cpp, written by the Makefile)
+const char* ugpu_build_id(void) { return ugpu_build_id_str; }
+
 int ugpu_dfa_info_get(const ugpu_dfa* d, ugpu_dfa_info* info)
 {
   if (!d || !info) return fail(UGPU_INVAL, "NULL argument");
