@@ -89,6 +89,7 @@ typedef struct ugpu_dfa_info
 #define UGPU_SHAPE_FINITE 1u     /* the language is finite (no cycle in the DFA) */
 #define UGPU_SHAPE_WORD_COND 2u  /* a state whose accept depends on a word boundary also has byte edges */
 #define UGPU_SHAPE_ONE_ACCEPT 4u /* every match has the same accept index: 12-byte records (ugpu_scan_offsets d_cap NULL) */
+#define UGPU_SHAPE_LOOKAHEAD 16u /* lookahead (X(?=Y): TAIL/HEAD words): the lookahead walk on wfind_kernel */
 #define UGPU_SHAPE_LOOP_NEEDLE 8u /* C+ N on the sparse kernel: the prefilter looks for the needle N and walks back
                                      (UGPU_LB=0 disables) */
 

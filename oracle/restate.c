@@ -17,16 +17,21 @@
  *     0x00FFFFFF, LONG idx 0xFFFE + next word, TAKE 0xFE..).  TAKE at the head
  *     of a block (lib/pattern.cpp:2945-2952) makes the state accepting; so
  *     does REDO (0xFD000000, a negative pattern's accept, ugrep -N
- *     '(?^...)'), with the accept ORC_REDO.  TAIL/HEAD, meta edges other than
- *     META_BOL / META_EOL and the word boundaries META_WBB .. META_EWE
- *     (pattern.h:933-943), and REDO in a table with meta edges are rejected
- *     (ORC_UNSUPPORTED); meta edges are kept per state in block order
- *     (orc_find_a).
+ *     '(?^...)'), with the accept ORC_REDO.  TAIL/HEAD (lookahead, indices
+ *     below ORC_MAXLOOK) are kept per state as bit masks (look[]); meta edges
+ *     other than META_BOL / META_EOL and the word boundaries META_WBB ..
+ *     META_EWE (pattern.h:933-943), REDO in a table with meta edges, and
+ *     lookahead with meta edges or REDO are rejected (ORC_UNSUPPORTED); meta
+ *     edges are kept per state in block order (orc_find_a).
  *   orc_find -- the FIND driver of Matcher::match (lib/matcher.cpp:42-750) for
  *     tables without meta/lookahead, options A/N/W off: from p walk the DFA,
  *     remember the last TAKE (:139-150, :207-217), stop on HALT/EOF (:448-459,
  *     :528-541); emit the longest non-empty match and resume at its end
- *     (:681, :735-737), otherwise retry at p+1 (:635-661, :692-713).  A match
+ *     (:681, :735-737), otherwise retry at p+1 (:635-661, :692-713).  With
+ *     lookahead (:157-175) every state entry runs its block in order: TAKE
+ *     (last = here), then each TAIL la (last = the position HEAD la recorded
+ *     in this walk, if any), then each HEAD la (record here); the records are
+ *     cleared per walk (:104).  A match
  *     whose last accept is REDO is not emitted and the search resumes at its
  *     end (:732-738 "ignore accept and continue"; an empty one moves to p+1
  *     as any empty match, :682-713).  The adv_
@@ -50,6 +55,7 @@
 #define ORC_NOMEM 3
 
 #define ORC_MAXMETA 4
+#define ORC_MAXLOOK 8 /* lookahead indices per table (TAIL/HEAD words) */
 #define ORC_REDO 0xffffffffu /* the accept of a REDO state (never an accept index: those have 24 bits) */
 typedef struct orc_dfa
 {
@@ -59,6 +65,8 @@ typedef struct orc_dfa
   uint32_t *accept; /* [nstates], 0 = not accepting */
   uint32_t *meta;   /* [nstates][ORC_MAXMETA]: (META - META_MIN) << 24 | target state, in block order; 0 = none */
   int anchored;     /* some state has a meta edge */
+  uint32_t *look;   /* [nstates]: TAIL la -> bit la, HEAD la -> bit 8 + la */
+  int lookahead;    /* some state has TAIL/HEAD words */
 } orc_dfa;
 
 static int is_goto(uint32_t w) { return (uint32_t)(w << 8) >= (w & 0xff000000u); }
@@ -71,6 +79,7 @@ void orc_dfa_free(orc_dfa *d)
   free(d->next);
   free(d->accept);
   free(d->meta);
+  free(d->look);
   free(d);
 }
 
@@ -89,7 +98,8 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
   d->next = (uint32_t *)calloc((size_t)cap * 256, sizeof(uint32_t));
   d->accept = (uint32_t *)calloc(cap, sizeof(uint32_t));
   d->meta = (uint32_t *)calloc((size_t)cap * ORC_MAXMETA, sizeof(uint32_t));
-  if (!d->next || !d->accept || !d->meta)
+  d->look = (uint32_t *)calloc(cap, sizeof(uint32_t));
+  if (!d->next || !d->accept || !d->meta || !d->look)
     goto nomem;
   id[0] = ns++;
   queue[nq++] = 0;
@@ -118,6 +128,13 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
           goto nomem;
         d->meta = nm;
         memset(d->meta + (size_t)cap * ORC_MAXMETA, 0, (size_t)(ncap - cap) * ORC_MAXMETA * sizeof(uint32_t));
+      }
+      {
+        uint32_t *nl = (uint32_t *)realloc(d->look, ncap * sizeof(uint32_t));
+        if (!nl)
+          goto nomem;
+        d->look = nl;
+        memset(d->look + cap, 0, (ncap - cap) * sizeof(uint32_t));
       }
       memset(d->next + (size_t)cap * 256, 0, (size_t)(ncap - cap) * 256 * sizeof(uint32_t));
       memset(d->accept + cap, 0, (ncap - cap) * sizeof(uint32_t));
@@ -151,8 +168,14 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
           if (idx == 0xfffe)
             ++g;
         }
+        else if ((op == 0xfc || op == 0xfb) && (w & 0xffffff) < ORC_MAXLOOK)
+        {
+          /* TAIL / HEAD (pattern.h:1167-1174, lookahead_of: the low 16 bits) */
+          d->look[s] |= (op == 0xfc ? 1u : 0x100u) << (w & 0xffff);
+          d->lookahead = 1;
+        }
         else
-          goto unsupported; /* REDO, TAIL, HEAD, other metas */
+          goto unsupported; /* other metas, lookahead indices past ORC_MAXLOOK */
         ++g;
       }
     }
@@ -220,8 +243,11 @@ int orc_dfa_build(const uint32_t *opc, uint32_t nop, orc_dfa **out)
           if (d->next[(size_t)t * 256 + b] != 0)
             goto unsupported;
       }
-    /* REDO with meta edges: not restated (the engine refuses it too) */
-    if (d->anchored)
+    /* REDO with meta edges, lookahead with meta edges or REDO: not restated
+       (the engine refuses them too) */
+    if (d->lookahead && d->anchored)
+      goto unsupported;
+    if (d->anchored || d->lookahead)
       for (s = 1; s < ns; ++s)
         if (d->accept[s] == ORC_REDO)
           goto unsupported;
@@ -250,11 +276,49 @@ nomem:
 uint32_t orc_dfa_nstates(const orc_dfa *d) { return d->nstates; }
 
 /* One FIND step at p (< n): returns match length (0 = none) and the accept. */
+/* a state's block on entry at q in a walk from p (lookahead tables):
+   TAKE, then TAIL la ascending, then HEAD la ascending (lib/matcher.cpp:139-175) */
+static inline void orc_enter(const orc_dfa *d, uint32_t s, uint64_t p, uint64_t q, uint64_t *last, uint32_t *a,
+                             int64_t *lap)
+{
+  uint32_t lk = d->look[s], la;
+  if (d->accept[s])
+  {
+    *last = q;
+    *a = d->accept[s];
+  }
+  for (la = 0; la < ORC_MAXLOOK; ++la)
+    if (((lk >> la) & 1u) && lap[la] >= 0)
+      *last = p + (uint64_t)lap[la];
+  for (la = 0; la < ORC_MAXLOOK; ++la)
+    if ((lk >> (8 + la)) & 1u)
+      lap[la] = (int64_t)(q - p);
+}
+
 static inline uint64_t orc_step(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t p, uint32_t *acc)
 {
   uint32_t s = d->start;
   uint64_t q = p, last = p;
   uint32_t a = 0;
+  if (d->lookahead)
+  {
+    int64_t lap[ORC_MAXLOOK];
+    int k;
+    for (k = 0; k < ORC_MAXLOOK; ++k)
+      lap[k] = -1;
+    orc_enter(d, s, p, q, &last, &a, lap);
+    while (q < n)
+    {
+      uint32_t t = d->next[(size_t)s * 256 + buf[q]];
+      if (t == 0)
+        break;
+      s = t;
+      ++q;
+      orc_enter(d, s, p, q, &last, &a, lap);
+    }
+    *acc = a;
+    return last - p;
+  }
   while (q < n)
   {
     uint32_t t = d->next[(size_t)s * 256 + buf[q]];

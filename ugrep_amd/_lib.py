@@ -19,7 +19,7 @@ UGPU_DEVICE = 4
 UGPU_HALO = 5
 UGPU_CAPACITY = 6
 
-SHAPE_FINITE, SHAPE_WORD_COND, SHAPE_ONE_ACCEPT, SHAPE_LOOP_NEEDLE = 1, 2, 4, 8
+SHAPE_FINITE, SHAPE_WORD_COND, SHAPE_ONE_ACCEPT, SHAPE_LOOP_NEEDLE, SHAPE_LOOKAHEAD = 1, 2, 4, 8, 16
 
 MODE_COUNT = 0
 MODE_OFFSETS = 1

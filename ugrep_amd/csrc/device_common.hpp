@@ -62,6 +62,8 @@ struct Win {
   const uint32_t* lb = nullptr;
   // dominated restarts (ScanParams::dom): bit = state id
   const uint32_t* dom = nullptr;
+  // lookahead (ScanParams::look, walk mode kWalkLook): per state TAIL / HEAD masks
+  const uint32_t* look = nullptr;
   // an LDS copy of bytes [wa, wa + wn) that the W / context walks read instead
   // of global memory (sparse_kernel's per-lane candidate window; wn = 0: none)
   const uint8_t* wl = nullptr;
@@ -78,7 +80,7 @@ __device__ __forceinline__ uint32_t wbyte(const struct Win& w, uint64_t k)
 }
 
 // Walk modes (template argument W of walk / chain_step / merge)
-constexpr int kWalkPlain = 0, kWalkWord = 1, kWalkCtx = 2;
+constexpr int kWalkPlain = 0, kWalkWord = 1, kWalkCtx = 2, kWalkLook = 3;
 
 // The window of a scan: bytes from global memory, W / anchor context from P.
 __device__ __forceinline__ Win win_of(const ScanParams& P)
@@ -101,6 +103,7 @@ __device__ __forceinline__ Win win_of(const ScanParams& P)
   w.amap = P.amap;
   w.lb = P.lb_cls;
   w.dom = P.dom;
+  w.look = P.look;
   return w;
 }
 
@@ -349,6 +352,39 @@ __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64
         last = q;
         le = e;
       }
+    }
+    if (!w.eof) ovf = 1;
+    return last - p;
+  }
+  if constexpr (W == kWalkLook) {
+    // lookahead (tables.hpp look): each state's block on entry, as the
+    // reference runs it (lib/matcher.cpp:139-175): TAKE (the match would end
+    // here), TAIL la (it ends where HEAD la was recorded in this walk, if it
+    // was), HEAD la (record here); records cleared per walk (:104)
+    uint32_t lap[4] = {~0u, ~0u, ~0u, ~0u};  // (offsets from p; ~0: not recorded)
+    auto enter = [&](uint32_t e, uint64_t at) __attribute__((always_inline)) {
+      if (e >= T.accb) {
+        last = at;
+        le = e;
+      }
+      const uint32_t lk = w.look[e >> w.log_row];
+      if (lk) {
+#pragma unroll
+        for (int la = 0; la < 4; ++la)
+          if (((lk >> la) & 1u) && lap[la] != ~0u) last = p + lap[la];
+#pragma unroll
+        for (int la = 0; la < 4; ++la)
+          if ((lk >> (8 + la)) & 1u) lap[la] = (uint32_t)(at - p);
+      }
+    };
+    enter(s, q);
+    if (last == p) le = 0;  // (an empty match at p is no match: the chain moves to p + 1)
+    while (q < w.rend) {
+      const uint32_t e = T.step(s, wbyte(w, q));
+      if (e == 0) return last - p;
+      s = e;
+      ++q;
+      enter(e, q);
     }
     if (!w.eof) ovf = 1;
     return last - p;

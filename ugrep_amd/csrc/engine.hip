@@ -103,6 +103,7 @@ struct ugpu_dfa {
   uint8_t lb_ft[20] = {};
   uint32_t* d_lbcls = nullptr;  // 256-bit mask of C
   uint32_t* d_dom = nullptr;    // dominated restarts (tables.hpp dom), or NULL
+  uint32_t* d_look = nullptr;   // lookahead TAIL / HEAD masks per state (tables.hpp look), or NULL
   // idle scanners of ugpu_find_all calls on this table (reused: creating one
   // costs device allocations and property queries)
   std::mutex pool_mu;
@@ -309,6 +310,7 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
               ((uint32_t)ft[4 * i + 3] << 24);
   P.lb_cls = d->lb ? d->d_lbcls : nullptr;
   P.dom = d->d_dom;
+  P.look = d->d_look;
   P.dom_all = d->d_dom && d->t.dom_all ? 1u : 0u;
   if (d->lb) P.wstart = 0;  // (the candidates are needle positions, not match starts)
 }
@@ -551,6 +553,12 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     ugpu_dfa_destroy(d);
     return hip_fail(e, "loop class upload");
   }
+  if (d->t.lookahead &&
+      ((e = hipMalloc(&d->d_look, d->t.look.size() * 4)) != hipSuccess ||
+       (e = hipMemcpy(d->d_look, d->t.look.data(), d->t.look.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)) {
+    ugpu_dfa_destroy(d);
+    return hip_fail(e, "lookahead upload");
+  }
   // (UGPU_DOM=0: no dominated-restart skips; testing)
   const char* domenv = std::getenv("UGPU_DOM");
   if (!d->t.dom.empty() && !(domenv && domenv[0] == '0') &&
@@ -658,6 +666,7 @@ int ugpu_dfa_destroy(ugpu_dfa* d)
   if (d->d_acap) (void)hipFree(d->d_acap);
   if (d->d_lbcls) (void)hipFree(d->d_lbcls);
   if (d->d_dom) (void)hipFree(d->d_dom);
+  if (d->d_look) (void)hipFree(d->d_look);
   delete d;
   return UGPU_OK;
 }
@@ -731,7 +740,9 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
   const bool sp_off = senv0 && senv0[0] == '0';
   const bool ctx_sparse = dfa->amode && dfa->t.filter && dfa->t.format == FMT_BYTE && !sp_off;
   const bool w_sparse = (dfa->t.filter || dfa->lb || dfa->wsparse) && dfa->t.format == FMT_BYTE && !sp_off;
-  if ((dfa->amode && !ctx_sparse) || dfa->t.format == FMT_WIDE || (dfa->d_wtab && !dfa->amode && !w_sparse)) {
+  // lookahead tables: the lookahead walk (kWalkLook) on wfind_kernel
+  if ((dfa->amode && !ctx_sparse) || dfa->t.format == FMT_WIDE || dfa->t.lookahead ||
+      (dfa->d_wtab && !dfa->amode && !w_sparse)) {
     const uint32_t nacap = !dfa->amode ? dfa->t.states
                            : dfa->t.ctx_word ? (uint32_t)dfa->t.acap_rows.size() : (uint32_t)dfa->t.acap.size();
     const uint32_t nmap = dfa->amode && dfa->t.ctx_word ? dfa->t.states : 0u;

@@ -422,6 +422,10 @@ hipError_t launch_forest(const ScanParams& P, uint32_t format, const ForestArgs&
     return format == 0   ? forest_fmt<0, kWalkWord>(P, A, entry, write, tot, st)
            : format == 1 ? forest_fmt<1, kWalkWord>(P, A, entry, write, tot, st)
                          : forest_fmt<2, kWalkWord>(P, A, entry, write, tot, st);
+  if (P.look)
+    return format == 0   ? forest_fmt<0, kWalkLook>(P, A, entry, write, tot, st)
+           : format == 1 ? forest_fmt<1, kWalkLook>(P, A, entry, write, tot, st)
+                         : forest_fmt<2, kWalkLook>(P, A, entry, write, tot, st);
   return format == 0   ? forest_fmt<0, kWalkPlain>(P, A, entry, write, tot, st)
          : format == 1 ? forest_fmt<1, kWalkPlain>(P, A, entry, write, tot, st)
                        : forest_fmt<2, kWalkPlain>(P, A, entry, write, tot, st);

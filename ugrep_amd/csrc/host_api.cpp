@@ -131,6 +131,13 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags, int lb)
   DfaPlan p;
   p.nul = (flags & UGPU_PAT_EMPTY) != 0;
   p.amode = t.anchored || (p.nul && t.start_acc);
+  if (t.lookahead) {
+    // lookahead tables: the lookahead walk on wfind_kernel (tables.hpp look);
+    // option W, and option N with empty matches, are not modelled with
+    // lookahead (the CPU matcher keeps those)
+    p.ok = !(flags & UGPU_PAT_WORD) && !p.amode;
+    return p;
+  }
   if (t.redo && ((flags & UGPU_PAT_WORD) || p.amode)) {
     // (negative patterns under option W, or with empty matches under option
     // N: the reference's REDO skips at_we and reports an empty REDO match;
@@ -194,7 +201,8 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* out)
   info->accepting = t.accepting;
   info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;
   info->shape = (t.finite ? UGPU_SHAPE_FINITE : 0u) | (t.word_cond_edges ? UGPU_SHAPE_WORD_COND : 0u) |
-                (t.cap1 != 0 && !t.anchored ? UGPU_SHAPE_ONE_ACCEPT : 0u) | (p.lb ? UGPU_SHAPE_LOOP_NEEDLE : 0u);
+                (t.cap1 != 0 && !t.anchored ? UGPU_SHAPE_ONE_ACCEPT : 0u) | (p.lb ? UGPU_SHAPE_LOOP_NEEDLE : 0u) |
+                (t.lookahead ? UGPU_SHAPE_LOOKAHEAD : 0u);
   const char* xenv = std::getenv("UGPU_XI");
   const char* genv = std::getenv("UGPU_XG");
   const char* cenv = std::getenv("UGPU_XC");
@@ -205,7 +213,9 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* out)
   const bool xc = t.xc && !t.filter && !p.lb && t.cap1 != 0 && (!p.wtab || p.xcw) && !(cenv && cenv[0] == '0');
   const bool xu = p.xu && (!p.wtab || p.wplus) && !(uenv && uenv[0] == '0');
   // (context accepts on a prefiltered table: sparse_kernel's context walks)
-  info->kernel = (p.amode && !byte_filter) || t.format == FMT_WIDE || (p.wtab && !p.wplus && !p.xcw && !byte_filter) ? 4u
+  info->kernel = (p.amode && !byte_filter) || t.format == FMT_WIDE || t.lookahead ||
+                         (p.wtab && !p.wplus && !p.xcw && !byte_filter)
+                     ? 4u
                  : byte_filter                                                                  ? 0u
                  : xc                                                                           ? 5u
                  : xu                                                                           ? 6u
@@ -234,7 +244,7 @@ int ugpu_dfa_plan_host(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags
   int rc = build_tables(opc, nop, t, err);
   if (rc != 0) return fail(rc == 1 ? UGPU_UNSUPPORTED : UGPU_INVAL, err);
   const DfaPlan pl = dfa_plan(t, pattern_flags);
-  if (!pl.ok) return fail(UGPU_UNSUPPORTED, "option W with line anchors, empty matches or negative patterns");
+  if (!pl.ok) return fail(UGPU_UNSUPPORTED, "option W with line anchors, empty matches, negative patterns or lookahead");
   dfa_info_fill(t, pl, info);
   return UGPU_OK;
 }

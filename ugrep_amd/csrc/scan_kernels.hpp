@@ -223,6 +223,9 @@ struct ScanParams {
   // bit = state id), or NULL: a failed walk skips the positions it crossed in
   // such states (device_common.hpp chain_step)
   const uint32_t* dom;
+  // lookahead tables (tables.hpp look): per state TAIL / HEAD masks, or NULL;
+  // every walk of such a table is the lookahead walk (device_common.hpp kWalkLook)
+  const uint32_t* look;
   // sparse_kernel: every non-accepting state dominates the start (tables.hpp
   // dom_all): a failed long walk moves the chain past the byte it died on
   uint32_t dom_all;

@@ -25,6 +25,7 @@ inline bool word_is_goto(uint32_t w) { return (uint32_t)(w << 8) >= (w & 0xff000
 inline bool word_is_meta(uint32_t w) { return (w & 0x00ff0000u) == 0 && (w >> 24) > 0; }
 
 constexpr uint32_t kHalt = 0xffff;
+constexpr uint32_t kMaxLook = 4;  // lookahead indices the engine keeps per walk (tables.hpp look)
 constexpr uint32_t kLong = 0xfffe;
 constexpr int64_t kDead = -1;
 
@@ -33,6 +34,7 @@ struct RawState {
   uint32_t cap;
   int64_t target_pc[256];
   std::vector<std::pair<uint32_t, uint32_t> > metas;  // (META code - 0x100, target pc) in block order
+  uint32_t look = 0;  // lookahead: TAIL la -> bit la, HEAD la -> bit 8 + la (tables.hpp look)
 };
 
 constexpr uint32_t kMetaBol = 0x09, kMetaEol = 0x0a;  // META_BOL / META_EOL - META_MIN (pattern.h:942-943)
@@ -465,6 +467,8 @@ bool tables_equivalent(const DfaTables& a, const DfaTables& b)
     } else if (a.caps[p.first] != b.caps[p.second]) {
       return false;
     }
+    // (lookahead: the same TAIL/HEAD words in both states)
+    if ((a.lookahead ? a.look[p.first] : 0u) != (b.lookahead ? b.look[p.second] : 0u)) return false;
     for (int c = 0; c < 256; ++c) {
       const std::pair<uint32_t, uint32_t> q(norm(la, step(a, p.first, c)), norm(lb, step(b, p.second, c)));
       if (seen.insert(q).second) work.push_back(q);
@@ -496,6 +500,12 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
         cap = w & 0xffffff;
       } else if (w == 0xFD000000u) {
         cap = kCapRedo;  // REDO (lib/pattern.cpp:2945-2947): a negative pattern's accept
+      } else if ((op == 0xfc || op == 0xfb) && (w & 0xffffff) < kMaxLook) {
+        // TAIL / HEAD la (lib/pattern.cpp:2953-2964; lookahead_of = the low 16 bits)
+        raw[qi].look |= (op == 0xfc ? 1u : 0x100u) << (w & 0xffff);
+      } else if (op == 0xfc || op == 0xfb) {
+        err = "more lookaheads than the engine keeps";
+        return 1;
       } else if (word_is_meta(w)) {
         const uint32_t idx = w & 0xffff;
         if (op != kMetaBol && op != kMetaEol && !(op >= kMetaWordMin && op <= kMetaWordMax)) {
@@ -521,7 +531,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
           raw.push_back(RawState{(uint32_t)t, 0, {}, {}});
         }
       } else {
-        err = "opcode table uses TAIL/HEAD (lookahead) or indent words";
+        err = "opcode table uses indent words";
         return 1;
       }
       ++k;
@@ -597,6 +607,12 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
     err = "REDO (a negative pattern) in a table with anchors or word boundaries";
     return 1;
   }
+  bool look = false;
+  for (uint32_t i = 0; i < n; ++i) look = look || raw[i].look != 0;
+  if (look && (anchored || redo)) {
+    err = "lookahead in a table with anchors, word boundaries or REDO";
+    return 1;
+  }
   const uint32_t nctx = word ? 64u : 4u;
   std::vector<uint32_t> acc4((size_t)n * nctx, 0);
   for (uint32_t i = 0; i < n; ++i) {
@@ -639,9 +655,10 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
 
   // dense next[sid][byte] in new ids
   std::vector<uint32_t> nxt((size_t)S * 256, 0);
-  std::vector<uint32_t> caps(S, 0), acap((size_t)S * nctx, 0);
+  std::vector<uint32_t> caps(S, 0), acap((size_t)S * nctx, 0), lookv(look ? S : 0, 0);
   for (uint32_t i = 0; i < n; ++i) {
     caps[sid[i]] = raw[i].cap;
+    if (look) lookv[sid[i]] = raw[i].look;
     for (uint32_t ctx = 0; ctx < nctx; ++ctx) acap[(size_t)sid[i] * nctx + ctx] = acc4[(size_t)i * nctx + ctx];
     if (anchored && !raw[i].cap) {  // (caps: the state's accept in some context, for the prefilter's superset)
       for (uint32_t ctx = 0; ctx < nctx && !caps[sid[i]]; ++ctx) caps[sid[i]] = acc4[(size_t)i * nctx + ctx];
@@ -704,6 +721,8 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   }
   }
   t.caps = caps;
+  t.look = lookv;
+  t.lookahead = look;
   t.acap = acap;
   t.anchored = anchored;
   t.ctx_word = word;
@@ -792,7 +811,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
     }
   }
   // dominated restarts (tables.hpp dom) for the plain walks
-  if (!anchored && !word) {
+  if (!anchored && !word && !look) {
     std::vector<int> reps;
     std::vector<bool> seen_cls(256, false);
     for (int c = 0; c < 256; ++c)
@@ -1073,6 +1092,19 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   // the sparse kernel pays off when few positions survive the prefilter
   // (a start state that accepts: empty matches anywhere, no candidate filter)
   t.filter = t.format == FMT_BYTE && !leads.empty() && t.fdensity <= 0.15 && start_sid < first_acc;
+  if (look) {
+    // lookahead tables: a match end can move back to a HEAD position, which
+    // none of the transducer forms or the candidate walks model; they take the
+    // lookahead walk (device_common.hpp kWalkLook) on wfind_kernel
+    t.filter = false;
+    t.restart_local = false;
+    t.xtrans.clear();
+    t.immediate = false;
+    t.xid.clear();
+    t.gap = false;
+    t.xc = false;
+    t.xu = false;
+  }
   out = std::move(t);
   return 0;
 }

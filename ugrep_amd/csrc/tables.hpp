@@ -156,6 +156,13 @@ struct DfaTables {
   // walk (it never accepts) then lets the chain skip every position it
   // crossed, up to the byte it died on (sparse_kernel's long walks)
   bool dom_all = false;
+  // Lookahead (X(?=Y), lib/pattern.cpp:2953-2964): per state, TAIL la in bit
+  // la and HEAD la in bit 8 + la (la < 4).  A walk runs each state's block on
+  // entry as the reference does (lib/matcher.cpp:139-175): TAKE, TAILs (the
+  // match end moves back to HEAD la's recorded position), HEADs (record).
+  // Empty unless some state has one; such tables take the lookahead walk only.
+  std::vector<uint32_t> look;
+  bool lookahead = false;
   std::vector<uint32_t> acap;  // states * 4, or states * 64 (ctx_word)
 };
 

@@ -184,6 +184,7 @@ hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStr
 {
   if (P.acap) return wfind_mode<kWalkCtx>(P, format, write, stream);
   if (P.wtab) return wfind_mode<kWalkWord>(P, format, write, stream);
+  if (P.look) return wfind_mode<kWalkLook>(P, format, write, stream);
   return wfind_mode<kWalkPlain>(P, format, write, stream);
 }
 
