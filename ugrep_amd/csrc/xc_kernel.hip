@@ -84,6 +84,16 @@ __device__ __forceinline__ uint32_t xu_swz(uint32_t x) { return UGPU_XU_SWZ ? ((
 #define UGPU_XU_PACK 1
 #endif
 constexpr int kUIter = UGPU_XU_ITER;  // U mode: fewer chunks in flight per wave, twice the waves
+// U mode: the byte masks of the code arithmetic held in VGPRs (CU::k*,
+// UGPU_XU_VK=1) instead of SGPRs / literals.  In isolation a v_bitop3 or v_add
+// with an SGPR operand issued at half rate and the same instruction with three
+// VGPR operands at full rate (tools/probe/valu_rate3.hip,
+// profiles/r06_valu_rate3.txt); in this kernel the VGPR form measured even or
+// slower (2.078-2.111 against 2.062-2.079 ms on C4, 13 against 6 spilled
+// VGPRs; profiles/r06_c4_vk_ab.json), so it stays off
+#ifndef UGPU_XU_VK
+#define UGPU_XU_VK 0
+#endif
 static_assert(kCIter <= 4 && kUIter <= 4, "CIt");
 constexpr int kCLook = 8;                 // look-back chunks before giving up
 constexpr uint32_t kOnes = 0x01010101u;
@@ -218,6 +228,16 @@ struct CU {
   // bytes right after a token byte (bit 0 of a byte; see umask)
   uint32_t risk = 0;
   uint32_t x8 = 0;  // lane (FAST main loop): OR of the codes, bit 3 = an XU_MIX or XU_SLOW lead
+  // the masks 0x70707070, 0x80808080, 0x01010101, 0xfcfcfcfc (UGPU_XU_VK: in VGPRs)
+  uint32_t k70 = 0x70707070u, k80 = 0x80808080u, k01 = 0x01010101u, kfc = 0xfcfcfcfcu;
+  __device__ __forceinline__ void vk()
+  {
+#if UGPU_XU_VK
+    // (an empty asm that "changes" them: the compiler can no longer fold them
+    // into literals or SGPRs, so they stay VGPR operands)
+    asm volatile("" : "+v"(k70), "+v"(k80), "+v"(k01), "+v"(kfc));
+#endif
+  }
 };
 
 // bytes of the dword at q inside [lo, rend) (0xff per byte)
@@ -268,7 +288,7 @@ __device__ __forceinline__ void ucode_lane(const CU& u, const uint32_t w[4], uin
     const uint32_t x = w[d];
 #if UGPU_XU_SWZ
     const uint32_t y = __builtin_amdgcn_alignbit(d < 3 ? w[d + 1] : nx, x, 8);
-    const uint32_t sw = y ^ ((x << 2) & 0xfcfcfcfcu);
+    const uint32_t sw = y ^ ((x << 2) & u.kfc);
 #pragma unroll
     for (int k = 0; k < 4; ++k) a[4 * d + k] = __builtin_amdgcn_perm(x, sw, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
 #else
@@ -331,7 +351,7 @@ template <bool EXACT = true>
 __device__ __forceinline__ uint32_t ucode_fix(const CU& u, uint32_t c, uint32_t x, uint32_t nx, uint32_t cn)
 {
   const uint32_t cy = __builtin_amdgcn_alignbit(cn, c, 8);  // code of byte k + 1, in byte k
-  uint32_t v7 = c & ((c & cy & 0x70707070u) + 0x70707070u) & 0x80808080u;
+  uint32_t v7 = c & ((c & cy & u.k70) + u.k70) & u.k80;
   if constexpr (!EXACT) {
     c |= (v7 >> 4) - (v7 >> 7);  // 0x07: the token covers x .. x + 2
     return c;
@@ -437,7 +457,7 @@ __device__ __forceinline__ void umask(CU& u, const uint4& v, uint64_t q, uint32_
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t pv = d ? c[d - 1] : cp;
-    m[d] = (c[d] | __builtin_amdgcn_alignbit(c[d], pv, 25) | __builtin_amdgcn_alignbit(c[d], pv, 18)) & kOnes;
+    m[d] = (c[d] | __builtin_amdgcn_alignbit(c[d], pv, 25) | __builtin_amdgcn_alignbit(c[d], pv, 18)) & u.k01;
   }
   if constexpr (UW) {
     // M of the byte before the lane's 16 bytes, from the previous lane's codes
@@ -1023,6 +1043,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     u.tab = reinterpret_cast<const uint8_t*>(utab);
     u.bm3 = ubm3;
     u.null4 = P.xu_null * 0x01010101u;
+    u.vk();
     u.lo = P.lo;
     u.rend = P.rend;
   } else {
