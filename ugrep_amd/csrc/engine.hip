@@ -288,7 +288,8 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.wtab = d->d_wtab;
   P.nwtab = d->nwtab;
   P.xc_cls = d->d_cls + 256;
-  P.xc_w = d->xcw ? 1u : 0u;
+  // (option W on xc_kernel: 1 = X is the ASCII word bytes, 2 = a subset of them)
+  P.xc_w = d->xcw ? (d->t.xc_w ? 1u : 2u) : 0u;
   P.xu_tab = dfa_xu(d) ? d->d_xu : nullptr;
   P.xu_bm3 = d->d_xu ? reinterpret_cast<const uint32_t*>(d->d_xu + kXuTab) : nullptr;
   P.xu_null = d->t.xu_null;

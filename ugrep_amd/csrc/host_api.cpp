@@ -165,7 +165,7 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags, int lb)
     p.wtab = true;
     const bool wf = !(std::getenv("UGPU_WFAST") && std::getenv("UGPU_WFAST")[0] == '0');
     p.wplus = wf && t.gap && !t.filter && !p.lb && t.cap1 != 0 && is_word_plus(t);
-    p.xcw = wf && t.xc && t.xc_w && !t.filter && !p.lb && t.cap1 != 0;
+    p.xcw = wf && t.xc && (t.xc_w || t.xc_wsub) && !t.filter && !p.lb && t.cap1 != 0;
     // option W without a selective prefilter: the sparse kernel when every
     // first byte is an ASCII word byte (then the word-start filter leaves about
     // the word starts: C2 -w '[A-Za-z]+' 229.7 -> 89.0 ms against

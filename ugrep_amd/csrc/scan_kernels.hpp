@@ -193,7 +193,7 @@ struct ScanParams {
   uint32_t* st_cap;
   uint32_t* st_n;
   uint32_t st_per;
-  uint32_t xc_w;          // option W on xc_kernel (X = the ASCII word bytes)
+  uint32_t xc_w;          // option W on xc_kernel: 1 = X is the ASCII word bytes, 2 = a proper subset of them
   uint32_t xu_w;          // option W on xc_kernel's U mode (tables equivalent to \w+): run edges checked
   uint32_t xu_exact;      // xc_kernel U mode: the exact main loop (XU_MIX / XU_SLOW checked per chunk)
   // code-point run tables (xc_kernel U mode, tables.hpp xu_*) or NULL

@@ -1026,11 +1026,17 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
       t.xc_tab.assign(256, 0);
       for (int c = 0; c < 256; ++c) t.xc_tab[c] = (uint8_t)((G[c] ? 0x80 : 0) | (X[c] ? 0x40 : 0));
       bool wordset = true;  // X = the ASCII word bytes [0-9A-Za-z_] (option W on xc_kernel)
+      bool wordsub = true;  // X inside them ([A-Za-z]+, [0-9]+, [a-z_]+ ...)
+      auto aword = [](int c) { return c < 0x80 && (std::isalnum(c) || c == '_'); };
       for (int c = 0; c < 256; ++c) {
-        const bool w = c < 0x80 && (std::isalnum(c) || c == '_');
-        wordset = wordset && X[c] == w;
+        wordset = wordset && X[c] == aword(c);
+        wordsub = wordsub && (!X[c] || aword(c));
       }
       t.xc_w = wordset;
+      t.xc_wsub = wordsub && !wordset;
+      if (t.xc_wsub)  // (bit 5: an ASCII word byte, for option W's subset mode)
+        for (int c = 0; c < 256; ++c)
+          if (aword(c)) t.xc_tab[c] |= 0x20;
     }
   }
   t.start = start_sid * R;

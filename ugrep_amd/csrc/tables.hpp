@@ -99,6 +99,10 @@ struct DfaTables {
   // are the kernel's byte classes.  xc_w: X is exactly the ASCII word bytes
   // [0-9A-Za-z_] (option W on xc_kernel).
   bool xc = false, xc_w = false;
+  // xc_wsub: X is a proper subset of the ASCII word bytes ([A-Za-z]+ ...):
+  // option W on xc_kernel too (ScanParams::xc_w = 2), the ASCII word bytes
+  // outside X coded apart (xc_tab bit 5) so that at_wb / at_we see them
+  bool xc_wsub = false;
   std::vector<uint8_t> xc_tab;
   // Code-point runs (xc_kernel U mode): the language is S+ for a prefix-free
   // set S of tokens (one UTF-8 code point each: an ASCII byte, or a lead byte

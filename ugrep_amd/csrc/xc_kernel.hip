@@ -152,10 +152,22 @@ struct CLim {
 // is ASCII (at_we holds).  Runs next to bytes >= 0x80 need the reference's
 // UTF-8 decode (include/reflex/matcher.h:1194-1237): the wave flags any such
 // byte and the host redoes the range with wfind_kernel.
+//
+// Subset mode (ScanParams::xc_w == 2, tables.cpp xc_wsub: X a proper subset of
+// the ASCII word bytes, [A-Za-z]+): the word bytes outside X get the code 0x02
+// -- K for the adder (0x02 + 0x01 + carry never carries, and bit 0 is clear: no
+// start), but bit 1 set, so the G -> P rule above sees them as word bytes.  A
+// match then still starts only after a non-word byte; it must also END before
+// one (at_we), which the forward chain cannot see at the start: a run of X
+// followed by a word byte outside X ("abc1") is no match.  The wave flags any
+// such end (an In byte followed by a 0x02 byte, wc.inv) and the host redoes the
+// range with wfind_kernel, as for bytes >= 0x80; letter-only text never flags.
 struct CW {
   uint32_t cx = 0;   // byte 3: the code of the byte before the chunk (uniform)
   uint32_t hi = 0;   // lane: OR of the bytes seen (bit 7s: a byte >= 0x80)
   uint64_t bob = 0;  // buffer start (base coordinates): at_wb holds there
+  uint32_t sub = 0;  // (uniform) subset mode
+  uint32_t inv = 0;  // lane: bit 0 of a byte: a match followed by a word byte outside X (subset mode)
 };
 
 // Codes and adder sums of one lane's 16 bytes.
@@ -852,6 +864,12 @@ __device__ __forceinline__ void cchunk(const CCodes& cc, const uint4& v, uint64_
   const uint64_t cin = clook(__ballot(gen), __ballot(prop), cw, cw);
   uint32_t sb[4];
   cfinish(L, __builtin_amdgcn_inverse_ballot_w64(cin) ? 1u : 0u, cs, ws, ls, cb, sb);
+  if constexpr (W && !U) {
+    if (wc.sub) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) wc.inv |= cb[d] & (L.E[d] >> 1) & ~(L.E[d] >> 7);  // In_{i-1} and code 0x02
+    }
+  }
   if constexpr (BM) {
     if constexpr (U) {
       uint32_t in[4];
@@ -1047,7 +1065,11 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     u.lo = P.lo;
     u.rend = P.rend;
   } else {
-    for (uint32_t i = threadIdx.x; i < 256; i += kCWaves * 64) bcode[i] = (uint8_t)ccode(P.xc_cls[i]);
+    for (uint32_t i = threadIdx.x; i < 256; i += kCWaves * 64) {
+      const uint32_t cls = P.xc_cls[i];
+      // (subset mode: the ASCII word bytes outside X, code 0x02; see CW)
+      bcode[i] = (uint8_t)(ccode(cls) | (P.xc_w == 2 && !(cls & 0xc0u) && (cls & 0x20u) ? 0x02u : 0u));
+    }
     __syncthreads();
   }
   if constexpr (kCPair && !U) {
@@ -1074,6 +1096,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
   const uint32_t lo16 = 16u * (uint32_t)lane;
   CW wc;
   wc.bob = P.bob;
+  wc.sub = P.xc_w == 2 ? 1u : 0u;
   COut out;
   if constexpr (WR) {
     out.cur = n ? P.out_base[gw] : 0;
@@ -1319,7 +1342,7 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
     return;  // (the records are the COUNT pass's)
   }
   if constexpr (W && !U) {
-    if (__ballot((wc.hi & 0x80808080u) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_WSLOW);
+    if (__ballot((wc.hi & 0x80808080u) != 0 || (wc.inv & kOnes) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_WSLOW);
   }
   if constexpr (W && U) {
     if (__ballot((u.risk & kOnes) != 0) && lane == 0) atomicOr(P.flags, UGPU_FLAG_WSLOW);
