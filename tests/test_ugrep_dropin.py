@@ -194,6 +194,20 @@ NEG_CMDS = [(["-co", "-N", "dolor", "-e", r"dolor\w*"], True), (["-on", "-N", "s
             (["-co", "-N", "lorem", "-e", r"\w+"], True)]
 
 
+# lookahead X(?=Y): the native compiler emits the
+# reference's TAIL/HEAD words (tests/test_lookahead_compile.py), so these
+# commands go to the GPU's lookahead walk; Unicode and -U, -i, -c/-o/-n
+LOOK_CMDS = [(["-co", "dolor(?= sit)"], True), (["-on", r"[a-z]+(?=,)"], True), (["-o", r"\w+(?=\.)"], True),
+             (["-c", r"(?:lorem|ipsum)(?= )"], True), (["-o", "-U", r"in(?=c|t)"], True),
+             (["-co", "-i", r"ut(?= [a-z]+)"], True), (["-o", r"[A-Z]\w*(?= [a-z])"], True)]
+
+
+@pytest.mark.gpu
+def test_dropin_lookahead_on_gpu(tmp_path):
+    """ugrep lookahead commands served by the GPU, byte-equal to the reference build."""
+    _dropin_ledger(tmp_path, LOOK_CMDS, "dropin_lookahead_ledger.json")
+
+
 @pytest.mark.gpu
 def test_dropin_word_boundaries_on_gpu(tmp_path):
     _dropin_ledger(tmp_path, WORDB_CMDS, "dropin_wordb_ledger.json")

@@ -34,9 +34,12 @@
 // (ctx_bits.hpp), encoded as exhaustive meta-edge splits (encode()).
 // Negative patterns (?^...) as whole top-level alternatives (ugrep -N,
 // src/ugrep.cpp:6487): their accepts become REDO words.
+// Lookahead X(?=Y) (round 6): HEAD/TAIL markers as the reference places them
+// (Parser::lookahead_group), emitted as TAIL la / HEAD la words.
 // Returns UGPU_UNSUPPORTED for what the GPU tables cannot express or this
 // compiler does not cover (other anchors, word boundaries, lazy quantifiers,
-// lookaround, backreferences, other \p names, \p{Lu} under -i): the caller keeps
+// negative lookahead, nested or adjacent lookaheads, backreferences, other \p
+// names, \p{Lu} under -i): the caller keeps
 // the CPU matcher for those, as for any unsupported opcode table.
 #include <stdint.h>
 #include <stdlib.h>
@@ -242,7 +245,8 @@ enum Kind
   STAR,
   PLUS,
   OPT,
-  EMPTY
+  EMPTY,
+  LOOK  // X(?=Y): kids[0] = Y (Node::look, Node::look_alt)
 };
 
 struct Node
@@ -250,6 +254,8 @@ struct Node
   Kind kind;
   ByteSet bytes;
   std::vector<int> kids;
+  int look = -1;     // LOOK: the lookahead index (TAIL/HEAD la)
+  int look_alt = 0;  // LOOK: its top-level alternative (accept index)
 };
 
 struct Tree
@@ -259,7 +265,7 @@ struct Tree
 
   int add(Kind k, std::vector<int> kids = {})
   {
-    nodes.push_back(Node{k, ByteSet(), std::move(kids)});
+    nodes.push_back(Node{k, ByteSet(), std::move(kids), -1, 0});
     return static_cast<int>(nodes.size() - 1);
   }
   int leaf(const ByteSet &b)
@@ -285,7 +291,10 @@ struct Tree
     std::vector<int> kids;
     for (int k : copy.kids)
       kids.push_back(clone(k));
-    return add(copy.kind, kids);
+    const int n2 = add(copy.kind, kids);
+    nodes[n2].look = copy.look;  // (a repeated lookahead keeps its index, as the
+    nodes[n2].look_alt = copy.look_alt;  // reference's iterated positions keep their location)
+    return n2;
   }
 
   // UTF-8 byte-range sequences of [lo, hi] (same encoded length, split so that
@@ -437,6 +446,7 @@ class Parser
       begin_.clear();
       end_.clear();
       neg_node_ = -1;
+      alt_index_ = static_cast<int>(alts.size()) + 1;
       const int a = parse_concat(true);
       alts.push_back(a);
       // a negative pattern (?^...) (ugrep -N, src/ugrep.cpp:6487): the whole
@@ -480,8 +490,13 @@ class Parser
     }
     if (any_neg && any_meta)
       fail(UGPU_UNSUPPORTED, "(?^...) with anchors or word boundaries");
+    if (look_count_ && (any_neg || any_meta))
+      fail(UGPU_UNSUPPORTED, "lookahead with anchors, word boundaries or (?^...)");
     return alts;
   }
+
+  // lookaheads (?=...) in the pattern (indices 0 .. looks - 1)
+  int looks() const { return look_count_; }
 
   // per top-level alternative: a negative pattern (?^...), whose accept is REDO
   std::vector<bool> negs;
@@ -502,6 +517,48 @@ class Parser
   int depth_ = 0;      // group nesting
   int neg_node_ = -1;  // the (?^...) group of the top-level alternative being parsed
   std::vector<uint8_t> begin_, end_;  // its begin / end assertions (META - META_MIN), as written
+  int alt_index_ = 1;              // the top-level alternative being parsed (its accept index)
+  int look_count_ = 0;             // lookaheads so far
+  bool in_look_ = false;           // parsing inside (?=...)
+  size_t look_end_ = std::string::npos;  // the ')' of the last lookahead
+
+  // "(?=" at p_ - 1 .. p_ + 1: X(?=Y) as the reference's Pattern compiles it
+  // (lib/pattern.cpp:1331-1359): a HEAD marker in Y's first positions (the
+  // states where Y starts record the position, HEAD la), a TAIL marker after
+  // Y's last positions (the accepting states where Y completes move the match
+  // end back to it, TAIL la, when their accept is this alternative's:
+  // :2395-2419).  Indices count the lookaheads per top-level alternative in
+  // order of their location, the alternatives in order (:2378-2393) -- the
+  // running count here.  The reference merges nested and adjacent lookahead
+  // ranges into one index (ORanges, include/reflex/ranges.h:664-671): refused.
+  int lookahead_group()
+  {
+    const size_t open = p_ - 1;
+    if (in_look_)
+      fail(UGPU_UNSUPPORTED, "nested lookahead");
+    if (look_end_ != std::string::npos && open == look_end_ + 1)
+      fail(UGPU_UNSUPPORTED, "adjacent lookaheads");
+    if (look_count_ >= 16)
+      fail(UGPU_UNSUPPORTED, "more than 16 lookaheads");
+    p_ += 2;
+    if (p_ >= s_.size() || s_[p_] == ')')
+      fail(UGPU_UNSUPPORTED, "empty lookahead");
+    const bool ic = ic_, dot = dotall_;
+    in_look_ = true;
+    ++depth_;
+    const int a = parse_alt();
+    --depth_;
+    in_look_ = false;
+    ic_ = ic;
+    dotall_ = dot;
+    if (p_ >= s_.size() || s_[p_] != ')')
+      fail(UGPU_INVAL, "missing ')'");
+    look_end_ = p_++;
+    const int n = t_.add(LOOK, {a});
+    t_.nodes[n].look = look_count_++;
+    t_.nodes[n].look_alt = alt_index_;
+    return n;
+  }
 
   // a word-boundary assertion at p_ (\b \B \< \>): its class mask (for the
   // begin of the match, bits 0-2; as the reference's META_WBB/NWB/BWB/EWB and
@@ -1185,6 +1242,8 @@ class Parser
         const bool ic = ic_, dot = dotall_;
         if (p_ + 1 < s_.size() && s_[p_] == '?' && s_[p_ + 1] == '^')
           return negative_group();
+        if (p_ + 1 < s_.size() && s_[p_] == '?' && s_[p_ + 1] == '=')
+          return lookahead_group();
         if (p_ < s_.size() && s_[p_] == '?')
         {
           // (?imsx-imsx) modifies the rest of the enclosing group,
@@ -1295,6 +1354,8 @@ class Parser
         ++p_;
         if (p_ + 1 < s_.size() && s_[p_] == '?' && s_[p_ + 1] == '^')
           return negative_group();
+        if (p_ + 1 < s_.size() && s_[p_] == '?' && s_[p_ + 1] == '=')
+          return lookahead_group();
         if (p_ < s_.size() && s_[p_] == '?')
         {
           if (p_ + 1 < s_.size() && s_[p_ + 1] == ':')
@@ -1388,6 +1449,10 @@ struct Glushkov
   std::vector<int> accept;               // position -> accept index (end markers), 0 otherwise
   std::vector<std::vector<uint8_t>> metas;  // end marker -> its alternative's meta edges (Parser::metaseqs)
   std::vector<bool> neg;                    // end marker of a negative pattern (Parser::negs): REDO
+  // lookahead markers (no bytes, never followed): HEAD la (the reference's
+  // "(" position) and TAIL la (its ticked ")" position, valid in states that
+  // accept alternative look_alt), -1 = none
+  std::vector<int> look_head, look_tail, look_alt;
 
   struct Info
   {
@@ -1417,6 +1482,9 @@ struct Glushkov
     accept.push_back(acc);
     metas.emplace_back();
     neg.push_back(false);
+    look_head.push_back(-1);
+    look_tail.push_back(-1);
+    look_alt.push_back(0);
     return static_cast<int>(bytes.size() - 1);
   }
 
@@ -1458,6 +1526,29 @@ struct Glushkov
           r.nullable = r.nullable || b.nullable;
           merge(r.first, b.first);
           merge(r.last, b.last);
+        }
+        return r;
+      }
+      case LOOK:
+      {
+        // lib/pattern.cpp:1346-1358: first(Y) + HEAD, last(Y) -> TAIL, last
+        // = last(Y) + TAIL; a nullable Y also starts with TAIL and ends with HEAD
+        Info y = walk(nd.kids[0]);
+        const int h = new_pos(ByteSet(), 0);
+        look_head[h] = nd.look;
+        const int tl = new_pos(ByteSet(), 0);
+        look_tail[tl] = nd.look;
+        look_alt[tl] = nd.look_alt;
+        link(y.last, std::vector<int>{tl});
+        r.nullable = y.nullable;
+        r.first = y.first;
+        merge(r.first, std::vector<int>{h});
+        r.last = y.last;
+        merge(r.last, std::vector<int>{tl});
+        if (y.nullable)
+        {
+          merge(r.first, std::vector<int>{tl});
+          merge(r.last, std::vector<int>{h});
         }
         return r;
       }
@@ -1585,7 +1676,11 @@ struct Dfa
   std::vector<CtxN> cx;                     // accept index per context
   uint32_t nctx = 4;                        // 4 (line anchors) or 64 (word boundaries)
   bool anchored = false;                    // some accept depends on the context
+  // lookahead per state: bits 0-15 TAIL la, bits 16-31 HEAD la (empty: none)
+  std::vector<uint32_t> look;
 };
+
+inline uint32_t look_of(const Dfa &d, size_t s) { return d.look.empty() ? 0u : d.look[s]; }
 
 Dfa subsets(Glushkov &g, const std::vector<int> &start)
 {
@@ -1643,6 +1738,23 @@ Dfa subsets(Glushkov &g, const std::vector<int> &start)
       for (uint32_t ctx = 0; ctx < d.nctx; ++ctx)
         cx[ctx] = redo ? kRedoAcc : meta_accept(acc, ctx, d.nctx == 64);
     d.acc.push_back(cx[0]);
+    {
+      // the state's lookahead block (lib/pattern.cpp:2374-2419): HEAD la for
+      // every "(" marker; TAIL la for a ")" marker of the alternative the state
+      // accepts (its lowest accept index)
+      uint32_t acc0 = 0, lk = 0;
+      for (int p : cur)
+        if (g.accept[p] && (acc0 == 0 || static_cast<uint32_t>(g.accept[p]) < acc0))
+          acc0 = static_cast<uint32_t>(g.accept[p]);
+      for (int p : cur)
+      {
+        if (g.look_head[p] >= 0)
+          lk |= 1u << (16 + g.look_head[p]);
+        if (g.look_tail[p] >= 0 && acc0 != 0 && static_cast<uint32_t>(g.look_alt[p]) == acc0)
+          lk |= 1u << g.look_tail[p];
+      }
+      d.look.push_back(lk);
+    }
     for (uint32_t ctx = 1; ctx < d.nctx; ++ctx)
       d.anchored = d.anchored || cx[ctx] != cx[0];
     d.cx.push_back(cx);
@@ -1669,10 +1781,31 @@ Dfa minimize(const Dfa &d, uint32_t start)
 {
   size_t n = d.acc.size();
   std::vector<uint32_t> part(n);
+  // lookahead blocks count only in states that can still reach an accept (a
+  // HEAD in a state that never accepts changes no match: such states stay dead)
+  std::vector<uint32_t> lk(n, 0);
+  if (!d.look.empty())
   {
-    std::map<CtxN, uint32_t> m;
+    std::vector<bool> live(n, false);
     for (size_t s = 0; s < n; ++s)
-      part[s] = m.emplace(d.cx[s], static_cast<uint32_t>(m.size())).first->second;
+      for (uint32_t v : d.cx[s])
+        live[s] = live[s] || v != 0;
+    for (bool grew = true; grew;)
+    {
+      grew = false;
+      for (size_t s = 0; s < n; ++s)
+        if (!live[s])
+          for (int b = 0; b < 256 && !live[s]; ++b)
+            if (live[d.next[s][b]])
+              live[s] = grew = true;
+    }
+    for (size_t s = 0; s < n; ++s)
+      lk[s] = live[s] ? d.look[s] : 0;
+  }
+  {
+    std::map<std::pair<CtxN, uint32_t>, uint32_t> m;
+    for (size_t s = 0; s < n; ++s)
+      part[s] = m.emplace(std::make_pair(d.cx[s], lk[s]), static_cast<uint32_t>(m.size())).first->second;
   }
   size_t nparts = 0;
   for (;;)
@@ -1706,6 +1839,8 @@ Dfa minimize(const Dfa &d, uint32_t start)
   out.acc.push_back(0);
   out.cx.push_back(CtxN(d.nctx, 0));
   out.next.push_back(std::vector<uint32_t>(256, 0));
+  if (!d.look.empty())
+    out.look.push_back(0);
   std::vector<uint32_t> order{part[start]};
   if (part[start] != dead)
     newid[part[start]] = 1;
@@ -1729,6 +1864,8 @@ Dfa minimize(const Dfa &d, uint32_t start)
     out.acc.push_back(d.acc[s]);
     out.cx.push_back(d.cx[s]);
     out.next.push_back(row);
+    if (!d.look.empty())
+      out.look.push_back(lk[s]);
   }
   return out;
 }
@@ -1746,6 +1883,9 @@ Dfa unfold_gaps(const Dfa &d)
   size_t n = d.acc.size();
   if (n < 2 || d.anchored)
     return d;  // (no gap transducer for context-dependent accepts: tables.cpp)
+  for (size_t s = 0; s < n; ++s)
+    if (look_of(d, s))
+      return d;  // (nor for lookahead tables)
   std::map<std::pair<uint32_t, int>, uint32_t> id;
   std::vector<std::pair<uint32_t, int>> order{{0, -1}, {1, 0}};
   id[order[0]] = 0;
@@ -1804,6 +1944,7 @@ std::vector<uint32_t> encode(const Dfa &d)
   struct Block
   {
     uint32_t take = 0;
+    uint32_t look = 0;  // TAIL la (bits 0-15), HEAD la (bits 16-31)
     std::vector<std::pair<uint32_t, uint32_t>> metas;  // (META - META_MIN, block index + 1)
     std::vector<Run> runs;
   };
@@ -1823,6 +1964,7 @@ std::vector<uint32_t> encode(const Dfa &d)
       blocks[s - 1].runs.push_back(Run{static_cast<unsigned>(e), static_cast<unsigned>(b), t});
       b = e - 1;
     }
+    blocks[s - 1].look = look_of(d, s);
   }
   // accept-only blocks: P(v) = TAKE v; Q(a, b) = TAKE a, then META_EOL -> P(b)
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> extra;
@@ -1994,6 +2136,7 @@ std::vector<uint32_t> encode(const Dfa &d)
     {
       at[i + 1] = w;
       w += blocks[i].take ? 1 : 0;
+      w += static_cast<uint32_t>(__builtin_popcount(blocks[i].look));
       w += static_cast<uint32_t>(blocks[i].metas.size()) * (lng ? 2 : 1);
       for (auto &r : blocks[i].runs)
         w += (lng && r.target != 0) ? 2 : 1;
@@ -2011,6 +2154,13 @@ std::vector<uint32_t> encode(const Dfa &d)
         out.push_back(0xFD000000u);  // REDO (lib/pattern.cpp:2945-2947)
       else if (k.take)
         out.push_back(0xFE000000u | k.take);
+      // TAIL la then HEAD la, each ascending (lib/pattern.cpp:2953-2964)
+      for (uint32_t i = 0; i < 16; ++i)
+        if (k.look >> i & 1u)
+          out.push_back(0xFC000000u | i);
+      for (uint32_t i = 0; i < 16; ++i)
+        if (k.look >> (16 + i) & 1u)
+          out.push_back(0xFB000000u | i);
       for (auto &m : k.metas)
       {
         if (lng)

@@ -613,6 +613,19 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
     err = "lookahead in a table with anchors, word boundaries or REDO";
     return 1;
   }
+  if (look) {
+    // a HEAD la in the start state with a TAIL la anywhere: the TAIL can move
+    // the match end back to the walk's start, an empty match, and the
+    // reference then asks its advance function for the next candidate and
+    // ends the FIND when it has none (lib/matcher.cpp:682-707) -- behaviour
+    // of the Pattern's prediction, not of the table (a*(?=b), (?=x))
+    uint32_t tails = 0;
+    for (uint32_t i = 0; i < n; ++i) tails |= raw[i].look & 0xffu;
+    if ((raw[0].look >> 8) & tails) {
+      err = "lookahead after a prefix that can be empty (empty matches)";
+      return 1;
+    }
+  }
   const uint32_t nctx = word ? 64u : 4u;
   std::vector<uint32_t> acc4((size_t)n * nctx, 0);
   for (uint32_t i = 0; i < n; ++i) {
