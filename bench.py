@@ -262,6 +262,9 @@ def main():
     ap.add_argument("--offsets", action="store_true",
                     help="each step also materialises the match records (start, len, accept) in HBM and, "
                          "for N > 1, all-gathers them to every rank (SURVEY.md §8e step 4)")
+    ap.add_argument("--offsets-pipeline", choices=("auto", "on", "off"), default="auto",
+                    help="N=1 --offsets: two scanners on two streams, so that one batch's record expansion "
+                         "overlaps the next batch's COUNT pass (auto: on)")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also scans the whole logical stream alone and checks the stitched totals")
     ap.add_argument("--compile", action="store_true",
@@ -367,16 +370,17 @@ def main():
     rec_bytes = 12 if one_accept else 16
     gather_limit = 8 << 30  # record bytes at the root that --offsets-exchange auto still gathers
 
-    def records(count, total_count=None):
-        if recs_dev.get("cap", -1) < count:
+    def records(count, total_count=None, lane=None):
+        sc_, sptr_, rd = (sc, sptr, recs_dev) if lane is None else lane
+        if rd.get("cap", -1) < count:
             cap = count + count // 8 + 1024
-            recs_dev.update(cap=cap, start=torch.empty(cap, dtype=torch.int64, device=dev),
-                            len=torch.empty(cap, dtype=torch.int32, device=dev),
-                            acc=None if one_accept else torch.empty(cap, dtype=torch.int32, device=dev))
-        acc = recs_dev["acc"]
-        sc.offsets(recs_dev["start"].data_ptr(), recs_dev["len"].data_ptr(), 0 if acc is None else acc.data_ptr(),
-                   count, sptr)
-        st, ln = recs_dev["start"][:count], recs_dev["len"][:count]
+            rd.update(cap=cap, start=torch.empty(cap, dtype=torch.int64, device=dev),
+                      len=torch.empty(cap, dtype=torch.int32, device=dev),
+                      acc=None if one_accept else torch.empty(cap, dtype=torch.int32, device=dev))
+        acc = rd["acc"]
+        sc_.offsets(rd["start"].data_ptr(), rd["len"].data_ptr(), 0 if acc is None else acc.data_ptr(),
+                    count, sptr_)
+        st, ln = rd["start"][:count], rd["len"][:count]
         ac = None if acc is None else acc[:count]
         if pg:
             ex = args.offsets_exchange
@@ -411,14 +415,50 @@ def main():
                 rec["verify"] = verify_sharded(sts[0], lns[0], acs[0], rec, device=xdev)
         return rec
 
-    for _ in range(args.warmup):
+    # N=1 --offsets, pipelined: batch i+1's COUNT pass is issued on the other
+    # scanner's stream before batch i's records are written, so the record
+    # expansion (write-bound) overlaps the next COUNT (read-bound); every
+    # batch still gets its whole COUNT and all of its records, into its own
+    # record arrays (two sets, alternating)
+    pipe = args.offsets and not pg and args.offsets_pipeline != "off"
+    if pipe:
+        sc2 = ugrep_amd.Scanner(pat, records=True)
+        sc2.stage(True)
+        stream2 = torch.cuda.Stream(dev)
+        lanes = [(sc, sptr, recs_dev), (sc2, stream2.cuda_stream, {})]
+        sc2.scan(shard.ptr, 0, shard.hi - shard.lo, shard.read_end - shard.lo, shard.eof, shard.lo, lanes[1][1])
+        sc2.totals()  # (its buffers sized outside the timed steps)
+
+        def issue(i):
+            s_, p_, _ = lanes[i % 2]
+            s_.scan(shard.ptr, 0, shard.hi - shard.lo, shard.read_end - shard.lo, shard.eof, shard.lo, p_)
+
+        def run_pipe(n):
+            issue(0)
+            out_ = None
+            for i in range(n):
+                s_ = lanes[i % 2][0]
+                t = s_.totals()
+                if i + 1 < n:
+                    issue(i + 1)  # the next batch's COUNT, on the other stream
+                kms.append(s_.kernel_ms())
+                out_ = dict(entry=t.entry + shard.lo, exit=t.exit + shard.lo, count=t.count, digest=t.digest,
+                            dcap=t.dcap)
+                out_["records"] = records(t.count, t.count, lane=lanes[i % 2])
+            return out_
+
+    if pipe:
+        res = run_pipe(max(2, args.warmup))  # (both record sets sized before the timed steps)
+    for _ in range(0 if pipe else args.warmup):
         res = step()
     kms.clear()
     if pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    if pipe:
+        res = run_pipe(args.steps)
+    for _ in range(0 if pipe else args.steps):
         res = step()
     torch.cuda.synchronize(dev)
     if pg:
@@ -526,7 +566,8 @@ def main():
             dg = sum(int((s_ * 31 + l_.to(torch.int64)).sum().item()) for s_, l_ in zip(sts, lns)) & m64  # (wraps as u64)
             out["offsets"] = {"records": nrec, "bytes_per_record": rec_bytes,
                               "gathered_to": "rank 0 (per-rank parts)" if pg else "local",
-                              "digest_matches_totals": nrec == res["count"] and dg == res["digest"]}
+                              "digest_matches_totals": nrec == res["count"] and dg == res["digest"],
+                              "pipelined": bool(pipe)}
         if shard.grown:
             out["offsets"]["halo_grown"] = shard.grown
     # (the committed PMC traffic is per BASELINE config and pattern)

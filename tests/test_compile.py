@@ -120,7 +120,7 @@ def test_config_tables_are_loadable():
         assert a["states"] <= b["states"]
 
 
-@pytest.mark.parametrize("rx", ["(^a)", "a$b", "a^", r"a\bfoo", r"(\<x)", r"\b+x", "a*?", "a+?", r"(a)\1", r"\p{Tangut}", "[[:^alpha:]]",
+@pytest.mark.parametrize("rx", ["(^a)", "a$b", "a^", r"a\bfoo", r"(\<x)", r"\b+x", "a*?", "a+?", r"(a)\1", r"\p{NoSuchScript}", "[[:^alpha:]]",
                                 "(?!x)", r"\Qa\E", r"\p{Lu}"])
 def test_unsupported_constructs(rx):
     import ugrep_amd as U

@@ -69,6 +69,32 @@ LONG = {"Letter": "L", "Mark": "M", "Number": "N", "Punctuation": "P", "Symbol":
         "Connector_Punctuation": "Pc", "Other_Punctuation": "Po", "Control": "Cc", "Format": "Cf"}
 SCRIPTS = ["Latin", "Greek", "Cyrillic", "Armenian", "Hebrew", "Arabic", "Devanagari", "Bengali", "Tamil", "Thai",
            "Georgian", "Hangul", "Hiragana", "Katakana", "Han", "Ethiopic", "Common"]
+# (round 6) every other name the reference's \\p{NAME} accepts (lib/language_scripts.cpp,
+# lib/unicode.cpp range[...]): the remaining scripts, the identifier classes
+# (Java/C#/Python/Unicode identifier parts and starts), Unicode,
+# Non_ASCII_Unicode, C / Other and the one-letter aliases
+MORE = ["Adlam", "Ahom", "Anatolian_Hieroglyphs", "Avestan", "Balinese", "Bamum", "Bassa_Vah", "Batak",
+        "Bhaiksuki", "Bopomofo", "Brahmi", "Braille", "Buginese", "Buhid", "C", "Canadian_Aboriginal", "Carian",
+        "Caucasian_Albanian", "Chakma", "Cham", "Cherokee", "Chorasmian", "Coptic", "CsIdentifierPart",
+        "CsIdentifierStart", "Cuneiform", "Cypriot", "Cypro_Minoan", "Deseret", "Dives_Akuru", "Dogra", "Duployan",
+        "Egyptian_Hieroglyphs", "Elbasan", "Elymaic", "Glagolitic", "Gothic", "Grantha", "Gujarati",
+        "Gunjala_Gondi", "Gurmukhi", "Hanifi_Rohingya", "Hanunoo", "Hatran", "IdentifierIgnorable",
+        "Imperial_Aramaic", "Inherited", "Inscriptional_Pahlavi", "Inscriptional_Parthian", "JavaIdentifierPart",
+        "JavaIdentifierStart", "Javanese", "Kaithi", "Kannada", "Kawi", "Kayah_Li", "Kharoshthi",
+        "Khitan_Small_Script", "Khmer", "Khojki", "Khudawadi", "Lao", "Lepcha", "Limbu", "Linear_A", "Linear_B",
+        "Lisu", "Lycian", "Lydian", "Mahajani", "Makasar", "Malayalam", "Mandaic", "Manichaean", "Marchen",
+        "Masaram_Gondi", "Medefaidrin", "Meetei_Mayek", "Mende_Kikakui", "Meroitic_Cursive",
+        "Meroitic_Hieroglyphs", "Miao", "Modi", "Mongolian", "Mro", "Multani", "Myanmar", "Nabataean",
+        "Nag_Mundari", "Nandinagari", "New_Tai_Lue", "Newa", "Nko", "Non_ASCII_Unicode", "Nushu",
+        "Nyiakeng_Puachue_Hmong", "Ogham", "Ol_Chiki", "Old_Hungarian", "Old_Italic", "Old_North_Arabian",
+        "Old_Permic", "Old_Persian", "Old_Sogdian", "Old_South_Arabian", "Old_Turkic", "Old_Uyghur", "Oriya",
+        "Osage", "Osmanya", "Other", "Pahawh_Hmong", "Palmyrene", "Pau_Cin_Hau", "Phags_Pa", "Phoenician",
+        "Psalter_Pahlavi", "PythonIdentifierPart", "PythonIdentifierStart", "Rejang", "Runic", "Samaritan",
+        "Saurashtra", "Sharada", "Shavian", "Siddham", "SignWriting", "Sinhala", "Sogdian", "Sora_Sompeng",
+        "Soyombo", "Sundanese", "Syloti_Nagri", "Syriac", "Tagalog", "Tagbanwa", "Tai_Le", "Tai_Tham", "Tai_Viet",
+        "Takri", "Tangsa", "Tangut", "Telugu", "Thaana", "Tibetan", "Tifinagh", "Tirhuta", "Toto", "Ugaritic",
+        "Unicode", "UnicodeIdentifierPart", "UnicodeIdentifierStart", "Vai", "Vithkuqi", "Wancho", "Warang_Citi",
+        "Yezidi", "Yi", "Zanabazar_Square", "d", "l", "s", "u", "w"]
 POSIX = ["ASCII", "Space", "XDigit", "Cntrl", "Print", "Alnum", "Alpha", "Blank", "Digit", "Graph", "Lower",
          "Punct", "Upper", "Word"]
 
@@ -99,11 +125,19 @@ def main():
         print("%s: %d ranges" % (name, n), file=sys.stderr)
     reg = []
     pnl = {}
-    for name in CATEGORIES + SCRIPTS + POSIX:
+    for name in CATEGORIES + SCRIPTS + POSIX + MORE:
         rx = r"\p{%s}" % name
         cname = "k_p_%s" % name
-        n = emit(lines, cname, members(rx), has_newline(rx))
-        pnl[cname] = int(has_newline(r"\P{%s}" % name))  # '\n' in the complement \P{NAME}
+        try:
+            cps, nl = members(rx), has_newline(rx)
+        except subprocess.CalledProcessError:
+            print("\\p{%s}: the reference refuses it, skipped" % name, file=sys.stderr)
+            continue
+        n = emit(lines, cname, cps, nl)
+        try:
+            pnl[cname] = int(has_newline(r"\P{%s}" % name))  # '\n' in the complement \P{NAME}
+        except subprocess.CalledProcessError:  # (\P{Unicode}: an empty class, which the reference refuses)
+            pnl[cname] = 0
         reg.append((name, cname))
         print("\\p{%s}: %d ranges" % (name, n), file=sys.stderr)
     for long, short in LONG.items():

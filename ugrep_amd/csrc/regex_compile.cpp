@@ -369,6 +369,23 @@ struct Tree
     return 4;
   }
 
+  // the byte ranges of s when its valid UTF-8 encodings are one product of
+  // byte ranges (one code point length, no alternation), else empty
+  std::vector<std::pair<uint8_t, uint8_t>> single_product(const CpSet &s0)
+  {
+    CpSet s = normalize(s0);
+    std::vector<std::vector<std::pair<uint8_t, uint8_t>>> seqs;
+    for (auto &r : s)
+    {
+      if (r.first < 0x80)
+        return {};
+      utf8_split(r.first, r.second, seqs);
+      if (seqs.size() > 1)
+        return {};
+    }
+    return seqs.size() == 1 ? seqs[0] : std::vector<std::pair<uint8_t, uint8_t>>();
+  }
+
   // subtree matching exactly the valid UTF-8 encodings of the code points in s
   int cpset(const CpSet &s0)
   {
@@ -518,6 +535,11 @@ class Parser
   int neg_node_ = -1;  // the (?^...) group of the top-level alternative being parsed
   std::vector<uint8_t> begin_, end_;  // its begin / end assertions (META - META_MIN), as written
   int alt_index_ = 1;              // the top-level alternative being parsed (its accept index)
+  // a \p{NAME} atom whose quantifier binds to its last byte-level atom only
+  // (parse_atom sets them, parse_repeat consumes them; see there)
+  bool p_quirk_ = false;
+  std::vector<int> p_prefix_;
+  int p_tail_ = -1;
   int look_count_ = 0;             // lookaheads so far
   bool in_look_ = false;           // parsing inside (?=...)
   size_t look_end_ = std::string::npos;  // the ')' of the last lookahead
@@ -768,7 +790,19 @@ class Parser
     // convert.cpp:2118-2160: a Unicode '.' becomes one UTF-8 character unless
     // it is followed by '*' or '+', where it stays the byte class [^\n]
     bool dot_byte = dot && p_ + 1 < s_.size() && (s_[p_ + 1] == '*' || s_[p_ + 1] == '+');
+    p_quirk_ = false;
     int a = parse_atom(dot_byte);
+    // Matcher::convert pastes a \p{NAME} class in as the text of its UTF-8
+    // byte regex, grouped only when that has alternatives; a class whose
+    // encoding is one sequence with leading single bytes (\p{Ogham} =
+    // \xe1\x9a[\x80-\x9c], \p{Braille} = \xe2(?:[\xa0-\xa3][\x80-\xbf]), \p{Zl})
+    // then takes a quantifier on its last atom only: \p{Ogham}+ is
+    // \xe1\x9a[\x80-\x9c]+ (measured on the reference's converted regexes,
+    // tests/test_pclass.py)
+    const bool quirk = p_quirk_;
+    std::vector<int> prefix = p_prefix_;
+    int q = quirk ? p_tail_ : a;
+    bool quantified = false;
     while (p_ < s_.size())
     {
       char c = s_[p_];
@@ -776,32 +810,37 @@ class Parser
       if (c == '*')
       {
         ++p_;
-        a = t_.add(STAR, {a});
+        q = t_.add(STAR, {q});
       }
       else if (c == '+')
       {
         ++p_;
-        a = t_.add(PLUS, {a});
+        q = t_.add(PLUS, {q});
       }
       else if (c == '?')
       {
         ++p_;
-        a = t_.add(OPT, {a});
+        q = t_.add(OPT, {q});
       }
       else if (c == '{')
       {
         if (!parse_braces(lo, hi))
           fail(UGPU_INVAL, "bad repeat");
-        a = repeat(a, lo, hi);
+        q = repeat(q, lo, hi);
       }
       else
         break;
+      quantified = true;
       if (p_ < s_.size() && s_[p_] == '?')
         fail(UGPU_UNSUPPORTED, "lazy quantifier");
       if (p_ < s_.size() && s_[p_] == '+' )
         fail(UGPU_UNSUPPORTED, "possessive quantifier");
     }
-    return a;
+    p_quirk_ = false;
+    if (!quirk || !quantified)
+      return quirk ? a : q;
+    prefix.push_back(q);
+    return t_.add(CAT, prefix);
   }
 
   uint32_t utf8_char()
@@ -1408,12 +1447,34 @@ class Parser
           fail(UGPU_UNSUPPORTED, std::string("escape \\") + s_[p_]);
         CpSet set;
         uint32_t cp;
+        const bool pclass = p_ < s_.size() && s_[p_] == 'p';
         if (parse_escape(set, cp, false))
         {
           if (icase())
           {
             add_ascii_case(set);
             add_unicode_case(set);
+          }
+          const std::vector<std::pair<uint8_t, uint8_t>> seq = pclass ? t_.single_product(set) : decltype(seq)();
+          if (seq.size() >= 2 && seq[0].first == seq[0].second)
+          {
+            // (parse_repeat: a quantifier takes the last atom of convert's text)
+            size_t j = 0;
+            while (j < seq.size() && seq[j].first == seq[j].second)
+              ++j;
+            if (j == seq.size())
+              --j;  // (one code point: the last byte is the last atom)
+            p_prefix_.clear();
+            for (size_t k = 0; k < j; ++k)
+              p_prefix_.push_back(t_.leaf_range(seq[k].first, seq[k].second));
+            std::vector<int> rest;
+            for (size_t k = j; k < seq.size(); ++k)
+              rest.push_back(t_.leaf_range(seq[k].first, seq[k].second));
+            p_tail_ = rest.size() == 1 ? rest[0] : t_.add(CAT, rest);
+            p_quirk_ = true;
+            std::vector<int> all(p_prefix_);
+            all.push_back(p_tail_);
+            return t_.add(CAT, all);
           }
           return t_.cpset(set);
         }
