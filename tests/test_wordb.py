@@ -395,7 +395,7 @@ def test_compiler_word_boundaries_match_reference():
 
 
 SPARSE_CTX = [r"\bfoo\b", r"\<(in|ut)\>", r"\bdolor\b", r"\Boo\B", r"x\>", r"\<con", r"um\>", r"^foo", r"ing$",
-              r"\b(lorem|ipsum|sit)\b"]
+              r"\b(lorem|ipsum|sit)\b", r"\<(foo|bar|baz)\>", r"\b(in|ut)\b"]
 
 
 def _ctx_corpus(n):
