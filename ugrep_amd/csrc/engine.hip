@@ -97,9 +97,6 @@ struct ugpu_dfa {
   uint32_t* d_acap = nullptr;  // acap, or (word boundaries) acap_rows then acap_map
   // no match starts right after a word character (ScanParams::wstart)
   bool wstart = false;
-  // every match is wend bytes long and none is followed by an ASCII letter
-  // (ScanParams::wend; 0 = unknown)
-  uint32_t wend = 0;
   // loop-needle tables (C+N, ScanParams::lb_cls): the prefilter finds N, and
   // each candidate walks back to its C-run's start (host_api.cpp loop_needle)
   bool lb = false;
@@ -303,7 +300,6 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.amap = P.ctx_word ? d->d_acap + d->t.acap_rows.size() : nullptr;
   P.nul = d->nul ? 1u : 0u;
   P.wstart = d->wstart && env_u64("UGPU_WSTART", 1) != 0 ? 1u : 0u;
-  P.wend = P.wstart && env_u64("UGPU_WEND", 1) != 0 ? d->wend : 0u;
   P.bol0 = 1;
   // chain bytes one stitch merge may cross before the chains count as not
   // resynchronising (two chains of a resynchronising table meet within a match
@@ -317,7 +313,7 @@ void fill_tables(ScanParams& P, const ugpu_dfa* d)
   P.dom = d->d_dom;
   P.look = d->d_look;
   P.dom_all = d->d_dom && d->t.dom_all ? 1u : 0u;
-  if (d->lb) P.wstart = P.wend = 0;  // (the candidates are needle positions, not match starts)
+  if (d->lb) P.wstart = 0;  // (the candidates are needle positions, not match starts)
 }
 
 // Translate a byte range of dbuf into the 16-byte aligned base coordinates
@@ -518,41 +514,6 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
       any = !(c & CTX_WB) && ((c & CTX_BW) || bw0) && d->t.acap[i] != 0;
     }
     d->wstart = !any && !d->t.acap.empty();
-    // the end side: when every match has one length L (each state is reached
-    // at one depth, accepting states at depth L with no byte edges) and no
-    // accepting state accepts where the next byte is an ASCII letter (that
-    // gives at_we = 0 and no line end: include/reflex/matcher.h:1194-1237,
-    // device_common.hpp at_we_meta), a candidate whose byte p + L is a letter
-    // starts no match -- \<(in|ut)\> keeps the words "in" / "ut", not every
-    // word that begins with them
-    const uint32_t R = d->t.row, S = d->t.states, ncol = d->t.format == FMT_BYTE ? 256u : d->t.classes;
-    std::vector<int> depth(S, -1);
-    std::vector<uint32_t> order{d->t.start >> d->t.log_row};
-    depth[order[0]] = 0;
-    bool ok = d->t.acap.size() == (size_t)S * 64;
-    int L = -1;
-    for (size_t i = 0; i < order.size() && ok; ++i) {
-      const uint32_t s = order[i];
-      const bool acc = s * R >= d->t.accb;
-      if (acc) {
-        ok = ok && (L < 0 || L == depth[s]);
-        L = depth[s];
-        for (uint32_t c = 0; c < 64 && ok; ++c)
-          ok = (c & (CTX_WE | CTX_EOL)) || d->t.acap[(size_t)s * 64 + c] == 0;
-      }
-      for (uint32_t col = 0; col < ncol && ok; ++col) {
-        const uint32_t t = d->t.trans[(size_t)s * R + col] >> d->t.log_row;
-        if (!t) continue;
-        ok = !acc;
-        if (depth[t] < 0) {
-          depth[t] = depth[s] + 1;
-          order.push_back(t);
-        } else if (depth[t] != depth[s] + 1) {
-          ok = false;
-        }
-      }
-    }
-    d->wend = ok && d->wstart && L >= 1 && L <= 15 ? (uint32_t)L : 0u;
   }
   const uint32_t* lbcls = pl.lb_cls;
   const std::string& needle = pl.lb_needle;

@@ -215,10 +215,6 @@ struct ScanParams {
   // at the match begin, lib/matcher.cpp:107; or a table whose every accept
   // needs CTX_WB), so candidates right after an ASCII letter are dropped
   uint32_t wstart;
-  // no match is followed by an ASCII letter, and every match is wend bytes
-  // long (1..15; 0 = off): a candidate whose byte p + wend is a letter is
-  // dropped (word-boundary tables such as \<(in|ut)\>, engine.hip)
-  uint32_t wend;
   // sparse_kernel, loop-needle tables (engine.hip loop_needle): the prefilter
   // (ft) finds the needle N; each candidate walks back over the bytes of C
   // (256-bit mask) to its run's start.  NULL: ft finds first bytes.

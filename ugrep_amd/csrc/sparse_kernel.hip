@@ -753,12 +753,6 @@ __device__ __forceinline__ void tile_pass(const uint4& v0, const uint4& v1, cons
     if (!tail && !__ballot(anyk[k] != 0)) continue;
     uint32_t mk = flags4(X[k][0]) | (flags4(X[k][1]) << 4) | (flags4(X[k][2]) << 8) | (flags4(X[k][3]) << 12);
     if (P.wstart) mk &= ~(((k < 2 ? lt01 : lt23) >> (16 * (k & 1))) << 1) & 0xffffu;
-    if (P.wend) {
-      // (P.wend: a candidate at byte i whose byte i + wend, in this lane's 16
-      // bytes, is an ASCII letter starts no match)
-      const uint32_t lk = ((k < 2 ? lt01 : lt23) >> (16 * (k & 1))) & 0xffffu;
-      mk &= ~((lk >> P.wend) & (0xffffu >> P.wend));
-    }
     const uint64_t p0 = ts + 1024u * k + 16u * lane;
     if (!P.at_eof && p0 + 18 > P.rend && p0 < P.rend) {
       // the last two readable positions of a non-final range: their prefilter
