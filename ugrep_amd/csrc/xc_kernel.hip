@@ -72,14 +72,27 @@ constexpr uint32_t kCTile = kCChunk * kCIter;
 #ifndef UGPU_XBM_NT
 #define UGPU_XBM_NT 1
 #endif
-// U mode pair-table layout: 1 = entry (x, y) at x << 8 | (y ^ (x << 2 & 0xfc))
-// (the swizzle spread ASCII lanes over the LDS banks); 0 = at x << 8 | y, so a
-// lookup address is one v_perm of the lane's bytes (no next-byte dword, no
-// XOR) -- bank conflicts no longer cost time
+// U mode pair-table layout: 2 (default since round 6) = entry (x, y) at
+// x << 8 | (y ^ x), one full-rate XOR per dword; 1 = at x << 8 | (y ^ (x << 2
+// & 0xfc)) (a half-rate shift and a masked XOR); both spread ASCII lanes over
+// the LDS banks.  0 = at x << 8 | y, so a lookup address is one v_perm of the
+// lane's bytes -- 2.53 against 2.07 ms: without a swizzle ASCII text piles onto
+// a few banks
 #ifndef UGPU_XU_SWZ
-#define UGPU_XU_SWZ 1
+#define UGPU_XU_SWZ 2
 #endif
-__device__ __forceinline__ uint32_t xu_swz(uint32_t x) { return UGPU_XU_SWZ ? ((x << 2) & 0xfcu) : 0u; }
+__device__ __forceinline__ uint32_t xu_swz(uint32_t x)
+{
+  return UGPU_XU_SWZ == 2 ? x : UGPU_XU_SWZ ? ((x << 2) & 0xfcu) : 0u;
+}
+// (round 6, on: C4 1.93-1.97 against 2.01-2.04 ms with the swizzle y ^ x and
+// the one-shift fill, C3 -0.3 %; profiles/r06_c4_valu_ab.txt)
+#ifndef UGPU_XC_ACC32
+#define UGPU_XC_ACC32 1
+#endif
+#ifndef UGPU_XU_FIX7
+#define UGPU_XU_FIX7 1
+#endif
 #ifndef UGPU_XU_PACK
 #define UGPU_XU_PACK 1
 #endif
@@ -266,7 +279,7 @@ __device__ __forceinline__ uint32_t ucode_dw(const CU& u, uint32_t x, uint32_t n
   // bank conflicts but 26 instead of 11 VALU per dword: 3.57 vs 3.17 ms on C4.)
 #if UGPU_XU_SWZ
   const uint32_t y = __builtin_amdgcn_alignbit(nx, x, 8);
-  const uint32_t sw = y ^ ((x << 2) & 0xfcfcfcfcu);
+  const uint32_t sw = UGPU_XU_SWZ == 2 ? y ^ x : y ^ ((x << 2) & 0xfcfcfcfcu);
 #endif
   uint32_t r = 0;
 #pragma unroll
@@ -300,7 +313,7 @@ __device__ __forceinline__ void ucode_lane(const CU& u, const uint32_t w[4], uin
     const uint32_t x = w[d];
 #if UGPU_XU_SWZ
     const uint32_t y = __builtin_amdgcn_alignbit(d < 3 ? w[d + 1] : nx, x, 8);
-    const uint32_t sw = y ^ ((x << 2) & u.kfc);
+    const uint32_t sw = UGPU_XU_SWZ == 2 ? y ^ x : y ^ ((x << 2) & u.kfc);
 #pragma unroll
     for (int k = 0; k < 4; ++k) a[4 * d + k] = __builtin_amdgcn_perm(x, sw, 0x0c0c0000u | (uint32_t)(4 + k) << 8 | (uint32_t)k);
 #else
@@ -365,7 +378,13 @@ __device__ __forceinline__ uint32_t ucode_fix(const CU& u, uint32_t c, uint32_t 
   const uint32_t cy = __builtin_amdgcn_alignbit(cn, c, 8);  // code of byte k + 1, in byte k
   uint32_t v7 = c & ((c & cy & u.k70) + u.k70) & u.k80;
   if constexpr (!EXACT) {
+#if UGPU_XU_FIX7
+    // (0x7f: bits 0-6; only bits 0-2 are read after the fix -- M, below -- so
+    // one shift less than 0x07)
+    c |= v7 - (v7 >> 7);
+#else
     c |= (v7 >> 4) - (v7 >> 7);  // 0x07: the token covers x .. x + 2
+#endif
     return c;
   }
   uint32_t mm = c & ~(c << 3) & 0x08080808u;  // XU_MIX leads
@@ -1208,7 +1227,10 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
       mprev = cw << 24;
     }
     CPend pend[2];  // (WR: the staged chunks of the tile)
-    for (uint64_t t = ftb; t < fte; ++t) {
+    // one tile of the main loop; c = its starts, cj = their chunk-weighted
+    // count, ws = in-chunk start offsets, ls = In bits (lane sums)
+    auto tile_step = [&](uint64_t t, uint32_t& c, uint32_t& cj, uint32_t& tws, uint32_t& tls)
+                         __attribute__((always_inline)) {
       const uint64_t ts = t * kTile;
       {
         // (U mode reads the next tile also after the last: its first dword is
@@ -1295,18 +1317,49 @@ __device__ __forceinline__ void xc_body(const ScanParams& P)
         }
         a.ls = __builtin_amdgcn_udot4(a.macc, kOnes, a.ls, false);
       }
-      uint32_t c = 0, cj = 0;
+      c = 0;
+      cj = 0;
 #pragma unroll
       for (int j = 0; j < kIt; ++j) {
         c += a.cs[j];
         cj += j * a.cs[j];
       }
-      cnt += c;
-      pos += (uint64_t)c * (ts + lo16) + a.ws + kCChunk * cj;
-      lbits += a.ls;
+      tws = a.ws;
+      tls = a.ls;
 #pragma unroll
       for (int j = 0; j < kIt; ++j) cur[j] = nxt[j];
       nfc = nfn;
+    };
+#if UGPU_XC_ACC32
+    // the main loop's lane sums in 32 bits, folded into cnt / pos / lbits once
+    // after the loop (the 64-bit multiply-adds per tile were ~12 VALU of the
+    // loop): c32 = starts, s32 = the running start count summed over the tiles
+    // (so sum_k k c_k = nt c32 - s32), l32 = in-tile offsets, b32 = In bits.
+    // Per lane and tile at most 16 starts at offsets < kTile, so up to kFold
+    // tiles per wave keep s32 < 2^30 and l32 < 2^29; longer wave ranges take
+    // the 64-bit loop.
+    constexpr uint64_t kFold = 8192;
+    if (fte - ftb <= kFold) {
+      uint32_t c32 = 0, s32 = 0, l32 = 0, b32 = 0;
+      for (uint64_t t = ftb; t < fte; ++t) {
+        uint32_t c, cj, tws, tls;
+        tile_step(t, c, cj, tws, tls);
+        c32 += c;
+        s32 += c32;
+        l32 += tws + kCChunk * cj;
+        b32 += tls;
+      }
+      cnt += c32;
+      pos += (uint64_t)c32 * (ftb * kTile + lo16) + (uint64_t)kTile * ((fte - ftb) * c32 - s32) + l32;
+      lbits += b32;
+    } else
+#endif
+    for (uint64_t t = ftb; t < fte; ++t) {
+      uint32_t c, cj, tws, tls;
+      tile_step(t, c, cj, tws, tls);
+      cnt += c;
+      pos += (uint64_t)c * (t * kTile + lo16) + tws + kCChunk * cj;
+      lbits += tls;
     }
   }
   if (fte > ftb) q0 = fte * kTile;
