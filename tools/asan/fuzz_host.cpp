@@ -4,7 +4,8 @@
 //
 // N random patterns from the grammar ugpu_compile supports (literals, classes
 // and their negations, \w \d \s \b \< \> ^ $, escapes, groups, alternation,
-// the quantifiers ? * + {m,n}, (?^...) negative alternatives), each with
+// the quantifiers ? * + {m,n}, (?^...) negative alternatives, (?=...)
+// lookaheads, \p{NAME} classes of one byte sequence), each with
 // random flags (-F, -i, RE/flex mode), plus byte-level mutations of them
 // (truncations, random bytes, unbalanced brackets: malformed input must fail
 // cleanly).  Every pattern that compiles is run through every host entry
@@ -34,7 +35,8 @@ uint32_t rnd(uint32_t n) { return (uint32_t)(rng() % n); }
 const char* kAtoms[] = {"a", "b", "foo", "x", "[a-z]", "[^a-z]", "[A-Za-z_]", "[0-9]", "\\d", "\\s", ".", "\\.",
                         "\\\\", "[[:digit:]]", "\\x41", "\\n", "\\t", "[-a]", "[a-]", "[]a]", "[^]a]", "\\bfoo",
                         "\\<x", "y\\>", "\\Bz", "^", "$", "ing", "ed", " "};
-const char* kWide[] = {"\\w", "\\W", "\\S", "[[:alpha:]]", "\\p{L}", "\\p{Greek}", "é", "€", "中", "[à-ÿ]"};
+const char* kWide[] = {"\\w", "\\W", "\\S", "[[:alpha:]]", "\\p{L}", "\\p{Greek}", "é", "€", "中", "[à-ÿ]",
+                       "\\p{Ogham}", "\\p{Zl}", "\\p{Braille}", "\\p{Thaana}", "\\p{Tangut}"};
 
 std::string gen(int depth)
 {
@@ -49,7 +51,8 @@ std::string gen(int depth)
     } else if (k < 8) {
       s += "(" + gen(depth - 1) + "|" + gen(depth - 1) + ")";
     } else if (k < 9) {
-      s += "(?:" + gen(depth - 1) + ")";
+      // (round 6: lookahead groups too)
+      s += (rnd(3) == 0 ? "(?=" : "(?:") + gen(depth - 1) + ")";
     } else {
       s += gen(depth - 1) + "|" + gen(depth - 1);
     }
