@@ -222,7 +222,7 @@ class GpuMatcher : public Matcher {
       : Matcher(m), tab_(m.tab_), tab_pat_(m.tab_pat_), tab_w_(m.tab_w_), tab_n_(m.tab_n_),
         tab_anchor_(m.tab_anchor_), tab_ok_(m.tab_ok_), sparse_(m.sparse_),
         min_bytes_(m.min_bytes_), chunk_(m.chunk_), multi_min_(m.multi_min_), sparse_max_(m.sparse_max_),
-        warm_async_(m.warm_async_)
+        warm_async_(m.warm_async_), warm_wait_(m.warm_wait_)
   {
     ++live();
   }
@@ -469,11 +469,13 @@ class GpuMatcher : public Matcher {
   // Device warm-up, once per process.  A fresh process pays ~0.2-0.4 s at its
   // first GPU call (HIP context, queues, pinned memory, code object:
   // ugpu_warmup, tools/probe/startup_probe.cpp); the first input the policy
-  // sends to the GPU starts it on a thread of its own and the CPU matcher
-  // answers (reason "warmup") until the devices are ready -- inputs then move
-  // to the GPU at their cursor, as after a device queue slot frees up.
-  // UGPU_ADAPTER_WARM=0: warm up on the calling thread (the first GPU input
-  // waits; tests that count GPU answers use it).  The thread is joined at exit.
+  // sends to the GPU starts it on a thread of its own, and workers that meet
+  // the device warming wait for it (warm_state).  UGPU_ADAPTER_WARM=cpu: the
+  // CPU matcher answers meanwhile (reason "warmup"; round 5's default) and
+  // inputs move to the GPU at their cursor once the devices are ready, as
+  // after a device queue slot frees up.  UGPU_ADAPTER_WARM=0: warm up on the
+  // calling thread (the first GPU input waits, the others answer on the CPU;
+  // tests that count GPU answers use it).  The thread is joined at exit.
   // Prefiltered tables do not start an asynchronous warm-up (reason "cold"):
   // on host buffers their GPU scans are PCIe-bound, ugrep's workers scan them
   // faster on their cores (tools/bench_ugrep.py: C2 at ~100 GB/s on 16
@@ -565,7 +567,21 @@ class GpuMatcher : public Matcher {
       }
       st = w.state.load(std::memory_order_acquire);
     }
+    if (st == 1)
+      st = warm_state();
     return st == 2;
+  }
+  // the warm-up state; under UGPU_ADAPTER_WARM=wait a warming device is
+  // waited for (polled every 200 us: it is ready within ~0.3 s)
+  int warm_state() const
+  {
+    int st = warm().state.load(std::memory_order_acquire);
+    while (warm_wait_ && st == 1)
+    {
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+      st = warm().state.load(std::memory_order_acquire);
+    }
+    return st;
   }
   static int warm_reason()
   {
@@ -831,6 +847,14 @@ class GpuMatcher : public Matcher {
     multi_min_ = e && *e ? static_cast<size_t>(std::strtoull(e, NULL, 0)) : (64u << 20);
     e = std::getenv("UGPU_ADAPTER_WARM");
     warm_async_ = !(e && *e == '0');
+    // By default (since round 6) a worker that meets the device warming waits
+    // for it instead of letting the CPU matcher answer (reason "warmup"):
+    // ugrep -co -J16 over 16 x 256 MiB, C3 0.602 against 0.663 s and C4 0.723
+    // against 0.873 s, with no FIND call answered by the CPU
+    // (profiles/r06_ugrep_e2e_wait.jsonl).  UGPU_ADAPTER_WARM=cpu restores the
+    // CPU answers, =0 warms up on the first GPU input's thread (the others
+    // answer on the CPU meanwhile).
+    warm_wait_ = !(e && (*e == '0' || std::strcmp(e, "cpu") == 0));
     e = std::getenv("UGPU_ADAPTER_CHUNK");
     // (2 MiB: a feed's bytes and records stay in the worker's caches between
     // the read, the H2D staging and the pops -- ugrep C3 3.2-3.5x against
@@ -1025,7 +1049,7 @@ class GpuMatcher : public Matcher {
   // small-input test comes first, so a small input never starts the warm-up.
   bool stream_may_feed()
   {
-    const int st = warm().state.load(std::memory_order_acquire);
+    const int st = warm_state();
     if (st == 1 || st == 3 || (st == 0 && sparse_ && warm_async_))
     {
       gst_why_ = warm_reason();
@@ -1154,6 +1178,7 @@ class GpuMatcher : public Matcher {
   int dev_ = -1;  // this matcher's device (dev(): assigned at the first GPU input)
   int sparse_max_ = 4;
   bool warm_async_ = true;  // device warm-up on its own thread (UGPU_ADAPTER_WARM)
+  bool warm_wait_ = true;   // workers wait for a warming device (UGPU_ADAPTER_WARM)
   ugpu_stream* gst_ = NULL;
   uint64_t sbase_ = 0, sfed_ = 0, gcur_abs_ = 0;
   bool sdone_ = false, cpu_stream_ = false;
