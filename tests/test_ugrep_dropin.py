@@ -259,3 +259,32 @@ def _dropin_ledger(tmp_path, cmds, ledger_name):
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, ledger_name), "w") as f:
         json.dump(ledger, f, indent=1)
+
+
+@pytest.mark.gpu
+def test_dropin_workers_wait_for_warmup(tmp_path):
+    """with the default warm-up policy, workers that meet the
+    device warming wait for it, so no FIND call goes to the reference matcher
+    (reason "warmup"), and the output equals the reference build's."""
+    exe_gpu = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")
+    exe_ref = os.path.join(ROOT, "oracle", "_ref", "ugrep")
+    if not (os.path.exists(exe_gpu) and os.path.exists(exe_ref)):
+        pytest.skip("ugrep builds missing (make -C oracle ref, build container)")
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import gen
+    files = []
+    for k in range(4):
+        p = tmp_path / ("c3_%d.txt" % k)
+        p.write_bytes(gen(3, 1, k << 23, 8 << 20).tobytes())
+        files.append(p.name)
+    env = dict(os.environ, UGPU_ADAPTER_MIN_BYTES="0", UGPU_ADAPTER_STATS="1")
+    env.pop("UGPU_ADAPTER_WARM", None)
+    args = ["--sort", "-co", "-J4", "[A-Za-z_][A-Za-z0-9_]*"] + files
+    ref = subprocess.run([exe_ref] + args, cwd=tmp_path, capture_output=True, timeout=120, env=env)
+    got = subprocess.run([exe_gpu] + args, cwd=tmp_path, capture_output=True, timeout=120, env=env)
+    assert got.returncode == ref.returncode and got.stdout == ref.stdout
+    st = _stats(got.stderr)
+    assert sum(m["gpu"] for m in st) > 0, st
+    assert not any("warmup" in m["why"] for m in st), st
+    assert sum(m["cpu"] for m in st) == 0, st
