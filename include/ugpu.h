@@ -149,6 +149,11 @@ typedef struct ugpu_result
 #define UGPU_PAT_WORD 1u
 #define UGPU_PAT_EMPTY 2u
 int ugpu_dfa_create(const uint32_t *opc, uint32_t nop, uint32_t pattern_flags, ugpu_dfa **out);
+/* Releases made once the process is exiting (exit() or a return from main:
+   static destructors, atexit handlers that run after the engine's own) free
+   nothing and return UGPU_OK -- the HIP runtime may already be torn down --
+   for ugpu_dfa_destroy, ugpu_scanner_destroy, ugpu_stream_destroy and
+   ugpu_records_free; ugpu_select_device makes no HIP call then. */
 int ugpu_dfa_destroy(ugpu_dfa *dfa);
 int ugpu_dfa_info_get(const ugpu_dfa *dfa, ugpu_dfa_info *info);
 

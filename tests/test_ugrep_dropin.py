@@ -288,3 +288,30 @@ def test_dropin_workers_wait_for_warmup(tmp_path):
     assert sum(m["gpu"] for m in st) > 0, st
     assert not any("warmup" in m["why"] for m in st), st
     assert sum(m["cpu"] for m in st) == 0, st
+
+
+@pytest.mark.gpu
+def test_dropin_exit_releases_nothing_after_teardown(tmp_path):
+    """ugrep keeps its matcher in a global unique_ptr (src/ugrep.cpp:4491), so
+    the adapter releases its last stream and tables from a static destructor,
+    after the engine's pools and the HIP runtime were torn down.  Before the
+    engine's exit guard (engine.hip exit_guard_arm) about 1 run in 20 of this
+    command aborted at exit ("corrupted double-linked list", rc 134); 280 runs
+    after it exited cleanly (profiles/r06_exit_abort.txt).  Here: 25 runs,
+    every one exits 0 with the reference build's output."""
+    exe_gpu = os.path.join(ROOT, "oracle", "_ref", "ugrep_gpu")
+    exe_ref = os.path.join(ROOT, "oracle", "_ref", "ugrep")
+    if not (os.path.exists(exe_gpu) and os.path.exists(exe_ref)):
+        pytest.skip("ugrep builds missing (make -C oracle ref, build container)")
+    lorem = open(os.path.join(CWD, "lorem.utf8.txt"), "rb").read()
+    (tmp_path / "lorem1m.txt").write_bytes((lorem * (1 + (1 << 20) // len(lorem)))[:1 << 20])
+    env = dict(os.environ, UGPU_ADAPTER_MIN_BYTES="0", UGPU_ADAPTER_STATS="1", UGPU_ADAPTER_WARM="0")
+    args = ["--sort", "-J1", "-o", r"\w+", "lorem1m.txt"]
+    ref = subprocess.run([exe_ref] + args, cwd=tmp_path, capture_output=True, timeout=120, env=env)
+    assert ref.returncode == 0
+    for i in range(25):
+        got = subprocess.run([exe_gpu] + args, cwd=tmp_path, capture_output=True, timeout=120, env=env)
+        assert got.returncode == 0, (i, got.returncode, got.stderr[-400:])
+        assert got.stdout == ref.stdout
+        st = _stats(got.stderr)
+        assert sum(m["gpu"] for m in st) > 0, st

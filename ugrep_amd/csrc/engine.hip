@@ -200,6 +200,30 @@ int hip_fail(hipError_t e, const char* what)
     if (_e != hipSuccess) return hip_fail(_e, #expr); \
   } while (0)
 
+// Process exit.  A caller may release handles from its own static
+// destructors (ugrep keeps its matcher in a global unique_ptr,
+// src/ugrep.cpp:4491, so the drop-in adapter's last stream and tables are
+// released after main returns).  Those run after this library's pools are
+// destroyed and after the HIP runtime's own exit teardown, both registered
+// later than such a global: a release there wrote into the freed pool vectors
+// and called into a torn-down runtime (an intermittent "corrupted
+// double-linked list" abort at ugrep_gpu's exit).  The first HIP call of the
+// process arms an atexit handler, registered after the runtime's, so it runs
+// before both; from then on the release calls free nothing (the process is
+// ending, the driver reclaims its device memory) and ugpu_select_device makes
+// no HIP call.
+std::atomic<bool> g_exiting{false};
+
+void on_process_exit() { g_exiting.store(true, std::memory_order_release); }
+
+void exit_guard_arm()
+{
+  static std::once_flag once;
+  std::call_once(once, [] { (void)std::atexit(on_process_exit); });
+}
+
+bool exiting() { return g_exiting.load(std::memory_order_acquire); }
+
 // UGPU_TRACE=1: one stderr line per pipeline step (debugging)
 bool trace_on()
 {
@@ -448,13 +472,16 @@ int ugpu_device_count(int* n)
   if (!n) return fail(UGPU_INVAL, "NULL argument");
   *n = 0;
   HIP_TRY(hipGetDeviceCount(n));
+  exit_guard_arm();
   return UGPU_OK;
 }
 
 int ugpu_select_device(int dev)
 {
+  if (exiting()) return UGPU_OK;  // (only releases follow, and they free nothing)
   int n = 0;
   HIP_TRY(hipGetDeviceCount(&n));
+  exit_guard_arm();
   if (dev < 0 || dev >= n) return fail(UGPU_INVAL, "no such device");
   HIP_TRY(hipSetDevice(dev));
   return UGPU_OK;
@@ -483,6 +510,7 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     delete d;
     return hip_fail(e, "hipGetDevice");
   }
+  exit_guard_arm();
   d->opc.assign(opc, opc + nop);
   d->plan = pl;
   d->pflags = pattern_flags;
@@ -642,7 +670,7 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
 
 int ugpu_dfa_destroy(ugpu_dfa* d)
 {
-  if (!d) return UGPU_OK;
+  if (!d || exiting()) return UGPU_OK;
   for (ugpu_dfa* r : d->reps) {
     if (r) {
       int cur = 0;
@@ -889,7 +917,7 @@ int scanner_create(const ugpu_dfa* dfa, ugpu_scanner** out, bool prefer_write)
 
 int ugpu_scanner_destroy(ugpu_scanner* s)
 {
-  if (!s) return UGPU_OK;
+  if (!s || exiting()) return UGPU_OK;
   (void)hipFree(s->d_recs);
   (void)hipFree(s->d_entries);
   (void)hipFree(s->d_obase);
@@ -1362,6 +1390,7 @@ FindWs* find_ws_acquire(int dev)
     delete w;
     return nullptr;
   }
+  exit_guard_arm();
   return w;
 }
 
@@ -1577,6 +1606,7 @@ uint8_t* pinned_get(size_t need, size_t& got)
   // (non-coherent: cached for the host reads that decode the records; every
   // read follows a stream synchronisation)
   if (hipHostMalloc(&p, c, hipHostMallocNonCoherent) != hipSuccess) return nullptr;
+  exit_guard_arm();
   got = c;
   return static_cast<uint8_t*>(p);
 }
@@ -1665,6 +1695,7 @@ RecWs* rec_ws_acquire(int dev)
   if (!w) return nullptr;
   w->dev = dev;
   if (w->init() != hipSuccess) return nullptr;  // (leaks the partial workspace on a broken device)
+  exit_guard_arm();
   return w;
 }
 
@@ -2034,6 +2065,7 @@ int ugpu_warmup(int dev)
 {
   int n = 0;
   HIP_TRY(hipGetDeviceCount(&n));
+  exit_guard_arm();
   if (dev < 0 || dev >= n) return fail(UGPU_INVAL, "no such device");
   HIP_TRY(hipSetDevice(dev));
   // the device context, one scan workspace and one records workspace (their
@@ -2380,6 +2412,7 @@ int ugpu_records_free(ugpu_records* r)
     r->cv.notify_all();
   }
   if (r->worker.joinable()) r->worker.join();
+  if (exiting()) return UGPU_OK;  // (the pinned blocks and events stay)
   for (auto& p : r->pieces) {
     if (p.landed) {  // (never popped: its copy may still be running)
       (void)hipEventSynchronize(p.landed);
@@ -3043,7 +3076,7 @@ int ugpu_stream_create(const ugpu_dfa* dfa, uint64_t keep, ugpu_stream** out)
 
 int ugpu_stream_destroy(ugpu_stream* st)
 {
-  if (!st) return UGPU_OK;
+  if (!st || exiting()) return UGPU_OK;
   (void)hipStreamSynchronize(st->ws->st);
   st->sc->bol0 = 1;
   scanner_release(st->dfa, st->sc);
