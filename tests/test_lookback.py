@@ -18,7 +18,10 @@ import pytest
 
 from oracle_lib import OracleDfa
 
-NO = ["[a-z]*ing", "ing", "[a-z]+", "[a-z]+ing|foo", "a[a-z]+ing", "[a-z]+ING", "[a-z]+i", "[a-z]+in[a-z]g"]
+NO = ["[a-z]*ing", "ing", "[a-z]+", "[a-z]+ing|foo", "a[a-z]+ing", "[a-z]+ING", "[a-z]+i", "[a-z]+in[a-z]g",
+      # (round 6 needle sets: an infinite set, a one-byte string, a string
+      # with a byte outside C, more than 16 strings)
+      "[a-z]+(ing|ed)[a-z]*", "[a-z]+(ed|ing|s)", "x+(xx|xy)", "[a-z]+in[a-z]g|[a-z]+ed"]
 
 
 def test_plan_loop_needle():
@@ -60,7 +63,11 @@ CASES = [("[a-z]+ing", "ing", "q"), ("[a-z]+aa", "aa", "q"), ("[a-z]+abab", "aba
          ("x+xx", "xx", "x"), ("[a-z_]+ing", "ing", "_"), ("[a-z@]+ing", "ing", "@"),
          # (no first-byte prefilter: 52 and 27 first bytes; the lookback alone
          # puts them on the sparse kernel)
-         ("[A-Za-z]+tion", "tion", "Q"), ("[a-z-]+ing", "ing", "-")]
+         ("[A-Za-z]+tion", "tion", "Q"), ("[a-z-]+ing", "ing", "-"),
+         # (round 6: a finite set of strings, C+ (N1|N2|...); the needle column is
+         # the one the text plants, "ing" comes with the random tokens)
+         ("[a-z]+(ing|ed)", "ed", "q"), ("[A-Za-z]+(tion|sion|ment)", "sion", "Q"), ("[0-9]+(00|50)", "50", "7"),
+         ("[a-z]+(ab|cd|ef)x", "cdx", "q")]
 
 
 def _text(seed, n_tok, needle, f):
@@ -139,7 +146,7 @@ def test_gpu_lookback_whole_and_starts(U):
 def test_gpu_lookback_shards_streams_records(U):
     import torch
     rng = np.random.default_rng(9)
-    for k in (0, 2, 3, 7):
+    for k in (0, 2, 3, 7, 9, 12):
         rx, needle, f = CASES[k]
         host = _text(20 + k, 100000, needle, f)
         dev = torch.from_numpy(host).to("cuda")
@@ -166,7 +173,7 @@ def test_gpu_lookback_shards_streams_records(U):
 @pytest.mark.gpu
 def test_gpu_lookback_word(U):
     import torch
-    for k in (0, 3, 1, 6, 5, 7, 8):
+    for k in (0, 3, 1, 6, 5, 7, 8, 9, 10, 11):
         rx, needle, f = CASES[k]
         host = _text(30 + k, 100000, needle, f)
         dev = torch.from_numpy(host).to("cuda")
@@ -288,3 +295,90 @@ def test_gpu_lookback_fuzz(U):
             pat, on = _pattern(U, nr, "1")
             assert not on, nr
             assert U.find_all(pat, dev, offsets=True).triples() == want[3], nr
+
+
+def _fuzz_multi_cases(seed, n):
+    """Random C+ (N1|N2|...) patterns: two to four strings of 2-5 bytes of C."""
+    rng = np.random.default_rng(seed)
+    pools = ["abcdefghijklmnopqrstuvwxyz", "abc", "ab", "0123456789", "xyz_", "aeiou", "ABCabc", "a@b#"]
+    out = []
+    for _ in range(n):
+        pool = pools[int(rng.integers(0, len(pools)))]
+        cset = sorted(set(rng.choice(list(pool), int(rng.integers(2, len(pool) + 1)), replace=True)))
+        needles = ["".join(rng.choice(cset, int(rng.integers(2, 6)))) for _ in range(int(rng.integers(2, 5)))]
+        cls = "[" + "".join(c if c not in "^]-\\" else "\\" + c for c in cset) + "]"
+        alt = "(" + "|".join(needles) + ")"
+        rx = cls + "+" + alt
+        near = [cls + "*" + alt, cls + "+" + alt + cls + "*"]
+        parts = []
+        for _ in range(4000):
+            r = rng.random()
+            if r < 0.5:
+                parts.append("".join(rng.choice(cset, int(rng.geometric(0.2)))))
+            elif r < 0.8:
+                parts.append(needles[int(rng.integers(0, len(needles)))])
+            elif r < 0.995:
+                parts.append(str(rng.choice([" ", "\n", ".", "-", "Z", "é", "\0"])))
+            else:
+                parts.append("".join(rng.choice(cset, int(rng.integers(100, 3000)))) + needles[0])
+        out.append((rx, near, "".join(parts).encode(), set(cset), cls + "+" + alt + "+"))
+    return out
+
+
+def test_plan_multi_needles():
+    """C+ (N1|...) with a finite set of strings of >= 2 bytes of C takes the
+    lookback (and C+ (N1|...)+, the same language)."""
+    import ugrep_amd as U
+    from ugrep_amd._lib import SHAPE_LOOP_NEEDLE as LB
+    for rx, _, _, _, same in _fuzz_multi_cases(5, 80):
+        assert U.host_plan(rx)["shape"] & LB, rx
+        assert U.host_plan(same)["shape"] & LB, same
+
+
+@pytest.mark.gpu
+def test_gpu_lookback_multi_fuzz(U):
+    """60 random C+ (N1|...) patterns over texts of C-runs holding their
+    strings, whole, in 3 shards and with option W, and their near misses
+    C* (N1|...) and C+ (N1|...) C* (the plan may or may not take those: the
+    results must equal the oracle either way), record by record."""
+    import torch
+    word = set("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_")
+    for rx, near, text, cset, _ in _fuzz_multi_cases(13, 60):
+        host = np.frombuffer(text, np.uint8).copy()
+        dev = torch.from_numpy(host).to("cuda")
+        o = OracleDfa(U.compile_regex(rx))
+        want = o.find(host, want_list=True)
+        pat, on = _pattern(U, rx, "1")
+        assert on, rx
+        assert U.find_all(pat, dev, offsets=True).triples() == want[3], rx
+        assert U.find_all_multi(pat, dev, ndev=3, offsets=True).triples() == want[3], (rx, "shards")
+        assert U.find_all(pat, dev, offsets=False).count == want[0], (rx, "count")
+        w = o.find_w(host, want_list=True)
+        patw, onw = _pattern(U, rx, "1", word=True)
+        assert onw == cset.issubset(word), rx
+        assert U.find_all(patw, dev, offsets=True).triples() == w[3], (rx, "W")
+        for nr in near:
+            want = OracleDfa(U.compile_regex(nr)).find(host, want_list=True)
+            pat, _ = _pattern(U, nr, "1")
+            assert U.find_all(pat, dev, offsets=True).triples() == want[3], nr
+
+
+@pytest.mark.gpu
+def test_gpu_lookback_multi_giant_run(U):
+    """A 32 MiB run of C whose only string of N ends it, after a short match,
+    for a needle-set table: the walks back cover it a bounded number of times
+    (the oracle walks it once, from its start)."""
+    import time
+    import torch
+    host = np.frombuffer(b" xxed " + b"q" * (32 << 20) + b"ing xing ", np.uint8).copy()
+    dev = torch.from_numpy(host).to("cuda")
+    rx = "[a-z]+(ing|ed)"
+    want = OracleDfa(U.compile_regex(rx)).find(host, want_list=True)
+    pat, on = _pattern(U, rx, "1")
+    assert on
+    U.find_all(pat, dev, offsets=False)
+    t0 = time.perf_counter()
+    r = U.find_all(pat, dev, offsets=True)
+    dt = time.perf_counter() - t0
+    assert r.triples() == want[3]
+    assert dt < 2.0, dt

@@ -544,23 +544,10 @@ int ugpu_dfa_create(const uint32_t* opc, uint32_t nop, uint32_t pattern_flags, u
     d->wstart = !any && !d->t.acap.empty();
   }
   const uint32_t* lbcls = pl.lb_cls;
-  const std::string& needle = pl.lb_needle;
   if (pl.lb) {
-    // the needle's first three bytes, one per prefilter set, group 0 (tables.hpp
-    // ft: bit 2 s + g of T0[b & 7], T1[(b >> 3) & 7], T2[b >> 6]); group 1 empty
+    // the prefilter over the strings of N (tables.cpp needle_filter)
     d->lb = true;
-    for (int s3 = 0; s3 < 3; ++s3) {
-      const uint8_t bit = (uint8_t)(1u << (2 * s3));
-      if (s3 >= (int)needle.size()) {
-        for (int v = 0; v < 8; ++v) d->lb_ft[v] |= bit, d->lb_ft[8 + v] |= bit;
-        for (int v = 0; v < 4; ++v) d->lb_ft[16 + v] |= bit;
-        continue;
-      }
-      const uint32_t b = (unsigned char)needle[s3];
-      d->lb_ft[b & 7] |= bit;
-      d->lb_ft[8 + ((b >> 3) & 7)] |= bit;
-      d->lb_ft[16 + (b >> 6)] |= bit;
-    }
+    std::copy(pl.lb_ft, pl.lb_ft + 20, d->lb_ft);
   }
   const size_t n = d->t.trans.size();
   d->ntrans_pad = (uint32_t)((n + 7) & ~size_t(7));

@@ -2,7 +2,9 @@
 // table planning, the host-only table entry points and the error string.  See
 // plan.hpp.  The device half (engine.hip) calls dfa_plan / dfa_info_fill and
 // reports its errors through host_fail, so ugpu_last_error answers for both.
+#include <array>
 #include <cstdlib>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -40,86 +42,189 @@ bool is_word_plus(const DfaTables& t)
   return ok && tables_equivalent(t, wp);
 }
 
-// Loop-needle tables: the language is C+ N for a byte set C and a string N
-// of >= 2 bytes of C (e.g. [a-z]+ing).  Then every FIND match is a whole C-run
-// prefix: it starts at a C-run's first byte (or at the scan start, inside a
-// run) and ends at the end of the run's last N -- after which no position of
-// the run starts a match -- so the chain enters every run at its start, and
-// a run holds a match iff N occurs in it after its first byte.  The sparse
-// kernel's prefilter then looks for N (3 bytes) instead of the first bytes
-// (here, common ones), and each candidate walks back over C to its run's
-// start (the reference's lookback, lib/matcher.cpp:636-656 lbk_ / cbk_,
-// restated for the FIND chain).  Recognised on the DFA: C = the start state's
-// live bytes, c N = the shortest accepted word, then the table must be
-// equivalent to the KMP automaton of C+ N (product walk over bytes).
-bool loop_needle(const DfaTables& t, uint32_t cls[8], std::string& needle)
+// Loop-needle tables: the language is C+ N for a byte set C and a finite set
+// N of strings of >= 2 bytes of C (e.g. [a-z]+ing, [a-z]+(ing|ed)).  Then
+// every FIND match is a whole C-run prefix: it starts at a C-run's first byte
+// (or at the scan start, inside a run) and ends at the end of the run's last
+// string of N -- after which no position of the run starts a match -- so the
+// chain enters every run at its start, and a run holds a match iff a string of
+// N occurs in it after its first byte.  The sparse kernel's prefilter then
+// looks for the strings of N (3 bytes deep) instead of the first bytes (here,
+// common ones), and each candidate walks back over C to its run's start (the
+// reference's lookback, lib/matcher.cpp:636-656 lbk_ / cbk_, restated for the
+// FIND chain).  Recognised on the DFA:
+//  - C = the start state's live bytes; s1 = the state after one byte c0 of C.
+//    If the language is C+ N, s1's language is M = C* N, and the shortest
+//    basis of N is the set of w in M with not (w[0] in C and w[1:] in M).
+//  - Those w are the paths of the product (state after w, state after w[1:])
+//    from (s1, none) to the nodes that accept in the first component only;
+//    the part of the product that reaches such a node must be acyclic (N
+//    finite) with at most kLbNeedles paths.
+//  - Then the table must equal the Aho-Corasick automaton of C+ N on every
+//    byte from the start (a product walk): dead exactly where the automaton
+//    leaves C, accepting exactly where a string of N has just ended.
+bool loop_needle(const DfaTables& t, uint32_t cls[8], std::vector<std::string>& needles)
 {
+  needles.clear();
   if (t.format != FMT_BYTE || t.anchored || t.redo || t.cap1 == 0 || t.start >= t.accb || t.row != 256) return false;
-  const uint32_t R = t.row;
+  const uint32_t R = t.row, S = t.states;
+  if (S > 128) return false;
   for (int i = 0; i < 8; ++i) cls[i] = 0;
+  uint32_t c0 = 256;
   for (uint32_t b = 0; b < 256; ++b)
-    if (t.trans[t.start + b]) cls[b >> 5] |= 1u << (b & 31);
+    if (t.trans[t.start + b]) {
+      cls[b >> 5] |= 1u << (b & 31);
+      if (c0 == 256) c0 = b;
+    }
+  if (c0 == 256) return false;
   auto inC = [&](uint32_t b) { return (cls[b >> 5] >> (b & 31)) & 1u; };
-  // the shortest accepted word (BFS over entries, bytes in order)
-  const uint32_t S = t.states;
-  std::vector<int32_t> par(S, -1);
-  std::vector<uint8_t> pb(S, 0);
-  std::vector<uint32_t> q{t.start / R};
-  par[t.start / R] = (int32_t)(t.start / R);
-  uint32_t hit = ~0u;
-  for (size_t qi = 0; qi < q.size() && hit == ~0u; ++qi) {
-    const uint32_t s = q[qi];
-    for (uint32_t b = 0; b < 256 && hit == ~0u; ++b) {
-      const uint32_t e = t.trans[(size_t)s * R + b];
-      if (!e) continue;
-      const uint32_t s2 = e / R;
-      if (par[s2] >= 0) continue;
-      par[s2] = (int32_t)s;
-      pb[s2] = (uint8_t)b;
-      if (e >= t.accb) hit = s2;
-      q.push_back(s2);
+  const uint32_t e1 = t.trans[t.start + c0];
+  if (e1 >= t.accb) return false;  // (a one-byte match)
+  const uint32_t s1 = e1 / R;
+  // product nodes a * (S + 1) + b, b == S: none (w empty)
+  const uint32_t NB = S + 1;
+  auto node = [&](uint32_t a, uint32_t bb) { return a * NB + bb; };
+  std::vector<int32_t> idx((size_t)S * NB, -1);
+  std::vector<uint32_t> nodes{node(s1, S)};
+  std::vector<uint8_t> end{0};
+  idx[nodes[0]] = 0;
+  // (successor of node i on byte x of C)
+  auto succ = [&](uint32_t i, uint32_t x) {
+    const uint32_t a = nodes[i] / NB, bb = nodes[i] % NB;
+    const uint32_t ea = t.trans[(size_t)a * R + x];
+    const uint32_t eb = bb == S ? e1 : t.trans[(size_t)bb * R + x];
+    return std::make_pair(ea, eb);
+  };
+  std::vector<std::vector<uint32_t>> in(1);  // predecessors
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    for (uint32_t x = 0; x < 256; ++x) {
+      if (!inC(x)) continue;
+      const auto [ea, eb] = succ((uint32_t)i, x);
+      if (!ea || !eb) return false;  // (C* N stays alive on C)
+      const uint32_t n2 = node(ea / R, eb / R);
+      if (idx[n2] < 0) {
+        idx[n2] = (int32_t)nodes.size();
+        nodes.push_back(n2);
+        end.push_back(ea >= t.accb && eb < t.accb);
+        in.emplace_back();
+      }
+      in[idx[n2]].push_back((uint32_t)i);
     }
   }
-  if (hit == ~0u) return false;
-  std::string w;
-  for (uint32_t s = hit; s != t.start / R; s = (uint32_t)par[s]) w.insert(w.begin(), (char)pb[s]);
-  if (w.size() < 3 || w.size() > 64) return false;
-  needle = w.substr(1);
-  const uint32_t m = (uint32_t)needle.size();
-  for (unsigned char c : needle)
-    if (!inC(c)) return false;
-  // KMP over the needle: the longest prefix of N that is a suffix of
-  // N[0, k) + b; state m (matched) continues like the failure of m
-  std::vector<uint32_t> fail(m + 1, 0);
-  for (uint32_t i = 1, k = 0; i < m; ++i) {
-    while (k && needle[i] != needle[k]) k = fail[k];
-    if (needle[i] == needle[k]) ++k;
-    fail[i + 1] = k;
-  }
-  auto delta = [&](uint32_t k, uint32_t b) {
-    if (k == m) k = fail[m];
-    while (k && (unsigned char)needle[k] != b) k = fail[k];
-    return (unsigned char)needle[k] == b ? k + 1 : 0u;
-  };
-  // product walk: (table entry, automaton state), automaton state m + 1 = start
-  const uint32_t K0 = m + 1;
-  std::vector<uint8_t> seen((size_t)S * (m + 2), 0);
-  std::vector<std::pair<uint32_t, uint32_t>> st{{t.start, K0}};
-  seen[(size_t)(t.start / R) * (m + 2) + K0] = 1;
+  // the nodes that reach an end node (or are one)
+  const size_t V = nodes.size();
+  std::vector<uint8_t> co(V, 0);
+  std::vector<uint32_t> st;
+  for (size_t i = 0; i < V; ++i)
+    if (end[i]) co[i] = 1, st.push_back((uint32_t)i);
   while (!st.empty()) {
-    const auto [e, k] = st.back();
+    const uint32_t j = st.back();
     st.pop_back();
+    for (uint32_t i : in[j])
+      if (!co[i]) co[i] = 1, st.push_back(i);
+  }
+  if (!co[0]) return false;
+  // the words: paths from the root through co-reachable nodes to end nodes;
+  // a cycle among those nodes means N is infinite (DFS with a path stack)
+  std::vector<uint8_t> onpath(V, 0);
+  std::string w;
+  bool bad = false;
+  std::function<void(uint32_t)> walk = [&](uint32_t i) {
+    if (bad) return;
+    if (end[i] && i != 0) {
+      if (needles.size() >= (size_t)kLbNeedles || w.size() < 2 || w.size() > 32) {
+        bad = true;
+        return;
+      }
+      needles.push_back(w);
+    }
+    onpath[i] = 1;
+    for (uint32_t x = 0; x < 256; ++x) {
+      if (!inC(x)) continue;
+      const auto [ea, eb] = succ(i, x);
+      const uint32_t j = (uint32_t)idx[node(ea / R, eb / R)];
+      if (!co[j]) continue;
+      if (onpath[j] || w.size() >= 32) {
+        bad = true;
+        return;
+      }
+      w.push_back((char)x);
+      walk(j);
+      w.pop_back();
+      if (bad) return;
+    }
+    onpath[i] = 0;
+  };
+  walk(0);
+  if (bad || needles.empty()) {
+    needles.clear();
+    return false;
+  }
+  // Aho-Corasick automaton of N: trie nodes, full goto over bytes, outputs
+  std::vector<std::array<int32_t, 256>> go(1);
+  go[0].fill(-1);
+  std::vector<uint8_t> outp(1, 0);
+  for (const std::string& n : needles) {
+    int32_t k = 0;
+    for (unsigned char x : n) {
+      if (go[k][x] < 0) {
+        go[k][x] = (int32_t)go.size();
+        go.emplace_back();
+        go.back().fill(-1);
+        outp.push_back(0);
+      }
+      k = go[k][x];
+    }
+    outp[k] = 1;
+  }
+  const uint32_t T = (uint32_t)go.size();
+  std::vector<int32_t> fl(T, 0);
+  std::vector<uint32_t> q;
+  for (uint32_t x = 0; x < 256; ++x) {
+    if (go[0][x] < 0) {
+      go[0][x] = 0;
+    } else {
+      fl[go[0][x]] = 0;
+      q.push_back((uint32_t)go[0][x]);
+    }
+  }
+  for (size_t qi = 0; qi < q.size(); ++qi) {
+    const uint32_t k = q[qi];
+    outp[k] |= outp[fl[k]];
+    for (uint32_t x = 0; x < 256; ++x) {
+      if (go[k][x] < 0) {
+        go[k][x] = go[fl[k]][x];
+      } else {
+        fl[go[k][x]] = go[fl[k]][x];
+        q.push_back((uint32_t)go[k][x]);
+      }
+    }
+  }
+  // product walk: (table entry, automaton node), node T = before the first byte
+  // (which C+ consumes: no string of N starts there)
+  std::vector<uint8_t> seen((size_t)S * (T + 1), 0);
+  std::vector<std::pair<uint32_t, uint32_t>> ps{{t.start, T}};
+  seen[(size_t)(t.start / R) * (T + 1) + T] = 1;
+  while (!ps.empty()) {
+    const auto [e, k] = ps.back();
+    ps.pop_back();
     for (uint32_t b = 0; b < 256; ++b) {
       const uint32_t e2 = t.trans[e + b];
       const bool alive = inC(b) != 0;
-      if (!e2 != !alive) return false;  // one side dead, the other not
+      if (!e2 != !alive) {  // one side dead, the other not
+        needles.clear();
+        return false;
+      }
       if (!e2) continue;
-      const uint32_t k2 = k == K0 ? 0u : delta(k, b);
-      if ((e2 >= t.accb) != (k2 == m)) return false;
-      uint8_t& v = seen[(size_t)(e2 / R) * (m + 2) + k2];
+      const uint32_t k2 = k == T ? 0u : (uint32_t)go[k][b];
+      if ((e2 >= t.accb) != (outp[k2] != 0)) {
+        needles.clear();
+        return false;
+      }
+      uint8_t& v = seen[(size_t)(e2 / R) * (T + 1) + k2];
       if (!v) {
         v = 1;
-        st.push_back({e2, k2});
+        ps.push_back({e2, k2});
       }
     }
   }
@@ -154,8 +259,9 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags, int lb)
   // starts inside a run: at_wb fails there)
   const char* lenv = std::getenv("UGPU_LB");
   if (lb < 0) lb = !(lenv && lenv[0] == '0');
-  if (lb && t.format == FMT_BYTE && loop_needle(t, p.lb_cls, p.lb_needle)) {
+  if (lb && t.format == FMT_BYTE && loop_needle(t, p.lb_cls, p.lb_needles)) {
     p.lb = true;
+    p.lb_density = needle_filter(p.lb_needles, p.lb_ft);
     if (flags & UGPU_PAT_WORD)
       for (uint32_t b = 0; b < 256 && p.lb; ++b)
         if ((p.lb_cls[b >> 5] >> (b & 31)) & 1u)
@@ -194,9 +300,8 @@ void dfa_info_fill(const DfaTables& t, const DfaPlan& p, void* out)
   info->row = t.row;
   info->format = t.format;
   info->table_bytes = (uint32_t)(t.trans.size() * 2 + t.trans32.size() * 4 + (t.format != FMT_BYTE ? 256 : 0));
-  // (loop-needle tables without a first-byte prefilter: 1, the needle's
-  // candidates are not estimated)
-  info->prefilter_ppm = t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : p.lb ? 1u : 0u;
+  // (loop-needle tables: the estimate of the prefilter over their strings)
+  info->prefilter_ppm = p.lb ? (uint32_t)(p.lb_density * 1e6) + 1 : t.filter ? (uint32_t)(t.fdensity * 1e6) + 1 : 0u;
   info->first_bytes = t.first_bytes;
   info->accepting = t.accepting;
   info->contexts = t.ctx_word ? 64u : t.anchored ? 4u : 1u;

@@ -23,20 +23,25 @@ namespace ugpu {
 // What ugpu_dfa_create uploads for a table under pattern flags, and so which
 // kernels its scans run: decided on the host alone (ugpu_dfa_plan_host answers
 // it without touching a device)
+constexpr int kLbNeedles = 16;
+
 struct DfaPlan {
   bool ok = true;  // false: option W with line anchors or empty matches (UGPU_UNSUPPORTED)
   bool nul = false, amode = false;
   bool wtab = false, wplus = false, xcw = false;
   bool xtrans = false, xid = false, xu = false, xg = false;
-  // loop-needle table (C+ N, host_api.cpp loop_needle): the sparse kernel's
-  // prefilter looks for N and its candidates walk back to their C-run's start
+  // loop-needle table (C+ N for a finite set N of strings over C,
+  // host_api.cpp loop_needle): the sparse kernel's prefilter looks for the
+  // strings of N and its candidates walk back to their C-run's start
   bool lb = false;
   // option W on a byte table without a selective prefilter: the sparse
   // kernel's W walks from the first-byte candidates that follow no ASCII
   // letter (ScanParams::wstart) instead of wfind_kernel (UGPU_WSPARSE)
   bool wsparse = false;
   uint32_t lb_cls[8] = {};
-  std::string lb_needle;
+  std::vector<std::string> lb_needles;  // (N, at most kLbNeedles strings of 2-32 bytes)
+  uint8_t lb_ft[20] = {};               // the prefilter over N (tables.cpp needle_filter)
+  double lb_density = 0;                // its estimated candidate fraction
 };
 
 // lb: loop-needle lookback 1 / 0, or -1 for the UGPU_LB default (on)

@@ -147,6 +147,24 @@ double group_leads(const std::vector<Lead>& leads, Lead (&g)[2])
   return n ? (best < 1.0 ? best : 1.0) : 0.0;
 }
 
+// The prefilter's byte tables (tables.hpp ft) from the two group leads: bit
+// 2 s + k of T0[b & 7], T1[(b >> 3) & 7], T2[b >> 6] for group k's set s
+void fill_ft(const Lead (&g)[2], uint8_t (&ft)[20])
+{
+  for (int k = 0; k < 2; ++k) {
+    const Bucket* bk[3] = {&g[k].b, &g[k].c, &g[k].d};
+    for (int s = 0; s < 3; ++s) {
+      const uint8_t bit = (uint8_t)(1u << (2 * s + k));
+      for (int v = 0; v < 8; ++v) {
+        if (bk[s]->lo >> v & 1) ft[v] |= bit;
+        if (bk[s]->mid >> v & 1) ft[8 + v] |= bit;
+      }
+      for (int v = 0; v < 4; ++v)
+        if (bk[s]->hi >> v & 1) ft[16 + v] |= bit;
+    }
+  }
+}
+
 // Restart-locality (tables.hpp): breadth-first over the configurations a FIND
 // walk can be in -- main walk state m, the live "shadow" walks the chain would
 // start at every position after the current anchor (p+1, or the end of the
@@ -1096,18 +1114,7 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   t.first_bytes = (uint32_t)leads.size();
   Lead g[2];
   t.fdensity = group_leads(leads, g);
-  for (int k = 0; k < 2; ++k) {
-    const Bucket* bk[3] = {&g[k].b, &g[k].c, &g[k].d};
-    for (int s = 0; s < 3; ++s) {
-      const uint8_t bit = (uint8_t)(1u << (2 * s + k));
-      for (int v = 0; v < 8; ++v) {
-        if (bk[s]->lo >> v & 1) t.ft[v] |= bit;
-        if (bk[s]->mid >> v & 1) t.ft[8 + v] |= bit;
-      }
-      for (int v = 0; v < 4; ++v)
-        if (bk[s]->hi >> v & 1) t.ft[16 + v] |= bit;
-    }
-  }
+  fill_ft(g, t.ft);
   // the sparse kernel pays off when few positions survive the prefilter
   // (a start state that accepts: empty matches anywhere, no candidate filter)
   t.filter = t.format == FMT_BYTE && !leads.empty() && t.fdensity <= 0.15 && start_sid < first_acc;
@@ -1126,6 +1133,30 @@ int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string&
   }
   out = std::move(t);
   return 0;
+}
+
+// Loop-needle tables (host_api.cpp loop_needle): the prefilter looks for the
+// strings of N -- one lead per string (its first three bytes, any byte past
+// its end), grouped as the first-byte leads are.  Returns the estimated
+// candidate density.
+double needle_filter(const std::vector<std::string>& needles, uint8_t (&ft)[20])
+{
+  std::vector<Lead> leads;
+  for (const std::string& n : needles) {
+    Lead l;
+    Bucket* bk[3] = {&l.b, &l.c, &l.d};
+    for (size_t s = 0; s < 3; ++s)
+      if (s < n.size())
+        bk[s]->add((unsigned char)n[s]);
+      else
+        *bk[s] = Bucket::all();
+    leads.push_back(l);
+  }
+  Lead g[2];
+  const double d = group_leads(leads, g);
+  for (int i = 0; i < 20; ++i) ft[i] = 0;
+  fill_ft(g, ft);
+  return d;
 }
 
 }  // namespace ugpu

@@ -219,5 +219,7 @@ constexpr uint16_t XT_LIVE = 2;  // the restart at this byte is alive (a walk be
 
 // Returns 0 (UGPU_OK), 1 (UNSUPPORTED) or 2 (INVAL); err gets a message.
 int build_tables(const uint32_t* opc, uint32_t nop, DfaTables& out, std::string& err);
+// the prefilter tables (ft) of a loop-needle table's strings; returns the estimated candidate density
+double needle_filter(const std::vector<std::string>& needles, uint8_t (&ft)[20]);
 
 }  // namespace ugpu
