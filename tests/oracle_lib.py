@@ -105,6 +105,8 @@ class OracleDfa:
 
     @property
     def anchored(self):
+        if self.h is None:
+            raise ValueError("the oracle refused this table (rc %d)" % self.rc)
         return bool(L.orc_dfa_anchored(self.h))
 
     def find(self, data, start=0, bias=0, want_list=False, nul=False):

@@ -199,7 +199,10 @@ def test_engine_context_tables_match_reference():
 
 # anchors the native compiler refuses (not a leading ^ / trailing $ of a
 # top-level alternative: regex_compile.cpp) -- the CPU matcher keeps them
-COMPILER_REFUSES = {"(^foo)", "(bar$)", "(^|,)foo", "foo($|,)"}
+# (round 6: anchors in a leading or trailing group are distributed over the
+# alternative, regex_compile.cpp rx_assertion_groups -- (^|,)foo compiles as
+# ^foo|,foo -- and these fixtures pin that the reference matches the same)
+COMPILER_REFUSES = set()
 
 
 def test_compiler_anchors_match_reference():
@@ -226,7 +229,10 @@ def test_compiler_anchors_match_reference():
                 continue
             tab = U.host_tables(opc)
             acap, anchored, _ = host_context(opc)
-            assert anchored == OracleDfa(c["opc"]).anchored, (c["pattern"], form)
+            ref = OracleDfa(c["opc"])
+            # (the reference's tables of anchor groups keep meta edges the
+            # oracle refuses; the compiled ones are anchored either way)
+            assert anchored == (ref.anchored if ref.supported else True), (c["pattern"], form)
             for r in c["results"]:
                 if r["list"] is None:
                     continue

@@ -103,9 +103,13 @@ def test_reflex_mode_rejects_meta():
     # buffer begin, and inside groups the reference keeps meta edges that go on
     # consuming bytes (word boundaries likewise: at the ends of top-level
     # alternatives only, tests/test_wordb.py)
-    for rx in (b"^a", b"(?m)(^a)", b"(?m)a$b", b"(?m)(a$)", b"(?m)a\\bfoo", b"(?m)(\\bfoo)", b"(?m)x*?y", b"(?m)(?!x)y", b"(?mx)a b", b"(?m)\\x{100}"):
+    for rx in (b"^a", b"(?m)x(^a)", b"(?m)a$b", b"(?m)(a$)b", b"(?m)a\\bfoo", b"(?m)(\\bfoo)+", b"(?m)x*?y", b"(?m)(?!x)y", b"(?mx)a b", b"(?m)\\x{100}"):
         with pytest.raises(U.Unsupported):
             U.compile_regex(rx, reflex=True)
+    # (round 6: a group at an alternative's start or end with the anchors at
+    # its own ends is distributed, tests/test_asgroup.py)
+    for rx in (b"(?m)(^a)", b"(?m)(a$)", b"(?m)(\\bfoo)"):
+        U.compile_regex(rx, reflex=True)
 
 
 def test_config_tables_are_loadable():
@@ -120,7 +124,7 @@ def test_config_tables_are_loadable():
         assert a["states"] <= b["states"]
 
 
-@pytest.mark.parametrize("rx", ["(^a)", "a$b", "a^", r"a\bfoo", r"(\<x)", r"\b+x", "a*?", "a+?", r"(a)\1", r"\p{NoSuchScript}", "[[:^alpha:]]",
+@pytest.mark.parametrize("rx", ["x(^a)", "a$b", "a^", r"a\bfoo", r"x(\<x)", r"\b+x", "a*?", "a+?", r"(a)\1", r"\p{NoSuchScript}", "[[:^alpha:]]",
                                 "(?!x)", r"\Qa\E", r"\p{Lu}"])
 def test_unsupported_constructs(rx):
     import ugrep_amd as U

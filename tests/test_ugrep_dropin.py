@@ -206,6 +206,18 @@ LOOK_CMDS = [(["-J1", "-co", "dolor(?= sit)"], True), (["-J1", "-on", r"[a-z]+(?
              (["-J1", "-o", r"[A-Z]\w*(?= [a-z])"], True)]
 
 
+# word boundaries inside a leading or trailing group (the compiler distributes
+# the group, tests/test_asgroup.py); line anchors in such groups compile too
+# but stay with the reference's match predictor (reason anchor_predictor)
+ASGROUP_CMDS = [(["-J1", "-co", r"(\bdolor|amet,)"], True), (["-J1", "-on", r"(\<in|ut\>)"], True),
+                (["-J1", "-o", r"(\bsit|\bamet)\b"], True), (["-J1", "-co", r"(^|, )[a-z]+"], False)]
+
+
+@pytest.mark.gpu
+def test_dropin_assertion_groups(tmp_path):
+    _dropin_ledger(tmp_path, ASGROUP_CMDS, "dropin_asgroup_ledger.json")
+
+
 @pytest.mark.gpu
 def test_dropin_lookahead_on_gpu(tmp_path):
     """ugrep lookahead commands served by the GPU, byte-equal to the reference build."""

@@ -2266,6 +2266,312 @@ void ugpu_word_ranges(std::vector<uint32_t> &out)
   }
 }
 
+// ---------------------------------------------------------------- assertion groups
+//
+// An alternative that begins with a group holding line anchors or word
+// boundaries at the start of its own alternatives -- (^|,)foo, (\<|_)id --
+// or ends with one holding them at their ends -- foo($|,) -- has those
+// assertions at the ends of the match only, but inside a group, which the
+// parser keeps for the per-context accepts of top-level alternatives.  Such a
+// group is distributed over its alternative: (^|,)foo -> ^foo|,foo, every
+// copy with the original alternative's accept index.  The reference's
+// matches for both forms are the same (checked with its matcher on
+// tests/golden/asgroup_cases.json, make_asgroup_golden.py).  Only plain
+// groups "(" and "(?:" without a quantifier are distributed, at most 64
+// alternatives; patterns with other "(?" constructs than a leading modifier
+// or with \Q are left to the parser (its error stands).
+namespace {
+
+// the end of the token at i: an escape pair, a bracket expression, or a byte
+size_t rx_token_end(const std::string &r, size_t i)
+{
+  if (r[i] == '\\')
+    return i + 2 <= r.size() ? i + 2 : r.size();
+  if (r[i] != '[')
+    return i + 1;
+  size_t j = i + 1;
+  if (j < r.size() && r[j] == '^')
+    ++j;
+  if (j < r.size() && r[j] == ']')
+    ++j;
+  while (j < r.size() && r[j] != ']')
+  {
+    if (r[j] == '\\')
+      j += 2;
+    else if (r[j] == '[' && j + 1 < r.size() && (r[j + 1] == ':' || r[j + 1] == '.' || r[j + 1] == '='))
+    {
+      const size_t e = r.find(std::string(1, r[j + 1]) + "]", j + 2);
+      j = e == std::string::npos ? r.size() : e + 2;
+    }
+    else
+      ++j;
+  }
+  return j < r.size() ? j + 1 : r.size();
+}
+
+// the top-level alternatives of r (split at '|' outside groups and brackets);
+// false when the parentheses do not balance
+bool rx_split(const std::string &r, std::vector<std::string> &out)
+{
+  out.clear();
+  int depth = 0;
+  size_t from = 0;
+  for (size_t i = 0; i < r.size(); i = rx_token_end(r, i))
+  {
+    if (r[i] == '(')
+      ++depth;
+    else if (r[i] == ')' && --depth < 0)
+      return false;
+    else if (r[i] == '|' && depth == 0)
+    {
+      out.push_back(r.substr(from, i - from));
+      from = i + 1;
+    }
+  }
+  out.push_back(r.substr(from));
+  return depth == 0;
+}
+
+// the index of the ')' closing the '(' at i (npos: none)
+size_t rx_close(const std::string &r, size_t i)
+{
+  int depth = 0;
+  for (size_t j = i; j < r.size(); j = rx_token_end(r, j))
+  {
+    if (r[j] == '(')
+      ++depth;
+    else if (r[j] == ')' && --depth == 0)
+      return j;
+  }
+  return std::string::npos;
+}
+
+bool rx_word_assertion_at(const std::string &r, size_t i)
+{
+  return i + 1 < r.size() && r[i] == '\\' && strchr("bB<>", r[i + 1]) != NULL;
+}
+
+bool rx_plain_group(const std::string &r, size_t i, size_t j, std::string &inner);
+bool rx_split(const std::string &r, std::vector<std::string> &out);
+size_t rx_close(const std::string &r, size_t i);
+
+// a group's alternative begins with an assertion and has something after it,
+// or with a plain group one of whose alternatives does
+bool rx_lead_assert(const std::string &a)
+{
+  if (!a.empty() && a[0] == '^')
+    return true;
+  if (rx_word_assertion_at(a, 0))
+    return a.size() > 2;
+  if (a.empty() || a[0] != '(')
+    return false;
+  const size_t j = rx_close(a, 0);
+  std::string inner;
+  std::vector<std::string> parts;
+  if (j == std::string::npos || !rx_plain_group(a, 0, j, inner) || !rx_split(inner, parts) ||
+      (j + 1 < a.size() && strchr("*+?{", a[j + 1]) != NULL))
+    return false;
+  for (const std::string &x : parts)
+    if (rx_lead_assert(x))
+      return true;
+  return false;
+}
+
+// a group's alternative ends with an assertion ($, or a word boundary after
+// something), or with a plain group one of whose alternatives does
+bool rx_tail_assert(const std::string &a)
+{
+  if (a.empty())
+    return false;
+  // (the last token: scan from the start, escapes decide; a group is one token)
+  size_t last = std::string::npos;
+  for (size_t i = 0; i < a.size();)
+  {
+    last = i;
+    if (a[i] == '(')
+    {
+      const size_t j = rx_close(a, i);
+      if (j == std::string::npos)
+        return false;
+      i = j + 1;
+    }
+    else
+      i = rx_token_end(a, i);
+  }
+  if (a[last] == '$')
+    return true;
+  if (rx_word_assertion_at(a, last))
+    return last > 0;
+  if (a[last] != '(' || a.back() != ')')
+    return false;
+  std::string inner;
+  std::vector<std::string> parts;
+  if (!rx_plain_group(a, last, a.size() - 1, inner) || !rx_split(inner, parts))
+    return false;
+  for (const std::string &x : parts)
+    if (rx_tail_assert(x))
+      return true;
+  return false;
+}
+
+// the contents of the plain group spanning [i, j] ("(" or "(?:"), or false
+bool rx_plain_group(const std::string &r, size_t i, size_t j, std::string &inner)
+{
+  size_t b = i + 1;
+  if (b < r.size() && r[b] == '?')
+  {
+    if (b + 1 < r.size() && r[b + 1] == ':')
+      b += 2;
+    else
+      return false;
+  }
+  inner = r.substr(b, j - b);
+  return true;
+}
+
+void rx_distribute(const std::string &a, std::vector<std::string> &out, size_t cap, bool &refuse)
+{
+  if (out.size() > cap || refuse)
+    return;
+  std::vector<std::string> parts;
+  std::string inner;
+  // a leading group with assertions at its alternatives' starts
+  if (!a.empty() && a[0] == '(')
+  {
+    const size_t j = rx_close(a, 0);
+    if (j != std::string::npos && rx_plain_group(a, 0, j, inner) &&
+        (j + 1 >= a.size() || strchr("*+?{", a[j + 1]) == NULL) && rx_split(inner, parts))
+    {
+      bool any = false;
+      for (const std::string &x : parts)
+        any = any || rx_lead_assert(x);
+      if (any)
+      {
+        for (const std::string &x : parts)
+          rx_distribute(x + a.substr(j + 1), out, cap, refuse);
+        return;
+      }
+    }
+  }
+  // a trailing group with assertions at its alternatives' ends
+  if (!a.empty() && a.back() == ')')
+  {
+    // (the '(' whose group closes at the end)
+    for (size_t i = 0; i < a.size(); i = rx_token_end(a, i))
+    {
+      if (a[i] != '(')
+        continue;
+      const size_t j = rx_close(a, i);
+      if (j == a.size() - 1)
+      {
+        if (rx_plain_group(a, i, j, inner) && rx_split(inner, parts))
+        {
+          bool any = false;
+          for (const std::string &x : parts)
+            any = any || rx_tail_assert(x);
+          if (any)
+          {
+            // ^...($|\s): the reference moves the begin anchor to the accept
+            // side, where its EOL edge (which holds before "\r\n") ends the
+            // match before a sibling that could consume the '\r' -- the
+            // distributed form would take the longer match (measured on
+            // (^|\s)foo(\s|$)); refused when a sibling is not a plain byte
+            bool eol = false, other = false;
+            for (const std::string &x : parts)
+            {
+              eol = eol || x == "$";
+              other = other || (x != "$" && !x.empty() && strchr("\\[.(", x[0]) != NULL);
+            }
+            if (a[0] == '^' && eol && other)
+            {
+              refuse = true;
+              return;
+            }
+            for (const std::string &x : parts)
+              rx_distribute(a.substr(0, i) + x, out, cap, refuse);
+            return;
+          }
+        }
+        break;
+      }
+      if (j == std::string::npos)
+        break;
+      i = j;  // (skip the group: rx_token_end moves past its ')')
+    }
+  }
+  out.push_back(a);
+}
+
+// r's top-level alternatives with their assertion groups distributed, and
+// each one's accept index; false when nothing was distributed
+bool rx_assertion_groups(const std::string &r, std::string &rewritten, std::vector<int> &accept)
+{
+  if (r.find("\\Q") != std::string::npos)
+    return false;
+  // a leading modifier (?imsx) applies to every alternative: kept in front
+  size_t body = 0;
+  if (r.size() > 2 && r[0] == '(' && r[1] == '?')
+  {
+    size_t k = 2;
+    while (k < r.size() && isalpha(static_cast<unsigned char>(r[k])))
+      ++k;
+    if (k < r.size() && r[k] == ')' && k > 2)
+      body = k + 1;
+  }
+  for (size_t q = r.find("(?", body); q != std::string::npos; q = r.find("(?", q + 1))
+    if (r.compare(q, 3, "(?:") != 0)
+      return false;
+  std::vector<std::string> alts;
+  if (!rx_split(r.substr(body), alts))
+    return false;
+  rewritten = r.substr(0, body);
+  accept.clear();
+  bool changed = false;
+  for (size_t k = 0; k < alts.size(); ++k)
+  {
+    std::vector<std::string> out;
+    bool refuse = false;
+    rx_distribute(alts[k], out, 64, refuse);
+    if (refuse || out.size() > 64 || accept.size() + out.size() > 64)
+      return false;
+    changed = changed || out.size() != 1 || out[0] != alts[k];
+    for (const std::string &x : out)
+    {
+      rewritten += (accept.empty() ? "" : "|") + x;
+      accept.push_back(static_cast<int>(k + 1));
+    }
+  }
+  return changed;
+}
+
+// opcode words of rx; accept: the accept index of each top-level alternative
+// (empty: 1, 2, ...)
+std::vector<uint32_t> compile_words(const std::string &rx, uint32_t flags, const std::vector<int> &accept)
+{
+  Tree tree;
+  Parser parser(rx, flags, tree);
+  std::vector<int> alts = parser.parse_top();
+  Glushkov g(tree);
+  std::vector<int> start;
+  for (size_t k = 0; k < alts.size(); ++k)
+  {
+    Glushkov::Info info = g.walk(alts[k]);
+    int end = g.new_pos(ByteSet(), k < accept.size() ? accept[k] : static_cast<int>(k + 1));
+    if (k < parser.metaseqs.size())
+      g.metas[end] = parser.metaseqs[k];
+    g.neg[end] = k < parser.negs.size() && parser.negs[k];
+    g.link(info.last, std::vector<int>{end});
+    Glushkov::merge(start, info.first);
+    if (info.nullable)
+      Glushkov::merge(start, std::vector<int>{end});
+  }
+  Dfa d = subsets(g, start);
+  Dfa m = unfold_gaps(minimize(d, 1));
+  return encode(m);
+}
+
+}  // namespace
+
 extern "C" {
 
 int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, uint32_t *nop)
@@ -2277,26 +2583,21 @@ int ugpu_compile(const char *regex, size_t len, uint32_t flags, uint32_t **opc, 
   try
   {
     std::string rx(regex ? regex : "", len);
-    Tree tree;
-    Parser parser(rx, flags, tree);
-    std::vector<int> alts = parser.parse_top();
-    Glushkov g(tree);
-    std::vector<int> start;
-    for (size_t k = 0; k < alts.size(); ++k)
+    std::vector<uint32_t> words;
+    try
     {
-      Glushkov::Info info = g.walk(alts[k]);
-      int end = g.new_pos(ByteSet(), static_cast<int>(k + 1));
-      if (k < parser.metaseqs.size())
-        g.metas[end] = parser.metaseqs[k];
-      g.neg[end] = k < parser.negs.size() && parser.negs[k];
-      g.link(info.last, std::vector<int>{end});
-      Glushkov::merge(start, info.first);
-      if (info.nullable)
-        Glushkov::merge(start, std::vector<int>{end});
+      words = compile_words(rx, flags, std::vector<int>());
     }
-    Dfa d = subsets(g, start);
-    Dfa m = unfold_gaps(minimize(d, 1));
-    std::vector<uint32_t> words = encode(m);
+    catch (const CompileError &e)
+    {
+      // assertions inside a leading or trailing group: distributed over the
+      // alternative (rx_assertion_groups), else the parser's error stands
+      std::string r2;
+      std::vector<int> accept;
+      if (e.code != UGPU_UNSUPPORTED || (flags & UGPU_RX_FIXED) || !rx_assertion_groups(rx, r2, accept))
+        throw;
+      words = compile_words(r2, flags, accept);
+    }
     uint32_t *buf = static_cast<uint32_t *>(malloc(words.size() * sizeof(uint32_t)));
     if (!buf)
       return UGPU_NOMEM;
