@@ -383,7 +383,9 @@ uint64_t orc_find(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t sta
  * Matcher::match with opt_.W (lib/matcher.cpp:76, :107, :142, :208, :664): a
  * walk starts at p only if at_wb() holds there, and a TAKE counts only if
  * at_we() holds at the match end (include/reflex/matcher.h:1194-1237, WITH_SPAN
- * forms); otherwise the search moves to p+1 as for no match.  iswword is the
+ * forms); otherwise the search moves to p+1 as for no match.  A REDO accept
+ * (ugrep -N) counts without at_we, and a match whose last accept is REDO is
+ * stepped over unreported, as without W.  iswword is the
  * Unicode 15.1 Word table (matcher.h:457-1192), the same ranges as \w: the
  * data file is shared with the product's compiler (it is pinned to the
  * reference by tools/gen_unicode_ranges.py, and this restatement by the W
@@ -486,7 +488,8 @@ static inline uint64_t orc_step_w(const orc_dfa *d, const uint8_t *buf, uint64_t
       break;
     s = t;
     ++q;
-    if (d->accept[s] && orc_at_we(buf, n, q))
+    /* (a REDO accept does not test at_we, lib/matcher.cpp:151-156, :218-225) */
+    if (d->accept[s] && (d->accept[s] == ORC_REDO || orc_at_we(buf, n, q)))
     {
       last = q;
       a = d->accept[s];
@@ -505,7 +508,13 @@ uint64_t orc_find_w(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t s
   {
     uint32_t a;
     uint64_t len = orc_step_w(d, buf, n, p, &a);
-    if (len > 0)
+    if (len > 0 && a == ORC_REDO)
+    {
+      /* a match whose last accept is REDO: not reported, the search goes on
+         at its end (lib/matcher.cpp:736-743) */
+      p += len;
+    }
+    else if (len > 0)
     {
       if (list && cnt < list_cap)
       {

@@ -229,6 +229,18 @@ def test_dropin_word_boundaries_on_gpu(tmp_path):
     _dropin_ledger(tmp_path, WORDB_CMDS, "dropin_wordb_ledger.json")
 
 
+# negative patterns under option W (ugrep -w -N; REDO accepts skip at_we,
+# tests/test_redo_w.py)
+NEG_W_CMDS = [(["-J1", "-cow", "-N", "dolor", "-e", r"dolor\w*"], True),
+              (["-J1", "-ow", "-N", "sit", "-e", r"s[a-z]+"], True),
+              (["-J1", "-cw", "-N", "lorem", "-e", r"\w+"], True)]
+
+
+@pytest.mark.gpu
+def test_dropin_negative_patterns_word_on_gpu(tmp_path):
+    _dropin_ledger(tmp_path, NEG_W_CMDS, "dropin_redo_w_ledger.json")
+
+
 @pytest.mark.gpu
 def test_dropin_negative_patterns_on_gpu(tmp_path):
     """ugrep -N commands served by the GPU (REDO accepts),

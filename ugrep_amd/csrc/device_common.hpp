@@ -60,6 +60,8 @@ struct Win {
   const uint32_t* amap = nullptr;  // cword: each state's row of acap (tables.hpp acap_map)
   // loop-needle tables (ScanParams::lb_cls): the 256-bit set C of C+ N
   const uint32_t* lb = nullptr;
+  // option W: per-state accept indices (ScanParams::caps; kCapRedo: REDO)
+  const uint32_t* caps = nullptr;
   // dominated restarts (ScanParams::dom): bit = state id
   const uint32_t* dom = nullptr;
   // lookahead (ScanParams::look, walk mode kWalkLook): per state TAIL / HEAD masks
@@ -102,6 +104,7 @@ __device__ __forceinline__ Win win_of(const ScanParams& P)
   w.cword = P.ctx_word;
   w.amap = P.amap;
   w.lb = P.lb_cls;
+  w.caps = P.caps;
   w.dom = P.dom;
   w.look = P.look;
   return w;
@@ -348,7 +351,9 @@ __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64
       if (e == 0) return last - p;
       s = e;
       ++q;
-      if (e >= T.accb && at_we(w, q, ovf)) {
+      // (a REDO accept, ugrep -N, does not test at_we: lib/matcher.cpp:151-156,
+      // :218-225; the emitters step over a match whose last accept is REDO)
+      if (e >= T.accb && ((w.caps && w.caps[e >> w.log_row] == kCapRedo) || at_we(w, q, ovf))) {
         last = q;
         le = e;
       }

@@ -243,10 +243,10 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags, int lb)
     p.ok = !(flags & UGPU_PAT_WORD) && !p.amode;
     return p;
   }
-  if (t.redo && ((flags & UGPU_PAT_WORD) || p.amode)) {
-    // (negative patterns under option W, or with empty matches under option
-    // N: the reference's REDO skips at_we and reports an empty REDO match;
-    // not modelled -- the CPU matcher keeps those)
+  if (t.redo && p.amode) {
+    // (negative patterns with empty matches under option N: the reference
+    // reports an empty REDO match; not modelled -- the CPU matcher keeps
+    // those.  Under option W a REDO accept skips at_we: walk<FMT, kWalkWord>)
     p.ok = false;
     return p;
   }
