@@ -47,7 +47,14 @@ std::string gen(int depth)
     if (k < 6) {
       s += rnd(12) == 0 ? kWide[rnd(sizeof(kWide) / sizeof(kWide[0]))] : kAtoms[rnd(sizeof(kAtoms) / sizeof(kAtoms[0]))];
     } else if (k < 7) {
-      s += "(" + gen(depth - 1) + ")";
+      // (round 6: groups with assertions at their alternatives' ends, which
+      // the compiler distributes over the alternative)
+      switch (rnd(4)) {
+        case 0: s += "(^|" + gen(depth - 1) + ")"; break;
+        case 1: s += "(" + gen(depth - 1) + "|$)"; break;
+        case 2: s += "(\\b" + gen(depth - 1) + "|" + gen(depth - 1) + ")"; break;
+        default: s += "(" + gen(depth - 1) + ")";
+      }
     } else if (k < 8) {
       s += "(" + gen(depth - 1) + "|" + gen(depth - 1) + ")";
     } else if (k < 9) {
