@@ -481,6 +481,42 @@ static inline uint64_t orc_step_w(const orc_dfa *d, const uint8_t *buf, uint64_t
   *acc = 0;
   if (!orc_at_wb(buf, n, p))
     return 0;
+  if (d->lookahead)
+  {
+    /* lookahead under W: orc_enter's block with the TAKE tested by at_we
+       (lib/matcher.cpp:142, :208); TAIL / HEAD unchanged (:157-175) */
+    int64_t lap[ORC_MAXLOOK];
+    int k;
+    uint32_t lk;
+    for (k = 0; k < ORC_MAXLOOK; ++k)
+      lap[k] = -1;
+    for (;;)
+    {
+      lk = d->look[s];
+      if (d->accept[s] && orc_at_we(buf, n, q))
+      {
+        last = q;
+        a = d->accept[s];
+      }
+      for (k = 0; k < ORC_MAXLOOK; ++k)
+        if (((lk >> k) & 1u) && lap[k] >= 0)
+          last = p + (uint64_t)lap[k];
+      for (k = 0; k < ORC_MAXLOOK; ++k)
+        if ((lk >> (8 + k)) & 1u)
+          lap[k] = (int64_t)(q - p);
+      if (q >= n)
+        break;
+      {
+        uint32_t t = d->next[(size_t)s * 256 + buf[q]];
+        if (t == 0)
+          break;
+        s = t;
+        ++q;
+      }
+    }
+    *acc = a;
+    return last - p;
+  }
   while (q < n)
   {
     uint32_t t = d->next[(size_t)s * 256 + buf[q]];
@@ -508,7 +544,14 @@ uint64_t orc_find_w(const orc_dfa *d, const uint8_t *buf, uint64_t n, uint64_t s
   {
     uint32_t a;
     uint64_t len = orc_step_w(d, buf, n, p, &a);
-    if (len > 0 && a == ORC_REDO)
+    if (len > 0 && a == 0)
+    {
+      /* lookahead under W: a TAIL moved the end of a walk whose TAKE failed
+         at_we -- no match (cap_ 0), and FIND goes on one past that end
+         (lib/matcher.cpp:621-637: adv_(cur_ + 1)) */
+      p += len + 1;
+    }
+    else if (len > 0 && a == ORC_REDO)
     {
       /* a match whose last accept is REDO: not reported, the search goes on
          at its end (lib/matcher.cpp:736-743) */

@@ -62,11 +62,20 @@ def run(args):
     return r.stdout.decode()
 
 
-def main():
+# option W only (ugrep -w): at_we is tested where the TAKE happens, before
+# TAIL moves the match end back
+W_PATTERNS = [("reU", r"[a-z]+(?= [a-z]+)"), ("reU", r"\w+(?=,)"), ("re", r"\w+(?=\.)"), ("reU", r"in(?=c|t)")]
+
+
+def main(word=False):
+    """word: Matcher option W (harness mode suffix "W"), written to
+    lookahead_w_cases.json"""
     cases = []
     ins = inputs()
-    for mode, rx in PATTERNS:
-        d = run(["dump", mode, rx])
+    for mode, rx in PATTERNS + (W_PATTERNS if word else []):
+        if word:
+            mode += "W"
+        d = run(["dump", mode.rstrip("W"), rx])
         if d is None:
             print("skip (reference refuses): %s" % rx, file=sys.stderr)
             continue
@@ -82,11 +91,11 @@ def main():
             res.append(dict(input=name, count=cnt, digest=dg, dcap=dc, list=lst))
         cases.append(dict(pattern=rx, mode=mode, opc=dd["opc"], conv=dd["conv_hex"], results=res))
     meta = dict(edge_hex=EDGE.hex(), inputs=[dict(name=n, spec=s.replace(REPO + "/", "")) for n, s, _ in ins])
-    out = os.path.join(GOLDEN, "lookahead_cases.json")
+    out = os.path.join(GOLDEN, "lookahead_w_cases.json" if word else "lookahead_cases.json")
     with open(out, "w") as f:
         json.dump(dict(meta=meta, cases=cases), f, separators=(",", ":"))
     print("%d cases -> %s (%d bytes)" % (len(cases), out, os.path.getsize(out)), file=sys.stderr)
 
 
 if __name__ == "__main__":
-    main()
+    main(word="--word" in sys.argv[1:])

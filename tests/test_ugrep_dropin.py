@@ -218,6 +218,16 @@ def test_dropin_assertion_groups(tmp_path):
     _dropin_ledger(tmp_path, ASGROUP_CMDS, "dropin_asgroup_ledger.json")
 
 
+# lookahead under option W (ugrep -w; tests/test_lookahead_w.py)
+LOOK_W_CMDS = [(["-J1", "-cow", "dolor(?= sit)"], True), (["-J1", "-onw", r"[a-z]+(?=,)"], True),
+               (["-J1", "-ow", r"\w+(?=\.)"], True)]
+
+
+@pytest.mark.gpu
+def test_dropin_lookahead_word_on_gpu(tmp_path):
+    _dropin_ledger(tmp_path, LOOK_W_CMDS, "dropin_lookahead_w_ledger.json")
+
+
 @pytest.mark.gpu
 def test_dropin_lookahead_on_gpu(tmp_path):
     """ugrep lookahead commands served by the GPU, byte-equal to the reference build."""

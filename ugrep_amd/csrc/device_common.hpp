@@ -367,8 +367,13 @@ __device__ __forceinline__ uint64_t walk(const Tab<FMT>& T, const Win& w, uint64
     // here), TAIL la (it ends where HEAD la was recorded in this walk, if it
     // was), HEAD la (record here); records cleared per walk (:104)
     uint32_t lap[4] = {~0u, ~0u, ~0u, ~0u};  // (offsets from p; ~0: not recorded)
+    // option W (lookahead tables have no word contexts, so a Word table means
+    // W): the walk starts where at_wb holds, a TAKE counts where at_we holds,
+    // TAIL / HEAD as without W (lib/matcher.cpp:107, :142, :157-175, :208)
+    const bool wm = w.nwtab != 0;
+    if (wm && !at_wb(w, p)) return 0;
     auto enter = [&](uint32_t e, uint64_t at) __attribute__((always_inline)) {
-      if (e >= T.accb) {
+      if (e >= T.accb && (!wm || at_we(w, at, ovf))) {
         last = at;
         le = e;
       }
@@ -551,6 +556,12 @@ __device__ __forceinline__ uint64_t chain_step(const Tab<FMT>& T, const Win& w, 
     }
   }
   const uint64_t len = walk<FMT, W>(T, w, p, le, ovf);
+  if constexpr (W == kWalkLook) {
+    // a TAIL moved the end of a walk whose TAKE failed (option W: at_we):
+    // no match, and FIND goes on one past that end (lib/matcher.cpp:621-637,
+    // adv_(cur_ + 1))
+    if (len && !le) return p + len + 1;
+  }
   if (len) {
     em.put(c, p, len, le, sign);
     return p + len;

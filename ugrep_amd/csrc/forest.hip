@@ -94,7 +94,10 @@ __device__ __forceinline__ void forest_n(const Tab<FMT>& T, const Win& w, uint64
   for (uint32_t r = tid; r < nb; r += nthr) {
     uint32_t le, ovf = 0;
     const uint64_t len = walk<FMT, W>(T, w, bs + r, le, ovf);
-    uint64_t nx = (uint64_t)r + (len ? len : 1);
+    // (lookahead under option W: a TAIL without a TAKE is no match, and the
+    // chain goes on one past its end, as chain_step)
+    const bool tail_only = W == kWalkLook && len && !le;
+    uint64_t nx = (uint64_t)r + (len ? len + (tail_only ? 1u : 0u) : 1);
     if (nx > kFNMask) {
       // a match longer than 512 MiB does not fit the entry: fail loudly (the
       // HALO flag: the caller gets UGPU_HALO and, in the drop-in adapter, the
@@ -103,7 +106,7 @@ __device__ __forceinline__ void forest_n(const Tab<FMT>& T, const Win& w, uint64
       ovf = 1;
     }
     const bool empty = W == kWalkCtx && !len && le && w.nul;  // option N: the empty match at p
-    N[r] = (uint32_t)nx | (len || empty ? kFMatch : 0u) | (empty ? kFEmpty : 0u) | (ovf ? kFOvf : 0u);
+    N[r] = (uint32_t)nx | ((len && !tail_only) || empty ? kFMatch : 0u) | (empty ? kFEmpty : 0u) | (ovf ? kFOvf : 0u);
     if constexpr (LE) le_out[r] = le;
   }
 }
@@ -418,14 +421,14 @@ hipError_t launch_forest(const ScanParams& P, uint32_t format, const ForestArgs&
     return format == 0   ? forest_fmt<0, kWalkCtx>(P, A, entry, write, tot, st)
            : format == 1 ? forest_fmt<1, kWalkCtx>(P, A, entry, write, tot, st)
                          : forest_fmt<2, kWalkCtx>(P, A, entry, write, tot, st);
+  if (P.look)  // (lookahead, with or without option W)
+    return format == 0   ? forest_fmt<0, kWalkLook>(P, A, entry, write, tot, st)
+           : format == 1 ? forest_fmt<1, kWalkLook>(P, A, entry, write, tot, st)
+                         : forest_fmt<2, kWalkLook>(P, A, entry, write, tot, st);
   if (P.wtab)
     return format == 0   ? forest_fmt<0, kWalkWord>(P, A, entry, write, tot, st)
            : format == 1 ? forest_fmt<1, kWalkWord>(P, A, entry, write, tot, st)
                          : forest_fmt<2, kWalkWord>(P, A, entry, write, tot, st);
-  if (P.look)
-    return format == 0   ? forest_fmt<0, kWalkLook>(P, A, entry, write, tot, st)
-           : format == 1 ? forest_fmt<1, kWalkLook>(P, A, entry, write, tot, st)
-                         : forest_fmt<2, kWalkLook>(P, A, entry, write, tot, st);
   return format == 0   ? forest_fmt<0, kWalkPlain>(P, A, entry, write, tot, st)
          : format == 1 ? forest_fmt<1, kWalkPlain>(P, A, entry, write, tot, st)
                        : forest_fmt<2, kWalkPlain>(P, A, entry, write, tot, st);

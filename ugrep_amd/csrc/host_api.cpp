@@ -237,10 +237,12 @@ DfaPlan dfa_plan(const DfaTables& t, uint32_t flags, int lb)
   p.nul = (flags & UGPU_PAT_EMPTY) != 0;
   p.amode = t.anchored || (p.nul && t.start_acc);
   if (t.lookahead) {
-    // lookahead tables: the lookahead walk on wfind_kernel (tables.hpp look);
-    // option W, and option N with empty matches, are not modelled with
-    // lookahead (the CPU matcher keeps those)
-    p.ok = !(flags & UGPU_PAT_WORD) && !p.amode;
+    // lookahead tables: the lookahead walk on wfind_kernel (tables.hpp look),
+    // with option W since round 6 (at_wb at the walk start, at_we on TAKE
+    // only: lib/matcher.cpp:107, :142, :208); option N with empty matches is
+    // not modelled with lookahead (the CPU matcher keeps those)
+    p.ok = !p.amode;
+    p.wtab = (flags & UGPU_PAT_WORD) != 0;
     return p;
   }
   if (t.redo && p.amode) {

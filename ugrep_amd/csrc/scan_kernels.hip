@@ -373,8 +373,8 @@ __device__ __forceinline__ bool fix_block(const ScanParams& P, const Tab<FMT>& T
   }
   if (!done)
     met = P.acap   ? merge<FMT, kWalkCtx>(T, w, C, po, nx, bhi, d, ne, ovf, P.merge_budget, &over)
-          : P.wtab ? merge<FMT, kWalkWord>(T, w, C, po, nx, bhi, d, ne, ovf, P.merge_budget, &over)
           : P.look ? merge<FMT, kWalkLook>(T, w, C, po, nx, bhi, d, ne, ovf, P.merge_budget, &over)
+          : P.wtab ? merge<FMT, kWalkWord>(T, w, C, po, nx, bhi, d, ne, ovf, P.merge_budget, &over)
                    : merge<FMT>(T, w, C, po, nx, bhi, d, ne, ovf, P.merge_budget, &over);
   r[2] += d.cnt;
   r[3] += d.dg;
@@ -539,8 +539,8 @@ __global__ void chain_fix_kernel(ScanParams P, uint64_t old_entry, uint64_t new_
   CountEm d;
   uint64_t ne = 0;
   bool met = P.acap   ? merge<FMT, kWalkCtx>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over)
-             : P.wtab ? merge<FMT, kWalkWord>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over)
              : P.look ? merge<FMT, kWalkLook>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over)
+             : P.wtab ? merge<FMT, kWalkWord>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over)
                       : merge<FMT>(T, w, C, old_entry, new_entry, P.hi, d, ne, ovf, P.merge_budget, &over);
   DevTotals* t = P.totals;
   t->count = d.cnt;

@@ -183,8 +183,8 @@ size_t wfind_smem_bytes(uint32_t ntrans_pad, uint32_t nstates, uint32_t nwtab, u
 hipError_t launch_wfind(const ScanParams& P, uint32_t format, bool write, hipStream_t stream)
 {
   if (P.acap) return wfind_mode<kWalkCtx>(P, format, write, stream);
+  if (P.look) return wfind_mode<kWalkLook>(P, format, write, stream);  // (with or without option W)
   if (P.wtab) return wfind_mode<kWalkWord>(P, format, write, stream);
-  if (P.look) return wfind_mode<kWalkLook>(P, format, write, stream);
   return wfind_mode<kWalkPlain>(P, format, write, stream);
 }
 
