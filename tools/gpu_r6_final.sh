@@ -2,7 +2,7 @@
 # round 6, closing: the whole GPU suite (one process), smoke(), the default bench line
 set -o pipefail
 cd "$(dirname "$0")/.."
-out=gpurun_out/r6f2; rm -rf $out; mkdir -p $out
+out=gpurun_out/r6f3; rm -rf $out; mkdir -p $out
 timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $out/tests.log 2>&1 || { tail -40 $out/tests.log; exit 1; }
 tail -3 $out/tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
